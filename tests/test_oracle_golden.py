@@ -1,0 +1,56 @@
+"""Pin the CPU oracle (oracle/stage1_ref.py) to the reference's own outputs.
+
+Fixtures come from running Stage1/projector_trainer.py (reference) on CPU in
+fp32 (tests/golden/make_golden.py).  fp32 restatement vs fp32 reference:
+tolerance rtol 1e-4 / atol 1e-6 (different op order in matmul/softmax)."""
+import numpy as np
+import pytest
+import torch
+
+from oracle import stage1_ref as R
+from tests import golden_util as G
+
+CASES = ["tiny", "tiny_gqa"]
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_weight_generator_stable(name):
+    d, _ = G.load(name)
+    cfg, vp, lp, pp = G.params_for(name)
+    np.testing.assert_array_equal(G.fingerprint(vp, lp, pp), d["weight_fingerprint"])
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_batch_contract(name):
+    """labels = ids with pad -> -100; vision labels -100; mask = 1 for vision, ids != pad."""
+    d, _ = G.load(name)
+    cfg = G.PRESETS[name]
+    for s in (0, 1):
+        ids = d[f"s{s}_token_ids"]
+        nv = cfg.num_vision_tokens
+        lab = d[f"s{s}_lm_labels"]
+        assert (lab[:, :nv] == -100).all()
+        np.testing.assert_array_equal(lab[:, nv:], np.where(ids == 0, -100, ids))
+        np.testing.assert_array_equal(d[f"s{s}_attention_mask"][:, nv:], (ids != 0).astype(np.int64))
+        assert (d[f"s{s}_attention_mask"][:, :nv] == 1).all()
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_matches_reference_two_steps(name):
+    torch.set_num_threads(4)
+    d, meta = G.load(name)
+    cfg, vp, lp, pp = G.params_for(name)
+    state = R.init_state(pp)
+    sc = R.StepConfig(learning_rate=meta["lr"], gradient_accumulation_steps=meta["gas"],
+                      total_steps=meta["max_train_steps"])
+    for s in range(meta["steps"]):
+        out = R.stage1_step(vp, cfg.vision, lp, cfg.text, state, G.batch(d, s), sc)
+        G.check_tensor(d, f"s{s}_patch", out["patch"], 1e-4, 1e-5)
+        G.check_tensor(d, f"s{s}_proj", out["proj"], 1e-4, 1e-5)
+        np.testing.assert_allclose(float(out["loss"]), float(d[f"s{s}_loss"]), rtol=1e-5)
+        np.testing.assert_allclose(out["lr"], float(d[f"s{s}_lr"]), rtol=1e-12)
+        G.check_tensor(d, f"s{s}_d_proj", out["d_proj"], 1e-3, 1e-7)
+        for k in pp:
+            G.check_tensor(d, f"s{s}_grad.{k}", out["grads"][k], 1e-3, 1e-7)
+            G.check_tensor(d, f"s{s}_clipped.{k}", out["clipped"][k], 1e-3, 1e-7)
+            G.check_tensor(d, f"s{s}_param.{k}", state.params[k], 1e-5, 2e-6)
