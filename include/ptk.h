@@ -1,0 +1,222 @@
+/* libptk — MI355X (gfx950) Stage-1 projector-training hot path, C ABI.
+ *
+ * The reference (SabaPivot/ProjectionTrainer) is pure Python: its Stage-1 step
+ * (Stage1/projector_trainer.py:152-245) calls HF transformers modules and
+ * torch ops.  This header is the boundary that replaces those calls: every
+ * entry point takes caller-owned device pointers (from torch tensors'
+ * data_ptr()), explicit sizes and a hipStream_t passed as void*.  Nothing here
+ * allocates, synchronises the host, or references torch types.  Every function
+ * returns 0 on success and <0 on error; ptk_last_error() returns a
+ * thread-local description of the last failure.
+ *
+ * Dtypes: "bf16" buffers hold raw bfloat16 bits (uint16), "f32" are float.
+ * Layouts are row-major; row strides are in elements.
+ */
+#ifndef PTK_H
+#define PTK_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define PTK_ABI_VERSION 1
+
+int ptk_abi_version(void);
+const char* ptk_last_error(void);
+
+/* ------------------------------------------------------------------------ *
+ * Primitive ops (unit-test surface; each replaces one torch/HF op family).  *
+ * ------------------------------------------------------------------------ */
+
+/* Row remap r -> (r / g) * gs + (r % g) + off, rows with (r % g) < skip are
+ * dropped (g == 0: r + off). */
+typedef struct {
+  int g;
+  int skip;
+  int64_t gs;
+  int64_t off;
+} ptk_rowmap;
+
+enum { PTK_ACT_NONE = 0, PTK_ACT_GELU_TANH = 1, PTK_ACT_GELU_ERF = 2, PTK_ACT_GEGLU = 3,
+       PTK_ACT_GELU_ERF_BWD = 4, PTK_ACT_GEGLU_BWD = 5 };
+enum { PTK_OUT_BF16 = 0, PTK_OUT_F32 = 1, PTK_OUT_F32_BF16ROUND = 2 };
+
+/* C[z] = epi(alpha * A[z] . B[z]^T); A [M,K] bf16, B [N,K] bf16 (both
+ * K-contiguous), K % 64 == 0.  Replaces nn.Linear / torch.matmul / the
+ * attention contractions (TF gemma3 :352-382, siglip :280-303,
+ * Stage1/projectors.py:17-19).  Epilogue order: +bias[c], +rowadd[r % period],
+ * activation, +resid (at the remapped row), store. */
+typedef struct {
+  const void* A;
+  const void* B;
+  void* C;
+  int M, N, K;
+  int64_t lda, ldb, ldc;
+  int batch;                 /* number of z */
+  int batch_inner;           /* z -> (z / batch_inner, z % batch_inner) */
+  int64_t sA0, sA1, sB0, sB1, sC0, sC1;
+  float alpha;
+  int act;                   /* PTK_ACT_* */
+  int out;                   /* PTK_OUT_* */
+  const float* bias;
+  const float* rowadd;
+  int rowadd_period;
+  int64_t ld_rowadd;
+  const float* resid;
+  int64_t ld_resid;
+  void* aux;                 /* GELU_ERF: pre-activation out; GEGLU: gate out */
+  void* aux2;                /* GEGLU: up out */
+  int64_t ld_aux;
+  const void* aux_in;        /* GELU_ERF_BWD: pre-activation; GEGLU_BWD: gate */
+  const void* aux_in2;       /* GEGLU_BWD: up */
+  int64_t ld_aux_in;
+  ptk_rowmap amap;
+  ptk_rowmap cmap;
+} ptk_gemm_desc;
+int ptk_gemm(const ptk_gemm_desc* d, void* stream);
+
+/* LayerNorm (SigLIP, modeling_siglip.py:329): x f32 [rows,cols] -> y bf16. */
+int ptk_layernorm(const float* x, const float* w, const float* b, void* y, int rows, int cols, float eps,
+                  void* stream);
+/* Gemma3RMSNorm (modeling_gemma3.py:136-150): y bf16 = x * rstd * (1 + w). */
+int ptk_rmsnorm(const float* x, const float* w, void* y, float* rstd, int rows, int cols, float eps,
+                void* stream);
+/* dx = dacc + d/dx RMSNorm(x; w) applied to dn (f32), dacc may be NULL or == dx. */
+int ptk_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* dn, const float* dacc,
+                    float* dx, int rows, int cols, void* stream);
+/* Masked softmax over the last dim (scores f32 -> P bf16), see ptk_internal MaskSpec. */
+int ptk_softmax(const float* S, void* P, int nz, int rows, int cols, int64_t ld, int rows_per_batch, int qdiv,
+                int zdiv, int causal, int window, const int32_t* key_valid, int key_len, void* stream);
+/* Fused cross-entropy forward+backward on bf16 logits (TF/loss/loss_utils.py:49-67):
+ * row_loss[r] = lse - logit[t]; logits overwritten with (softmax - onehot) * gscale[0]. */
+int ptk_cross_entropy(void* logits, int64_t ld, int rows, int vocab, const int64_t* targets, float* row_loss,
+                      const float* gscale, void* stream);
+int ptk_transpose_bf16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int nz, int64_t s_in,
+                       int64_t s_out, int rows, int cols, int rows_pad, void* stream);
+int ptk_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream);
+int ptk_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float std, float mean, void* stream);
+/* Live GEMM timing: when enabled, HIP events are recorded on the launch stream
+ * around every GEMM launch, grouped by epilogue class (PTK_ACT_*).  read()
+ * synchronises those events and returns the summed kernel time and count. */
+int ptk_gemm_timer_enable(int on);
+int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
+
+/* ------------------------------------------------------------------------ *
+ * SigLIP vision tower, frozen forward                                      *
+ * replaces vision_tower(pixel_values=...).last_hidden_state                *
+ * (Stage1/projector_trainer.py:158-171 -> modeling_siglip.py:576-619;      *
+ * the unused MAP head is skipped: its output is discarded at :173).        *
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int image_size, patch_size, channels, hidden, heads, intermediate, layers;
+  float eps;
+} ptk_siglip_config;
+
+typedef struct {
+  const void* wqkv;  const float* bqkv;   /* bf16 [3D, D] rows q|k|v, f32 [3D] */
+  const void* wo;    const float* bo;     /* bf16 [D, D], f32 [D] */
+  const void* w1;    const float* b1;     /* bf16 [I, D], f32 [I] */
+  const void* w2;    const float* b2;     /* bf16 [D, I], f32 [D] */
+  const float* ln1_w; const float* ln1_b;
+  const float* ln2_w; const float* ln2_b;
+} ptk_siglip_layer;
+
+typedef struct {
+  const void* patch_w;          /* bf16 [D, C*P*P] (conv weight flattened c,ky,kx) */
+  const float* patch_b;         /* f32 [D] */
+  const float* pos;             /* f32 [N, D] */
+  const float* post_w; const float* post_b;
+  const ptk_siglip_layer* layers;   /* HOST array [layers] */
+} ptk_siglip_weights;
+
+size_t ptk_siglip_workspace_bytes(const ptk_siglip_config* c, int batch);
+/* pixels bf16 [B, C, H, W]; out bf16 [B*N, D] = last_hidden_state (all N patches). */
+int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* w, int batch, const void* pixels,
+                   void* out, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * MLPProjector (Stage1/projectors.py:13-29): Linear -> GELU(erf) -> Linear  *
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int vision_dim, inter_dim, llm_dim;
+  const void* w1;   const float* b1;    /* bf16 [I, Dv], f32 [I] */
+  const void* w2;   const float* b2;    /* bf16 [Dl, I], f32 [Dl] */
+  const void* w2t;                      /* bf16 [I, Dl] (backward) */
+} ptk_projector;
+
+/* x bf16 [rows, Dv] -> a (pre-activation, bf16 [rows, I]), h (bf16 [rows, I]),
+ * out f32 [*, Dl] at rows remapped by out_map (the LLM input slots);
+ * round_bf16 != 0 stores the bf16-rounded value (autocast output semantics). */
+int ptk_projector_fwd(const ptk_projector* p, int rows, const void* x, void* a, void* h, float* out,
+                      ptk_rowmap out_map, int64_t ld_out, int round_bf16, void* stream);
+size_t ptk_projector_workspace_bytes(const ptk_projector* p, int rows);
+/* dy bf16 [rows, Dl] -> dw1 [I, Dv], db1 [I], dw2 [Dl, I], db2 [Dl] (f32, overwritten). */
+int ptk_projector_bwd(const ptk_projector* p, int rows, const void* x, const void* a, const void* h,
+                      const void* dy, float* dw1, float* db1, float* dw2, float* db2, void* ws, size_t ws_bytes,
+                      void* stream);
+/* dy[(b,i)] = bf16(dx_llm[b*seq_pad + i - 1]) (i >= 1), 0 for i == 0 (the dropped patch). */
+int ptk_gather_vision_grad(const float* dx_llm, int batch, int num_patches, int seq_pad, int llm_dim, void* dy,
+                           void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * Gemma3 frozen forward + dX backward with causal-LM loss                   *
+ * replaces language_model(inputs_embeds, attention_mask, labels).loss and   *
+ * accelerator.backward(loss) down to d(inputs_embeds)                       *
+ * (Stage1/projector_trainer.py:183-237 -> modeling_gemma3.py:511-659).      *
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int vocab, hidden, inter, layers, heads, kv_heads, head_dim;
+  int sliding_window, sliding_pattern;     /* layer i full iff (i+1) % pattern == 0 */
+  int pad_token_id;
+  float query_pre_attn_scalar, eps;
+} ptk_gemma3_config;
+
+typedef struct {
+  const void* wqkv;  const void* wqkv_t;  /* bf16 [Dq+2Dkv, H], [H, Dq+2Dkv] */
+  const void* wo;    const void* wo_t;    /* bf16 [H, Dq], [Dq, H] */
+  const void* wgu;   const void* wgu_t;   /* bf16 [2I, H] gate/up interleaved per 16 rows, [H, 2I] */
+  const void* wd;    const void* wd_t;    /* bf16 [H, I], [I, H] */
+  const float* ln_in; const float* ln_post_attn; const float* ln_pre_ff; const float* ln_post_ff;  /* [H] */
+  const float* q_norm; const float* k_norm;                                                        /* [hd] */
+} ptk_gemma3_layer;
+
+typedef struct {
+  const void* embed;      /* bf16 [V, H] (tied lm_head) */
+  const void* embed_t;    /* bf16 [H, V] */
+  const float* final_norm;
+  const float* rope_cos_local; const float* rope_sin_local;    /* f32 [max_pos, hd/2] */
+  const float* rope_cos_global; const float* rope_sin_global;
+  int rope_max_pos;
+  const ptk_gemma3_layer* layers;    /* HOST array [layers] */
+} ptk_gemma3_weights;
+
+typedef struct {
+  int batch, text_len, num_vision, seq_pad;   /* S = num_vision + text_len <= seq_pad, seq_pad % 64 == 0 */
+  const int64_t* token_ids;                   /* [B, T] */
+  const int64_t* labels;                      /* [B, T] (pad -> -100) */
+  float* x;        /* f32 [B*seq_pad, H]: vision rows pre-filled; text/pad rows written here */
+  float* dx;       /* f32 [B*seq_pad, H]: out, d(loss*loss_scale)/dx */
+  float loss_scale;
+  float* loss;     /* device f32 [1]: mean CE over valid targets */
+} ptk_gemma3_batch;
+
+size_t ptk_gemma3_workspace_bytes(const ptk_gemma3_config* c, int batch, int text_len, int seq_pad);
+int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_batch* b,
+                            void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * clip_grad_norm_(max_norm) + AdamW over a flat f32 parameter buffer        *
+ * (Stage1/projector_trainer.py:75-79, :240-242).  grad_scale multiplies g   *
+ * first (DDP 1/world).  partial: >= 1024 floats scratch.  norm_out: [1].    *
+ * ------------------------------------------------------------------------ */
+int ptk_clip_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
+                   float grad_scale, float max_norm, float lr, float beta1, float beta2, float eps,
+                   float weight_decay, int step, float* partial, float* norm_out, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* PTK_H */

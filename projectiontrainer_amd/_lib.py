@@ -1,0 +1,152 @@
+"""ctypes binding of libptk.so (include/ptk.h).  Fails loudly if the library
+is missing: there is no CPU fallback on the product path."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libptk.so")
+
+c_void_p, c_int, c_int64, c_float, c_size_t, c_uint64 = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t, C.c_uint64
+c_float_p = C.POINTER(C.c_float)
+
+ACT_NONE, ACT_GELU_TANH, ACT_GELU_ERF, ACT_GEGLU, ACT_GELU_ERF_BWD, ACT_GEGLU_BWD = range(6)
+OUT_BF16, OUT_F32, OUT_F32_BF16ROUND = range(3)
+
+
+class RowMap(C.Structure):
+    _fields_ = [("g", c_int), ("skip", c_int), ("gs", c_int64), ("off", c_int64)]
+
+
+class GemmDesc(C.Structure):
+    _fields_ = [("A", c_void_p), ("B", c_void_p), ("C", c_void_p),
+                ("M", c_int), ("N", c_int), ("K", c_int),
+                ("lda", c_int64), ("ldb", c_int64), ("ldc", c_int64),
+                ("batch", c_int), ("batch_inner", c_int),
+                ("sA0", c_int64), ("sA1", c_int64), ("sB0", c_int64), ("sB1", c_int64),
+                ("sC0", c_int64), ("sC1", c_int64),
+                ("alpha", c_float), ("act", c_int), ("out", c_int),
+                ("bias", c_void_p), ("rowadd", c_void_p), ("rowadd_period", c_int),
+                ("ld_rowadd", c_int64), ("resid", c_void_p), ("ld_resid", c_int64),
+                ("aux", c_void_p), ("aux2", c_void_p), ("ld_aux", c_int64),
+                ("aux_in", c_void_p), ("aux_in2", c_void_p), ("ld_aux_in", c_int64),
+                ("amap", RowMap), ("cmap", RowMap)]
+
+
+class SiglipConfigC(C.Structure):
+    _fields_ = [("image_size", c_int), ("patch_size", c_int), ("channels", c_int), ("hidden", c_int),
+                ("heads", c_int), ("intermediate", c_int), ("layers", c_int), ("eps", c_float)]
+
+
+class SiglipLayerC(C.Structure):
+    _fields_ = [("wqkv", c_void_p), ("bqkv", c_void_p), ("wo", c_void_p), ("bo", c_void_p),
+                ("w1", c_void_p), ("b1", c_void_p), ("w2", c_void_p), ("b2", c_void_p),
+                ("ln1_w", c_void_p), ("ln1_b", c_void_p), ("ln2_w", c_void_p), ("ln2_b", c_void_p)]
+
+
+class SiglipWeightsC(C.Structure):
+    _fields_ = [("patch_w", c_void_p), ("patch_b", c_void_p), ("pos", c_void_p),
+                ("post_w", c_void_p), ("post_b", c_void_p), ("layers", C.POINTER(SiglipLayerC))]
+
+
+class ProjectorC(C.Structure):
+    _fields_ = [("vision_dim", c_int), ("inter_dim", c_int), ("llm_dim", c_int),
+                ("w1", c_void_p), ("b1", c_void_p), ("w2", c_void_p), ("b2", c_void_p), ("w2t", c_void_p)]
+
+
+class Gemma3ConfigC(C.Structure):
+    _fields_ = [("vocab", c_int), ("hidden", c_int), ("inter", c_int), ("layers", c_int), ("heads", c_int),
+                ("kv_heads", c_int), ("head_dim", c_int), ("sliding_window", c_int),
+                ("sliding_pattern", c_int), ("pad_token_id", c_int),
+                ("query_pre_attn_scalar", c_float), ("eps", c_float)]
+
+
+class Gemma3LayerC(C.Structure):
+    _fields_ = [("wqkv", c_void_p), ("wqkv_t", c_void_p), ("wo", c_void_p), ("wo_t", c_void_p),
+                ("wgu", c_void_p), ("wgu_t", c_void_p), ("wd", c_void_p), ("wd_t", c_void_p),
+                ("ln_in", c_void_p), ("ln_post_attn", c_void_p), ("ln_pre_ff", c_void_p),
+                ("ln_post_ff", c_void_p), ("q_norm", c_void_p), ("k_norm", c_void_p)]
+
+
+class Gemma3WeightsC(C.Structure):
+    _fields_ = [("embed", c_void_p), ("embed_t", c_void_p), ("final_norm", c_void_p),
+                ("rope_cos_local", c_void_p), ("rope_sin_local", c_void_p),
+                ("rope_cos_global", c_void_p), ("rope_sin_global", c_void_p),
+                ("rope_max_pos", c_int), ("layers", C.POINTER(Gemma3LayerC))]
+
+
+class Gemma3BatchC(C.Structure):
+    _fields_ = [("batch", c_int), ("text_len", c_int), ("num_vision", c_int), ("seq_pad", c_int),
+                ("token_ids", c_void_p), ("labels", c_void_p), ("x", c_void_p), ("dx", c_void_p),
+                ("loss_scale", c_float), ("loss", c_void_p)]
+
+
+# exported symbol -> (restype, argtypes)
+SIGNATURES = {
+    "ptk_abi_version": (c_int, []),
+    "ptk_last_error": (C.c_char_p, []),
+    "ptk_gemm": (c_int, [C.POINTER(GemmDesc), c_void_p]),
+    "ptk_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "ptk_rmsnorm": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
+    "ptk_rmsnorm_bwd": (c_int, [c_void_p] * 6 + [c_int, c_int, c_void_p]),
+    "ptk_softmax": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
+                            c_int, c_void_p, c_int, c_void_p]),
+    "ptk_cross_entropy": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+    "ptk_transpose_bf16": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int64, c_int64, c_int,
+                                   c_int, c_int, c_void_p]),
+    "ptk_cast_f32_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "ptk_fill_normal_bf16": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_void_p]),
+    "ptk_gemm_timer_enable": (c_int, [c_int]),
+    "ptk_gemm_timer_read": (c_int, [c_int, C.POINTER(C.c_double), C.POINTER(c_int)]),
+    "ptk_siglip_workspace_bytes": (c_size_t, [C.POINTER(SiglipConfigC), c_int]),
+    "ptk_siglip_fwd": (c_int, [C.POINTER(SiglipConfigC), C.POINTER(SiglipWeightsC), c_int, c_void_p, c_void_p,
+                               c_void_p, c_size_t, c_void_p]),
+    "ptk_projector_fwd": (c_int, [C.POINTER(ProjectorC), c_int, c_void_p, c_void_p, c_void_p, c_void_p, RowMap,
+                                  c_int64, c_int, c_void_p]),
+    "ptk_projector_workspace_bytes": (c_size_t, [C.POINTER(ProjectorC), c_int]),
+    "ptk_projector_bwd": (c_int, [C.POINTER(ProjectorC), c_int] + [c_void_p] * 8 + [c_void_p, c_size_t, c_void_p]),
+    "ptk_gather_vision_grad": (c_int, [c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_void_p]),
+    "ptk_gemma3_workspace_bytes": (c_size_t, [C.POINTER(Gemma3ConfigC), c_int, c_int, c_int]),
+    "ptk_gemma3_loss_fwd_bwd": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC),
+                                        C.POINTER(Gemma3BatchC), c_void_p, c_size_t, c_void_p]),
+    "ptk_clip_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
+                               c_float, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_void_p]),
+}
+
+_lib = None
+
+
+class PtkError(RuntimeError):
+    pass
+
+
+def lib():
+    """Load libptk.so once; raise if it is absent (build with __graft_entry__.build())."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise PtkError(f"libptk.so not found at {LIB_PATH}: run `python -c 'import __graft_entry__ as g; g.build()'`")
+        L = C.CDLL(LIB_PATH)
+        for name, (res, args) in SIGNATURES.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        if L.ptk_abi_version() != 1:
+            raise PtkError("libptk ABI version mismatch")
+        _lib = L
+    return _lib
+
+
+def check(rc: int, what: str = ""):
+    if rc != 0:
+        raise PtkError(f"{what}: {lib().ptk_last_error().decode()}")
+
+
+def ptr(t) -> int | None:
+    """Device pointer of a torch tensor (None for None)."""
+    return None if t is None else t.data_ptr()
+
+
+def stream_ptr(device=None) -> int:
+    import torch
+    return torch.cuda.current_stream(device).cuda_stream

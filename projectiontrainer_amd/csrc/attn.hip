@@ -1,0 +1,270 @@
+// Attention side kernels: fused q/k RMSNorm + RoPE (fwd/bwd) and masked row
+// softmax (fwd/bwd).  The QK^T and PV contractions run on the MFMA GEMM.
+//
+// Gemma3Attention.forward (TF/models/gemma3/modeling_gemma3.py:341-383):
+//   q,k = RMSNorm_hd(q,k) (scale 1+w, bf16 out) -> RoPE (rotate_half, fp32 cos/sin)
+// masks: causal, key padding, sliding window kv > q - W (TF/masking_utils.py:92-101).
+#include "common.h"
+#include "ptk_internal.h"
+
+namespace ptk {
+
+// One wave per (token m, head h) of the fused qkv row.  EPL = head_dim / 64
+// contiguous elements per lane; RoPE partner i +- D/2 sits in lane ^ 32.
+template <int EPL>
+__global__ void __launch_bounds__(256) qknorm_rope_fwd_kernel(const bf16_t* __restrict__ qkv,
+                                                              const float* __restrict__ qw,
+                                                              const float* __restrict__ kw,
+                                                              const float* __restrict__ cos_t,
+                                                              const float* __restrict__ sin_t, AttnShape sh,
+                                                              float eps, bf16_t* __restrict__ Q,
+                                                              bf16_t* __restrict__ K, bf16_t* __restrict__ V,
+                                                              float* __restrict__ rstd_q, float* __restrict__ rstd_k) {
+  constexpr int D = EPL * 64;
+  const int lane = threadIdx.x & 63;
+  const int nh = sh.Hq + 2 * sh.Hkv;
+  const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long M = (long)sh.B * sh.S;
+  if (gw >= M * nh) return;
+  const long m = gw / nh;
+  const int h = (int)(gw - m * nh);
+  const int b = (int)(m / sh.S), s = (int)(m - (long)b * sh.S);
+  const int G = sh.Hq / sh.Hkv;
+  const bf16_t* src = qkv + m * (long)nh * D + (long)h * D + lane * EPL;
+  float x[EPL];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) x[e] = bf2f(src[e]);
+  if (h >= sh.Hq + sh.Hkv) {   // v head: relayout only
+    const int kvh = h - sh.Hq - sh.Hkv;
+    bf16_t* dst = V + (((long)b * sh.Hkv + kvh) * sh.S + s) * D + lane * EPL;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) dst[e] = src[e];
+    return;
+  }
+  const bool isq = h < sh.Hq;
+  const float* w = isq ? qw : kw;
+  float ss = 0.f;
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) ss += x[e] * x[e];
+  const float rs = rsqrtf(warp_sum(ss) / D + eps);
+  float xn[EPL], part[EPL];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) xn[e] = bfround(x[e] * rs * (1.f + w[lane * EPL + e]));
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) part[e] = __shfl_xor(xn[e], 32, 64);
+  const int fi = (lane & 31) * EPL;   // frequency index (cos[i] == cos[i + D/2])
+  const float sgn = lane < 32 ? -1.f : 1.f;
+  bf16_t* dst;
+  if (isq) {
+    const int kvh = h / G, j = h - kvh * G;
+    dst = Q + ((((long)b * sh.Hkv + kvh) * sh.S + s) * G + j) * D + lane * EPL;
+    if (lane == 0) rstd_q[m * sh.Hq + h] = rs;
+  } else {
+    const int kvh = h - sh.Hq;
+    dst = K + (((long)b * sh.Hkv + kvh) * sh.S + s) * D + lane * EPL;
+    if (lane == 0) rstd_k[m * sh.Hkv + kvh] = rs;
+  }
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const float c = cos_t[(long)s * (D / 2) + fi + e], sn = sin_t[(long)s * (D / 2) + fi + e];
+    dst[e] = f2bf(xn[e] * c + sgn * part[e] * sn);
+  }
+}
+
+template <int EPL>
+__global__ void __launch_bounds__(256) qknorm_rope_bwd_kernel(
+    const bf16_t* __restrict__ qkv, const float* __restrict__ qw, const float* __restrict__ kw,
+    const float* __restrict__ cos_t, const float* __restrict__ sin_t, AttnShape sh, const float* __restrict__ rstd_q,
+    const float* __restrict__ rstd_k, const bf16_t* __restrict__ dQ, const bf16_t* __restrict__ dK,
+    const bf16_t* __restrict__ dV, bf16_t* __restrict__ dqkv) {
+  constexpr int D = EPL * 64;
+  const int lane = threadIdx.x & 63;
+  const int nh = sh.Hq + 2 * sh.Hkv;
+  const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  const long M = (long)sh.B * sh.S;
+  if (gw >= M * nh) return;
+  const long m = gw / nh;
+  const int h = (int)(gw - m * nh);
+  const int b = (int)(m / sh.S), s = (int)(m - (long)b * sh.S);
+  const int G = sh.Hq / sh.Hkv;
+  bf16_t* out = dqkv + m * (long)nh * D + (long)h * D + lane * EPL;
+  if (h >= sh.Hq + sh.Hkv) {
+    const int kvh = h - sh.Hq - sh.Hkv;
+    const bf16_t* src = dV + (((long)b * sh.Hkv + kvh) * sh.S + s) * D + lane * EPL;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) out[e] = src[e];
+    return;
+  }
+  const bool isq = h < sh.Hq;
+  const float* w = isq ? qw : kw;
+  const bf16_t* dy;
+  float rs;
+  if (isq) {
+    const int kvh = h / G, j = h - kvh * G;
+    dy = dQ + ((((long)b * sh.Hkv + kvh) * sh.S + s) * G + j) * D + lane * EPL;
+    rs = rstd_q[m * sh.Hq + h];
+  } else {
+    const int kvh = h - sh.Hq;
+    dy = dK + (((long)b * sh.Hkv + kvh) * sh.S + s) * D + lane * EPL;
+    rs = rstd_k[m * sh.Hkv + kvh];
+  }
+  const int fi = (lane & 31) * EPL;
+  float ds[EPL], dc[EPL], part[EPL];
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    const float g = bf2f(dy[e]);
+    dc[e] = g * cos_t[(long)s * (D / 2) + fi + e];
+    ds[e] = g * sin_t[(long)s * (D / 2) + fi + e];
+  }
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) part[e] = __shfl_xor(ds[e], 32, 64);
+  // rot^T(v)_i = v_{i+D/2} (i < D/2), -v_{i-D/2} (i >= D/2)
+  const float sgn = lane < 32 ? 1.f : -1.f;
+  const bf16_t* xs = qkv + m * (long)nh * D + (long)h * D + lane * EPL;
+  float x[EPL], dxn[EPL];
+  float sdot = 0.f;
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) {
+    x[e] = bf2f(xs[e]);
+    dxn[e] = bfround(dc[e] + sgn * part[e]) * (1.f + w[lane * EPL + e]);
+    sdot += dxn[e] * x[e];
+  }
+  sdot = warp_sum(sdot);
+  const float c3 = rs * rs * rs * sdot / D;
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) out[e] = f2bf(rs * dxn[e] - c3 * x[e]);
+}
+
+constexpr int SMAXV = 8;   // float4 per lane -> cols <= 2048
+
+__global__ void __launch_bounds__(256) softmax_fwd_kernel(const float* __restrict__ S, bf16_t* __restrict__ P,
+                                                          long nrows, int rows, int cols, long ld, MaskSpec mk) {
+  const int lane = threadIdx.x & 63;
+  const long gr = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gr >= nrows) return;
+  const long z = gr / rows;
+  const int r = (int)(gr - z * rows);
+  const int q = (r % mk.rows_per_batch) / mk.qdiv;
+  const long b = z / mk.zdiv;
+  const float* srow = S + gr * ld;
+  bf16_t* prow = P + gr * ld;
+  float4 v[SMAXV];
+  float mx = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < SMAXV; ++i) {
+    const int c0 = lane * 4 + i * 256;
+    if (c0 >= cols) break;
+    float4 t = *reinterpret_cast<const float4*>(srow + c0);
+    float tv[4] = {t.x, t.y, t.z, t.w};
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      const int k = c0 + e;
+      bool ok = mk.key_valid ? (mk.key_valid[b * cols + k] != 0) : (k < mk.key_len);
+      if (mk.causal) ok = ok && (k <= q);
+      if (mk.window) ok = ok && (k > q - mk.window);
+      tv[e] = ok ? tv[e] : -INFINITY;
+      mx = fmaxf(mx, tv[e]);
+    }
+    v[i] = make_float4(tv[0], tv[1], tv[2], tv[3]);
+  }
+  mx = warp_max(mx);
+  float sum = 0.f;
+#pragma unroll
+  for (int i = 0; i < SMAXV; ++i) {
+    const int c0 = lane * 4 + i * 256;
+    if (c0 >= cols) break;
+    float4 t = v[i];
+    t.x = t.x == -INFINITY ? 0.f : __expf(t.x - mx);
+    t.y = t.y == -INFINITY ? 0.f : __expf(t.y - mx);
+    t.z = t.z == -INFINITY ? 0.f : __expf(t.z - mx);
+    t.w = t.w == -INFINITY ? 0.f : __expf(t.w - mx);
+    v[i] = t;
+    sum += t.x + t.y + t.z + t.w;
+  }
+  sum = warp_sum(sum);
+  const float inv = sum > 0.f ? 1.f / sum : 0.f;
+#pragma unroll
+  for (int i = 0; i < SMAXV; ++i) {
+    const int c0 = lane * 4 + i * 256;
+    if (c0 >= cols) break;
+    u16x4_t o;
+    o[0] = f2bf(v[i].x * inv); o[1] = f2bf(v[i].y * inv); o[2] = f2bf(v[i].z * inv); o[3] = f2bf(v[i].w * inv);
+    *reinterpret_cast<u16x4_t*>(prow + c0) = o;
+  }
+}
+
+__global__ void __launch_bounds__(256) softmax_bwd_kernel(const bf16_t* __restrict__ P, const float* __restrict__ dP,
+                                                          bf16_t* __restrict__ dS, long nrows, int cols, long ld,
+                                                          float scale) {
+  const int lane = threadIdx.x & 63;
+  const long gr = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gr >= nrows) return;
+  float4 pv[SMAXV], gv[SMAXV];
+  float dot = 0.f;
+#pragma unroll
+  for (int i = 0; i < SMAXV; ++i) {
+    const int c0 = lane * 4 + i * 256;
+    if (c0 >= cols) break;
+    u16x4_t u = *reinterpret_cast<const u16x4_t*>(P + gr * ld + c0);
+    pv[i] = make_float4(bf2f(u[0]), bf2f(u[1]), bf2f(u[2]), bf2f(u[3]));
+    gv[i] = *reinterpret_cast<const float4*>(dP + gr * ld + c0);
+    dot += pv[i].x * gv[i].x + pv[i].y * gv[i].y + pv[i].z * gv[i].z + pv[i].w * gv[i].w;
+  }
+  dot = warp_sum(dot);
+#pragma unroll
+  for (int i = 0; i < SMAXV; ++i) {
+    const int c0 = lane * 4 + i * 256;
+    if (c0 >= cols) break;
+    u16x4_t o;
+    o[0] = f2bf(pv[i].x * (gv[i].x - dot) * scale);
+    o[1] = f2bf(pv[i].y * (gv[i].y - dot) * scale);
+    o[2] = f2bf(pv[i].z * (gv[i].z - dot) * scale);
+    o[3] = f2bf(pv[i].w * (gv[i].w - dot) * scale);
+    *reinterpret_cast<u16x4_t*>(dS + gr * ld + c0) = o;
+  }
+}
+
+#define QKR_DISPATCH(KERNEL, ...)                                                                     \
+  switch (s.D) {                                                                                      \
+    case 64: hipLaunchKernelGGL(KERNEL<1>, grid, dim3(256), 0, st, __VA_ARGS__); break;              \
+    case 128: hipLaunchKernelGGL(KERNEL<2>, grid, dim3(256), 0, st, __VA_ARGS__); break;             \
+    case 256: hipLaunchKernelGGL(KERNEL<4>, grid, dim3(256), 0, st, __VA_ARGS__); break;             \
+    default: return set_error("qknorm_rope: head_dim %d unsupported", s.D);                          \
+  }
+
+int launch_qknorm_rope_fwd(const bf16_t* qkv, const float* qw, const float* kw, const float* cos_t,
+                           const float* sin_t, AttnShape s, float eps, bf16_t* Q, bf16_t* K, bf16_t* V,
+                           float* rstd_q, float* rstd_k, hipStream_t st) {
+  if (s.Hq % s.Hkv) return set_error("qknorm_rope: Hq %% Hkv != 0");
+  const long waves = (long)s.B * s.S * (s.Hq + 2 * s.Hkv);
+  dim3 grid((unsigned)((waves + 3) / 4));
+  QKR_DISPATCH(qknorm_rope_fwd_kernel, qkv, qw, kw, cos_t, sin_t, s, eps, Q, K, V, rstd_q, rstd_k)
+  return hipGetLastError() == hipSuccess ? 0 : set_error("qknorm_rope_fwd launch failed");
+}
+int launch_qknorm_rope_bwd(const bf16_t* qkv, const float* qw, const float* kw, const float* cos_t,
+                           const float* sin_t, AttnShape s, const float* rstd_q, const float* rstd_k,
+                           const bf16_t* dQ, const bf16_t* dK, const bf16_t* dV, bf16_t* dqkv, hipStream_t st) {
+  if (s.Hq % s.Hkv) return set_error("qknorm_rope: Hq %% Hkv != 0");
+  const long waves = (long)s.B * s.S * (s.Hq + 2 * s.Hkv);
+  dim3 grid((unsigned)((waves + 3) / 4));
+  QKR_DISPATCH(qknorm_rope_bwd_kernel, qkv, qw, kw, cos_t, sin_t, s, rstd_q, rstd_k, dQ, dK, dV, dqkv)
+  return hipGetLastError() == hipSuccess ? 0 : set_error("qknorm_rope_bwd launch failed");
+}
+int launch_softmax_fwd(const float* S, bf16_t* P, int nz, int rows, int cols, long ld, MaskSpec m, hipStream_t st) {
+  if (cols % 4 || cols > SMAXV * 256 || ld % 4) return set_error("softmax: cols=%d unsupported", cols);
+  const long nrows = (long)nz * rows;
+  if (nrows <= 0) return 0;
+  hipLaunchKernelGGL(softmax_fwd_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, st, S, P, nrows, rows,
+                     cols, ld, m);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("softmax_fwd launch failed");
+}
+int launch_softmax_bwd(const bf16_t* P, const float* dP, bf16_t* dS, int nrows, int cols, long ld, float scale,
+                       hipStream_t st) {
+  if (cols % 4 || cols > SMAXV * 256 || ld % 4) return set_error("softmax_bwd: cols=%d unsupported", cols);
+  if (nrows <= 0) return 0;
+  hipLaunchKernelGGL(softmax_bwd_kernel, dim3((unsigned)((nrows + 3) / 4)), dim3(256), 0, st, P, dP, dS,
+                     (long)nrows, cols, ld, scale);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("softmax_bwd launch failed");
+}
+
+}  // namespace ptk

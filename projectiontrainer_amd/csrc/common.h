@@ -1,0 +1,91 @@
+// Shared device helpers for libptk (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef uint16_t bf16_t;                                         // raw bf16 bits
+typedef __attribute__((ext_vector_type(8))) short bf16x8_t;      // MFMA A/B fragment
+typedef __attribute__((ext_vector_type(4))) float f32x4_t;       // 16x16 accumulator
+typedef __attribute__((ext_vector_type(4))) unsigned short u16x4_t;
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8_t;
+
+#define PTK_DEV __device__ __forceinline__
+
+PTK_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
+
+// round-to-nearest-even f32 -> bf16 (NaN stays NaN)
+PTK_DEV bf16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (bf16_t)(u >> 16);
+}
+PTK_DEV float bfround(float f) { return bf2f(f2bf(f)); }
+
+PTK_DEV float warp_sum(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+PTK_DEV float warp_max(float v) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+  return v;
+}
+
+// block-wide sum for blockDim.x == NT (multiple of 64); `red` holds NT/64 floats
+template <int NT>
+PTK_DEV float block_sum(float v, float* red) {
+  v = warp_sum(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = 0.f;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t += red[i];
+  return t;
+}
+template <int NT>
+PTK_DEV float block_max(float v, float* red) {
+  v = warp_max(v);
+  const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
+  __syncthreads();
+  if (l == 0) red[w] = v;
+  __syncthreads();
+  float t = -INFINITY;
+#pragma unroll
+  for (int i = 0; i < NT / 64; ++i) t = fmaxf(t, red[i]);
+  return t;
+}
+
+// GELU variants (TF/activations.py: gelu_pytorch_tanh; torch nn.GELU default = erf)
+PTK_DEV float gelu_tanh(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+}
+PTK_DEV float gelu_tanh_grad(float x) {
+  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
+  float x2 = x * x;
+  float inner = k0 * (x + k1 * x2 * x);
+  float t = tanhf(inner);
+  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+}
+PTK_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
+PTK_DEV float gelu_erf_grad(float x) {
+  return 0.5f * (1.f + erff(x * 0.7071067811865476f)) + x * 0.3989422804014327f * __expf(-0.5f * x * x);
+}
+
+// Row remap r -> (r / g) * gs + (r % g) + off   (g == 0: identity)
+struct RowMap {
+  int g;
+  int skip;      // rows with (r % g) < skip map to -1 (not stored)
+  long gs;
+  long off;
+};
+PTK_DEV long map_row(const RowMap& m, long r) {
+  if (m.g == 0) return r + m.off;
+  long q = r / m.g, s = r - q * m.g;
+  if (s < m.skip) return -1;
+  return q * m.gs + s + m.off;
+}

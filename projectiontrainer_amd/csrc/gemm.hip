@@ -1,0 +1,273 @@
+// bf16 MFMA GEMM for gfx950 with fused epilogues.
+//
+//   C[z][M,N] = epi( alpha * A[z][M,K] . B[z][N,K]^T )
+//
+// Both operands K-contiguous ("NT"): A is an activation [tokens, K], B is a
+// weight stored like nn.Linear ([out, in]) or a pre-transposed copy of one.
+// Every dense contraction of the Stage-1 step maps onto this one kernel:
+// Linear forwards (x . W^T), frozen-weight dX (dY . (W^T)^T with W^T stored),
+// attention scores (Q . K^T) and P.V (P . (V^T)^T), projector weight grads
+// (dY^T . (H^T)^T).
+//
+// Tile 128x128x64, 256 threads = 4 waves (2x2), each wave 64x64 as 4x4
+// v_mfma_f32_16x16x32_bf16 tiles (fp32 accumulate).  Operands are staged
+// global->LDS with global_load_lds_dwordx4 (LDS-DMA, 1 KiB per wave
+// instruction = 8 rows x 128 B), double-buffered so the next K-tile's DMA
+// overlaps the current tile's MFMAs.  LDS rows are 128 B; the 16-B chunk of
+// logical k-chunk c in row r sits at c ^ ((r>>1)&7), applied on the DMA
+// *source* address (LDS stays lane-linear) and on the ds_read_b128 address,
+// which makes every 16-lane ds_read_b128 group conflict-free.
+// Block ids are remapped so each XCD walks a contiguous range of tiles in
+// GROUP_M-row groups (L2 reuse of A row-panels and B column-panels).
+#include "common.h"
+#include "ptk_internal.h"
+
+#include <vector>
+
+namespace ptk {
+
+constexpr int BM = 128, BN = 128, BK = 64, GROUP_M = 8;
+constexpr int STAGE_BYTES = (BM + BN) * BK * 2;   // 32 KiB
+
+typedef const __attribute__((address_space(1))) void* gptr_t;
+typedef __attribute__((address_space(3))) void* lptr_t;
+
+PTK_DEV void glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 16, 0, 0);
+}
+
+template <int ACT, int OUT>
+PTK_DEV void epi_store(const GemmArgs& p, char* Cz, long r, long c, float v) {
+  // r, c in GEMM output space (r < M, c < N)
+  if (p.bias) v += p.bias[c];
+  if (p.rowadd) v += p.rowadd[(r % p.rowadd_period) * p.ld_rowadd + c];
+  if constexpr (ACT == ACT_GELU_TANH) {
+    v = gelu_tanh(bfround(v));
+  } else if constexpr (ACT == ACT_GELU_ERF) {
+    // pre-activation kept (bf16) for the backward: Stage1/projectors.py:17-18
+    float a = bfround(v);
+    if (p.aux) p.aux[r * p.ld_aux + c] = f2bf(a);
+    v = gelu_erf(a);
+  } else if constexpr (ACT == ACT_GELU_ERF_BWD) {
+    v = bfround(v) * gelu_erf_grad(bf2f(p.aux_in[r * p.ld_aux_in + c]));
+  }
+  const long cr = map_row(p.cmap, r);
+  if (cr < 0) return;
+  if (p.resid) v += p.resid[cr * p.ld_resid + c];
+  if constexpr (OUT == OUT_BF16) {
+    reinterpret_cast<bf16_t*>(Cz)[cr * p.ldc + c] = f2bf(v);
+  } else if constexpr (OUT == OUT_F32) {
+    reinterpret_cast<float*>(Cz)[cr * p.ldc + c] = v;
+  } else {
+    reinterpret_cast<float*>(Cz)[cr * p.ldc + c] = bfround(v);
+  }
+}
+
+template <int ACT, int OUT>
+__global__ void __launch_bounds__(256, 2) gemm_nt_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 1, wc = wave & 1;
+
+  const int nbm = (p.M + BM - 1) / BM, nbn = (p.N + BN - 1) / BN;
+  const int ntile = nbm * nbn;
+  int bid = blockIdx.x;
+  {  // XCD remap (bijective): blocks b, b+8, ... share an XCD -> give them consecutive tiles
+    const int q = ntile >> 3, rr = ntile & 7, x = bid & 7;
+    bid = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (bid >> 3);
+  }
+  const int per_group = GROUP_M * nbn;
+  const int first_m = (bid / per_group) * GROUP_M;
+  const int gsz = min(nbm - first_m, GROUP_M);
+  const int bm = first_m + (bid % per_group) % gsz;
+  const int bn = (bid % per_group) / gsz;
+
+  const int z = blockIdx.z;
+  const int z0 = z / p.zin, z1 = z - z0 * p.zin;
+  const bf16_t* A = p.A + z0 * p.sA0 + z1 * p.sA1;
+  const bf16_t* B = p.B + z0 * p.sB0 + z1 * p.sB1;
+
+  // staging: lane i of a wave instruction writes LDS row (i>>3) chunk (i&7) of an 8-row group
+  const int sr = lane >> 3, sc = lane & 7;
+  const bf16_t* asrc[4];
+  const bf16_t* bsrc[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int lr = wave * 32 + j * 8 + sr;
+    const int lc = sc ^ ((lr >> 1) & 7);
+    const long gm = min(bm * BM + lr, p.M - 1);
+    const long am = map_row(p.amap, gm);
+    asrc[j] = A + am * p.lda + lc * 8;
+    const long gn = min(bn * BN + lr, p.N - 1);
+    bsrc[j] = B + gn * p.ldb + lc * 8;
+  }
+  auto stage = [&](int t, int s) {
+    char* base = smem + s * STAGE_BYTES + wave * 32 * 128;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds16(asrc[j] + t * BK, base + j * 8 * 128);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) glds16(bsrc[j] + t * BK, base + BM * 128 + j * 8 * 128);
+  };
+
+  f32x4_t acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  // per-lane fragment offset: row (lane&15), logical chunk (lane>>4), swizzled by (row>>1)&7
+  const int frag_off = (lane & 15) * 128 + (((lane >> 4) ^ ((lane >> 1) & 7)) << 4);
+
+  const int nt = p.K / BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  for (int t = 0; t < nt; ++t) {
+    const int s = t & 1;
+    if (t + 1 < nt) stage(t + 1, s ^ 1);
+    const char* As = smem + s * STAGE_BYTES + wr * 64 * 128;
+    const char* Bs = smem + s * STAGE_BYTES + BM * 128 + wc * 64 * 128;
+#pragma unroll
+    for (int ks = 0; ks < 2; ++ks) {
+      bf16x8_t a[4], b[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        a[i] = *reinterpret_cast<const bf16x8_t*>(As + i * 16 * 128 + (frag_off ^ (ks << 6)));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+        b[i] = *reinterpret_cast<const bf16x8_t*>(Bs + i * 16 * 128 + (frag_off ^ (ks << 6)));
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i], b[j], acc[i][j], 0, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: lane holds C[row fq*4+j][col fr] of each 16x16 tile
+  char* Cz = reinterpret_cast<char*>(p.C) + (z0 * p.sC0 + z1 * p.sC1) * (OUT == OUT_BF16 ? 2 : 4);
+  const int fr = lane & 15, fq = lane >> 4;
+  const long row0 = (long)bm * BM + wr * 64 + fq * 4;
+  const long col0 = (long)bn * BN + wc * 64 + fr;
+  if constexpr (ACT == ACT_GEGLU) {
+    // interleaved gate/up weights: GEMM cols [32q, 32q+16) = gate[16q..], [32q+16, 32q+32) = up[16q..]
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 2; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long r = row0 + i * 16 + j;
+          const long hc = ((long)bn * BN + wc * 64) / 2 + k * 16 + fr;
+          if (r >= p.M || 2 * hc >= p.N) continue;
+          const float g = bfround(p.alpha * acc[i][2 * k][j]);
+          const float u = bfround(p.alpha * acc[i][2 * k + 1][j]);
+          if (p.aux) p.aux[r * p.ld_aux + hc] = f2bf(g);
+          if (p.aux2) p.aux2[r * p.ld_aux + hc] = f2bf(u);
+          const float h = bfround(gelu_tanh(g)) * u;     // TF gemma3 :131-133, bf16 ops
+          const long cr = map_row(p.cmap, r);
+          if (cr >= 0) reinterpret_cast<bf16_t*>(Cz)[cr * p.ldc + hc] = f2bf(h);
+        }
+  } else if constexpr (ACT == ACT_GEGLU_BWD) {
+    // GEMM output = dh [M, I]; write d(gate), d(up) into the interleaved [M, 2I] layout
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long r = row0 + i * 16 + j;
+          const long c = col0 + k * 16;
+          if (r >= p.M || c >= p.N) continue;
+          const float dh = bfround(p.alpha * acc[i][k][j]);
+          const float g = bf2f(p.aux_in[r * p.ld_aux_in + c]);
+          const float u = bf2f(p.aux_in2[r * p.ld_aux_in + c]);
+          const float dg = bfround(dh * u) * gelu_tanh_grad(g);
+          const float du = dh * bfround(gelu_tanh(g));
+          const long cr = map_row(p.cmap, r);
+          if (cr < 0) continue;
+          const long gc = (c >> 4) * 32 + (c & 15);
+          bf16_t* C = reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc;
+          C[gc] = f2bf(dg);
+          C[gc + 16] = f2bf(du);
+        }
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int k = 0; k < 4; ++k)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const long r = row0 + i * 16 + j;
+          const long c = col0 + k * 16;
+          if (r < p.M && c < p.N) epi_store<ACT, OUT>(p, Cz, r, c, p.alpha * acc[i][k][j]);
+        }
+  }
+}
+
+// ---- optional live per-class timing (HIP events around launches; bench.py roofline)
+static bool g_timing = false;
+static std::vector<hipEvent_t> g_ev[8];
+static size_t g_ev_used[8];
+
+void timer_enable(int on) {
+  g_timing = on != 0;
+  if (g_timing)
+    for (int c = 0; c < 8; ++c) g_ev_used[c] = 0;   // a new measurement window starts
+}
+static hipEvent_t next_event(int cls) {
+  auto& v = g_ev[cls];
+  if (g_ev_used[cls] == v.size()) {
+    hipEvent_t e;
+    if (hipEventCreate(&e) != hipSuccess) return nullptr;
+    v.push_back(e);
+  }
+  return v[g_ev_used[cls]++];
+}
+int timer_read(int cls, double* total_ms, int* count) {
+  *total_ms = 0;
+  *count = 0;
+  if (cls < 0 || cls >= 8) return set_error("timer: class out of range");
+  for (size_t i = 0; i + 1 < g_ev_used[cls]; i += 2) {
+    float ms = 0;
+    if (hipEventSynchronize(g_ev[cls][i + 1]) != hipSuccess) return set_error("timer: sync failed");
+    if (hipEventElapsedTime(&ms, g_ev[cls][i], g_ev[cls][i + 1]) != hipSuccess) return set_error("timer: elapsed");
+    *total_ms += ms;
+    *count += 1;
+  }
+  return 0;
+}
+
+#define PTK_GEMM_CASE(ACT_, OUT_)                                                              \
+  if (act == ACT_ && out == OUT_) {                                                            \
+    hipEvent_t e0 = nullptr, e1 = nullptr;                                                     \
+    if (g_timing) { e0 = next_event(act); e1 = next_event(act); }                              \
+    if (e0) (void)hipEventRecord(e0, st);                                                          \
+    hipLaunchKernelGGL((gemm_nt_kernel<ACT_, OUT_>), grid, dim3(256), 0, st, a);              \
+    if (e1) (void)hipEventRecord(e1, st);                                                          \
+    return hipGetLastError() == hipSuccess ? 0 : set_error("gemm launch failed");             \
+  }
+
+int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) {
+  if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
+  if (a.K <= 0 || a.K % BK) return set_error("gemm: K=%d must be a positive multiple of 64", a.K);
+  if ((a.lda % 8) || (a.ldb % 8)) return set_error("gemm: lda/ldb must be multiples of 8 (16-B rows)");
+  if (((uintptr_t)a.A | (uintptr_t)a.B) & 15) return set_error("gemm: A/B must be 16-B aligned");
+  if (a.zin <= 0) return set_error("gemm: zin must be >= 1");
+  const long ntile = (long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  if (ntile > 0x7fffffffL) return set_error("gemm: too many tiles");
+  dim3 grid((unsigned)ntile, 1, (unsigned)batch);
+  PTK_GEMM_CASE(ACT_NONE, OUT_BF16)
+  PTK_GEMM_CASE(ACT_NONE, OUT_F32)
+  PTK_GEMM_CASE(ACT_NONE, OUT_F32_BFR)
+  PTK_GEMM_CASE(ACT_GELU_TANH, OUT_BF16)
+  PTK_GEMM_CASE(ACT_GELU_ERF, OUT_BF16)
+  PTK_GEMM_CASE(ACT_GEGLU, OUT_BF16)
+  PTK_GEMM_CASE(ACT_GELU_ERF_BWD, OUT_BF16)
+  PTK_GEMM_CASE(ACT_GEGLU_BWD, OUT_BF16)
+  return set_error("gemm: unsupported (act=%d, out=%d)", act, out);
+}
+
+}  // namespace ptk

@@ -1,0 +1,368 @@
+// Byte-moving and reduction kernels of the Stage-1 step (all HBM-bound):
+// transpose, im2col, LLM input assembly, fused cross-entropy fwd/bwd,
+// projector-grad gather, column sums, grad-norm + clip + AdamW, synthetic init.
+#include "common.h"
+#include "ptk_internal.h"
+
+namespace ptk {
+
+#define RET_OK(name) return hipGetLastError() == hipSuccess ? 0 : set_error(name " launch failed")
+
+// ---------------------------------------------------------------- transpose
+// in[z] [rows][cols] (ld_in) -> out[z] [cols][rows_pad] (ld_out), 64x64 tiles via LDS.
+__global__ void __launch_bounds__(256) transpose_kernel(const bf16_t* __restrict__ in, long ld_in, long sin0, long sin1,
+                                                        int zin, bf16_t* __restrict__ out, long ld_out, long sout0,
+                                                        long sout1, int rows, int cols, int rows_pad) {
+  __shared__ bf16_t tile[64][66];
+  const int z = blockIdx.z, z0 = z / zin, z1 = z - z0 * zin;
+  const bf16_t* src = in + z0 * sin0 + z1 * sin1;
+  bf16_t* dst = out + z0 * sout0 + z1 * sout1;
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = r0 + ty + 16 * k;
+    const int c = c0 + tx * 4;
+    u16x4_t v = {0, 0, 0, 0};
+    if (r < rows) {
+      if (c + 3 < cols && ((ld_in & 3) == 0)) {
+        v = *reinterpret_cast<const u16x4_t*>(src + (long)r * ld_in + c);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (c + e < cols) ? src[(long)r * ld_in + c + e] : 0;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[ty + 16 * k][tx * 4 + e] = v[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int oc = c0 + ty + 16 * k;      // output row = input col
+    const int orr = r0 + tx * 4;          // output col = input row
+    if (oc >= cols) continue;
+    u16x4_t v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = tile[tx * 4 + e][ty + 16 * k];
+    if (orr + 3 < rows_pad && ((ld_out & 3) == 0)) {
+      *reinterpret_cast<u16x4_t*>(dst + (long)oc * ld_out + orr) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (orr + e < rows_pad) dst[(long)oc * ld_out + orr + e] = v[e];
+    }
+  }
+}
+
+int launch_transpose(const bf16_t* in, long ld_in, long sin0, long sin1, int zin, bf16_t* out, long ld_out,
+                     long sout0, long sout1, int nz, int rows, int cols, int rows_pad, hipStream_t st) {
+  if (rows <= 0 || cols <= 0 || nz <= 0) return 0;
+  if (rows_pad < rows) return set_error("transpose: rows_pad < rows");
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows_pad + 63) / 64), (unsigned)nz);
+  hipLaunchKernelGGL(transpose_kernel, grid, dim3(256), 0, st, in, ld_in, sin0, sin1, zin, out, ld_out, sout0,
+                     sout1, rows, cols, rows_pad);
+  RET_OK("transpose");
+}
+
+// ---------------------------------------------------------------- im2col (Conv2d k=P, stride=P)
+// px [B][C][H][W] bf16 -> out [B*N][C*P*P], column order (c, ky, kx) = conv weight flatten order.
+__global__ void __launch_bounds__(256) im2col_kernel(const bf16_t* __restrict__ px, bf16_t* __restrict__ out, int B,
+                                                     int C, int H, int W, int P) {
+  const int gx = W / P, gy = H / P;
+  const int oct = P / 8;                                      // 8-wide kx groups per kernel row
+  const long total = (long)B * gy * gx * C * P * oct;
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  long t = i;
+  const int o = t % oct; t /= oct;
+  const int ky = t % P; t /= P;
+  const int c = t % C; t /= C;
+  const int px_ = t % gx; t /= gx;
+  const int py = t % gy; t /= gy;
+  const int b = (int)t;
+  const bf16_t* s = px + (((long)b * C + c) * H + (py * P + ky)) * W + px_ * P + o * 8;
+  const long row = ((long)b * gy + py) * gx + px_;
+  bf16_t* d = out + row * (C * P * P) + (long)c * P * P + ky * P + o * 8;
+  *reinterpret_cast<u16x8_t*>(d) = *reinterpret_cast<const u16x8_t*>(s);
+}
+
+int launch_im2col(const bf16_t* px, bf16_t* out, int B, int C, int H, int W, int P, hipStream_t st) {
+  if (P % 8 || H % P || W % P) return set_error("im2col: patch %d must be a multiple of 8 dividing %dx%d", P, H, W);
+  const long total = (long)B * (H / P) * (W / P) * C * P * (P / 8);
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(im2col_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, px, out, B, C, H, W, P);
+  RET_OK("im2col");
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ in, bf16_t* __restrict__ out, long n) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i + 3 < n) {
+    float4 v = *reinterpret_cast<const float4*>(in + i);
+    u16x4_t o;
+    o[0] = f2bf(v.x); o[1] = f2bf(v.y); o[2] = f2bf(v.z); o[3] = f2bf(v.w);
+    *reinterpret_cast<u16x4_t*>(out + i) = o;
+  } else {
+    for (long j = i; j < n; ++j) out[j] = f2bf(in[j]);
+  }
+}
+int launch_cast_f32_bf16(const float* in, bf16_t* out, long n, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3((unsigned)((n / 4 + 256) / 256)), dim3(256), 0, st, in, out, n);
+  RET_OK("cast");
+}
+
+// ---------------------------------------------------------------- LLM input assembly
+// Stage1/projector_trainer.py:183-212: text rows = E[ids] * bf16(sqrt(H)) (bf16 math,
+// TF gemma3 :116-117), padded rows zeroed, key_valid = [1]*Nv ++ (ids != pad) ++ [0]*(Spad-S).
+// Vision rows (s < Nv) are written by the projector GEMM epilogue and left alone.
+__global__ void __launch_bounds__(256) build_llm_inputs_kernel(const bf16_t* __restrict__ E,
+                                                               const int64_t* __restrict__ ids, int T, int Nv,
+                                                               int S, int Spad, int H, float scale, int pad_id,
+                                                               float* __restrict__ x, int32_t* __restrict__ kv) {
+  const long row = blockIdx.x;
+  const int b = (int)(row / Spad), s = (int)(row - (long)b * Spad);
+  if (threadIdx.x == 0) {
+    int valid = 0;
+    if (s < Nv) valid = 1;
+    else if (s < S) valid = ids[(long)b * T + (s - Nv)] != pad_id;
+    kv[row] = valid;
+  }
+  if (s < Nv) return;
+  float* xr = x + row * H;
+  if (s >= S) {
+    for (int c = threadIdx.x * 4; c < H; c += 1024) *reinterpret_cast<float4*>(xr + c) = make_float4(0, 0, 0, 0);
+    return;
+  }
+  const long id = ids[(long)b * T + (s - Nv)];
+  const bf16_t* er = E + id * H;
+  for (int c = threadIdx.x * 4; c < H; c += 1024) {
+    u16x4_t u = *reinterpret_cast<const u16x4_t*>(er + c);
+    *reinterpret_cast<float4*>(xr + c) = make_float4(bfround(bf2f(u[0]) * scale), bfround(bf2f(u[1]) * scale),
+                                                     bfround(bf2f(u[2]) * scale), bfround(bf2f(u[3]) * scale));
+  }
+}
+int launch_build_llm_inputs(const bf16_t* embed, const int64_t* ids, int B, int T, int Nv, int S, int Spad, int H,
+                            float scale_bf16, int pad_id, float* x, int32_t* key_valid, hipStream_t st) {
+  if (H % 4) return set_error("build_llm_inputs: hidden %% 4");
+  hipLaunchKernelGGL(build_llm_inputs_kernel, dim3((unsigned)((long)B * Spad)), dim3(256), 0, st, embed, ids, T, Nv,
+                     S, Spad, H, scale_bf16, pad_id, x, key_valid);
+  RET_OK("build_llm_inputs");
+}
+
+// ---------------------------------------------------------------- cross entropy
+// ForCausalLMLoss (TF/loss/loss_utils.py:49-67): logits (bf16, as the reference's
+// autocast lm_head produces) upcast to fp32, CE mean over valid targets.
+// One block per row: pass 1 online max/sum-exp, pass 2 writes
+// dlogits = (softmax - onehot) * gscale in place (bf16).
+__global__ void __launch_bounds__(256) ce_kernel(bf16_t* __restrict__ logits, long ld, int V,
+                                                 const int64_t* __restrict__ targets, float* __restrict__ row_loss,
+                                                 const float* __restrict__ gscale) {
+  __shared__ float red[8];
+  const long r = blockIdx.x;
+  bf16_t* lr = logits + r * ld;
+  const long tgt = targets[r];
+  float m = -INFINITY, s = 0.f;
+  for (int c = threadIdx.x * 8; c < V; c += 2048) {
+    u16x8_t u = *reinterpret_cast<const u16x8_t*>(lr + c);
+    float v[8], vm = -INFINITY;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) { v[e] = bf2f(u[e]); vm = fmaxf(vm, v[e]); }
+    const float mn = fmaxf(m, vm);
+    float acc = s * __expf(m - mn);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc += __expf(v[e] - mn);
+    m = mn;
+    s = acc;
+  }
+  const float M = block_max<256>(m, red);
+  const float Ssum = block_sum<256>(m == -INFINITY ? 0.f : s * __expf(m - M), red);
+  const float lse = M + __logf(Ssum);
+  const bool valid = tgt >= 0;
+  if (threadIdx.x == 0) row_loss[r] = valid ? lse - bf2f(lr[tgt]) : 0.f;
+  __syncthreads();   // target logit read before it is overwritten
+  const float g = valid ? gscale[0] : 0.f;
+  for (int c = threadIdx.x * 8; c < V; c += 2048) {
+    u16x8_t u = *reinterpret_cast<const u16x8_t*>(lr + c);
+    u16x8_t o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float p = __expf(bf2f(u[e]) - lse);
+      if (c + e == tgt) p -= 1.f;
+      o[e] = f2bf(p * g);
+    }
+    *reinterpret_cast<u16x8_t*>(lr + c) = o;
+  }
+}
+int launch_ce_fwd_bwd(bf16_t* logits, long ld, int R, int V, const int64_t* targets, float* row_loss,
+                      const float* gscale, hipStream_t st) {
+  if (V % 8 || ld % 8) return set_error("ce: vocab %% 8");
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(ce_kernel, dim3(R), dim3(256), 0, st, logits, ld, V, targets, row_loss, gscale);
+  RET_OK("ce");
+}
+
+__global__ void __launch_bounds__(256) count_valid_kernel(const int64_t* __restrict__ labels, int n, float loss_scale,
+                                                          float* gscale, float* count) {
+  __shared__ float red[4];
+  float c = 0.f;
+  for (int i = threadIdx.x; i < n; i += 256) c += labels[i] != -100 ? 1.f : 0.f;
+  c = block_sum<256>(c, red);
+  if (threadIdx.x == 0) {
+    count[0] = c;
+    gscale[0] = c > 0.f ? loss_scale / c : 0.f;
+  }
+}
+int launch_count_valid(const int64_t* labels, int n, float loss_scale, float* gscale, float* count, hipStream_t st) {
+  hipLaunchKernelGGL(count_valid_kernel, dim3(1), dim3(256), 0, st, labels, n, loss_scale, gscale, count);
+  RET_OK("count_valid");
+}
+
+__global__ void __launch_bounds__(256) loss_reduce_kernel(const float* __restrict__ rl, int R, const float* count,
+                                                          float* loss) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < R; i += 256) s += rl[i];
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) loss[0] = count[0] > 0.f ? s / count[0] : NAN;
+}
+int launch_loss_reduce(const float* row_loss, int R, const float* count, float* loss, hipStream_t st) {
+  hipLaunchKernelGGL(loss_reduce_kernel, dim3(1), dim3(256), 0, st, row_loss, R, count, loss);
+  RET_OK("loss_reduce");
+}
+
+// ---------------------------------------------------------------- projector grad plumbing
+// dy[(b,i)] = bf16(dX_llm[b*Spad + i - 1]) for i >= 1, 0 for the dropped patch 0
+// (Stage1/projector_trainer.py:173 slices [:,1:,:] before the projector).
+__global__ void __launch_bounds__(256) gather_dy_kernel(const float* __restrict__ dx, int N, int Spad, int H,
+                                                        bf16_t* __restrict__ dy) {
+  const long row = blockIdx.x;
+  const int b = (int)(row / N), i = (int)(row - (long)b * N);
+  bf16_t* o = dy + row * H;
+  for (int c = threadIdx.x * 4; c < H; c += 1024) {
+    u16x4_t u = {0, 0, 0, 0};
+    if (i > 0) {
+      float4 v = *reinterpret_cast<const float4*>(dx + ((long)b * Spad + i - 1) * H + c);
+      u[0] = f2bf(v.x); u[1] = f2bf(v.y); u[2] = f2bf(v.z); u[3] = f2bf(v.w);
+    }
+    *reinterpret_cast<u16x4_t*>(o + c) = u;
+  }
+}
+int launch_gather_dy(const float* dx, int B, int N, int Spad, int H, bf16_t* dy, hipStream_t st) {
+  if (H % 4) return set_error("gather_dy: hidden %% 4");
+  hipLaunchKernelGGL(gather_dy_kernel, dim3((unsigned)((long)B * N)), dim3(256), 0, st, dx, N, Spad, H, dy);
+  RET_OK("gather_dy");
+}
+
+// column sums of bf16 [rows][cols] -> f32 [cols]; stage 1 over row chunks, stage 2 over chunks
+constexpr int CS_CHUNKS = 64;
+__global__ void __launch_bounds__(256) colsum_partial_kernel(const bf16_t* __restrict__ x, int rows, int cols,
+                                                             float* __restrict__ partial) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  const int per = (rows + CS_CHUNKS - 1) / CS_CHUNKS;
+  const int r0 = blockIdx.y * per, r1 = min(rows, r0 + per);
+  float s = 0.f;
+  for (int r = r0; r < r1; ++r) s += bf2f(x[(long)r * cols + c]);
+  partial[(long)blockIdx.y * cols + c] = s;
+}
+__global__ void __launch_bounds__(256) colsum_final_kernel(const float* __restrict__ partial, int cols,
+                                                           float* __restrict__ out) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int k = 0; k < CS_CHUNKS; ++k) s += partial[(long)k * cols + c];
+  out[c] = s;
+}
+int launch_colsum_bf16(const bf16_t* x, int rows, int cols, float* out, float* partial, hipStream_t st) {
+  hipLaunchKernelGGL(colsum_partial_kernel, dim3((cols + 255) / 256, CS_CHUNKS), dim3(256), 0, st, x, rows, cols,
+                     partial);
+  hipLaunchKernelGGL(colsum_final_kernel, dim3((cols + 255) / 256), dim3(256), 0, st, partial, cols, out);
+  RET_OK("colsum");
+}
+
+// ---------------------------------------------------------------- grad norm + clip + AdamW
+// clip_grad_norm_(5.0) then torch.optim.AdamW (Stage1/projector_trainer.py:75-79, :240-242)
+// over the projector's flat fp32 parameter buffer.  grad_scale folds DDP's 1/W.
+__global__ void __launch_bounds__(256) sumsq_kernel(const float* __restrict__ x, long n, float* __restrict__ partial) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4; i < n; i += (long)gridDim.x * 1024) {
+    if (i + 3 < n) {
+      float4 v = *reinterpret_cast<const float4*>(x + i);
+      s += v.x * v.x + v.y * v.y + v.z * v.z + v.w * v.w;
+    } else {
+      for (long j = i; j < n; ++j) s += x[j] * x[j];
+    }
+  }
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+int launch_sumsq_partial(const float* x, long n, float* partial, int nparts, hipStream_t st) {
+  hipLaunchKernelGGL(sumsq_kernel, dim3(nparts), dim3(256), 0, st, x, n, partial);
+  RET_OK("sumsq");
+}
+
+__global__ void __launch_bounds__(256) clip_adamw_kernel(float* __restrict__ p, const float* __restrict__ g,
+                                                         float* __restrict__ m, float* __restrict__ v, long n,
+                                                         const float* __restrict__ partial, int nparts,
+                                                         float grad_scale, float max_norm, float lr, float b1,
+                                                         float b2, float eps, float wd, float bc1, float bc2s,
+                                                         float* norm_out) {
+  __shared__ float red[4];
+  __shared__ float coef_s;
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nparts; i += 256) s += partial[i];
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) {
+    const float norm = sqrtf(s) * grad_scale;
+    coef_s = fminf(max_norm / (norm + 1e-6f), 1.f) * grad_scale;
+    if (blockIdx.x == 0 && norm_out) norm_out[0] = norm;
+  }
+  __syncthreads();
+  const float coef = coef_s;
+  const float step_size = lr / bc1;
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    const float gi = g[i] * coef;
+    float pi = p[i] * (1.f - lr * wd);
+    const float mi = m[i] + (1.f - b1) * (gi - m[i]);
+    const float vi = v[i] * b2 + (1.f - b2) * gi * gi;
+    pi -= step_size * mi / (sqrtf(vi) / bc2s + eps);
+    p[i] = pi;
+    m[i] = mi;
+    v[i] = vi;
+  }
+}
+int launch_clip_adamw(float* p, const float* g, float* m, float* v, long n, const float* partial, int nparts,
+                      float grad_scale, float max_norm, float lr, float b1, float b2, float eps, float wd, int step,
+                      float* norm_out, hipStream_t st) {
+  const float bc1 = 1.f - powf(b1, (float)step);
+  const float bc2s = sqrtf(1.f - powf(b2, (float)step));
+  hipLaunchKernelGGL(clip_adamw_kernel, dim3(1024), dim3(256), 0, st, p, g, m, v, n, partial, nparts, grad_scale,
+                     max_norm, lr, b1, b2, eps, wd, bc1, bc2s, norm_out);
+  RET_OK("clip_adamw");
+}
+
+// ---------------------------------------------------------------- synthetic init (bench weights)
+PTK_DEV uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+__global__ void fill_normal_kernel(bf16_t* __restrict__ out, long n, uint64_t seed, float std, float mean) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t h = splitmix64(seed ^ splitmix64((uint64_t)i));
+  const float u1 = ((h >> 40) + 1) * (1.0f / 16777217.0f);
+  const float u2 = ((h & 0xFFFFFF) + 0.5f) * (1.0f / 16777216.0f);
+  const float z = sqrtf(-2.f * __logf(u1)) * __cosf(6.283185307f * u2);
+  out[i] = f2bf(mean + std * z);
+}
+int launch_fill_normal_bf16(bf16_t* out, long n, uint64_t seed, float std, float mean, hipStream_t st) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(fill_normal_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, st, out, n, seed, std,
+                     mean);
+  RET_OK("fill_normal");
+}
+
+}  // namespace ptk

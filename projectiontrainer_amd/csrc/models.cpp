@@ -1,0 +1,377 @@
+// Model-level orchestration of the Stage-1 hot path (host side of libptk).
+//
+// ptk_siglip_fwd        SigLIP vision tower forward (modeling_siglip.py:576-619)
+// ptk_gemma3_loss_fwd_bwd  Gemma3 forward + causal-LM loss + dX backward
+//                       (modeling_gemma3.py:511-659, loss_utils.py:49-67)
+//
+// Each call is a fixed sequence of kernel launches on the caller's stream using
+// a caller-provided workspace (sized by the *_workspace_bytes query), so it can
+// be captured into a hipGraph.  Layouts (row-major, token rows b*S + s):
+//   LLM hidden x: f32 [B*Spad, H] (fp32 residual stream, as the reference's
+//   autocast keeps it); GEMM operands bf16.  Attention per (b, kv-head) z:
+//   Q [B,Hkv,S,G,D] (rows (s,j) contiguous), K/V [B,Hkv,S,D], scores/P
+//   [B*Hkv, S*G, S].  QK^T and P.V run on the MFMA GEMM; masks/softmax are
+//   row kernels.
+#include <math.h>
+#include <string.h>
+
+#include <vector>
+
+#include "../../include/ptk.h"
+#include "ptk_internal.h"
+
+using namespace ptk;
+
+namespace {
+
+struct Bump {
+  char* base;
+  size_t off = 0;
+  explicit Bump(void* b) : base((char*)b) {}
+  template <class T>
+  T* take(size_t n) {
+    off = (off + 255) & ~(size_t)255;
+    T* p = base ? reinterpret_cast<T*>(base + off) : nullptr;
+    off += n * sizeof(T);
+    return p;
+  }
+};
+
+float bfround_host(float f) {
+  uint32_t u;
+  memcpy(&u, &f, 4);
+  u += 0x7fffu + ((u >> 16) & 1u);
+  u &= 0xffff0000u;
+  memcpy(&f, &u, 4);
+  return f;
+}
+
+#define CK(x) \
+  do {        \
+    if ((x)) return -1; \
+  } while (0)
+
+GemmArgs gemm(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K) {
+  GemmArgs g;
+  g.A = (const bf16_t*)A; g.B = (const bf16_t*)B; g.C = C;
+  g.lda = lda; g.ldb = ldb; g.ldc = ldc;
+  g.M = M; g.N = N; g.K = K;
+  return g;
+}
+
+// ------------------------------------------------------------------ SigLIP
+struct SiglipWs {
+  bf16_t *patches, *a, *qkv, *vt, *P, *o, *mlp;
+  float *h, *S;
+};
+
+SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
+  const long D = c->hidden, I = c->intermediate, P = c->patch_size, Nn = (c->image_size / P) * (c->image_size / P);
+  const long Np = (Nn + 63) / 64 * 64, M = B * Nn, H = c->heads, hd = D / H, Kp = (long)c->channels * P * P;
+  SiglipWs w;
+  w.patches = bp.take<bf16_t>(M * Kp);
+  w.h = bp.take<float>(M * D);
+  w.a = bp.take<bf16_t>(M * D);
+  w.qkv = bp.take<bf16_t>(M * 3 * D);
+  w.vt = bp.take<bf16_t>((long)B * H * hd * Np);
+  w.S = bp.take<float>((long)B * H * Nn * Np);
+  w.P = bp.take<bf16_t>((long)B * H * Nn * Np);
+  w.o = bp.take<bf16_t>(M * D);
+  w.mlp = bp.take<bf16_t>(M * I);
+  return w;
+}
+
+// ------------------------------------------------------------------ Gemma3
+struct GemmaLayerSave {
+  float *x2, *rstd_in, *rstd_ao, *rstd_pre, *rstd_dn, *rstd_q, *rstd_k;
+  bf16_t *qkv, *Q, *K, *V, *P, *ao, *g, *u, *dn;
+};
+struct GemmaWs {
+  std::vector<float*> x;          // L+1 residual-stream snapshots
+  std::vector<GemmaLayerSave> L;
+  bf16_t *xn, *O, *h, *Vt, *Kt, *Qt, *dqkv, *dgu, *dao, *dO, *dS, *dST, *PT, *dOT, *dQ, *dK, *dV, *xf, *logits;
+  float *S, *dtmp, *rstd_f, *row_loss, *dxf, *count, *gscale;
+  int32_t* key_valid;
+};
+
+GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp) {
+  const long H = c->hidden, I = c->inter, D = c->head_dim, Hq = c->heads, Hkv = c->kv_heads, G = Hq / Hkv;
+  const long M = (long)B * Sp, Dq = Hq * D, Dqkv = (Hq + 2 * Hkv) * D, R = (long)B * T, V = c->vocab;
+  const long Z = (long)B * Hkv, SG = (long)Sp * G;
+  GemmaWs w;
+  w.key_valid = bp.take<int32_t>(M);
+  w.x.push_back(nullptr);   // x[0] is the caller's input buffer
+  for (int l = 1; l <= c->layers; ++l) w.x.push_back(bp.take<float>(M * H));
+  for (int l = 0; l < c->layers; ++l) {
+    GemmaLayerSave s;
+    s.x2 = bp.take<float>(M * H);
+    s.rstd_in = bp.take<float>(M);
+    s.rstd_ao = bp.take<float>(M);
+    s.rstd_pre = bp.take<float>(M);
+    s.rstd_dn = bp.take<float>(M);
+    s.rstd_q = bp.take<float>(M * Hq);
+    s.rstd_k = bp.take<float>(M * Hkv);
+    s.qkv = bp.take<bf16_t>(M * Dqkv);
+    s.Q = bp.take<bf16_t>(Z * SG * D);
+    s.K = bp.take<bf16_t>(Z * Sp * D);
+    s.V = bp.take<bf16_t>(Z * Sp * D);
+    s.P = bp.take<bf16_t>(Z * SG * Sp);
+    s.ao = bp.take<bf16_t>(M * H);
+    s.g = bp.take<bf16_t>(M * I);
+    s.u = bp.take<bf16_t>(M * I);
+    s.dn = bp.take<bf16_t>(M * H);
+    w.L.push_back(s);
+  }
+  w.xn = bp.take<bf16_t>(M * H);
+  w.O = bp.take<bf16_t>(M * Dq);
+  w.h = bp.take<bf16_t>(M * I);
+  w.Vt = bp.take<bf16_t>(Z * D * Sp);
+  w.Kt = bp.take<bf16_t>(Z * D * Sp);
+  w.Qt = bp.take<bf16_t>(Z * D * SG);
+  w.S = bp.take<float>(Z * SG * Sp);
+  w.dqkv = bp.take<bf16_t>(M * Dqkv);
+  w.dgu = bp.take<bf16_t>(M * 2 * I);
+  w.dtmp = bp.take<float>(M * H);
+  w.dao = bp.take<bf16_t>(M * H);
+  w.dO = bp.take<bf16_t>(Z * SG * D);
+  w.dS = bp.take<bf16_t>(Z * SG * Sp);
+  w.dST = bp.take<bf16_t>(Z * Sp * SG);
+  w.PT = bp.take<bf16_t>(Z * Sp * SG);
+  w.dOT = bp.take<bf16_t>(Z * D * SG);
+  w.dQ = bp.take<bf16_t>(Z * SG * D);
+  w.dK = bp.take<bf16_t>(Z * Sp * D);
+  w.dV = bp.take<bf16_t>(Z * Sp * D);
+  w.xf = bp.take<bf16_t>(R * H);
+  w.rstd_f = bp.take<float>(R);
+  w.logits = bp.take<bf16_t>(R * V);
+  w.row_loss = bp.take<float>(R);
+  w.dxf = bp.take<float>(R * H);
+  w.count = bp.take<float>(4);
+  w.gscale = bp.take<float>(4);
+  return w;
+}
+
+}  // namespace
+
+extern "C" {
+
+size_t ptk_siglip_workspace_bytes(const ptk_siglip_config* c, int batch) {
+  Bump bp(nullptr);
+  siglip_layout(bp, c, batch);
+  return bp.off + 256;
+}
+
+int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int B, const void* pixels, void* out,
+                   void* ws, size_t ws_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (ws_bytes < ptk_siglip_workspace_bytes(c, B)) return set_error("siglip_fwd: workspace too small");
+  if (c->hidden % c->heads) return set_error("siglip_fwd: hidden %% heads");
+  const int D = c->hidden, I = c->intermediate, P = c->patch_size, Hh = c->heads, hd = D / Hh;
+  const int Nn = (c->image_size / P) * (c->image_size / P), Np = (Nn + 63) / 64 * 64, M = B * Nn;
+  const int Kp = c->channels * P * P;
+  if (Kp % 64 || hd % 64) return set_error("siglip_fwd: patch dim %d and head dim %d must be multiples of 64", Kp, hd);
+  Bump bp(ws);
+  SiglipWs w = siglip_layout(bp, c, B);
+
+  // K1 patch embed: im2col + GEMM (+bias +pos) -> fp32 residual stream
+  CK(launch_im2col((const bf16_t*)pixels, w.patches, B, c->channels, c->image_size, c->image_size, P, st));
+  {
+    GemmArgs g = gemm(w.patches, Kp, wt->patch_w, Kp, w.h, D, M, D, Kp);
+    g.bias = wt->patch_b;
+    g.rowadd = wt->pos; g.rowadd_period = Nn; g.ld_rowadd = D;
+    CK(launch_gemm(g, ACT_NONE, OUT_F32, 1, st));
+  }
+  for (int l = 0; l < c->layers; ++l) {
+    const ptk_siglip_layer& L = wt->layers[l];
+    CK(launch_layernorm(w.h, L.ln1_w, L.ln1_b, w.a, M, D, c->eps, st));
+    {  // fused q|k|v projection
+      GemmArgs g = gemm(w.a, D, L.wqkv, D, w.qkv, 3 * D, M, 3 * D, D);
+      g.bias = L.bqkv;
+      CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
+    }
+    // V^T per (b, head), zero-padded keys
+    CK(launch_transpose(w.qkv + 2 * D, 3 * D, (long)Nn * 3 * D, hd, Hh, w.vt, Np, (long)Hh * hd * Np, (long)hd * Np,
+                        B * Hh, Nn, hd, Np, st));
+    {  // scores = Q K^T / sqrt(hd)
+      GemmArgs g = gemm(w.qkv, 3 * D, w.qkv + D, 3 * D, w.S, Np, Nn, Nn, hd);
+      g.zin = Hh;
+      g.sA0 = g.sB0 = (long)Nn * 3 * D; g.sA1 = g.sB1 = hd;
+      g.sC0 = (long)Hh * Nn * Np; g.sC1 = (long)Nn * Np;
+      g.alpha = 1.0f / sqrtf((float)hd);
+      CK(launch_gemm(g, ACT_NONE, OUT_F32, B * Hh, st));
+    }
+    MaskSpec mk{Nn, 1, Hh, 0, 0, nullptr, Nn};
+    CK(launch_softmax_fwd(w.S, w.P, B * Hh, Nn, Np, Np, mk, st));
+    {  // O = P V  -> [B*N, D] at head column offset
+      GemmArgs g = gemm(w.P, Np, w.vt, Np, w.o, D, Nn, hd, Np);
+      g.zin = Hh;
+      g.sA0 = (long)Hh * Nn * Np; g.sA1 = (long)Nn * Np;
+      g.sB0 = (long)Hh * hd * Np; g.sB1 = (long)hd * Np;
+      g.sC0 = (long)Nn * D; g.sC1 = hd;
+      CK(launch_gemm(g, ACT_NONE, OUT_BF16, B * Hh, st));
+    }
+    {  // out_proj + bias + residual
+      GemmArgs g = gemm(w.o, D, L.wo, D, w.h, D, M, D, D);
+      g.bias = L.bo; g.resid = w.h; g.ld_resid = D;
+      CK(launch_gemm(g, ACT_NONE, OUT_F32, 1, st));
+    }
+    CK(launch_layernorm(w.h, L.ln2_w, L.ln2_b, w.a, M, D, c->eps, st));
+    {
+      GemmArgs g = gemm(w.a, D, L.w1, D, w.mlp, I, M, I, D);
+      g.bias = L.b1;
+      CK(launch_gemm(g, ACT_GELU_TANH, OUT_BF16, 1, st));
+    }
+    {
+      GemmArgs g = gemm(w.mlp, I, L.w2, I, w.h, D, M, D, I);
+      g.bias = L.b2; g.resid = w.h; g.ld_resid = D;
+      CK(launch_gemm(g, ACT_NONE, OUT_F32, 1, st));
+    }
+  }
+  CK(launch_layernorm(w.h, wt->post_w, wt->post_b, (bf16_t*)out, M, D, c->eps, st));
+  return 0;
+}
+
+size_t ptk_gemma3_workspace_bytes(const ptk_gemma3_config* c, int batch, int text_len, int seq_pad) {
+  Bump bp(nullptr);
+  gemma_layout(bp, c, batch, text_len, seq_pad);
+  return bp.off + 256;
+}
+
+int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,
+                            void* ws, size_t ws_bytes, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const int B = bt->batch, T = bt->text_len, Nv = bt->num_vision, Sp = bt->seq_pad, S = Nv + T;
+  if (Sp % 64 || S > Sp) return set_error("gemma3: seq_pad %d must be a multiple of 64 and >= %d", Sp, S);
+  if (Sp > wt->rope_max_pos) return set_error("gemma3: seq_pad %d exceeds rope table (%d)", Sp, wt->rope_max_pos);
+  if (c->heads % c->kv_heads) return set_error("gemma3: heads %% kv_heads");
+  if (Nv < 1) return set_error("gemma3: num_vision must be >= 1");
+  if (ws_bytes < ptk_gemma3_workspace_bytes(c, B, T, Sp)) return set_error("gemma3: workspace too small");
+  const int H = c->hidden, I = c->inter, D = c->head_dim, Hq = c->heads, Hkv = c->kv_heads, G = Hq / Hkv;
+  const int M = B * Sp, Dq = Hq * D, Dqkv = (Hq + 2 * Hkv) * D, R = B * T, V = c->vocab;
+  const int Z = B * Hkv, SG = Sp * G, nl = c->layers;
+  const float eps = c->eps, scale = 1.0f / sqrtf(c->query_pre_attn_scalar);
+  Bump bp(ws);
+  GemmaWs w = gemma_layout(bp, c, B, T, Sp);
+  AttnShape ash{B, Sp, Hq, Hkv, D};
+
+  // K11/K12: text embeddings (x bf16(sqrt H)), padded rows, key-valid mask; vision rows already in x
+  const float escale = bfround_host(sqrtf((float)H));
+  CK(launch_build_llm_inputs((const bf16_t*)wt->embed, bt->token_ids, B, T, Nv, S, Sp, H, escale, c->pad_token_id,
+                             bt->x, w.key_valid, st));
+  w.x[0] = bt->x;
+  CK(launch_rmsnorm_fwd(w.x[0], H, RowMap{0, 0, 0, 0}, wt->layers[0].ln_in, w.xn, w.L[0].rstd_in, M, H, eps, st));
+
+  // ---------------- forward
+  for (int l = 0; l < nl; ++l) {
+    const ptk_gemma3_layer& L = wt->layers[l];
+    GemmaLayerSave& sv = w.L[l];
+    const bool sliding = (l + 1) % c->sliding_pattern != 0;
+    const float* cs = sliding ? wt->rope_cos_local : wt->rope_cos_global;
+    const float* sn = sliding ? wt->rope_sin_local : wt->rope_sin_global;
+    CK(launch_gemm(gemm(w.xn, H, L.wqkv, H, sv.qkv, Dqkv, M, Dqkv, H), ACT_NONE, OUT_BF16, 1, st));
+    CK(launch_qknorm_rope_fwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, eps, sv.Q, sv.K, sv.V, sv.rstd_q, sv.rstd_k,
+                              st));
+    CK(launch_transpose(sv.V, D, (long)Sp * D, 0, 1, w.Vt, Sp, (long)D * Sp, 0, Z, Sp, D, Sp, st));
+    {  // scores[z] = Q[z] K[z]^T * scale   (z = b*Hkv + kvh)
+      GemmArgs g = gemm(sv.Q, D, sv.K, D, w.S, Sp, SG, Sp, D);
+      g.sA0 = (long)SG * D; g.sB0 = (long)Sp * D; g.sC0 = (long)SG * Sp;
+      g.alpha = scale;
+      CK(launch_gemm(g, ACT_NONE, OUT_F32, Z, st));
+    }
+    MaskSpec mk{SG, G, Hkv, 1, sliding ? c->sliding_window : 0, w.key_valid, Sp};
+    CK(launch_softmax_fwd(w.S, sv.P, Z, SG, Sp, Sp, mk, st));
+    {  // O = P V, scattered to token-major [M, Hq*D]
+      GemmArgs g = gemm(sv.P, Sp, w.Vt, Sp, w.O, D, SG, D, Sp);
+      g.zin = Hkv;
+      g.sA0 = (long)Hkv * SG * Sp; g.sA1 = (long)SG * Sp;
+      g.sB0 = (long)Hkv * D * Sp; g.sB1 = (long)D * Sp;
+      g.sC0 = (long)Sp * Hq * D; g.sC1 = (long)G * D;
+      g.cmap = RowMap{G, 0, Hq, 0};
+      CK(launch_gemm(g, ACT_NONE, OUT_BF16, Z, st));
+    }
+    CK(launch_gemm(gemm(w.O, Dq, L.wo, Dq, sv.ao, H, M, H, Dq), ACT_NONE, OUT_BF16, 1, st));
+    CK(launch_residual_norm_fwd(sv.ao, w.x[l], L.ln_post_attn, L.ln_pre_ff, sv.x2, w.xn, sv.rstd_ao, sv.rstd_pre, M,
+                                H, eps, st));
+    {
+      GemmArgs g = gemm(w.xn, H, L.wgu, H, w.h, I, M, 2 * I, H);
+      g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
+      CK(launch_gemm(g, ACT_GEGLU, OUT_BF16, 1, st));
+    }
+    CK(launch_gemm(gemm(w.h, I, L.wd, I, sv.dn, H, M, H, I), ACT_NONE, OUT_BF16, 1, st));
+    const float* wnext = (l + 1 < nl) ? wt->layers[l + 1].ln_in : nullptr;
+    float* rnext = (l + 1 < nl) ? w.L[l + 1].rstd_in : nullptr;
+    CK(launch_residual_norm_fwd(sv.dn, sv.x2, L.ln_post_ff, wnext, w.x[l + 1], w.xn, sv.rstd_dn, rnext, M, H, eps,
+                                st));
+  }
+
+  // ---------------- loss (text-predicting rows only: position Nv-1+t predicts token t)
+  const RowMap lossmap{T, 0, Sp, Nv - 1};
+  CK(launch_rmsnorm_fwd(w.x[nl], H, lossmap, wt->final_norm, w.xf, w.rstd_f, R, H, eps, st));
+  CK(launch_gemm(gemm(w.xf, H, wt->embed, H, w.logits, V, R, V, H), ACT_NONE, OUT_BF16, 1, st));
+  CK(launch_count_valid(bt->labels, R, bt->loss_scale, w.gscale, w.count, st));
+  CK(launch_ce_fwd_bwd(w.logits, V, R, V, bt->labels, w.row_loss, w.gscale, st));
+  CK(launch_loss_reduce(w.row_loss, R, w.count, bt->loss, st));
+  CK(launch_gemm(gemm(w.logits, V, wt->embed_t, V, w.dxf, H, R, H, V), ACT_NONE, OUT_F32, 1, st));
+  float* dR = bt->dx;
+  CK(hipMemsetAsync(dR, 0, (size_t)M * H * 4, st) != hipSuccess);
+  CK(launch_rmsnorm_bwd_scatter(w.x[nl], lossmap, wt->final_norm, w.rstd_f, w.dxf, dR, R, H, st));
+
+  // ---------------- backward (dX only: weights are frozen)
+  for (int l = nl - 1; l >= 0; --l) {
+    const ptk_gemma3_layer& L = wt->layers[l];
+    GemmaLayerSave& sv = w.L[l];
+    const bool sliding = (l + 1) % c->sliding_pattern != 0;
+    const float* cs = sliding ? wt->rope_cos_local : wt->rope_cos_global;
+    const float* sn = sliding ? wt->rope_sin_local : wt->rope_sin_global;
+    // MLP half
+    CK(launch_post_norm_bwd(dR, sv.dn, L.ln_post_ff, sv.rstd_dn, w.dao, M, H, st));
+    {
+      GemmArgs g = gemm(w.dao, H, L.wd_t, H, w.dgu, 2 * I, M, I, H);
+      g.aux_in = sv.g; g.aux_in2 = sv.u; g.ld_aux_in = I;
+      CK(launch_gemm(g, ACT_GEGLU_BWD, OUT_BF16, 1, st));
+    }
+    CK(launch_gemm(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), ACT_NONE, OUT_F32, 1, st));
+    CK(launch_residual_norm_bwd(sv.x2, L.ln_pre_ff, sv.rstd_pre, w.dtmp, dR, sv.ao, L.ln_post_attn, sv.rstd_ao, w.dao,
+                                M, H, st));
+    {  // dO (Q layout) = dao . Wo, one GEMM per kv head group of output columns
+      GemmArgs g = gemm(w.dao, H, L.wo_t, H, w.dO, (long)G * D, M, G * D, H);
+      g.sB0 = (long)G * D * H; g.sC0 = (long)Sp * G * D;
+      g.cmap = RowMap{Sp, 0, (long)Hkv * Sp, 0};
+      CK(launch_gemm(g, ACT_NONE, OUT_BF16, Hkv, st));
+    }
+    // attention backward
+    CK(launch_transpose(sv.K, D, (long)Sp * D, 0, 1, w.Kt, Sp, (long)D * Sp, 0, Z, Sp, D, Sp, st));
+    CK(launch_transpose(sv.Q, D, (long)SG * D, 0, 1, w.Qt, SG, (long)D * SG, 0, Z, SG, D, SG, st));
+    CK(launch_transpose(w.dO, D, (long)SG * D, 0, 1, w.dOT, SG, (long)D * SG, 0, Z, SG, D, SG, st));
+    CK(launch_transpose(sv.P, Sp, (long)SG * Sp, 0, 1, w.PT, SG, (long)Sp * SG, 0, Z, SG, Sp, SG, st));
+    {  // dP = dO V^T
+      GemmArgs g = gemm(w.dO, D, sv.V, D, w.S, Sp, SG, Sp, D);
+      g.sA0 = (long)SG * D; g.sB0 = (long)Sp * D; g.sC0 = (long)SG * Sp;
+      CK(launch_gemm(g, ACT_NONE, OUT_F32, Z, st));
+    }
+    CK(launch_softmax_bwd(sv.P, w.S, w.dS, Z * SG, Sp, Sp, scale, st));
+    CK(launch_transpose(w.dS, Sp, (long)SG * Sp, 0, 1, w.dST, SG, (long)Sp * SG, 0, Z, SG, Sp, SG, st));
+    {  // dQ = dS K
+      GemmArgs g = gemm(w.dS, Sp, w.Kt, Sp, w.dQ, D, SG, D, Sp);
+      g.sA0 = (long)SG * Sp; g.sB0 = (long)D * Sp; g.sC0 = (long)SG * D;
+      CK(launch_gemm(g, ACT_NONE, OUT_BF16, Z, st));
+    }
+    {  // dK = dS^T Q
+      GemmArgs g = gemm(w.dST, SG, w.Qt, SG, w.dK, D, Sp, D, SG);
+      g.sA0 = (long)Sp * SG; g.sB0 = (long)D * SG; g.sC0 = (long)Sp * D;
+      CK(launch_gemm(g, ACT_NONE, OUT_BF16, Z, st));
+    }
+    {  // dV = P^T dO
+      GemmArgs g = gemm(w.PT, SG, w.dOT, SG, w.dV, D, Sp, D, SG);
+      g.sA0 = (long)Sp * SG; g.sB0 = (long)D * SG; g.sC0 = (long)Sp * D;
+      CK(launch_gemm(g, ACT_NONE, OUT_BF16, Z, st));
+    }
+    CK(launch_qknorm_rope_bwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, sv.rstd_q, sv.rstd_k, w.dQ, w.dK, w.dV, w.dqkv,
+                              st));
+    CK(launch_gemm(gemm(w.dqkv, Dqkv, L.wqkv_t, Dqkv, w.dtmp, H, M, H, Dqkv), ACT_NONE, OUT_F32, 1, st));
+    CK(launch_rmsnorm_bwd_f32(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, dR, M, H, st));
+  }
+  return 0;
+}
+
+}  // extern "C"

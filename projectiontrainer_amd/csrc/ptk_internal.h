@@ -1,0 +1,123 @@
+// Internal (C++) interface between the HIP kernels and the C-ABI layer.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "common.h"
+
+namespace ptk {
+
+int set_error(const char* fmt, ...);   // records the thread-local message, returns -1
+
+enum Act { ACT_NONE = 0, ACT_GELU_TANH = 1, ACT_GELU_ERF = 2, ACT_GEGLU = 3,
+           ACT_GELU_ERF_BWD = 4, ACT_GEGLU_BWD = 5 };
+enum Out { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_BFR = 2 };
+
+struct GemmArgs {
+  const bf16_t* A = nullptr;
+  const bf16_t* B = nullptr;
+  void* C = nullptr;
+  int M = 0, N = 0, K = 0;
+  long lda = 0, ldb = 0, ldc = 0;
+  int zin = 1;                                   // batch z -> (z / zin, z % zin)
+  long sA0 = 0, sA1 = 0, sB0 = 0, sB1 = 0, sC0 = 0, sC1 = 0;   // element strides
+  float alpha = 1.f;
+  const float* bias = nullptr;                   // [N]
+  const float* rowadd = nullptr;                 // rowadd[(r % period) * ld + c]
+  int rowadd_period = 1;
+  long ld_rowadd = 0;
+  const float* resid = nullptr;                  // resid[mapped r * ld + c] (may alias C)
+  long ld_resid = 0;
+  bf16_t* aux = nullptr;                         // activation side outputs [M, *]
+  bf16_t* aux2 = nullptr;
+  long ld_aux = 0;
+  const bf16_t* aux_in = nullptr;                // saved activations for backward epilogues
+  const bf16_t* aux_in2 = nullptr;
+  long ld_aux_in = 0;
+  RowMap amap{0, 0, 0, 0};                       // A row remap (gather)
+  RowMap cmap{0, 0, 0, 0};                       // C row remap (scatter / skip)
+};
+
+int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
+// live GEMM timing per activation class (events recorded around each launch when enabled)
+void timer_enable(int on);
+int timer_read(int cls, double* total_ms, int* count);
+
+// ---- row-wise normalisation (norm.hip) ----
+// SigLIP LayerNorm: y(bf16) = LN(x f32 or bf16) * w + b
+int launch_layernorm(const float* x, const float* w, const float* b, bf16_t* y, int rows, int cols,
+                     float eps, hipStream_t st);
+// RMSNorm (Gemma3, scale 1+w) of x (f32) -> y bf16, rstd f32; optional row gather map
+int launch_rmsnorm_fwd(const float* x, long ldx, RowMap xmap, const float* w, bf16_t* y, float* rstd,
+                       int rows, int cols, float eps, hipStream_t st);
+// Fused sandwich-norm residual step:
+//   y = bf16(rms(t)(1+w_post)); xo = xi + y; n = bf16(rms(xo)(1+w_next))  (w_next may be null)
+int launch_residual_norm_fwd(const bf16_t* t, const float* xi, const float* w_post, const float* w_next,
+                             float* xo, bf16_t* n, float* rstd_t, float* rstd_x, int rows, int cols,
+                             float eps, hipStream_t st);
+// dxi_out = dacc + rms_bwd(x (f32), w, rstd, dn)     (dn f32);  optional row scatter of the result
+int launch_rmsnorm_bwd_f32(const float* x, const float* w, const float* rstd, const float* dn,
+                           const float* dacc, float* dx, int rows, int cols, hipStream_t st);
+// Fused: dR += rms_bwd(x2, w_pre, rstd_pre, dn);  dt = bf16(rms_bwd(t bf16, w_post, rstd_t, bf16(dR)))
+int launch_residual_norm_bwd(const float* x2, const float* w_pre, const float* rstd_pre, const float* dn,
+                             float* dR, const bf16_t* t, const float* w_post, const float* rstd_t,
+                             bf16_t* dt, int rows, int cols, hipStream_t st);
+// dt = bf16(rms_bwd(t bf16, w, rstd_t, bf16(dR)))
+int launch_post_norm_bwd(const float* dR, const bf16_t* t, const float* w, const float* rstd_t, bf16_t* dt,
+                         int rows, int cols, hipStream_t st);
+// final norm backward on gathered rows, scatter-add into dR rows given by map
+int launch_rmsnorm_bwd_scatter(const float* x, RowMap xmap, const float* w, const float* rstd,
+                               const float* dn, float* dR, int rows, int cols, hipStream_t st);
+
+// ---- attention helpers (attn.hip) ----
+struct AttnShape {
+  int B, S, Hq, Hkv, D;     // S = padded sequence length (multiple of 64)
+};
+int launch_qknorm_rope_fwd(const bf16_t* qkv, const float* qw, const float* kw, const float* cos_t,
+                           const float* sin_t, AttnShape s, float eps, bf16_t* Q, bf16_t* K, bf16_t* V,
+                           float* rstd_q, float* rstd_k, hipStream_t st);
+int launch_qknorm_rope_bwd(const bf16_t* qkv, const float* qw, const float* kw, const float* cos_t,
+                           const float* sin_t, AttnShape s, const float* rstd_q, const float* rstd_k,
+                           const bf16_t* dQ, const bf16_t* dK, const bf16_t* dV, bf16_t* dqkv,
+                           hipStream_t st);
+// masked softmax over score rows: P = softmax(S) (bf16), masked entries 0.
+struct MaskSpec {
+  int rows_per_batch;   // score rows per z
+  int qdiv;             // query position = (row % rows_per_batch) / qdiv
+  int zdiv;             // sample index b = z / zdiv
+  int causal;
+  int window;           // 0 = none; else key must satisfy k > q - window
+  const int32_t* key_valid;   // [B, cols] or null
+  int key_len;          // keys >= key_len are masked (when key_valid is null)
+};
+int launch_softmax_fwd(const float* S, bf16_t* P, int nz, int rows, int cols, long ld, MaskSpec m,
+                       hipStream_t st);
+// dS = P * (dP - rowsum(P*dP)) * scale  (bf16 out)
+int launch_softmax_bwd(const bf16_t* P, const float* dP, bf16_t* dS, int nrows, int cols, long ld,
+                       float scale, hipStream_t st);
+
+// ---- misc (misc.hip) ----
+// batched 2-D transpose of bf16 [nz][rows][cols] (ld_in) -> [nz][cols][rows] (ld_out); zero-fills
+// output columns in [rows, rows_pad)
+int launch_transpose(const bf16_t* in, long ld_in, long sin0, long sin1, int zin, bf16_t* out, long ld_out,
+                     long sout0, long sout1, int nz, int rows, int cols, int rows_pad, hipStream_t st);
+int launch_im2col(const bf16_t* px, bf16_t* out, int B, int C, int H, int W, int P, hipStream_t st);
+int launch_cast_f32_bf16(const float* in, bf16_t* out, long n, hipStream_t st);
+int launch_build_llm_inputs(const bf16_t* embed, const int64_t* ids, int B, int T, int Nv, int S, int Spad,
+                            int H, float scale_bf16, int pad_id, float* x, int32_t* key_valid,
+                            hipStream_t st);
+int launch_ce_fwd_bwd(bf16_t* logits, long ld, int R, int V, const int64_t* targets, float* row_loss,
+                      const float* gscale, hipStream_t st);
+int launch_count_valid(const int64_t* labels, int n, float loss_scale, float* gscale, float* count,
+                       hipStream_t st);
+int launch_loss_reduce(const float* row_loss, int R, const float* count, float* loss, hipStream_t st);
+int launch_gather_dy(const float* dx, int B, int N, int Spad, int H, bf16_t* dy, hipStream_t st);
+int launch_colsum_bf16(const bf16_t* x, int rows, int cols, float* out, float* partial, hipStream_t st);
+int launch_sumsq_partial(const float* x, long n, float* partial, int nparts, hipStream_t st);
+int launch_clip_adamw(float* p, const float* g, float* m, float* v, long n, const float* partial,
+                      int nparts, float grad_scale, float max_norm, float lr, float b1, float b2,
+                      float eps, float wd, int step, float* norm_out, hipStream_t st);
+int launch_fill_normal_bf16(bf16_t* out, long n, uint64_t seed, float std, float mean, hipStream_t st);
+
+}  // namespace ptk

@@ -1,0 +1,45 @@
+"""Algorithmic FLOP count of one Stage-1 step per image.
+
+Counts only what the math requires: dense 2·M·N·K on real tokens (no padding),
+causal / sliding-window attention pairs only, the SigLIP MAP head excluded
+(its output is discarded), lm_head on the T text-predicting rows only, and the
+frozen models' backward as dX only.  cfg2 -> 2.637 TFLOP/img.
+"""
+from __future__ import annotations
+
+from .config import Stage1Config
+
+
+def attention_pairs(S: int, window: int | None) -> int:
+    """Number of (q, k) pairs with k <= q (and k > q - window)."""
+    if window is None or window >= S:
+        return S * (S + 1) // 2
+    return window * (window + 1) // 2 + (S - window) * window
+
+
+def flops_per_image(cfg: Stage1Config) -> dict:
+    v, t = cfg.vision, cfg.text
+    N, D, I = v.num_patches, v.hidden_size, v.intermediate_size
+    vit = 2 * N * v.patch_dim * D
+    vit += v.num_hidden_layers * (2 * N * D * 3 * D + 2 * 2 * N * N * D + 2 * N * D * D + 2 * 2 * N * D * I)
+    Nv, Ip = cfg.num_vision_tokens, D * cfg.expansion_factor
+    proj_f = 2 * Nv * (D * Ip + Ip * t.hidden_size)
+    proj_b = 2 * Nv * (t.hidden_size * Ip) * 2 + 2 * Nv * Ip * D      # dW2, dH, dW1 (no dX)
+    S, H = cfg.seq_len, t.hidden_size
+    dense = 2 * S * H * (t.q_dim + 2 * t.kv_dim) + 2 * S * t.q_dim * H + 2 * S * H * 2 * t.intermediate_size \
+        + 2 * S * t.intermediate_size * H
+    attn = 0
+    for i in range(t.num_hidden_layers):
+        pairs = attention_pairs(S, t.sliding_window if t.is_sliding(i) else None)
+        attn += 2 * 2 * pairs * t.head_dim * t.num_attention_heads
+    head = 2 * cfg.text_len * H * t.vocab_size
+    g_f = t.num_hidden_layers * dense + attn + head
+    g_b = t.num_hidden_layers * dense + 2 * attn + head
+    total = vit + proj_f + proj_b + g_f + g_b
+    return dict(vit_fwd=vit, proj_fwd=proj_f, proj_bwd=proj_b, llm_fwd=g_f, llm_bwd=g_b, total=total)
+
+
+def geglu_gemm_flops(cfg: Stage1Config) -> float:
+    """One Gemma3 gate|up projection launch (the step's largest kernel): 2·(B·S)·(2I)·H."""
+    t = cfg.text
+    return 2.0 * cfg.batch_size * cfg.seq_len * 2 * t.intermediate_size * t.hidden_size

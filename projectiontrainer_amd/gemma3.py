@@ -1,0 +1,168 @@
+"""Frozen Gemma3 causal LM on libptk (`ptk_gemma3_loss_fwd_bwd`).
+
+Replaces `language_model(inputs_embeds=, attention_mask=, labels=).loss`
+followed by `accelerator.backward(...)` down to d(inputs_embeds)
+(Stage1/projector_trainer.py:183-237 -> TF/models/gemma3/modeling_gemma3.py
+:511-659, TF/loss/loss_utils.py:49-67).  The frozen weights get no grads, so
+only the dX chain is computed.
+
+Kernel layouts built once from HF-named weights: q|k|v fused rows, gate/up
+interleaved in 16-row blocks (the GEGLU GEMM epilogue pairs them in
+registers), and a pre-transposed copy of every matrix for the dX GEMMs.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+import torch
+
+from . import _lib as L
+from . import kernels as K
+from .config import Gemma3TextConfig
+
+
+def _dev(a, dtype, device):
+    t = torch.from_numpy(a) if isinstance(a, np.ndarray) else a
+    return t.to(device=device, dtype=dtype).contiguous()
+
+
+def interleave_gate_up(gate, up):
+    """[I,H],[I,H] -> [2I,H]: rows 32q..32q+15 = gate[16q..16q+15], 32q+16.. = up[16q..]."""
+    I, H = gate.shape
+    return torch.stack([gate.view(I // 16, 16, H), up.view(I // 16, 16, H)], dim=1).reshape(2 * I, H).contiguous()
+
+
+def rope_tables(cfg: Gemma3TextConfig, max_pos: int, sliding: bool):
+    """Gemma3RotaryEmbedding math (modeling_gemma3.py:156-205) in fp32 on the host:
+    returns cos, sin [max_pos, head_dim/2] (emb = [f, f] so the second half repeats)."""
+    d = cfg.head_dim
+    theta = cfg.rope_local_base_freq if sliding else cfg.rope_theta
+    inv = 1.0 / (theta ** (torch.arange(0, d, 2, dtype=torch.int64).float() / d))
+    if not sliding and cfg.rope_linear_factor != 1.0:
+        inv = inv / cfg.rope_linear_factor
+    f = torch.arange(max_pos, dtype=torch.float32)[:, None] * inv[None, :]
+    return f.cos().contiguous(), f.sin().contiguous()
+
+
+class Gemma3CausalLM:
+    def __init__(self, cfg: Gemma3TextConfig, params: dict | None, device="cuda", max_pos: int = 2048):
+        self.cfg, self.device, self.max_pos = cfg, torch.device(device), max_pos
+        self._ws = None
+        if params is not None:
+            self._load(params)
+            self._build_c()
+
+    # ------------------------------------------------------------------ weights
+    def _load(self, params):
+        cfg, dev = self.cfg, self.device
+        bf, f32 = torch.bfloat16, torch.float32
+        g = lambda n, dt: _dev(params[n], dt, dev)
+        self.embed = g("model.embed_tokens.weight", bf)
+        self.final_norm = g("model.norm.weight", f32)
+        self.layers = []
+        for i in range(cfg.num_hidden_layers):
+            p = f"model.layers.{i}."
+            wqkv = torch.cat([g(p + f"self_attn.{n}_proj.weight", bf) for n in "qkv"]).contiguous()
+            wgu = interleave_gate_up(g(p + "mlp.gate_proj.weight", bf), g(p + "mlp.up_proj.weight", bf))
+            lay = dict(wqkv=wqkv, wo=g(p + "self_attn.o_proj.weight", bf), wgu=wgu,
+                       wd=g(p + "mlp.down_proj.weight", bf),
+                       ln_in=g(p + "input_layernorm.weight", f32),
+                       ln_post_attn=g(p + "post_attention_layernorm.weight", f32),
+                       ln_pre_ff=g(p + "pre_feedforward_layernorm.weight", f32),
+                       ln_post_ff=g(p + "post_feedforward_layernorm.weight", f32),
+                       q_norm=g(p + "self_attn.q_norm.weight", f32), k_norm=g(p + "self_attn.k_norm.weight", f32))
+            self.layers.append(lay)
+        self._derive()
+
+    def _derive(self):
+        for lay in self.layers:
+            for k in ("wqkv", "wo", "wgu", "wd"):
+                lay[k + "_t"] = K.transpose(lay[k])
+        self.embed_t = K.transpose(self.embed)
+        tabs = [rope_tables(self.cfg, self.max_pos, s) for s in (True, False)]
+        (self.cos_l, self.sin_l), (self.cos_g, self.sin_g) = [(c.to(self.device), s.to(self.device))
+                                                              for c, s in tabs]
+
+    @classmethod
+    def from_hf(cls, model, device="cuda", max_pos=2048):
+        c = model.config
+        lt = list(c.layer_types)
+        pattern = lt.index("full_attention") + 1 if "full_attention" in lt else len(lt) + 1
+        rp = c.rope_parameters
+        cfg = Gemma3TextConfig(vocab_size=c.vocab_size, hidden_size=c.hidden_size,
+                               intermediate_size=c.intermediate_size, num_hidden_layers=c.num_hidden_layers,
+                               num_attention_heads=c.num_attention_heads, num_key_value_heads=c.num_key_value_heads,
+                               head_dim=c.head_dim, sliding_window=c.sliding_window, sliding_window_pattern=pattern,
+                               rope_theta=rp["full_attention"]["rope_theta"],
+                               rope_local_base_freq=rp["sliding_attention"]["rope_theta"],
+                               rope_linear_factor=float(rp["full_attention"].get("factor", 1.0)),
+                               query_pre_attn_scalar=c.query_pre_attn_scalar, rms_norm_eps=c.rms_norm_eps,
+                               pad_token_id=c.pad_token_id if c.pad_token_id is not None else 0)
+        sd = {k: v.detach().float() for k, v in model.state_dict().items()}
+        return cls(cfg, sd, device, max_pos)
+
+    @classmethod
+    def random_init(cls, cfg: Gemma3TextConfig, device="cuda", seed=1, max_pos=2048):
+        """Synthetic bf16 weights generated on the device (N(0, 0.02^2); norm weights 0)."""
+        self = cls(cfg, None, device, max_pos)
+        dev = self.device
+        H, I = cfg.hidden_size, cfg.intermediate_size
+        s = [seed * 100000]
+
+        def nb(*shape, std=0.02):
+            s[0] += 1
+            return K.fill_normal_(torch.empty(shape, dtype=torch.bfloat16, device=dev), s[0], std)
+        z = lambda n: torch.zeros(n, dtype=torch.float32, device=dev)
+        self.embed = nb(cfg.vocab_size, H)
+        self.final_norm = z(H)
+        self.layers = [dict(wqkv=nb(cfg.q_dim + 2 * cfg.kv_dim, H), wo=nb(H, cfg.q_dim), wgu=nb(2 * I, H),
+                            wd=nb(H, I), ln_in=z(H), ln_post_attn=z(H), ln_pre_ff=z(H), ln_post_ff=z(H),
+                            q_norm=z(cfg.head_dim), k_norm=z(cfg.head_dim))
+                       for _ in range(cfg.num_hidden_layers)]
+        self._derive()
+        self._build_c()
+        return self
+
+    def _build_c(self):
+        c = self.cfg
+        self.c_cfg = L.Gemma3ConfigC(c.vocab_size, c.hidden_size, c.intermediate_size, c.num_hidden_layers,
+                                     c.num_attention_heads, c.num_key_value_heads, c.head_dim, c.sliding_window,
+                                     c.sliding_window_pattern, c.pad_token_id, float(c.query_pre_attn_scalar),
+                                     c.rms_norm_eps)
+        keys = ("wqkv", "wqkv_t", "wo", "wo_t", "wgu", "wgu_t", "wd", "wd_t", "ln_in", "ln_post_attn", "ln_pre_ff",
+                "ln_post_ff", "q_norm", "k_norm")
+        arr = (L.Gemma3LayerC * len(self.layers))()
+        for i, lay in enumerate(self.layers):
+            arr[i] = L.Gemma3LayerC(*[lay[k].data_ptr() for k in keys])
+        self._c_layers = arr
+        self.c_w = L.Gemma3WeightsC(self.embed.data_ptr(), self.embed_t.data_ptr(), self.final_norm.data_ptr(),
+                                    self.cos_l.data_ptr(), self.sin_l.data_ptr(), self.cos_g.data_ptr(),
+                                    self.sin_g.data_ptr(), self.max_pos, C.cast(arr, C.POINTER(L.Gemma3LayerC)))
+
+    # ------------------------------------------------------------------ compute
+    @staticmethod
+    def seq_pad(seq_len: int) -> int:
+        return (seq_len + 63) // 64 * 64
+
+    def workspace(self, batch, text_len, seq_pad):
+        n = L.lib().ptk_gemma3_workspace_bytes(self.c_cfg, batch, text_len, seq_pad)
+        if self._ws is None or self._ws.numel() < n:
+            self._ws = None
+            self._ws = torch.empty(n, dtype=torch.uint8, device=self.device)
+        return self._ws
+
+    def loss_and_input_grad(self, x, dx, token_ids, labels, num_vision, loss_scale, loss):
+        """x: f32 [B*Spad, H] LLM input rows (vision rows filled by the caller),
+        token_ids/labels int64 [B, T].  Writes loss [1] (mean CE) and dx (grad of
+        loss*loss_scale w.r.t. x)."""
+        B, T = token_ids.shape
+        Sp = x.shape[0] // B
+        ws = self.workspace(B, T, Sp)
+        bt = L.Gemma3BatchC(B, T, num_vision, Sp, token_ids.data_ptr(), labels.data_ptr(), x.data_ptr(),
+                            dx.data_ptr(), loss_scale, loss.data_ptr())
+        L.check(L.lib().ptk_gemma3_loss_fwd_bwd(self.c_cfg, self.c_w, bt, ws.data_ptr(), ws.numel(),
+                                                L.stream_ptr(self.device)), "ptk_gemma3_loss_fwd_bwd")
+
+    def get_input_embeddings(self):
+        return self.embed

@@ -1,0 +1,128 @@
+"""Tensor-level wrappers over libptk primitive ops (device tensors in, device
+tensors out, launched on torch's current HIP stream).  Used by the model
+classes and by the kernel parity tests."""
+from __future__ import annotations
+
+import torch
+
+from . import _lib as L
+from ._lib import check, ptr
+
+
+def _require_cuda(*ts):
+    for t in ts:
+        if t is not None and not t.is_cuda:
+            raise L.PtkError("libptk ops need HIP device tensors (no CPU fallback)")
+
+
+def _bits(t):
+    """bf16 tensors are passed as raw 16-bit storage."""
+    return ptr(t)
+
+
+def gemm(A, B, *, C=None, out_dtype=torch.bfloat16, act=L.ACT_NONE, alpha=1.0, bias=None, rowadd=None,
+         resid=None, aux=None, aux2=None, aux_in=None, aux_in2=None, M=None, N=None, K=None,
+         lda=None, ldb=None, ldc=None, batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0),
+         amap=(0, 0, 0, 0), cmap=(0, 0, 0, 0), out_mode=None):
+    """C = epi(alpha * A . B^T) with A [M,K], B [N,K] bf16 (K-contiguous)."""
+    _require_cuda(A, B)
+    M = A.shape[-2] if M is None else M
+    K = A.shape[-1] if K is None else K
+    N = B.shape[-2] if N is None else N
+    n_out = N // 2 if act == L.ACT_GEGLU else (2 * N if act == L.ACT_GEGLU_BWD else N)
+    if C is None:
+        C = torch.empty((M, n_out), dtype=out_dtype, device=A.device)
+    if out_mode is None:
+        out_mode = L.OUT_BF16 if C.dtype == torch.bfloat16 else L.OUT_F32
+    d = L.GemmDesc()
+    d.A, d.B, d.C = ptr(A), ptr(B), ptr(C)
+    d.M, d.N, d.K = M, N, K
+    d.lda = A.stride(-2) if lda is None else lda
+    d.ldb = B.stride(-2) if ldb is None else ldb
+    d.ldc = C.stride(-2) if ldc is None else ldc
+    d.batch, d.batch_inner = batch, batch_inner
+    d.sA0, d.sA1, d.sB0, d.sB1, d.sC0, d.sC1 = strides
+    d.alpha, d.act, d.out = alpha, act, out_mode
+    d.bias = ptr(bias)
+    if rowadd is not None:
+        d.rowadd, d.rowadd_period, d.ld_rowadd = ptr(rowadd), rowadd.shape[0], rowadd.stride(0)
+    if resid is not None:
+        d.resid, d.ld_resid = ptr(resid), resid.stride(-2)
+    if aux is not None:
+        d.aux, d.ld_aux = ptr(aux), aux.stride(-2)
+    d.aux2 = ptr(aux2)
+    if aux_in is not None:
+        d.aux_in, d.ld_aux_in = ptr(aux_in), aux_in.stride(-2)
+    d.aux_in2 = ptr(aux_in2)
+    d.amap = L.RowMap(*amap)
+    d.cmap = L.RowMap(*cmap)
+    check(L.lib().ptk_gemm(d, L.stream_ptr(A.device)), "ptk_gemm")
+    return C
+
+
+def layernorm(x, w, b, eps):
+    _require_cuda(x)
+    y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    rows, cols = x.numel() // x.shape[-1], x.shape[-1]
+    check(L.lib().ptk_layernorm(ptr(x), ptr(w), ptr(b), ptr(y), rows, cols, eps, L.stream_ptr(x.device)), "layernorm")
+    return y
+
+
+def rmsnorm(x, w, eps):
+    _require_cuda(x)
+    rows, cols = x.numel() // x.shape[-1], x.shape[-1]
+    y = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device)
+    rstd = torch.empty(rows, dtype=torch.float32, device=x.device)
+    check(L.lib().ptk_rmsnorm(ptr(x), ptr(w), ptr(y), ptr(rstd), rows, cols, eps, L.stream_ptr(x.device)), "rmsnorm")
+    return y, rstd
+
+
+def rmsnorm_bwd(x, w, rstd, dn, dacc=None):
+    rows, cols = x.numel() // x.shape[-1], x.shape[-1]
+    dx = torch.empty_like(x)
+    check(L.lib().ptk_rmsnorm_bwd(ptr(x), ptr(w), ptr(rstd), ptr(dn), ptr(dacc), ptr(dx), rows, cols,
+                                  L.stream_ptr(x.device)), "rmsnorm_bwd")
+    return dx
+
+
+def softmax(S, *, nz, rows, cols, rows_per_batch=0, qdiv=1, zdiv=1, causal=False, window=0, key_valid=None,
+            key_len=None):
+    P = torch.empty(S.shape, dtype=torch.bfloat16, device=S.device)
+    check(L.lib().ptk_softmax(ptr(S), ptr(P), nz, rows, cols, S.stride(-2), rows_per_batch, qdiv, zdiv, int(causal),
+                              window, ptr(key_valid), cols if key_len is None else key_len,
+                              L.stream_ptr(S.device)), "softmax")
+    return P
+
+
+def cross_entropy_(logits, targets, gscale):
+    """In-place fused CE fwd/bwd on bf16 logits [R, V]; returns per-row loss."""
+    R, V = logits.shape
+    row_loss = torch.empty(R, dtype=torch.float32, device=logits.device)
+    check(L.lib().ptk_cross_entropy(ptr(logits), logits.stride(0), R, V, ptr(targets), ptr(row_loss), ptr(gscale),
+                                    L.stream_ptr(logits.device)), "cross_entropy")
+    return row_loss
+
+
+def transpose(x, rows_pad=None):
+    """[Z, rows, cols] or [rows, cols] bf16 -> [.., cols, rows_pad] (zero-padded)."""
+    squeeze = x.dim() == 2
+    x3 = x.unsqueeze(0) if squeeze else x
+    Z, rows, cols = x3.shape
+    rp = rows if rows_pad is None else rows_pad
+    out = torch.empty((Z, cols, rp), dtype=x.dtype, device=x.device)
+    check(L.lib().ptk_transpose_bf16(ptr(x3), x3.stride(1), ptr(out), rp, Z, x3.stride(0), cols * rp, rows, cols, rp,
+                                     L.stream_ptr(x.device)), "transpose")
+    return out[0] if squeeze else out
+
+
+def cast_bf16(x, out=None):
+    out = torch.empty(x.shape, dtype=torch.bfloat16, device=x.device) if out is None else out
+    check(L.lib().ptk_cast_f32_bf16(ptr(x), ptr(out), x.numel(), L.stream_ptr(x.device)), "cast")
+    return out
+
+
+def fill_normal_(t, seed, std=0.02, mean=0.0):
+    assert t.dtype == torch.bfloat16 and t.is_contiguous()
+    check(L.lib().ptk_fill_normal_bf16(ptr(t), t.numel(), seed & (2**64 - 1), std, mean, L.stream_ptr(t.device)),
+          "fill_normal")
+    return t

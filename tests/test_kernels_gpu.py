@@ -1,0 +1,193 @@
+"""Per-kernel parity: libptk HIP kernels vs a plain PyTorch fp32 reference of
+the same op (on the same bf16-valued inputs).  Tolerances are stated per test:
+bf16 outputs are compared at ~1 bf16 ulp relative scale (rtol 1e-2), fp32
+outputs of bf16-input GEMMs at rtol 2e-3 (fp32 accumulate, order differs)."""
+import math
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+
+def _k():
+    from projectiontrainer_amd import kernels as K, _lib as L
+    return K, L
+
+
+def rnd(*shape, dev, dtype=torch.bfloat16, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(dev).to(dtype)
+
+
+def close(got, ref, rtol, atol_scale=1e-2):
+    got, ref = got.float(), ref.float()
+    atol = atol_scale * ref.abs().max().item() * rtol / 1e-2 if ref.numel() else 0
+    torch.testing.assert_close(got, ref, rtol=rtol, atol=max(atol, 1e-6))
+
+
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 1024), (200, 130, 192), (1000, 1152, 1152),
+                                   (77, 64, 64)])
+def test_gemm_plain_f32_and_bf16(gpu, M, N, K):
+    Kn, L = _k()
+    A, B = rnd(M, K, dev=gpu, seed=1), rnd(N, K, dev=gpu, seed=2)
+    ref = A.float() @ B.float().T
+    C = Kn.gemm(A, B, out_dtype=torch.float32)
+    torch.testing.assert_close(C, ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
+    Cb = Kn.gemm(A, B, out_dtype=torch.bfloat16)
+    torch.testing.assert_close(Cb.float(), ref, rtol=1e-2, atol=1e-2 * math.sqrt(K))
+
+
+def test_gemm_asymmetric_identity(gpu):
+    """A = I with an asymmetric B catches a transposed C write."""
+    Kn, L = _k()
+    n = 128
+    A = torch.eye(n, device=gpu, dtype=torch.bfloat16)
+    B = (torch.arange(n * n, device=gpu, dtype=torch.float32).view(n, n) % 97).to(torch.bfloat16)
+    C = Kn.gemm(A, B, out_dtype=torch.float32)
+    torch.testing.assert_close(C, B.float().T)
+
+
+def test_gemm_epilogues(gpu):
+    Kn, L = _k()
+    M, N, K = 300, 256, 128
+    A, B = rnd(M, K, dev=gpu, seed=3), rnd(N, K, dev=gpu, seed=4, scale=0.1)
+    bias = rnd(N, dev=gpu, dtype=torch.float32, seed=5)
+    pos = rnd(7, N, dev=gpu, dtype=torch.float32, seed=6)
+    res = rnd(M, N, dev=gpu, dtype=torch.float32, seed=7)
+    base = A.float() @ B.float().T + bias
+    # bias + periodic row add + residual (SigLIP patch embed / out_proj)
+    C = res.clone()
+    Kn.gemm(A, B, C=C, bias=bias, rowadd=pos, resid=C, alpha=1.0)
+    ref = base + pos[torch.arange(M, device=gpu) % 7] + res
+    torch.testing.assert_close(C, ref, rtol=2e-3, atol=2e-2)
+    # gelu tanh
+    C = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_TANH)
+    torch.testing.assert_close(C.float(), F.gelu(base, approximate="tanh"), rtol=2e-2, atol=2e-2)
+    # gelu erf with pre-activation aux
+    aux = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+    C = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_ERF, aux=aux)
+    torch.testing.assert_close(aux.float(), base, rtol=1e-2, atol=2e-2)
+    torch.testing.assert_close(C.float(), F.gelu(aux.float()), rtol=1e-2, atol=1e-2)
+    # gelu erf backward: C = (A B^T) * gelu'(aux)
+    C = Kn.gemm(A, B, act=L.ACT_GELU_ERF_BWD, aux_in=aux)
+    x = aux.float().requires_grad_(True)
+    F.gelu(x).backward((A.float() @ B.float().T).to(torch.bfloat16).float())
+    torch.testing.assert_close(C.float(), x.grad, rtol=2e-2, atol=2e-2)
+    # alpha + row remap (scatter into padded layout, skipping the first row of each group)
+    out = torch.zeros(4 * 80, N, device=gpu)
+    Kn.gemm(A[:240], B, C=out, M=240, alpha=0.5, out_mode=L.OUT_F32, cmap=(60, 1, 80, -1))
+    ref = 0.5 * (A[:240].float() @ B.float().T)
+    for g in range(4):
+        torch.testing.assert_close(out[g * 80: g * 80 + 59], ref[g * 60 + 1: g * 60 + 60], rtol=2e-3, atol=2e-3)
+        assert out[g * 80 + 59:(g + 1) * 80].abs().sum() == 0
+
+
+def test_gemm_geglu_and_bwd(gpu):
+    Kn, L = _k()
+    from projectiontrainer_amd.gemma3 import interleave_gate_up
+    M, H, I = 200, 128, 256
+    x = rnd(M, H, dev=gpu, seed=8)
+    Wg, Wu = rnd(I, H, dev=gpu, seed=9, scale=0.1), rnd(I, H, dev=gpu, seed=10, scale=0.1)
+    Wgu = interleave_gate_up(Wg, Wu)
+    g = torch.empty(M, I, dtype=torch.bfloat16, device=gpu)
+    u = torch.empty_like(g)
+    h = Kn.gemm(x, Wgu, act=L.ACT_GEGLU, aux=g, aux2=u)
+    gr, ur = (x.float() @ Wg.float().T), (x.float() @ Wu.float().T)
+    torch.testing.assert_close(g.float(), gr, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(u.float(), ur, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(h.float(), F.gelu(g.float(), approximate="tanh") * u.float(), rtol=2e-2, atol=2e-2)
+    # backward: dh . Wd^T... here dh = y . Wd_t^T with Wd_t [I, H]
+    y = rnd(M, H, dev=gpu, seed=11)
+    Wd = rnd(H, I, dev=gpu, seed=12, scale=0.1)
+    Wd_t = Wd.T.contiguous()
+    dgu = Kn.gemm(y, Wd_t, act=L.ACT_GEGLU_BWD, aux_in=g, aux_in2=u)
+    dh = (y.float() @ Wd.float()).to(torch.bfloat16).float()
+    gg, uu = g.float().requires_grad_(True), u.float().requires_grad_(True)
+    (F.gelu(gg, approximate="tanh") * uu).backward(dh)
+    dg = dgu.view(M, I // 16, 2, 16)[:, :, 0].reshape(M, I)
+    du = dgu.view(M, I // 16, 2, 16)[:, :, 1].reshape(M, I)
+    torch.testing.assert_close(dg.float(), gg.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(du.float(), uu.grad, rtol=3e-2, atol=3e-2)
+
+
+def test_gemm_batched_strided(gpu):
+    Kn, L = _k()
+    Bz, H, S, D = 3, 2, 96, 64
+    q = rnd(Bz, S, H * D, dev=gpu, seed=13)
+    k = rnd(Bz, S, H * D, dev=gpu, seed=14)
+    Np = 128
+    C = torch.full((Bz, H, S, Np), float("nan"), device=gpu)
+    Kn.gemm(q, k, C=C, M=S, N=S, K=D, lda=H * D, ldb=H * D, ldc=Np, batch=Bz * H, batch_inner=H,
+            strides=(S * H * D, D, S * H * D, D, H * S * Np, S * Np), alpha=0.125, out_mode=L.OUT_F32)
+    qh = q.float().view(Bz, S, H, D).transpose(1, 2)
+    kh = k.float().view(Bz, S, H, D).transpose(1, 2)
+    ref = (qh @ kh.transpose(-1, -2)) * 0.125
+    torch.testing.assert_close(C[..., :S], ref, rtol=2e-3, atol=2e-3)
+
+
+def test_layernorm_rmsnorm(gpu):
+    Kn, L = _k()
+    for cols in (128, 1152, 1024):
+        x = rnd(37, cols, dev=gpu, dtype=torch.float32, seed=15) * 3 + 1
+        w = rnd(cols, dev=gpu, dtype=torch.float32, seed=16)
+        b = rnd(cols, dev=gpu, dtype=torch.float32, seed=17)
+        y = Kn.layernorm(x, w, b, 1e-6)
+        torch.testing.assert_close(y.float(), F.layer_norm(x, (cols,), w, b, 1e-6), rtol=1e-2, atol=1e-2)
+        y, rstd = Kn.rmsnorm(x, w, 1e-6)
+        xr = x.clone().requires_grad_(True)
+        ref = xr * torch.rsqrt(xr.pow(2).mean(-1, keepdim=True) + 1e-6) * (1 + w)
+        torch.testing.assert_close(y.float(), ref.detach(), rtol=1e-2, atol=1e-2)
+        dn = rnd(37, cols, dev=gpu, dtype=torch.float32, seed=18)
+        dacc = rnd(37, cols, dev=gpu, dtype=torch.float32, seed=19)
+        dx = Kn.rmsnorm_bwd(x, w, rstd, dn, dacc)
+        ref.backward(dn)
+        torch.testing.assert_close(dx, xr.grad + dacc, rtol=1e-4, atol=1e-5)
+
+
+def test_softmax_masks(gpu):
+    Kn, L = _k()
+    B, Hkv, G, S = 2, 1, 4, 128
+    SG = S * G
+    Sc = rnd(B * Hkv, SG, S, dev=gpu, dtype=torch.float32, seed=20) * 4
+    kv = torch.ones(B, S, dtype=torch.int32, device=gpu)
+    kv[0, 70:75] = 0
+    kv[1, 100:] = 0
+    for window in (0, 16):
+        P = Kn.softmax(Sc, nz=B * Hkv, rows=SG, cols=S, rows_per_batch=SG, qdiv=G, zdiv=Hkv, causal=True,
+                       window=window, key_valid=kv)
+        q = torch.arange(SG, device=gpu)[:, None] // G
+        kk = torch.arange(S, device=gpu)[None, :]
+        m = (kk <= q)
+        if window:
+            m = m & (kk > q - window)
+        m = m[None] & kv.bool()[:, None, :]
+        ref = torch.softmax(Sc.masked_fill(~m, float("-inf")), -1)
+        ref = torch.nan_to_num(ref, nan=0.0)     # fully masked rows -> all-zero P (kernel convention)
+        torch.testing.assert_close(P.float(), ref, rtol=1e-2, atol=4e-3)
+
+
+def test_transpose(gpu):
+    Kn, L = _k()
+    x = rnd(3, 100, 70, dev=gpu, seed=21)
+    t = Kn.transpose(x, rows_pad=128)
+    torch.testing.assert_close(t[..., :100], x.transpose(1, 2))
+    assert t[..., 100:].abs().sum() == 0
+
+
+def test_cross_entropy(gpu):
+    Kn, L = _k()
+    R, V = 33, 4096
+    logits = rnd(R, V, dev=gpu, seed=22, scale=3)
+    tgt = torch.randint(0, V, (R,), device=gpu)
+    tgt[5] = -100
+    cnt = (tgt != -100).sum().float()
+    gscale = (0.25 / cnt).reshape(1).float()
+    x = logits.float().requires_grad_(True)
+    loss = F.cross_entropy(x, tgt, ignore_index=-100) * 0.25
+    loss.backward()
+    lg = logits.clone()
+    rl = Kn.cross_entropy_(lg, tgt, gscale)
+    torch.testing.assert_close(rl.sum() / cnt * 0.25, loss.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(lg.float(), x.grad, rtol=1e-2, atol=1e-6)

@@ -1,0 +1,29 @@
+#!/bin/bash
+# GPU-box check runner: each step has its own time limit; stops at the first
+# step that ends in anything but success (0) or a plain test failure (1).
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+mkdir -p gpurun_out
+export PYTHONUNBUFFERED=1
+run() {
+  local name=$1 to=$2
+  shift 2
+  echo "== $name: $*"
+  timeout -k 10 "$to" "$@" > "gpurun_out/$name.log" 2>&1
+  local rc=$?
+  echo "== $name rc=$rc"
+  tail -n 25 "gpurun_out/$name.log"
+  if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
+  return 0
+}
+for step in "$@"; do
+  case $step in
+    kernels) run kernels 400 python -m pytest tests/test_kernels_gpu.py -q -x -rs ;;
+    stage1)  run stage1 600 python -m pytest tests/test_stage1_gpu.py -q -x -rs ;;
+    gputests) run gputests 900 python -m pytest tests -m gpu -q -x -rs ;;
+    smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
+    bench)   run bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    benchfull) run benchfull 900 python bench.py ;;
+    prof)    run prof 900 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    *) echo "unknown step $step" ;;
+  esac
+done
