@@ -60,16 +60,18 @@ PTK_DEV float block_max(float v, float* red) {
 }
 
 // GELU variants (TF/activations.py: gelu_pytorch_tanh; torch nn.GELU default = erf)
+// 0.5 * (1 + tanh(u)) == sigmoid(2u): one exp + one reciprocal instead of tanhf
 PTK_DEV float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  return 0.5f * x * (1.f + tanhf(k0 * (x + k1 * x * x * x)));
+  const float u = k0 * (x + k1 * x * x * x);
+  return __fdividef(x, 1.f + __expf(-2.f * u));
 }
 PTK_DEV float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  float x2 = x * x;
-  float inner = k0 * (x + k1 * x2 * x);
-  float t = tanhf(inner);
-  return 0.5f * (1.f + t) + 0.5f * x * (1.f - t * t) * k0 * (1.f + 3.f * k1 * x2);
+  const float x2 = x * x;
+  const float u = k0 * (x + k1 * x2 * x);
+  const float s = __fdividef(1.f, 1.f + __expf(-2.f * u));
+  return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x2);
 }
 PTK_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
 PTK_DEV float gelu_erf_grad(float x) {

@@ -28,6 +28,7 @@ namespace ptk {
 
 constexpr int BM = 128, BN = 128, BK = 64, GROUP_M = 8;
 constexpr int STAGE_BYTES = (BM + BN) * BK * 2;   // 32 KiB
+static_assert(4 * 64 * 68 * 4 >= 2 * STAGE_BYTES, "epilogue staging must cover the pipeline buffers");
 
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
@@ -36,15 +37,72 @@ PTK_DEV void glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 16, 0, 0);
 }
 
+// ---------------------------------------------------------------- epilogue
+// The wave's 64x64 fp32 accumulator tile is staged through LDS ([64][68] f32,
+// 17 KiB per wave) and re-read row-contiguously, so every global access of the
+// epilogue (bias, row-add, residual, aux in/out, C) is a 8/16-byte vector and
+// consecutive lanes touch consecutive addresses.
+constexpr int EPI_LD = 68;                       // floats per staged row (64 + 4 pad)
+constexpr int EPI_WAVE_BYTES = 64 * EPI_LD * 4;  // 17408
+
+PTK_DEV float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+PTK_DEV float4 ldbf4(const bf16_t* p) {
+  u16x4_t u = *reinterpret_cast<const u16x4_t*>(p);
+  return make_float4(bf2f(u[0]), bf2f(u[1]), bf2f(u[2]), bf2f(u[3]));
+}
+PTK_DEV void stbf4(bf16_t* p, float4 v) {
+  u16x4_t u;
+  u[0] = f2bf(v.x); u[1] = f2bf(v.y); u[2] = f2bf(v.z); u[3] = f2bf(v.w);
+  *reinterpret_cast<u16x4_t*>(p) = u;
+}
+PTK_DEV float& el(float4& v, int e) { return reinterpret_cast<float*>(&v)[e]; }
+PTK_DEV float el(const float4& v, int e) { return reinterpret_cast<const float*>(&v)[e]; }
+
 template <int ACT, int OUT>
-PTK_DEV void epi_store(const GemmArgs& p, char* Cz, long r, long c, float v) {
-  // r, c in GEMM output space (r < M, c < N)
+PTK_DEV void epi_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 v) {
+  // r < M; c..c+3 < N (checked by caller); c % 4 == 0
+  if (p.bias) { float4 b = ldf4(p.bias + c); v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w; }
+  if (p.rowadd) {
+    float4 b = ldf4(p.rowadd + (r % p.rowadd_period) * p.ld_rowadd + c);
+    v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+  }
+  if constexpr (ACT == ACT_GELU_TANH) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) el(v, e) = gelu_tanh(bfround(el(v, e)));
+  } else if constexpr (ACT == ACT_GELU_ERF) {
+    // pre-activation kept (bf16) for the backward: Stage1/projectors.py:17-18
+#pragma unroll
+    for (int e = 0; e < 4; ++e) el(v, e) = bfround(el(v, e));
+    if (p.aux) stbf4(p.aux + r * p.ld_aux + c, v);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) el(v, e) = gelu_erf(el(v, e));
+  } else if constexpr (ACT == ACT_GELU_ERF_BWD) {
+    float4 a = ldbf4(p.aux_in + r * p.ld_aux_in + c);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) el(v, e) = bfround(el(v, e)) * gelu_erf_grad(el(a, e));
+  }
+  const long cr = map_row(p.cmap, r);
+  if (cr < 0) return;
+  if (p.resid) {
+    float4 b = ldf4(p.resid + cr * p.ld_resid + c);
+    v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+  }
+  if constexpr (OUT == OUT_BF16) {
+    stbf4(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + c, v);
+  } else {
+    if constexpr (OUT == OUT_F32_BFR) v = make_float4(bfround(v.x), bfround(v.y), bfround(v.z), bfround(v.w));
+    *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cz) + cr * p.ldc + c) = v;
+  }
+}
+
+// scalar fallback for ragged column tails / unaligned leading dims
+template <int ACT, int OUT>
+PTK_DEV void epi_scalar(const GemmArgs& p, char* Cz, long r, long c, float v) {
   if (p.bias) v += p.bias[c];
   if (p.rowadd) v += p.rowadd[(r % p.rowadd_period) * p.ld_rowadd + c];
   if constexpr (ACT == ACT_GELU_TANH) {
     v = gelu_tanh(bfround(v));
   } else if constexpr (ACT == ACT_GELU_ERF) {
-    // pre-activation kept (bf16) for the backward: Stage1/projectors.py:17-18
     float a = bfround(v);
     if (p.aux) p.aux[r * p.ld_aux + c] = f2bf(a);
     v = gelu_erf(a);
@@ -63,9 +121,99 @@ PTK_DEV void epi_store(const GemmArgs& p, char* Cz, long r, long c, float v) {
   }
 }
 
+// GEGLU: GEMM cols [32q, 32q+16) = gate[16q..], [32q+16, 32q+32) = up[16q..] (interleaved
+// weights); writes h = bf16(gelu_tanh(g)) * u and the bf16 g, u side outputs (TF gemma3 :131-133).
+PTK_DEV void geglu_vec4(const GemmArgs& p, char* Cz, long r, long hc, float4 g, float4 u) {
+  float4 h;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    el(g, e) = bfround(el(g, e));
+    el(u, e) = bfround(el(u, e));
+    el(h, e) = bfround(gelu_tanh(el(g, e))) * el(u, e);
+  }
+  if (p.aux) stbf4(p.aux + r * p.ld_aux + hc, g);
+  if (p.aux2) stbf4(p.aux2 + r * p.ld_aux + hc, u);
+  const long cr = map_row(p.cmap, r);
+  if (cr >= 0) stbf4(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + hc, h);
+}
+
+// GEGLU backward: GEMM output = dh [M, I]; writes dg, du into the interleaved [M, 2I] layout.
+PTK_DEV void geglu_bwd_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 dh) {
+  const float4 g = ldbf4(p.aux_in + r * p.ld_aux_in + c);
+  const float4 u = ldbf4(p.aux_in2 + r * p.ld_aux_in + c);
+  float4 dg, du;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const float d = bfround(el(dh, e));
+    el(dg, e) = bfround(d * el(u, e)) * gelu_tanh_grad(el(g, e));
+    el(du, e) = d * bfround(gelu_tanh(el(g, e)));
+  }
+  const long cr = map_row(p.cmap, r);
+  if (cr < 0) return;
+  bf16_t* C = reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + (c >> 4) * 32 + (c & 15);
+  stbf4(C, dg);
+  stbf4(C + 16, du);
+}
+
+template <int ACT, int OUT>
+PTK_DEV void epilogue(const GemmArgs& p, char* smem, int wave, int lane, f32x4_t (&acc)[4][4], long row0,
+                      long col0, char* Cz) {
+  // stage: lane holds C[16i + 4fq + j][16k + fr]
+  float* T = reinterpret_cast<float*>(smem + wave * EPI_WAVE_BYTES);
+  const int fr = lane & 15, fq = lane >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int k = 0; k < 4; ++k)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) T[(16 * i + 4 * fq + j) * EPI_LD + 16 * k + fr] = p.alpha * acc[i][k][j];
+  __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): own LDS writes done (wave-private region)
+  __builtin_amdgcn_wave_barrier();
+  const bool vec_ok = ((p.ldc & 3) == 0) && (!p.resid || (p.ld_resid & 3) == 0) &&
+                      (!p.rowadd || (p.ld_rowadd & 3) == 0) && (!p.aux || (p.ld_aux & 3) == 0) &&
+                      (!p.aux_in || (p.ld_aux_in & 3) == 0);
+  if constexpr (ACT == ACT_GEGLU) {
+    // 8 lanes per row, each 4 h-columns; 8 rows per pass
+    const int rr = lane >> 3, cg = lane & 7, q = cg >> 2, cc = (cg & 3) * 4;
+    const long hc = col0 / 2 + q * 16 + cc;
+#pragma unroll 2
+    for (int it = 0; it < 8; ++it) {
+      const int lr = it * 8 + rr;
+      const long r = row0 + lr;
+      if (r >= p.M || 2 * hc >= p.N) continue;
+      const float4 g = *reinterpret_cast<const float4*>(T + lr * EPI_LD + q * 32 + cc);
+      const float4 u = *reinterpret_cast<const float4*>(T + lr * EPI_LD + q * 32 + 16 + cc);
+      geglu_vec4(p, Cz, r, hc, g, u);
+    }
+  } else {
+    // 16 lanes per row, each 4 columns; 4 rows per pass
+    const int rr = lane >> 4, c4 = (lane & 15) * 4;
+    const long c = col0 + c4;
+#pragma unroll 4
+    for (int it = 0; it < 16; ++it) {
+      const int lr = it * 4 + rr;
+      const long r = row0 + lr;
+      if (r >= p.M) continue;
+      const float4 v = *reinterpret_cast<const float4*>(T + lr * EPI_LD + c4);
+      if constexpr (ACT == ACT_GEGLU_BWD) {
+        if (c + 3 < p.N) geglu_bwd_vec4(p, Cz, r, c, v);
+      } else {
+        if (vec_ok && c + 3 < p.N) {
+          epi_vec4<ACT, OUT>(p, Cz, r, c, v);
+        } else {
+          float vv[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            if (c + e < p.N) epi_scalar<ACT, OUT>(p, Cz, r, c + e, vv[e]);
+        }
+      }
+    }
+  }
+}
+
 template <int ACT, int OUT>
 __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * STAGE_BYTES];
+  __shared__ __attribute__((aligned(16))) char smem[4 * EPI_WAVE_BYTES];   // >= 2 * STAGE_BYTES
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 1, wc = wave & 1;
 
@@ -146,65 +294,9 @@ __global__ void __launch_bounds__(256, 2) gemm_nt_kernel(GemmArgs p) {
     __syncthreads();
   }
 
-  // epilogue: lane holds C[row fq*4+j][col fr] of each 16x16 tile
+  // epilogue (LDS free after the loop's final barrier)
   char* Cz = reinterpret_cast<char*>(p.C) + (z0 * p.sC0 + z1 * p.sC1) * (OUT == OUT_BF16 ? 2 : 4);
-  const int fr = lane & 15, fq = lane >> 4;
-  const long row0 = (long)bm * BM + wr * 64 + fq * 4;
-  const long col0 = (long)bn * BN + wc * 64 + fr;
-  if constexpr (ACT == ACT_GEGLU) {
-    // interleaved gate/up weights: GEMM cols [32q, 32q+16) = gate[16q..], [32q+16, 32q+32) = up[16q..]
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int k = 0; k < 2; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const long r = row0 + i * 16 + j;
-          const long hc = ((long)bn * BN + wc * 64) / 2 + k * 16 + fr;
-          if (r >= p.M || 2 * hc >= p.N) continue;
-          const float g = bfround(p.alpha * acc[i][2 * k][j]);
-          const float u = bfround(p.alpha * acc[i][2 * k + 1][j]);
-          if (p.aux) p.aux[r * p.ld_aux + hc] = f2bf(g);
-          if (p.aux2) p.aux2[r * p.ld_aux + hc] = f2bf(u);
-          const float h = bfround(gelu_tanh(g)) * u;     // TF gemma3 :131-133, bf16 ops
-          const long cr = map_row(p.cmap, r);
-          if (cr >= 0) reinterpret_cast<bf16_t*>(Cz)[cr * p.ldc + hc] = f2bf(h);
-        }
-  } else if constexpr (ACT == ACT_GEGLU_BWD) {
-    // GEMM output = dh [M, I]; write d(gate), d(up) into the interleaved [M, 2I] layout
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const long r = row0 + i * 16 + j;
-          const long c = col0 + k * 16;
-          if (r >= p.M || c >= p.N) continue;
-          const float dh = bfround(p.alpha * acc[i][k][j]);
-          const float g = bf2f(p.aux_in[r * p.ld_aux_in + c]);
-          const float u = bf2f(p.aux_in2[r * p.ld_aux_in + c]);
-          const float dg = bfround(dh * u) * gelu_tanh_grad(g);
-          const float du = dh * bfround(gelu_tanh(g));
-          const long cr = map_row(p.cmap, r);
-          if (cr < 0) continue;
-          const long gc = (c >> 4) * 32 + (c & 15);
-          bf16_t* C = reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc;
-          C[gc] = f2bf(dg);
-          C[gc + 16] = f2bf(du);
-        }
-  } else {
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int k = 0; k < 4; ++k)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const long r = row0 + i * 16 + j;
-          const long c = col0 + k * 16;
-          if (r < p.M && c < p.N) epi_store<ACT, OUT>(p, Cz, r, c, p.alpha * acc[i][k][j]);
-        }
-  }
+  epilogue<ACT, OUT>(p, smem, wave, lane, acc, (long)bm * BM + wr * 64, (long)bn * BN + wc * 64, Cz);
 }
 
 // ---- optional live per-class timing (HIP events around launches; bench.py roofline)
