@@ -102,6 +102,8 @@ int ptk_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float std, float m
  * around every GEMM launch, grouped by epilogue class (PTK_ACT_*).  read()
  * synchronises those events and returns the summed kernel time and count. */
 int ptk_gemm_timer_enable(int on);
+/* Route every GEMM through the 128x128 kernel (tests compare both tile paths). */
+int ptk_gemm_force_small_tiles(int on);
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
 
 /* ------------------------------------------------------------------------ *

@@ -98,6 +98,7 @@ SIGNATURES = {
     "ptk_cast_f32_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "ptk_fill_normal_bf16": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_void_p]),
     "ptk_gemm_timer_enable": (c_int, [c_int]),
+    "ptk_gemm_force_small_tiles": (c_int, [c_int]),
     "ptk_gemm_timer_read": (c_int, [c_int, C.POINTER(C.c_double), C.POINTER(c_int)]),
     "ptk_siglip_workspace_bytes": (c_size_t, [C.POINTER(SiglipConfigC), c_int]),
     "ptk_siglip_fwd": (c_int, [C.POINTER(SiglipConfigC), C.POINTER(SiglipWeightsC), c_int, c_void_p, c_void_p,

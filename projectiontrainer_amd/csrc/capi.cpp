@@ -88,6 +88,10 @@ int ptk_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream) {
   return launch_cast_f32_bf16(in, (bf16_t*)out, n, ST);
 }
 
+int ptk_gemm_force_small_tiles(int on) {
+  force_small_tiles(on);
+  return 0;
+}
 int ptk_gemm_timer_enable(int on) {
   timer_enable(on);
   return 0;

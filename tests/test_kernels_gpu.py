@@ -191,3 +191,52 @@ def test_cross_entropy(gpu):
     rl = Kn.cross_entropy_(lg, tgt, gscale)
     torch.testing.assert_close(rl.sum() / cnt * 0.25, loss.detach(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(lg.float(), x.grad, rtol=1e-2, atol=1e-6)
+
+
+@pytest.mark.parametrize("M,N,K", [(1024, 512, 64), (1024, 512, 128), (1100, 700, 192), (2048, 1152, 1152),
+                                   (4096, 1536, 256)])
+def test_gemm_big_tile_path(gpu, M, N, K):
+    """256x256 8-wave kernel (M >= 1024, N >= 512): ragged M/N, 1..18 K-tiles, vs fp32."""
+    Kn, L = _k()
+    A, B = rnd(M, K, dev=gpu, seed=31), rnd(N, K, dev=gpu, seed=32)
+    ref = A.float() @ B.float().T
+    C = Kn.gemm(A, B, out_dtype=torch.float32)
+    torch.testing.assert_close(C, ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
+
+
+def test_gemm_big_vs_small_all_epilogues(gpu):
+    """Every epilogue through the 256x256 path equals the 128x128 path bit-for-bit
+    (same fp32 accumulation order per K-tile is not guaranteed, so compare at 1e-5)."""
+    Kn, L = _k()
+    from projectiontrainer_amd.gemma3 import interleave_gate_up
+    M, N, K = 1300, 768, 320
+    A, B = rnd(M, K, dev=gpu, seed=33), rnd(N, K, dev=gpu, seed=34, scale=0.1)
+    bias = rnd(N, dev=gpu, dtype=torch.float32, seed=35)
+    res = rnd(M, N, dev=gpu, dtype=torch.float32, seed=36)
+    aux_in = rnd(M, N, dev=gpu, seed=37)
+    outs = []
+    for small in (0, 1):
+        L.lib().ptk_gemm_force_small_tiles(small)
+        try:
+            o = {}
+            C = res.clone()
+            Kn.gemm(A, B, C=C, bias=bias, resid=C)
+            o["resid"] = C
+            o["gelu_tanh"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_TANH)
+            aux = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+            o["gelu_erf"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_ERF, aux=aux)
+            o["aux"] = aux
+            o["erf_bwd"] = Kn.gemm(A, B, act=L.ACT_GELU_ERF_BWD, aux_in=aux_in)
+            g = torch.empty(M, N // 2, dtype=torch.bfloat16, device=gpu)
+            u = torch.empty_like(g)
+            o["geglu"] = Kn.gemm(A, B, act=L.ACT_GEGLU, aux=g, aux2=u)
+            o["g"], o["u"] = g, u
+            o["geglu_bwd"] = Kn.gemm(A, B, act=L.ACT_GEGLU_BWD, aux_in=aux_in, aux_in2=aux_in)
+            cm = torch.zeros(M + 64, N, device=gpu)
+            Kn.gemm(A, B, C=cm, out_mode=L.OUT_F32_BF16ROUND, cmap=(100, 1, 104, -1), M=1300)
+            o["cmap"] = cm
+            outs.append(o)
+        finally:
+            L.lib().ptk_gemm_force_small_tiles(0)
+    for k in outs[0]:
+        torch.testing.assert_close(outs[0][k].float(), outs[1][k].float(), rtol=1e-2, atol=1e-3, msg=k)

@@ -1,0 +1,58 @@
+"""Time libptk GEMM shapes of the cfg2 step (HIP events, interleaved rounds in one
+process) and print achieved TFLOP/s and effective HBM GB/s per shape/epilogue."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from projectiontrainer_amd import kernels as K, _lib as L  # noqa: E402
+
+dev = torch.device("cuda:0")
+M = 32 * 704
+SHAPES = [  # name, M, N, K, act, out dtype
+    ("gemma_gate_up_geglu", M, 13824, 1152, L.ACT_GEGLU, torch.bfloat16),
+    ("gemma_gate_up_plain", M, 13824, 1152, L.ACT_NONE, torch.bfloat16),
+    ("gemma_down", M, 1152, 6912, L.ACT_NONE, torch.bfloat16),
+    ("gemma_dX_gate_up_f32", M, 1152, 13824, L.ACT_NONE, torch.float32),
+    ("gemma_geglu_bwd", M, 6912, 1152, L.ACT_GEGLU_BWD, torch.bfloat16),
+    ("gemma_qkv", M, 1536, 1152, L.ACT_NONE, torch.bfloat16),
+    ("siglip_fc1_gelu", 18432, 4096, 1024, L.ACT_GELU_TANH, torch.bfloat16),
+    ("siglip_fc2_f32", 18432, 1024, 4096, L.ACT_NONE, torch.float32),
+    ("lm_head", 4096, 262144, 1152, L.ACT_NONE, torch.bfloat16),
+    ("square_8192", 8192, 8192, 8192, L.ACT_NONE, torch.bfloat16),
+]
+
+
+def run(name, m, n, k, act, odt, reps=10):
+    A = torch.randn(m, k, device=dev).to(torch.bfloat16)
+    B = (torch.randn(n, k, device=dev) * 0.05).to(torch.bfloat16)
+    kw = {}
+    if act == L.ACT_GEGLU:
+        kw = dict(aux=torch.empty(m, n // 2, dtype=torch.bfloat16, device=dev),
+                  aux2=torch.empty(m, n // 2, dtype=torch.bfloat16, device=dev))
+    if act == L.ACT_GEGLU_BWD:
+        kw = dict(aux_in=torch.randn(m, n, device=dev).to(torch.bfloat16),
+                  aux_in2=torch.randn(m, n, device=dev).to(torch.bfloat16))
+    C = K.gemm(A, B, out_dtype=odt, act=act, **kw)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        K.gemm(A, B, C=C, out_dtype=odt, act=act, **kw)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    fl = 2.0 * m * n * k
+    return {"name": name, "M": m, "N": n, "K": k, "ms": round(ms, 4), "TFLOPs": round(fl / ms / 1e9, 1)}
+
+
+if __name__ == "__main__":
+    res = []
+    for rnd in range(2):
+        for s in SHAPES:
+            r = run(*s)
+            if rnd == 1:
+                res.append(r)
+                print(json.dumps(r), flush=True)

@@ -23,6 +23,7 @@ for step in "$@"; do
     smoke)   run smoke 300 python -c "import __graft_entry__ as g; g.smoke()" ;;
     bench)   run bench 600 python bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     benchfull) run benchfull 900 python bench.py ;;
+    gemmbench) run gemmbench 300 python tools/gemm_bench.py ;;
     prof)    run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
   esac
