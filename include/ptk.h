@@ -106,6 +106,24 @@ int ptk_gemm_timer_enable(int on);
 int ptk_gemm_force_small_tiles(int on);
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
 
+/* Flash attention forward: O = softmax(scale * Q K^T + mask) V per z, bf16 in/out,
+ * LSE (natural log) per query row.  z -> (z0, z1) = (z / batch_inner, z % batch_inner);
+ * Q row r of z at Q + z0*sQ0 + z1*sQ1 + qmap(r)*ldq; keys/values at K/V + ... + k*ldk;
+ * query position = r / qdiv (causal, window); key_valid[(z / zdiv) * nkeys + k] (or NULL).
+ * Replaces sdpa in modeling_siglip.py:289-300 and modeling_gemma3.py:365-379. */
+typedef struct {
+  const void* Q; const void* K; const void* V; void* O; float* lse;
+  int rows, nkeys, head_dim;
+  int64_t ldq, ldk, ldo;
+  int batch, batch_inner, zdiv;
+  int64_t sQ0, sQ1, sK0, sK1, sO0, sO1;
+  ptk_rowmap qmap, omap;
+  int qdiv, causal, window;
+  const int32_t* key_valid;
+  float scale;
+} ptk_flash_desc;
+int ptk_flash_attn_fwd(const ptk_flash_desc* d, void* stream);
+
 /* ------------------------------------------------------------------------ *
  * SigLIP vision tower, frozen forward                                      *
  * replaces vision_tower(pixel_values=...).last_hidden_state                *

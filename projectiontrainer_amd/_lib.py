@@ -34,6 +34,17 @@ class GemmDesc(C.Structure):
                 ("amap", RowMap), ("cmap", RowMap)]
 
 
+class FlashDesc(C.Structure):
+    _fields_ = [("Q", c_void_p), ("K", c_void_p), ("V", c_void_p), ("O", c_void_p), ("lse", c_void_p),
+                ("rows", c_int), ("nkeys", c_int), ("head_dim", c_int),
+                ("ldq", c_int64), ("ldk", c_int64), ("ldo", c_int64),
+                ("batch", c_int), ("batch_inner", c_int), ("zdiv", c_int),
+                ("sQ0", c_int64), ("sQ1", c_int64), ("sK0", c_int64), ("sK1", c_int64),
+                ("sO0", c_int64), ("sO1", c_int64), ("qmap", RowMap), ("omap", RowMap),
+                ("qdiv", c_int), ("causal", c_int), ("window", c_int), ("key_valid", c_void_p),
+                ("scale", c_float)]
+
+
 class SiglipConfigC(C.Structure):
     _fields_ = [("image_size", c_int), ("patch_size", c_int), ("channels", c_int), ("hidden", c_int),
                 ("heads", c_int), ("intermediate", c_int), ("layers", c_int), ("eps", c_float)]
@@ -100,6 +111,7 @@ SIGNATURES = {
     "ptk_gemm_timer_enable": (c_int, [c_int]),
     "ptk_gemm_force_small_tiles": (c_int, [c_int]),
     "ptk_gemm_timer_read": (c_int, [c_int, C.POINTER(C.c_double), C.POINTER(c_int)]),
+    "ptk_flash_attn_fwd": (c_int, [C.POINTER(FlashDesc), c_void_p]),
     "ptk_siglip_workspace_bytes": (c_size_t, [C.POINTER(SiglipConfigC), c_int]),
     "ptk_siglip_fwd": (c_int, [C.POINTER(SiglipConfigC), C.POINTER(SiglipWeightsC), c_int, c_void_p, c_void_p,
                                c_void_p, c_size_t, c_void_p]),

@@ -102,6 +102,20 @@ int ptk_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float std, float m
   return launch_fill_normal_bf16((bf16_t*)out, n, seed, std, mean, ST);
 }
 
+int ptk_flash_attn_fwd(const ptk_flash_desc* d, void* stream) {
+  if (!d) return set_error("flash: null desc");
+  FlashArgs a;
+  a.Q = (const bf16_t*)d->Q; a.K = (const bf16_t*)d->K; a.V = (const bf16_t*)d->V; a.O = (bf16_t*)d->O;
+  a.lse = d->lse; a.rows = d->rows; a.nkeys = d->nkeys; a.D = d->head_dim;
+  a.ldq = d->ldq; a.ldk = d->ldk; a.ldo = d->ldo;
+  a.zin = d->batch_inner > 0 ? d->batch_inner : 1; a.zdiv = d->zdiv > 0 ? d->zdiv : 1;
+  a.sQ0 = d->sQ0; a.sQ1 = d->sQ1; a.sK0 = d->sK0; a.sK1 = d->sK1; a.sO0 = d->sO0; a.sO1 = d->sO1;
+  a.qmap = to_map(d->qmap); a.omap = to_map(d->omap);
+  a.qdiv = d->qdiv > 0 ? d->qdiv : 1; a.causal = d->causal; a.window = d->window;
+  a.key_valid = d->key_valid; a.scale = d->scale;
+  return launch_attn_fwd(a, d->batch > 0 ? d->batch : 1, ST);
+}
+
 // ---------------------------------------------------------------- projector
 int ptk_projector_fwd(const ptk_projector* p, int rows, const void* x, void* a, void* h, float* out,
                       ptk_rowmap out_map, int64_t ld_out, int round_bf16, void* stream) {

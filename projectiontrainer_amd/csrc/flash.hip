@@ -1,0 +1,219 @@
+// Flash attention forward for gfx950 (bf16 in/out, fp32 softmax state).
+//
+// One workgroup = 8 waves = 128 query rows of one (batch, kv-head) z; each
+// wave owns 16 rows.  Per 64-key tile (K and V staged global->LDS by
+// LDS-DMA, double-buffered):
+//   S^T[64 keys x 16 q] = K . Q^T        MFMA 16x16x32, A = K rows from LDS,
+//                                        B = Q fragments kept in registers
+//   online softmax per query column      (lane's column = its query row; the
+//                                        column's 64 keys live in 4 lanes:
+//                                        2 shuffles per reduction)
+//   O^T[D x 16 q] += V^T . P^T           A = V^T via ds_read_b64_tr_b16 on
+//                                        the row-major V tile, B = P^T taken
+//                                        straight from the S^T accumulators
+//                                        (k order permuted identically on
+//                                        both operands: no LDS round trip)
+// O^T's layout puts a query on the same lane as its softmax state, so the
+// per-tile rescale needs no cross-lane traffic.  Masks: key padding / key
+// length, causal (query position = row / qdiv), sliding window k > q - W.
+// Writes O (bf16, row-remapped) and LSE = ln(sum exp(score)) per row (fp32)
+// for the backward.  Semantics: softmax(scale * Q K^T + mask) V, as
+// TF/models/siglip/modeling_siglip.py:289-300 and gemma3 :365-379 (sdpa).
+#include "common.h"
+#include "ptk_internal.h"
+
+namespace ptk {
+
+typedef __attribute__((ext_vector_type(4))) short s16x4_t;
+typedef const __attribute__((address_space(1))) void* fa_gptr_t;
+typedef __attribute__((address_space(3))) void* fa_lptr_t;
+
+PTK_DEV void fa_glds16(const void* src, void* lds) {
+  __builtin_amdgcn_global_load_lds((fa_gptr_t)src, (fa_lptr_t)lds, 16, 0, 0);
+}
+
+// 16-B chunk swizzles (chunk index within a row of D/8 chunks)
+template <int D>
+PTK_DEV int swz_k(int r) { return D == 256 ? (r & 15) : ((r >> 1) & 7); }     // ds_read_b128 row reads
+template <int D>
+PTK_DEV int swz_v(int r) { return D == 256 ? 2 * (r & 7) : 2 * ((r >> 1) & 3); }  // ds_read_b64_tr_b16
+
+template <int D>
+__global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
+  constexpr int CPR = D / 8;                 // 16-B chunks per row
+  constexpr int TILE_BYTES = 64 * D * 2;     // one K or V tile
+  constexpr int KS = D / 32;                 // MFMA k-steps over the head dim
+  constexpr int DS = D / 16;                 // 16-wide d sub-tiles
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];   // K0 V0 K1 V1
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int z = blockIdx.y, z0 = z / a.zin, z1 = z - z0 * a.zin;
+  const int r0 = blockIdx.x * 128;
+  const bf16_t* Q = a.Q + z0 * a.sQ0 + z1 * a.sQ1;
+  const bf16_t* K = a.K + z0 * a.sK0 + z1 * a.sK1;
+  const bf16_t* V = a.V + z0 * a.sK0 + z1 * a.sK1;
+  const long b = z / a.zdiv;
+
+  // key range of the block (causal / window skip)
+  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
+  int k_hi = a.nkeys;
+  int k_lo = 0;
+  if (a.causal) {
+    k_hi = min(k_hi, pos_hi + 1);
+    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
+  }
+  const int t_lo = k_lo / 64, t_hi = (k_hi + 63) / 64;
+
+  // Q fragments: B operand of S^T = K Q^T, lane holds Q[row c16][8g + 32ks .. +7]
+  const int qrow = r0 + wave * 16 + c16;
+  const int qrow_c = min(qrow, a.rows - 1);
+  bf16x8_t qf[KS];
+  {
+    const long qa = map_row(a.qmap, qrow_c);
+    const bf16_t* qp = Q + qa * a.ldq + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * ks);
+  }
+  const int qpos = qrow_c / a.qdiv;
+
+  // staging: wave-instruction i covers 64 chunks = (64 / CPR) rows of the tile
+  constexpr int ROWS_PER_INST = 64 / CPR;
+  constexpr int INSTS = 64 * CPR / 64 / 8;   // per wave per tile (K or V)
+  auto stage = [&](int t, int buf) {
+    char* kb = smem + buf * 2 * TILE_BYTES;
+    char* vb = kb + TILE_BYTES;
+#pragma unroll
+    for (int j = 0; j < INSTS; ++j) {
+      const int inst = wave * INSTS + j;
+      const int row = inst * ROWS_PER_INST + lane / CPR;
+      const int pch = lane % CPR;
+      const int key = min(t * 64 + row, a.nkeys - 1);
+      const bf16_t* ks_ = K + (long)key * a.ldk + 8 * (pch ^ swz_k<D>(row));
+      const bf16_t* vs_ = V + (long)key * a.ldk + 8 * (pch ^ swz_v<D>(row));
+      fa_glds16(ks_, kb + inst * 1024);
+      fa_glds16(vs_, vb + inst * 1024);
+    }
+  };
+
+  f32x4_t o[DS];
+#pragma unroll
+  for (int i = 0; i < DS; ++i) o[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl2 = a.scale * 1.4426950408889634f;   // scores in log2 units
+
+  if (t_lo < t_hi) stage(t_lo, 0);
+  for (int t = t_lo; t < t_hi; ++t) {
+    const int buf = (t - t_lo) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < t_hi) stage(t + 1, buf ^ 1);
+    const char* kb = smem + buf * 2 * TILE_BYTES;
+    const char* vb = kb + TILE_BYTES;
+
+    // ---- S^T = K Q^T : acc[ms] holds keys 16ms + 4g + j, query column c16
+    f32x4_t s[4];
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms) {
+      s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      const int row = ms * 16 + c16;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int ch = (ks * 4 + g) ^ swz_k<D>(row);
+        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + row * (D * 2) + ch * 16);
+        s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
+      }
+    }
+    // ---- mask + online softmax (log2 domain)
+    float mt = -INFINITY;
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms) {
+      const int kbase = t * 64 + ms * 16 + 4 * g;
+      int kv[4] = {1, 1, 1, 1};
+      if (a.key_valid) {
+        const int4 v4 = *reinterpret_cast<const int4*>(a.key_valid + b * a.nkeys + min(kbase, a.nkeys - 4));
+        kv[0] = v4.x; kv[1] = v4.y; kv[2] = v4.z; kv[3] = v4.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = kbase + j;
+        bool ok = key < a.nkeys && kv[j] != 0;
+        if (a.causal) ok = ok && key <= qpos;
+        if (a.window > 0) ok = ok && key > qpos - a.window;
+        const float v = ok ? s[ms][j] * sl2 : -INFINITY;
+        s[ms][j] = v;
+        mt = fmaxf(mt, v);
+      }
+    }
+    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
+    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    const float m_new = fmaxf(m_run, mt);
+    const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m_run - m_new);
+    float rs = 0.f;
+    bf16x8_t pf[2];
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = (s[ms][j] == -INFINITY) ? 0.f : exp2f(s[ms][j] - m_new);
+        const bf16_t pb = f2bf(p);
+        rs += bf2f(pb);
+        pf[ms >> 1][(ms & 1) * 4 + j] = (short)pb;
+      }
+    rs += __shfl_xor(rs, 16, 64);
+    rs += __shfl_xor(rs, 32, 64);
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+#pragma unroll
+    for (int i = 0; i < DS; ++i) o[i] *= alpha;
+
+    // ---- O^T += V^T P^T : A = V^T (tr reads), k order = {16(2s)+4g+0..3, 16(2s+1)+4g+0..3}
+    const int q4 = c16 >> 2, p4 = c16 & 3;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8_t vf;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int row = (2 * st + hh) * 16 + 4 * g + q4;
+          const int ch = (2 * ds + (p4 >> 1)) ^ swz_v<D>(row);
+          const char* addr = vb + row * (D * 2) + ch * 16 + 8 * (p4 & 1);
+          const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
+          vf[4 * hh + 0] = r[0]; vf[4 * hh + 1] = r[1]; vf[4 * hh + 2] = r[2]; vf[4 * hh + 3] = r[3];
+        }
+        o[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[st], o[ds], 0, 0, 0);
+      }
+    }
+  }
+
+  // ---- epilogue: O[q][d] = O^T[d][q] / l ; lane holds d = 16ds + 4g + j for query c16
+  if (qrow >= a.rows) return;
+  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+  const long orow = map_row(a.omap, qrow);
+  bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + orow * a.ldo + 4 * g;
+#pragma unroll
+  for (int ds = 0; ds < DS; ++ds) {
+    u16x4_t u;
+    u[0] = f2bf(o[ds][0] * inv); u[1] = f2bf(o[ds][1] * inv);
+    u[2] = f2bf(o[ds][2] * inv); u[3] = f2bf(o[ds][3] * inv);
+    *reinterpret_cast<u16x4_t*>(op + 16 * ds) = u;
+  }
+  if (a.lse && g == 0) a.lse[(long)z * a.rows + qrow] = (m_run + log2f(l_run)) * 0.6931471805599453f;
+}
+
+int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
+  if (a.rows <= 0 || nz <= 0) return 0;
+  if (a.nkeys < 4) return set_error("attn_fwd: nkeys must be >= 4");
+  if ((a.ldq | a.ldk | a.ldo) & 7) return set_error("attn_fwd: row strides must be multiples of 8");
+  if (a.key_valid && (a.nkeys & 3)) return set_error("attn_fwd: key_valid rows must be a multiple of 4");
+  dim3 grid((unsigned)((a.rows + 127) / 128), (unsigned)nz);
+  switch (a.D) {
+    case 64: hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(512), 0, st, a); break;
+    case 256: hipLaunchKernelGGL(attn_fwd_kernel<256>, grid, dim3(512), 0, st, a); break;
+    default: return set_error("attn_fwd: head_dim %d unsupported (64, 256)", a.D);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : set_error("attn_fwd launch failed");
+}
+
+}  // namespace ptk

@@ -73,9 +73,9 @@ SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
   w.h = bp.take<float>(M * D);
   w.a = bp.take<bf16_t>(M * D);
   w.qkv = bp.take<bf16_t>(M * 3 * D);
-  w.vt = bp.take<bf16_t>((long)B * H * hd * Np);
-  w.S = bp.take<float>((long)B * H * Nn * Np);
-  w.P = bp.take<bf16_t>((long)B * H * Nn * Np);
+  w.vt = nullptr;
+  w.S = nullptr;
+  w.P = nullptr;
   w.o = bp.take<bf16_t>(M * D);
   w.mlp = bp.take<bf16_t>(M * I);
   return w;
@@ -84,12 +84,13 @@ SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
 // ------------------------------------------------------------------ Gemma3
 struct GemmaLayerSave {
   float *x2, *rstd_in, *rstd_ao, *rstd_pre, *rstd_dn, *rstd_q, *rstd_k;
-  bf16_t *qkv, *Q, *K, *V, *P, *ao, *g, *u, *dn;
+  bf16_t *qkv, *Q, *K, *V, *ao, *g, *u, *dn;
+  float* lse;
 };
 struct GemmaWs {
   std::vector<float*> x;          // L+1 residual-stream snapshots
   std::vector<GemmaLayerSave> L;
-  bf16_t *xn, *O, *h, *Vt, *Kt, *Qt, *dqkv, *dgu, *dao, *dO, *dS, *dST, *PT, *dOT, *dQ, *dK, *dV, *xf, *logits;
+  bf16_t *P, *xn, *O, *h, *Vt, *Kt, *Qt, *dqkv, *dgu, *dao, *dO, *dS, *dST, *PT, *dOT, *dQ, *dK, *dV, *xf, *logits;
   float *S, *dtmp, *rstd_f, *row_loss, *dxf, *count, *gscale;
   int32_t* key_valid;
 };
@@ -115,13 +116,14 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp)
     s.Q = bp.take<bf16_t>(Z * SG * D);
     s.K = bp.take<bf16_t>(Z * Sp * D);
     s.V = bp.take<bf16_t>(Z * Sp * D);
-    s.P = bp.take<bf16_t>(Z * SG * Sp);
+    s.lse = bp.take<float>(Z * SG);
     s.ao = bp.take<bf16_t>(M * H);
     s.g = bp.take<bf16_t>(M * I);
     s.u = bp.take<bf16_t>(M * I);
     s.dn = bp.take<bf16_t>(M * H);
     w.L.push_back(s);
   }
+  w.P = bp.take<bf16_t>(Z * SG * Sp);
   w.xn = bp.take<bf16_t>(M * H);
   w.O = bp.take<bf16_t>(M * Dq);
   w.h = bp.take<bf16_t>(M * I);
@@ -189,26 +191,16 @@ int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int
       g.bias = L.bqkv;
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
     }
-    // V^T per (b, head), zero-padded keys
-    CK(launch_transpose(w.qkv + 2 * D, 3 * D, (long)Nn * 3 * D, hd, Hh, w.vt, Np, (long)Hh * hd * Np, (long)hd * Np,
-                        B * Hh, Nn, hd, Np, st));
-    {  // scores = Q K^T / sqrt(hd)
-      GemmArgs g = gemm(w.qkv, 3 * D, w.qkv + D, 3 * D, w.S, Np, Nn, Nn, hd);
-      g.zin = Hh;
-      g.sA0 = g.sB0 = (long)Nn * 3 * D; g.sA1 = g.sB1 = hd;
-      g.sC0 = (long)Hh * Nn * Np; g.sC1 = (long)Nn * Np;
-      g.alpha = 1.0f / sqrtf((float)hd);
-      CK(launch_gemm(g, ACT_NONE, OUT_F32, B * Hh, st));
-    }
-    MaskSpec mk{Nn, 1, Hh, 0, 0, nullptr, Nn};
-    CK(launch_softmax_fwd(w.S, w.P, B * Hh, Nn, Np, Np, mk, st));
-    {  // O = P V  -> [B*N, D] at head column offset
-      GemmArgs g = gemm(w.P, Np, w.vt, Np, w.o, D, Nn, hd, Np);
-      g.zin = Hh;
-      g.sA0 = (long)Hh * Nn * Np; g.sA1 = (long)Nn * Np;
-      g.sB0 = (long)Hh * hd * Np; g.sB1 = (long)hd * Np;
-      g.sC0 = (long)Nn * D; g.sC1 = hd;
-      CK(launch_gemm(g, ACT_NONE, OUT_BF16, B * Hh, st));
+    {  // softmax(Q K^T / sqrt(hd)) V per (b, head), flash (no score matrix in HBM)
+      FlashArgs fa;
+      fa.Q = w.qkv; fa.K = w.qkv + D; fa.V = w.qkv + 2 * D; fa.O = w.o;
+      fa.rows = Nn; fa.nkeys = Nn; fa.D = hd;
+      fa.ldq = fa.ldk = 3 * D; fa.ldo = D;
+      fa.zin = Hh; fa.zdiv = Hh;
+      fa.sQ0 = fa.sK0 = (long)Nn * 3 * D; fa.sQ1 = fa.sK1 = hd;
+      fa.sO0 = (long)Nn * D; fa.sO1 = hd;
+      fa.scale = 1.0f / sqrtf((float)hd);
+      CK(launch_attn_fwd(fa, B * Hh, st));
     }
     {  // out_proj + bias + residual
       GemmArgs g = gemm(w.o, D, L.wo, D, w.h, D, M, D, D);
@@ -271,23 +263,20 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
     CK(launch_gemm(gemm(w.xn, H, L.wqkv, H, sv.qkv, Dqkv, M, Dqkv, H), ACT_NONE, OUT_BF16, 1, st));
     CK(launch_qknorm_rope_fwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, eps, sv.Q, sv.K, sv.V, sv.rstd_q, sv.rstd_k,
                               st));
-    CK(launch_transpose(sv.V, D, (long)Sp * D, 0, 1, w.Vt, Sp, (long)D * Sp, 0, Z, Sp, D, Sp, st));
-    {  // scores[z] = Q[z] K[z]^T * scale   (z = b*Hkv + kvh)
-      GemmArgs g = gemm(sv.Q, D, sv.K, D, w.S, Sp, SG, Sp, D);
-      g.sA0 = (long)SG * D; g.sB0 = (long)Sp * D; g.sC0 = (long)SG * Sp;
-      g.alpha = scale;
-      CK(launch_gemm(g, ACT_NONE, OUT_F32, Z, st));
-    }
-    MaskSpec mk{SG, G, Hkv, 1, sliding ? c->sliding_window : 0, w.key_valid, Sp};
-    CK(launch_softmax_fwd(w.S, sv.P, Z, SG, Sp, Sp, mk, st));
-    {  // O = P V, scattered to token-major [M, Hq*D]
-      GemmArgs g = gemm(sv.P, Sp, w.Vt, Sp, w.O, D, SG, D, Sp);
-      g.zin = Hkv;
-      g.sA0 = (long)Hkv * SG * Sp; g.sA1 = (long)SG * Sp;
-      g.sB0 = (long)Hkv * D * Sp; g.sB1 = (long)D * Sp;
-      g.sC0 = (long)Sp * Hq * D; g.sC1 = (long)G * D;
-      g.cmap = RowMap{G, 0, Hq, 0};
-      CK(launch_gemm(g, ACT_NONE, OUT_BF16, Z, st));
+    {  // causal / sliding-window GQA attention, flash; O token-major, LSE kept for the backward
+      FlashArgs fa;
+      fa.Q = sv.Q; fa.K = sv.K; fa.V = sv.V; fa.O = w.O; fa.lse = sv.lse;
+      fa.rows = SG; fa.nkeys = Sp; fa.D = D;
+      fa.ldq = D; fa.ldk = D; fa.ldo = D;
+      fa.zin = Hkv; fa.zdiv = Hkv;
+      fa.sQ0 = (long)Hkv * SG * D; fa.sQ1 = (long)SG * D;
+      fa.sK0 = (long)Hkv * Sp * D; fa.sK1 = (long)Sp * D;
+      fa.sO0 = (long)Sp * Hq * D; fa.sO1 = (long)G * D;
+      fa.omap = RowMap{G, 0, Hq, 0};
+      fa.qdiv = G; fa.causal = 1; fa.window = sliding ? c->sliding_window : 0;
+      fa.key_valid = w.key_valid;
+      fa.scale = scale;
+      CK(launch_attn_fwd(fa, Z, st));
     }
     CK(launch_gemm(gemm(w.O, Dq, L.wo, Dq, sv.ao, H, M, H, Dq), ACT_NONE, OUT_BF16, 1, st));
     CK(launch_residual_norm_fwd(sv.ao, w.x[l], L.ln_post_attn, L.ln_pre_ff, sv.x2, w.xn, sv.rstd_ao, sv.rstd_pre, M,
@@ -339,17 +328,25 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
       g.cmap = RowMap{Sp, 0, (long)Hkv * Sp, 0};
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, Hkv, st));
     }
-    // attention backward
+    // attention backward: P recomputed (scores GEMM + masked softmax), then materialised dP/dS
+    {
+      GemmArgs g = gemm(sv.Q, D, sv.K, D, w.S, Sp, SG, Sp, D);
+      g.sA0 = (long)SG * D; g.sB0 = (long)Sp * D; g.sC0 = (long)SG * Sp;
+      g.alpha = scale;
+      CK(launch_gemm(g, ACT_NONE, OUT_F32, Z, st));
+      MaskSpec mk{SG, G, Hkv, 1, sliding ? c->sliding_window : 0, w.key_valid, Sp};
+      CK(launch_softmax_fwd(w.S, w.P, Z, SG, Sp, Sp, mk, st));
+    }
     CK(launch_transpose(sv.K, D, (long)Sp * D, 0, 1, w.Kt, Sp, (long)D * Sp, 0, Z, Sp, D, Sp, st));
     CK(launch_transpose(sv.Q, D, (long)SG * D, 0, 1, w.Qt, SG, (long)D * SG, 0, Z, SG, D, SG, st));
     CK(launch_transpose(w.dO, D, (long)SG * D, 0, 1, w.dOT, SG, (long)D * SG, 0, Z, SG, D, SG, st));
-    CK(launch_transpose(sv.P, Sp, (long)SG * Sp, 0, 1, w.PT, SG, (long)Sp * SG, 0, Z, SG, Sp, SG, st));
+    CK(launch_transpose(w.P, Sp, (long)SG * Sp, 0, 1, w.PT, SG, (long)Sp * SG, 0, Z, SG, Sp, SG, st));
     {  // dP = dO V^T
       GemmArgs g = gemm(w.dO, D, sv.V, D, w.S, Sp, SG, Sp, D);
       g.sA0 = (long)SG * D; g.sB0 = (long)Sp * D; g.sC0 = (long)SG * Sp;
       CK(launch_gemm(g, ACT_NONE, OUT_F32, Z, st));
     }
-    CK(launch_softmax_bwd(sv.P, w.S, w.dS, Z * SG, Sp, Sp, scale, st));
+    CK(launch_softmax_bwd(w.P, w.S, w.dS, Z * SG, Sp, Sp, scale, st));
     CK(launch_transpose(w.dS, Sp, (long)SG * Sp, 0, 1, w.dST, SG, (long)Sp * SG, 0, Z, SG, Sp, SG, st));
     {  // dQ = dS K
       GemmArgs g = gemm(w.dS, Sp, w.Kt, Sp, w.dQ, D, SG, D, Sp);

@@ -98,6 +98,24 @@ int launch_softmax_fwd(const float* S, bf16_t* P, int nz, int rows, int cols, lo
 int launch_softmax_bwd(const bf16_t* P, const float* dP, bf16_t* dS, int nrows, int cols, long ld,
                        float scale, hipStream_t st);
 
+// ---- flash attention (flash.hip) ----
+struct FlashArgs {
+  const bf16_t* Q = nullptr;
+  const bf16_t* K = nullptr;
+  const bf16_t* V = nullptr;
+  bf16_t* O = nullptr;
+  float* lse = nullptr;          // [nz][rows] (optional)
+  int rows = 0, nkeys = 0, D = 0;
+  long ldq = 0, ldk = 0, ldo = 0;  // V shares K's strides
+  int zin = 1, zdiv = 1;         // z -> (z / zin, z % zin); sample b = z / zdiv (key_valid row)
+  long sQ0 = 0, sQ1 = 0, sK0 = 0, sK1 = 0, sO0 = 0, sO1 = 0;
+  RowMap qmap{0, 0, 0, 0}, omap{0, 0, 0, 0};
+  int qdiv = 1, causal = 0, window = 0;
+  const int32_t* key_valid = nullptr;   // [B][nkeys]
+  float scale = 1.f;
+};
+int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st);
+
 // ---- misc (misc.hip) ----
 // batched 2-D transpose of bf16 [nz][rows][cols] (ld_in) -> [nz][cols][rows] (ld_out); zero-fills
 // output columns in [rows, rows_pad)

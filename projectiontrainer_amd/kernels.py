@@ -126,3 +126,21 @@ def fill_normal_(t, seed, std=0.02, mean=0.0):
     check(L.lib().ptk_fill_normal_bf16(ptr(t), t.numel(), seed & (2**64 - 1), std, mean, L.stream_ptr(t.device)),
           "fill_normal")
     return t
+
+
+def flash_attn(Q, K, V, O, *, rows, nkeys, head_dim, ldq, ldk, ldo, batch, batch_inner=1, zdiv=1,
+               strides=(0, 0, 0, 0, 0, 0), qmap=(0, 0, 0, 0), omap=(0, 0, 0, 0), qdiv=1, causal=False,
+               window=0, key_valid=None, scale=1.0, lse=None):
+    """Flash attention forward (ptk_flash_attn_fwd); O written in place."""
+    _require_cuda(Q, K, V, O)
+    d = L.FlashDesc()
+    d.Q, d.K, d.V, d.O, d.lse = ptr(Q), ptr(K), ptr(V), ptr(O), ptr(lse)
+    d.rows, d.nkeys, d.head_dim = rows, nkeys, head_dim
+    d.ldq, d.ldk, d.ldo = ldq, ldk, ldo
+    d.batch, d.batch_inner, d.zdiv = batch, batch_inner, zdiv
+    d.sQ0, d.sQ1, d.sK0, d.sK1, d.sO0, d.sO1 = strides
+    d.qmap, d.omap = L.RowMap(*qmap), L.RowMap(*omap)
+    d.qdiv, d.causal, d.window = qdiv, int(causal), window
+    d.key_valid, d.scale = ptr(key_valid), scale
+    check(L.lib().ptk_flash_attn_fwd(d, L.stream_ptr(Q.device)), "flash_attn_fwd")
+    return O

@@ -240,3 +240,64 @@ def test_gemm_big_vs_small_all_epilogues(gpu):
             L.lib().ptk_gemm_force_small_tiles(0)
     for k in outs[0]:
         torch.testing.assert_close(outs[0][k].float(), outs[1][k].float(), rtol=1e-2, atol=1e-3, msg=k)
+
+
+def _attn_ref(q, k, v, mask, scale):
+    s = (q.float() @ k.float().transpose(-1, -2)) * scale
+    s = s.masked_fill(~mask, float("-inf"))
+    m = s.amax(-1, keepdim=True)
+    p = torch.exp(s - m)
+    l = p.sum(-1, keepdim=True)
+    return (p / l) @ v.float(), (m + torch.log(l)).squeeze(-1)
+
+
+@pytest.mark.parametrize("N", [576, 196, 16])
+def test_flash_fwd_siglip_layout(gpu, N):
+    """Non-causal, head_dim 64, Q/K/V read in place from the fused [B*N, 3D] qkv buffer."""
+    Kn, L = _k()
+    B, H, hd = 2, 4, 64
+    D = H * hd
+    qkv = rnd(B * N, 3 * D, dev=gpu, seed=40)
+    O = torch.zeros(B * N, D, dtype=torch.bfloat16, device=gpu)
+    Kn.flash_attn(qkv, qkv[:, D:], qkv[:, 2 * D:], O, rows=N, nkeys=N, head_dim=hd, ldq=3 * D, ldk=3 * D, ldo=D,
+                  batch=B * H, batch_inner=H, zdiv=H, strides=(N * 3 * D, hd, N * 3 * D, hd, N * D, hd),
+                  scale=hd ** -0.5)
+    x = qkv.float().view(B, N, 3, H, hd)
+    q, k, v = (x[:, :, i].transpose(1, 2) for i in range(3))
+    ref, _ = _attn_ref(q, k, v, torch.ones(N, N, dtype=torch.bool, device=gpu), hd ** -0.5)
+    ref = ref.transpose(1, 2).reshape(B * N, D)
+    torch.testing.assert_close(O.float(), ref, rtol=2e-2, atol=2e-2)
+
+
+@pytest.mark.parametrize("Hkv,G,window", [(1, 4, 0), (1, 4, 100), (2, 2, 64)])
+def test_flash_fwd_gemma_layout(gpu, Hkv, G, window):
+    """Causal GQA, head_dim 256, key padding, sliding window, token-major O via row map, LSE."""
+    Kn, L = _k()
+    B, S, hd = 2, 320, 256
+    Hq = Hkv * G
+    Q = rnd(B, Hkv, S, G, hd, dev=gpu, seed=41)
+    Kt = rnd(B, Hkv, S, hd, dev=gpu, seed=42)
+    Vt = rnd(B, Hkv, S, hd, dev=gpu, seed=43)
+    kv = torch.ones(B, S, dtype=torch.int32, device=gpu)
+    kv[0, 200:215] = 0
+    kv[1, 290:] = 0
+    O = torch.zeros(B * S, Hq * hd, dtype=torch.bfloat16, device=gpu)
+    lse = torch.zeros(B * Hkv, S * G, dtype=torch.float32, device=gpu)
+    scale = 256 ** -0.5
+    Kn.flash_attn(Q, Kt, Vt, O, lse=lse, rows=S * G, nkeys=S, head_dim=hd, ldq=hd, ldk=hd, ldo=hd,
+                  batch=B * Hkv, batch_inner=Hkv, zdiv=Hkv,
+                  strides=(Hkv * S * G * hd, S * G * hd, Hkv * S * hd, S * hd, S * Hq * hd, G * hd),
+                  omap=(G, 0, Hq, 0), qdiv=G, causal=True, window=window, key_valid=kv, scale=scale)
+    q = Q.float().permute(0, 1, 3, 2, 4).reshape(B, Hq, S, hd)          # head h = kvh*G + j
+    k = Kt.float().repeat_interleave(G, dim=1)
+    v = Vt.float().repeat_interleave(G, dim=1)
+    i = torch.arange(S, device=gpu)
+    m = i[None, :] <= i[:, None]
+    if window:
+        m = m & (i[None, :] > i[:, None] - window)
+    m = m[None, None] & kv.bool()[:, None, None, :]
+    ref, lref = _attn_ref(q, k, v, m, scale)
+    ref = ref.transpose(1, 2).reshape(B * S, Hq * hd)
+    torch.testing.assert_close(O.float(), ref, rtol=2e-2, atol=2e-2)
+    lg = lse.view(B, Hkv, S, G).permute(0, 1, 3, 2).reshape(B, Hq, S)
+    torch.testing.assert_close(lg, lref, rtol=1e-3, atol=1e-3)
