@@ -1,0 +1,92 @@
+"""Process-group plumbing: one process per GPU, torch.distributed over RCCL
+("nccl" backend on ROCm) on the GPU box, gloo for CPU tests.
+
+`DistState` exposes the subset of `accelerate.Accelerator` the reference's
+trainer touches (`Stage1/accelerator_setup.py:7-54`):
+`device, is_main_process, process_index, num_processes,
+gradient_accumulation_steps, sync_gradients, gather`.
+"""
+from __future__ import annotations
+
+import os
+
+import torch
+import torch.distributed as dist
+
+
+class DistState:
+    def __init__(self, gradient_accumulation_steps: int = 1, backend: str | None = None, device=None):
+        self.gradient_accumulation_steps = gradient_accumulation_steps
+        self.sync_gradients = True          # Stage 1 never enters accumulate()
+        world = int(os.environ.get("WORLD_SIZE", "1"))
+        if world > 1 and not dist.is_initialized():
+            if backend is None:
+                backend = "nccl" if torch.cuda.is_available() else "gloo"
+            local = int(os.environ.get("LOCAL_RANK", "0"))
+            if backend == "nccl":
+                torch.cuda.set_device(local)
+                dist.init_process_group(backend, device_id=torch.device("cuda", local))
+            else:
+                dist.init_process_group(backend)
+        self.initialized = dist.is_initialized()
+        self.num_processes = dist.get_world_size() if self.initialized else 1
+        self.process_index = dist.get_rank() if self.initialized else 0
+        if device is None:
+            device = (torch.device("cuda", int(os.environ.get("LOCAL_RANK", "0"))) if torch.cuda.is_available()
+                      else torch.device("cpu"))
+        self.device = torch.device(device)
+
+    @property
+    def is_main_process(self) -> bool:
+        return self.process_index == 0
+
+    def all_reduce_sum_(self, t):
+        if self.num_processes > 1:
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        return t
+
+    def gather(self, t):
+        """accelerator.gather for a scalar / 1-D tensor (all_gather_into_tensor)."""
+        t = t.reshape(-1)
+        if self.num_processes == 1:
+            return t
+        out = torch.empty(self.num_processes * t.numel(), dtype=t.dtype, device=t.device)
+        dist.all_gather_into_tensor(out, t.contiguous())
+        return out
+
+    def wait_for_everyone(self):
+        if self.num_processes > 1:
+            dist.barrier()
+
+
+def from_accelerator(acc) -> DistState:
+    """Wrap an accelerate.Accelerator (process group already initialised by it)."""
+    st = DistState.__new__(DistState)
+    st.gradient_accumulation_steps = getattr(acc, "gradient_accumulation_steps", 1)
+    st.sync_gradients = True
+    st.initialized = dist.is_initialized()
+    st.num_processes = acc.num_processes
+    st.process_index = acc.process_index
+    st.device = torch.device(acc.device)
+    st.all_reduce_sum_ = DistState.all_reduce_sum_.__get__(st)
+    return st
+
+
+def shard_batches(n_items: int, batch_size: int, rank: int, world: int, epoch: int, seed: int = 0,
+                  shuffle: bool = True):
+    """Index batches for this rank: a seeded permutation cut into batches of
+    `batch_size`, batch i going to rank i % world (accelerate's prepared
+    DataLoader dispatch; the last incomplete batch is kept as in DataLoader)."""
+    g = torch.Generator().manual_seed(seed + epoch)
+    order = torch.randperm(n_items, generator=g) if shuffle else torch.arange(n_items)
+    batches = [order[i:i + batch_size] for i in range(0, n_items, batch_size)]
+    return [b for i, b in enumerate(batches) if i % world == rank]
+
+
+def allreduce_grads_(flat_grad, world: int, group=None):
+    """DDP gradient semantics (projector_trainer.py:237 -> DDP reducer): sum the
+    flat fp32 grads over ranks in ONE collective; the 1/world average is folded
+    into the fused clip+AdamW kernel (grad_scale), so this returns the scale."""
+    if world > 1:
+        dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
+    return 1.0 / world

@@ -1,0 +1,168 @@
+"""ProjectionTrainerStage1 — the reference's Stage-1 trainer API
+(`Stage1/projector_trainer.py:18-521`) running its step on libptk.
+
+Same constructor signature, `.train()` and `.save_projection(epoch, is_best)`.
+What changes underneath:
+  * the frozen towers run as HIP kernel sequences (`SiglipVisionTower`,
+    `Gemma3CausalLM`); HF `SiglipModel` / `Gemma3ForCausalLM` instances passed
+    in are converted once (weights re-laid out for the kernels);
+  * one process per GPU with torch.distributed/RCCL instead of accelerate+DDP:
+    batches are dealt round-robin per rank, the projector's flat fp32 grads
+    are all-reduced once per step, clip + AdamW is one fused kernel;
+  * the arithmetic quirks of the reference are kept on purpose:
+    loss / gas twice before backward, an optimizer step on every micro-batch,
+    the scheduler advanced `num_processes` times per step with its horizon
+    computed from the unsharded loader, cosine lambda without a clamp;
+  * checkpoints are byte-compatible: `torch.save(state_dict)` with keys
+    model.0/2.{weight,bias} + projector_config.json (`:455-521`).
+Validation by `generate` (`:292-448`) is out of scope; a validation loss is
+computed when val_dataset is given.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import math
+import os
+import time
+
+import torch
+
+from . import dist as D
+from .gemma3 import Gemma3CausalLM
+from .projectors import MLPProjector
+from .siglip import SiglipVisionTower
+from .stage1 import Stage1Engine, cosine_lambda
+
+logger = logging.getLogger(__name__)
+
+
+def _collate(items):
+    return {k: torch.stack([it[k] for it in items]) for k in items[0]}
+
+
+class ProjectionTrainerStage1:
+    def __init__(self, accelerator, vision_encoder, language_model, projection_layer, processor, tokenizer,
+                 train_dataset, val_dataset=None, output_dir="./trained_projection_stage1", batch_size=8,
+                 learning_rate=1e-4, weight_decay=0.01, num_epochs=10, gradient_accumulation_steps=1,
+                 warmup_ratio=0.0, wandb_project="xray_projection_training", save_every_n_epochs=0,
+                 log_fn=None, seed=0):
+        if accelerator is None:
+            accelerator = D.DistState(gradient_accumulation_steps)
+        elif not isinstance(accelerator, D.DistState):
+            accelerator = D.from_accelerator(accelerator)
+        self.accelerator = acc = accelerator
+        self.device = acc.device
+        self.output_dir, self.num_epochs, self.batch_size = output_dir, num_epochs, batch_size
+        self.save_every_n_epochs, self.wandb_project = save_every_n_epochs, wandb_project
+        self.train_dataset, self.val_dataset = train_dataset, val_dataset
+        self.processor, self.tokenizer = processor, tokenizer
+        self.log_fn = log_fn
+        self.seed = seed
+        if acc.is_main_process:
+            os.makedirs(output_dir, exist_ok=True)
+
+        # frozen towers on the HIP device
+        self.vision_encoder = vision_encoder if isinstance(vision_encoder, SiglipVisionTower) \
+            else SiglipVisionTower.from_hf(vision_encoder, self.device)
+        self.language_model = language_model if isinstance(language_model, Gemma3CausalLM) \
+            else Gemma3CausalLM.from_hf(language_model, self.device)
+        if not isinstance(projection_layer, MLPProjector):
+            sd = projection_layer.state_dict()
+            p = MLPProjector(sd["model.0.weight"].shape[1], sd["model.2.weight"].shape[0])
+            p.load_state_dict({k: v.detach().float().cpu() for k, v in sd.items()})
+            projection_layer = p
+        self.projection_layer = projection_layer.to(self.device)
+        pad = getattr(tokenizer, "pad_token_id", None)
+        self.pad_token_id = 0 if pad is None else pad
+
+        # schedule horizon from the UNSHARDED loader (projector_trainer.py:82-95, F7)
+        n_batches = math.ceil(len(train_dataset) / batch_size)
+        self.max_train_steps = num_epochs * math.ceil(n_batches / gradient_accumulation_steps)
+        self.num_warmup_steps = math.ceil(warmup_ratio * self.max_train_steps)
+        self.engine = Stage1Engine(self.vision_encoder, self.language_model, self.projection_layer,
+                                   learning_rate=learning_rate, weight_decay=weight_decay,
+                                   gradient_accumulation_steps=acc.gradient_accumulation_steps,
+                                   warmup_steps=self.num_warmup_steps, total_steps=self.max_train_steps,
+                                   world_size=acc.num_processes)
+        self.global_step = 0
+
+    # ------------------------------------------------------------------ data
+    def _batches(self, dataset, epoch, shuffle=True):
+        acc = self.accelerator
+        for idx in D.shard_batches(len(dataset), self.batch_size, acc.process_index, acc.num_processes, epoch,
+                                   self.seed, shuffle):
+            b = _collate([dataset[int(i)] for i in idx])
+            yield {k: v.to(self.device, non_blocking=True) for k, v in b.items()}
+
+    def _log(self, d, step):
+        if self.accelerator.is_main_process:
+            if self.log_fn is not None:
+                self.log_fn(d, step)
+            else:
+                logger.info("step %d %s", step, d)
+
+    # ------------------------------------------------------------------ train
+    def train_step(self, batch):
+        """One reference iteration (projector_trainer.py:152-271); returns the gathered mean loss."""
+        loss = self.engine.step(batch["pixel_values"], batch["token_ids"], batch["labels"])
+        self.global_step += 1
+        return self.accelerator.gather(loss).mean()
+
+    def train(self):
+        acc = self.accelerator
+        logger.info("Process %d: Stage 1 training for %d epochs on %s", acc.process_index, self.num_epochs,
+                    self.device)
+        best_val = float("inf")
+        for epoch in range(self.num_epochs):
+            epoch_loss, n = 0.0, 0
+            for batch in self._batches(self.train_dataset, epoch):
+                avg = float(self.train_step(batch))          # host sync, as the reference's .item()
+                epoch_loss += avg
+                n += 1
+                self._log({"train/batch_loss": avg, "train/learning_rate": self.engine.last_lr,
+                           "step": self.global_step}, self.global_step)
+            n_opt = math.ceil(math.ceil(len(self.train_dataset) / self.batch_size) /
+                              max(1, acc.gradient_accumulation_steps))
+            self._log({"train/epoch_loss": epoch_loss / max(1, n_opt), "epoch": epoch + 1}, self.global_step)
+            if acc.is_main_process and self.save_every_n_epochs > 0 and (epoch + 1) % self.save_every_n_epochs == 0:
+                self.save_projection(epoch=epoch + 1)
+            if self.val_dataset is not None:
+                vl = self.validation_loss()
+                self._log({"validation/loss": vl, "epoch": epoch + 1}, self.global_step)
+                if vl < best_val:
+                    best_val = vl
+                    self.save_projection(is_best=True)
+        logger.info("Stage 1 Training finished.")
+        self.save_projection(epoch=self.num_epochs)
+
+    def validation_loss(self):
+        """Mean LM loss over the validation set (no optimizer step; grads are discarded)."""
+        tot, n = torch.zeros(1, device=self.device), 0
+        for batch in self._batches(self.val_dataset, 0, shuffle=False):
+            tot += self.engine.forward_backward(batch["pixel_values"], batch["token_ids"], batch["labels"])
+            n += 1
+        cnt = torch.tensor([float(n)], device=self.device)
+        self.accelerator.all_reduce_sum_(tot)
+        self.accelerator.all_reduce_sum_(cnt)
+        return float(tot / cnt.clamp(min=1))
+
+    def save_projection(self, epoch=None, is_best=False):
+        """projector_{best,epoch_N,final}.bin + projector_config.json (projector_trainer.py:455-521)."""
+        if not self.accelerator.is_main_process:
+            return
+        if is_best:
+            name = "projector_best.bin"
+        elif epoch is not None:
+            name = f"projector_epoch_{epoch}.bin"
+        else:
+            name = "projector_final.bin"
+        path = os.path.join(self.output_dir, name)
+        sd = {k: v.detach().cpu().clone() for k, v in self.projection_layer.state_dict().items()}
+        torch.save(sd, path)
+        cfg = {"vision_dim": self.projection_layer.model[0].in_features,
+               "llm_dim": self.projection_layer.model[2].out_features}
+        with open(os.path.join(self.output_dir, "projector_config.json"), "w") as f:
+            json.dump(cfg, f, indent=4)
+        logger.info("Projection layer state dict saved to %s", path)
+        return path

@@ -20,11 +20,11 @@ from __future__ import annotations
 import math
 
 import torch
-import torch.distributed as dist
 
 from . import _lib as L
 from . import kernels as K
 from .config import Stage1Config
+from .dist import allreduce_grads_
 from .gemma3 import Gemma3CausalLM
 from .projectors import MLPProjector
 from .siglip import SiglipVisionTower
@@ -101,14 +101,13 @@ class Stage1Engine:
 
     def optimizer_step(self):
         """DDP all-reduce (sum; 1/W folded into the update), clip + AdamW, schedule."""
-        if self.world > 1:
-            dist.all_reduce(self.proj.flat_grad, op=dist.ReduceOp.SUM, group=self.pg)
+        grad_scale = allreduce_grads_(self.proj.flat_grad, self.world, self.pg)
         lr = self.lr0 * cosine_lambda(self.sched_step, self.warmup, self.total)
         self.opt_step += 1
         b1, b2 = self.betas
         L.check(L.lib().ptk_clip_adamw(self.proj.flat.data_ptr(), self.proj.flat_grad.data_ptr(),
                                        self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.proj.flat.numel(),
-                                       1.0 / self.world, self.max_norm, lr, b1, b2, self.eps, self.wd, self.opt_step,
+                                       grad_scale, self.max_norm, lr, b1, b2, self.eps, self.wd, self.opt_step,
                                        self._partial.data_ptr(), self.grad_norm.data_ptr(),
                                        L.stream_ptr(self.device)), "clip_adamw")
         self.proj.refresh_shadows()
