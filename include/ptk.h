@@ -124,6 +124,23 @@ typedef struct {
 } ptk_flash_desc;
 int ptk_flash_attn_fwd(const ptk_flash_desc* d, void* stream);
 
+/* Flash attention backward (dQ, dK, dV; bf16).  Q/dO/dQ [batch][rows][hd], K/V/dK/dV
+ * [batch][nkeys][hd], lse/delta [batch][rows] (delta is scratch); O = forward output
+ * addressed like ptk_flash_desc.O (batch_inner split, omap, ldo).  rows, nkeys % 64 == 0. */
+typedef struct {
+  const void* Q; const void* K; const void* V; const void* O; const void* dO;
+  const float* lse; float* delta;
+  void* dQ; void* dK; void* dV;
+  int rows, nkeys, head_dim;
+  int batch, batch_inner, zdiv;
+  int64_t ldo, sO0, sO1;
+  ptk_rowmap omap;
+  int qdiv, causal, window;
+  const int32_t* key_valid;
+  float scale;
+} ptk_flash_bwd_desc;
+int ptk_flash_attn_bwd(const ptk_flash_bwd_desc* d, void* stream);
+
 /* ------------------------------------------------------------------------ *
  * SigLIP vision tower, frozen forward                                      *
  * replaces vision_tower(pixel_values=...).last_hidden_state                *

@@ -45,6 +45,16 @@ class FlashDesc(C.Structure):
                 ("scale", c_float)]
 
 
+class FlashBwdDesc(C.Structure):
+    _fields_ = [("Q", c_void_p), ("K", c_void_p), ("V", c_void_p), ("O", c_void_p), ("dO", c_void_p),
+                ("lse", c_void_p), ("delta", c_void_p), ("dQ", c_void_p), ("dK", c_void_p), ("dV", c_void_p),
+                ("rows", c_int), ("nkeys", c_int), ("head_dim", c_int),
+                ("batch", c_int), ("batch_inner", c_int), ("zdiv", c_int),
+                ("ldo", c_int64), ("sO0", c_int64), ("sO1", c_int64), ("omap", RowMap),
+                ("qdiv", c_int), ("causal", c_int), ("window", c_int), ("key_valid", c_void_p),
+                ("scale", c_float)]
+
+
 class SiglipConfigC(C.Structure):
     _fields_ = [("image_size", c_int), ("patch_size", c_int), ("channels", c_int), ("hidden", c_int),
                 ("heads", c_int), ("intermediate", c_int), ("layers", c_int), ("eps", c_float)]
@@ -112,6 +122,7 @@ SIGNATURES = {
     "ptk_gemm_force_small_tiles": (c_int, [c_int]),
     "ptk_gemm_timer_read": (c_int, [c_int, C.POINTER(C.c_double), C.POINTER(c_int)]),
     "ptk_flash_attn_fwd": (c_int, [C.POINTER(FlashDesc), c_void_p]),
+    "ptk_flash_attn_bwd": (c_int, [C.POINTER(FlashBwdDesc), c_void_p]),
     "ptk_siglip_workspace_bytes": (c_size_t, [C.POINTER(SiglipConfigC), c_int]),
     "ptk_siglip_fwd": (c_int, [C.POINTER(SiglipConfigC), C.POINTER(SiglipWeightsC), c_int, c_void_p, c_void_p,
                                c_void_p, c_size_t, c_void_p]),

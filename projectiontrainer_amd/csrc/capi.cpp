@@ -116,6 +116,20 @@ int ptk_flash_attn_fwd(const ptk_flash_desc* d, void* stream) {
   return launch_attn_fwd(a, d->batch > 0 ? d->batch : 1, ST);
 }
 
+int ptk_flash_attn_bwd(const ptk_flash_bwd_desc* d, void* stream) {
+  if (!d) return set_error("flash_bwd: null desc");
+  FlashBwdArgs a;
+  a.Q = (const bf16_t*)d->Q; a.K = (const bf16_t*)d->K; a.V = (const bf16_t*)d->V; a.O = (const bf16_t*)d->O;
+  a.dO = (const bf16_t*)d->dO; a.lse = d->lse; a.delta = d->delta;
+  a.dQ = (bf16_t*)d->dQ; a.dK = (bf16_t*)d->dK; a.dV = (bf16_t*)d->dV;
+  a.rows = d->rows; a.nkeys = d->nkeys; a.D = d->head_dim;
+  a.zin = d->batch_inner > 0 ? d->batch_inner : 1; a.zdiv = d->zdiv > 0 ? d->zdiv : 1;
+  a.ldo = d->ldo; a.sO0 = d->sO0; a.sO1 = d->sO1; a.omap = to_map(d->omap);
+  a.qdiv = d->qdiv > 0 ? d->qdiv : 1; a.causal = d->causal; a.window = d->window;
+  a.key_valid = d->key_valid; a.scale = d->scale;
+  return launch_attn_bwd(a, d->batch > 0 ? d->batch : 1, ST);
+}
+
 // ---------------------------------------------------------------- projector
 int ptk_projector_fwd(const ptk_projector* p, int rows, const void* x, void* a, void* h, float* out,
                       ptk_rowmap out_map, int64_t ld_out, int round_bf16, void* stream) {

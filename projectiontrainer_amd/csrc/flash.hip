@@ -202,6 +202,339 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
   if (a.lse && g == 0) a.lse[(long)z * a.rows + qrow] = (m_run + log2f(l_run)) * 0.6931471805599453f;
 }
 
+// ============================================================================ backward
+// FA2-style split without atomics:
+//   delta[r] = sum_d dO[r][d] * O[r][d]
+//   dQ kernel  (per 128 query rows, 8 waves x 16 rows, K/V tiles streamed):
+//     S^T = K Q^T, dP^T = V dO^T, P^T = exp(S^T*scale - LSE), dS^T = P^T (dP^T - delta)
+//     dQ^T += K^T dS^T            (A = K^T by ds_read_b64_tr_b16, B = dS^T from registers)
+//   dKV kernel (per 64 keys; wave = 16 keys x half of each 64-row query chunk):
+//     S = Q K^T, dP = dO V^T (keys on the lane), P, dS
+//     dV^T += dO^T P, dK^T += Q^T dS   (A = dO^T / Q^T by tr reads, B = P / dS from registers)
+//   then dQ *= scale, dK *= scale.  GQA: the query rows of all G heads of a kv head are one
+//   z-batch, so dK/dV sum over the group for free.
+template <int D>
+__global__ void __launch_bounds__(256) attn_delta_kernel(FlashBwdArgs a, int nz) {
+  constexpr int EPL = D / 64;
+  const int lane = threadIdx.x & 63;
+  const long gr = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (gr >= (long)nz * a.rows) return;
+  const long z = gr / a.rows;
+  const int r = (int)(gr - z * a.rows);
+  const int z0 = (int)(z / a.zin), z1 = (int)(z - (long)z0 * a.zin);
+  const bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, r) * a.ldo + lane * EPL;
+  const bf16_t* dp = a.dO + gr * D + lane * EPL;
+  float s = 0.f;
+#pragma unroll
+  for (int e = 0; e < EPL; ++e) s += bf2f(op[e]) * bf2f(dp[e]);
+  s = warp_sum(s);
+  if (lane == 0) a.delta[gr] = s;
+}
+
+template <int D>
+__global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
+  constexpr int CPR = D / 8;
+  constexpr int TILE_BYTES = 64 * D * 2;
+  constexpr int KS = D / 32;
+  constexpr int DS = D / 16;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];   // K0 V0 K1 V1
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const long z = blockIdx.y;
+  const int r0 = blockIdx.x * 128;
+  const bf16_t* K = a.K + z * (long)a.nkeys * D;
+  const bf16_t* V = a.V + z * (long)a.nkeys * D;
+  const long b = z / a.zdiv;
+  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
+  int k_hi = a.nkeys, k_lo = 0;
+  if (a.causal) {
+    k_hi = min(k_hi, pos_hi + 1);
+    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
+  }
+  const int t_lo = k_lo / 64, t_hi = (k_hi + 63) / 64;
+
+  const int qrow = r0 + wave * 16 + c16;
+  const int qrow_c = min(qrow, a.rows - 1);
+  const long qoff = (z * a.rows + qrow_c) * (long)D + 8 * g;
+  bf16x8_t qf[KS], df[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = *reinterpret_cast<const bf16x8_t*>(a.Q + qoff + 32 * ks);
+    df[ks] = *reinterpret_cast<const bf16x8_t*>(a.dO + qoff + 32 * ks);
+  }
+  const float L2E = 1.4426950408889634f;
+  const float lse2 = a.lse[z * a.rows + qrow_c] * L2E;
+  const float dlt = a.delta[z * a.rows + qrow_c];
+  const int qpos = qrow_c / a.qdiv;
+  const float sl2 = a.scale * L2E;
+
+  constexpr int ROWS_PER_INST = 64 / CPR;
+  constexpr int INSTS = CPR / 8;
+  auto stage = [&](int t, int buf) {
+    char* kb = smem + buf * 2 * TILE_BYTES;
+    char* vb = kb + TILE_BYTES;
+#pragma unroll
+    for (int j = 0; j < INSTS; ++j) {
+      const int inst = wave * INSTS + j;
+      const int row = inst * ROWS_PER_INST + lane / CPR;
+      const int pch = lane % CPR;
+      const int key = min(t * 64 + row, a.nkeys - 1);
+      const int lch = pch ^ swz_k<D>(row);
+      fa_glds16(K + (long)key * D + 8 * lch, kb + inst * 1024);
+      fa_glds16(V + (long)key * D + 8 * lch, vb + inst * 1024);
+    }
+  };
+
+  f32x4_t acc[DS];
+#pragma unroll
+  for (int i = 0; i < DS; ++i) acc[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  if (t_lo < t_hi) stage(t_lo, 0);
+  for (int t = t_lo; t < t_hi; ++t) {
+    const int buf = (t - t_lo) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (t + 1 < t_hi) stage(t + 1, buf ^ 1);
+    const char* kb = smem + buf * 2 * TILE_BYTES;
+    const char* vb = kb + TILE_BYTES;
+    f32x4_t s[4], dp[4];
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms) {
+      s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      dp[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      const int row = ms * 16 + c16;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int ch = (ks * 4 + g) ^ swz_k<D>(row);
+        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + row * (D * 2) + ch * 16);
+        const bf16x8_t vf = *reinterpret_cast<const bf16x8_t*>(vb + row * (D * 2) + ch * 16);
+        s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
+        dp[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[ks], dp[ms], 0, 0, 0);
+      }
+    }
+    bf16x8_t dsf[2];
+#pragma unroll
+    for (int ms = 0; ms < 4; ++ms) {
+      const int kbase = t * 64 + ms * 16 + 4 * g;
+      int kv[4] = {1, 1, 1, 1};
+      if (a.key_valid) {
+        const int4 v4 = *reinterpret_cast<const int4*>(a.key_valid + b * a.nkeys + min(kbase, a.nkeys - 4));
+        kv[0] = v4.x; kv[1] = v4.y; kv[2] = v4.z; kv[3] = v4.w;
+      }
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int key = kbase + j;
+        bool ok = key < a.nkeys && kv[j] != 0;
+        if (a.causal) ok = ok && key <= qpos;
+        if (a.window > 0) ok = ok && key > qpos - a.window;
+        const float p = ok ? exp2f(s[ms][j] * sl2 - lse2) : 0.f;
+        const float d = bfround(p) * (dp[ms][j] - dlt);
+        dsf[ms >> 1][(ms & 1) * 4 + j] = (short)f2bf(d);
+      }
+    }
+    const int q4 = c16 >> 2, p4 = c16 & 3;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+#pragma unroll
+      for (int st = 0; st < 2; ++st) {
+        bf16x8_t kt;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int row = (2 * st + hh) * 16 + 4 * g + q4;
+          const int ch = (2 * ds + (p4 >> 1)) ^ swz_k<D>(row);
+          const char* addr = kb + row * (D * 2) + ch * 16 + 8 * (p4 & 1);
+          const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
+          kt[4 * hh + 0] = r[0]; kt[4 * hh + 1] = r[1]; kt[4 * hh + 2] = r[2]; kt[4 * hh + 3] = r[3];
+        }
+        acc[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, dsf[st], acc[ds], 0, 0, 0);
+      }
+    }
+  }
+  if (qrow >= a.rows) return;
+  bf16_t* op = a.dQ + (z * a.rows + qrow) * (long)D + 4 * g;
+#pragma unroll
+  for (int ds = 0; ds < DS; ++ds) {
+    u16x4_t u;
+    u[0] = f2bf(acc[ds][0] * a.scale); u[1] = f2bf(acc[ds][1] * a.scale);
+    u[2] = f2bf(acc[ds][2] * a.scale); u[3] = f2bf(acc[ds][3] * a.scale);
+    *reinterpret_cast<u16x4_t*>(op + 16 * ds) = u;
+  }
+}
+
+template <int D>
+__global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
+  constexpr int CPR = D / 8;
+  constexpr int TILE_BYTES = 64 * D * 2;     // 64 query rows of Q or dO
+  constexpr int KS = D / 32;
+  constexpr int DS = D / 16;
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];   // Q0 dO0 Q1 dO1
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  const int kw = wave & 3, qh = wave >> 2;   // 16 keys per kw; q sub-tiles {2qh, 2qh+1} of each chunk
+  const long z = blockIdx.y;
+  const int k0 = blockIdx.x * 64;
+  const int key = k0 + kw * 16 + c16;
+  const int key_c = min(key, a.nkeys - 1);
+  const long b = z / a.zdiv;
+  const bf16_t* Qz = a.Q + z * (long)a.rows * D;
+  const bf16_t* dOz = a.dO + z * (long)a.rows * D;
+  bf16x8_t kf[KS], vf[KS];
+  {
+    const long ko = (z * a.nkeys + key_c) * (long)D + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[ks] = *reinterpret_cast<const bf16x8_t*>(a.K + ko + 32 * ks);
+      vf[ks] = *reinterpret_cast<const bf16x8_t*>(a.V + ko + 32 * ks);
+    }
+  }
+  const bool key_ok = key < a.nkeys && (!a.key_valid || a.key_valid[b * a.nkeys + key_c] != 0);
+  // query rows that can see this key block
+  int r_lo = 0, r_hi = a.rows;
+  if (a.causal) {
+    r_lo = min(a.rows, k0 * a.qdiv);
+    if (a.window > 0) r_hi = min(a.rows, (k0 + 64 + a.window - 1) * a.qdiv);
+  }
+  const int c_lo = r_lo / 64, c_hi = (r_hi + 63) / 64;
+  const float L2E = 1.4426950408889634f;
+  const float sl2 = a.scale * L2E;
+
+  constexpr int ROWS_PER_INST = 64 / CPR;
+  constexpr int INSTS = CPR / 8;
+  auto stage = [&](int c, int buf) {
+    char* qb = smem + buf * 2 * TILE_BYTES;
+    char* ob = qb + TILE_BYTES;
+#pragma unroll
+    for (int j = 0; j < INSTS; ++j) {
+      const int inst = wave * INSTS + j;
+      const int row = inst * ROWS_PER_INST + lane / CPR;
+      const int pch = lane % CPR;
+      const int qr = min(c * 64 + row, a.rows - 1);
+      const int lch = pch ^ swz_k<D>(row);
+      fa_glds16(Qz + (long)qr * D + 8 * lch, qb + inst * 1024);
+      fa_glds16(dOz + (long)qr * D + 8 * lch, ob + inst * 1024);
+    }
+  };
+
+  f32x4_t dv[DS], dk[DS];
+#pragma unroll
+  for (int i = 0; i < DS; ++i) {
+    dv[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    dk[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  }
+  if (c_lo < c_hi) stage(c_lo, 0);
+  for (int c = c_lo; c < c_hi; ++c) {
+    const int buf = (c - c_lo) & 1;
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (c + 1 < c_hi) stage(c + 1, buf ^ 1);
+    const char* qb = smem + buf * 2 * TILE_BYTES;
+    const char* ob = qb + TILE_BYTES;
+    bf16x8_t pf, dsf;
+#pragma unroll
+    for (int hh = 0; hh < 2; ++hh) {
+      const int qt = 2 * qh + hh;
+      f32x4_t s = (f32x4_t){0.f, 0.f, 0.f, 0.f}, dp = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      const int row = qt * 16 + c16;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int ch = (ks * 4 + g) ^ swz_k<D>(row);
+        const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(qb + row * (D * 2) + ch * 16);
+        const bf16x8_t oa = *reinterpret_cast<const bf16x8_t*>(ob + row * (D * 2) + ch * 16);
+        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ks], s, 0, 0, 0);
+        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[ks], dp, 0, 0, 0);
+      }
+      // C layout: row = query 4g + j of sub-tile qt, column = this lane's key
+      const int qbase = c * 64 + qt * 16 + 4 * g;
+      const float4 l4 = *reinterpret_cast<const float4*>(a.lse + z * a.rows + min(qbase, a.rows - 4));
+      const float4 d4 = *reinterpret_cast<const float4*>(a.delta + z * a.rows + min(qbase, a.rows - 4));
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int q = qbase + j;
+        const int pos = q / a.qdiv;
+        bool ok = key_ok && q < a.rows;
+        if (a.causal) ok = ok && key <= pos;
+        if (a.window > 0) ok = ok && key > pos - a.window;
+        const float p = ok ? exp2f(s[j] * sl2 - lv[j] * L2E) : 0.f;
+        const bf16_t pb = f2bf(p);
+        pf[4 * hh + j] = (short)pb;
+        dsf[4 * hh + j] = (short)f2bf(bf2f(pb) * (dp[j] - dl[j]));
+      }
+    }
+    // dV^T += dO^T P, dK^T += Q^T dS over this wave's 32 query rows (k order = tr-read rows)
+    const int q4 = c16 >> 2, p4 = c16 & 3;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      bf16x8_t ot, qt_;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int row = (2 * qh + hh) * 16 + 4 * g + q4;
+        const int ch = (2 * ds + (p4 >> 1)) ^ swz_k<D>(row);
+        const int off = row * (D * 2) + ch * 16 + 8 * (p4 & 1);
+        const s16x4_t ro = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(ob + off));
+        const s16x4_t rq = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(qb + off));
+        ot[4 * hh + 0] = ro[0]; ot[4 * hh + 1] = ro[1]; ot[4 * hh + 2] = ro[2]; ot[4 * hh + 3] = ro[3];
+        qt_[4 * hh + 0] = rq[0]; qt_[4 * hh + 1] = rq[1]; qt_[4 * hh + 2] = rq[2]; qt_[4 * hh + 3] = rq[3];
+      }
+      dv[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ot, pf, dv[ds], 0, 0, 0);
+      dk[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt_, dsf, dk[ds], 0, 0, 0);
+    }
+  }
+  // combine the two query halves (waves kw and kw+4) through LDS, then store
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  float* red = reinterpret_cast<float*>(smem) + kw * (2 * DS * 4 * 64);
+  if (qh == 1) {
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        red[((ds * 4 + j) * 64) + lane] = dv[ds][j];
+        red[((DS + ds) * 4 + j) * 64 + lane] = dk[ds][j];
+      }
+  }
+  __syncthreads();
+  if (qh == 1 || key >= a.nkeys) return;
+  bf16_t* dvp = a.dV + (z * a.nkeys + key) * (long)D + 4 * g;
+  bf16_t* dkp = a.dK + (z * a.nkeys + key) * (long)D + 4 * g;
+#pragma unroll
+  for (int ds = 0; ds < DS; ++ds) {
+    u16x4_t uv, uk;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uv[j] = f2bf(dv[ds][j] + red[((ds * 4 + j) * 64) + lane]);
+      uk[j] = f2bf((dk[ds][j] + red[((DS + ds) * 4 + j) * 64 + lane]) * a.scale);
+    }
+    *reinterpret_cast<u16x4_t*>(dvp + 16 * ds) = uv;
+    *reinterpret_cast<u16x4_t*>(dkp + 16 * ds) = uk;
+  }
+}
+
+int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st) {
+  if (a.rows <= 0 || nz <= 0) return 0;
+  if (a.rows % 64 || a.nkeys % 64) return set_error("attn_bwd: rows (%d) and keys (%d) must be multiples of 64",
+                                                   a.rows, a.nkeys);
+  if (a.ldo & 7) return set_error("attn_bwd: O stride must be a multiple of 8");
+  const dim3 gd((unsigned)((long)nz * a.rows / 4 + 1)), gq((unsigned)((a.rows + 127) / 128), (unsigned)nz),
+      gk((unsigned)(a.nkeys / 64), (unsigned)nz);
+  switch (a.D) {
+    case 64:
+      hipLaunchKernelGGL(attn_delta_kernel<64>, gd, dim3(256), 0, st, a, nz);
+      hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, gk, dim3(512), 0, st, a);
+      hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, gq, dim3(512), 0, st, a);
+      break;
+    case 256:
+      hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, a, nz);
+      hipLaunchKernelGGL(attn_bwd_dkv_kernel<256>, gk, dim3(512), 0, st, a);
+      hipLaunchKernelGGL(attn_bwd_dq_kernel<256>, gq, dim3(512), 0, st, a);
+      break;
+    default: return set_error("attn_bwd: head_dim %d unsupported (64, 256)", a.D);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : set_error("attn_bwd launch failed");
+}
+
 int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
   if (a.rows <= 0 || nz <= 0) return 0;
   if (a.nkeys < 4) return set_error("attn_fwd: nkeys must be >= 4");

@@ -176,7 +176,7 @@ PTK_DEV void epilogue(const GemmArgs& p, char* smem, int wave, int lane, f32x4_t
     // 8 lanes per row, each 4 h-columns; 8 rows per pass
     const int rr = lane >> 3, cg = lane & 7, q = cg >> 2, cc = (cg & 3) * 4;
     const long hc = col0 / 2 + q * 16 + cc;
-#pragma unroll 2
+#pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int lr = it * 8 + rr;
       const long r = row0 + lr;
@@ -189,7 +189,7 @@ PTK_DEV void epilogue(const GemmArgs& p, char* smem, int wave, int lane, f32x4_t
     // 16 lanes per row, each 4 columns; 4 rows per pass
     const int rr = lane >> 4, c4 = (lane & 15) * 4;
     const long c = col0 + c4;
-#pragma unroll 4
+#pragma unroll 8
     for (int it = 0; it < 16; ++it) {
       const int lr = it * 4 + rr;
       const long r = row0 + lr;

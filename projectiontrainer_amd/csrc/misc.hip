@@ -366,3 +366,24 @@ int launch_fill_normal_bf16(bf16_t* out, long n, uint64_t seed, float std, float
 }
 
 }  // namespace ptk
+
+namespace ptk {
+// out[i] = sum_s part[s][i]  (split-K partial reduction, fixed order: deterministic)
+__global__ void __launch_bounds__(256) sum_partials_kernel(const float* __restrict__ part, int nsplit, long n,
+                                                           float* __restrict__ out) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= n) return;
+  float4 acc = *reinterpret_cast<const float4*>(part + i);
+  for (int s = 1; s < nsplit; ++s) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (long)s * n + i);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  *reinterpret_cast<float4*>(out + i) = acc;
+}
+int launch_sum_partials(const float* part, int nsplit, long n, float* out, hipStream_t st) {
+  if (n % 4) return set_error("sum_partials: n %% 4");
+  hipLaunchKernelGGL(sum_partials_kernel, dim3((unsigned)((n / 4 + 255) / 256)), dim3(256), 0, st, part, nsplit, n,
+                     out);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("sum_partials launch failed");
+}
+}  // namespace ptk

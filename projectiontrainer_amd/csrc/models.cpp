@@ -46,6 +46,8 @@ float bfround_host(float f) {
   return f;
 }
 
+constexpr int LM_SPLITK = 8;   // split-K for the vocab-long lm_head dX GEMM (R x H output, K = V)
+
 #define CK(x) \
   do {        \
     if ((x)) return -1; \
@@ -84,14 +86,14 @@ SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
 // ------------------------------------------------------------------ Gemma3
 struct GemmaLayerSave {
   float *x2, *rstd_in, *rstd_ao, *rstd_pre, *rstd_dn, *rstd_q, *rstd_k;
-  bf16_t *qkv, *Q, *K, *V, *ao, *g, *u, *dn;
+  bf16_t *qkv, *Q, *K, *V, *O, *ao, *g, *u, *dn;
   float* lse;
 };
 struct GemmaWs {
   std::vector<float*> x;          // L+1 residual-stream snapshots
   std::vector<GemmaLayerSave> L;
   bf16_t *P, *xn, *O, *h, *Vt, *Kt, *Qt, *dqkv, *dgu, *dao, *dO, *dS, *dST, *PT, *dOT, *dQ, *dK, *dV, *xf, *logits;
-  float *S, *dtmp, *rstd_f, *row_loss, *dxf, *count, *gscale;
+  float *S, *dtmp, *rstd_f, *row_loss, *dxf, *dxf_part, *count, *gscale, *delta;
   int32_t* key_valid;
 };
 
@@ -117,29 +119,31 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp)
     s.K = bp.take<bf16_t>(Z * Sp * D);
     s.V = bp.take<bf16_t>(Z * Sp * D);
     s.lse = bp.take<float>(Z * SG);
+    s.O = bp.take<bf16_t>(M * Dq);
     s.ao = bp.take<bf16_t>(M * H);
     s.g = bp.take<bf16_t>(M * I);
     s.u = bp.take<bf16_t>(M * I);
     s.dn = bp.take<bf16_t>(M * H);
     w.L.push_back(s);
   }
-  w.P = bp.take<bf16_t>(Z * SG * Sp);
+  w.P = nullptr;
   w.xn = bp.take<bf16_t>(M * H);
-  w.O = bp.take<bf16_t>(M * Dq);
+  w.O = nullptr;
   w.h = bp.take<bf16_t>(M * I);
-  w.Vt = bp.take<bf16_t>(Z * D * Sp);
-  w.Kt = bp.take<bf16_t>(Z * D * Sp);
-  w.Qt = bp.take<bf16_t>(Z * D * SG);
-  w.S = bp.take<float>(Z * SG * Sp);
+  w.Vt = nullptr;
+  w.Kt = nullptr;
+  w.Qt = nullptr;
+  w.S = nullptr;
+  w.delta = bp.take<float>(Z * SG);
   w.dqkv = bp.take<bf16_t>(M * Dqkv);
   w.dgu = bp.take<bf16_t>(M * 2 * I);
   w.dtmp = bp.take<float>(M * H);
   w.dao = bp.take<bf16_t>(M * H);
   w.dO = bp.take<bf16_t>(Z * SG * D);
-  w.dS = bp.take<bf16_t>(Z * SG * Sp);
-  w.dST = bp.take<bf16_t>(Z * Sp * SG);
-  w.PT = bp.take<bf16_t>(Z * Sp * SG);
-  w.dOT = bp.take<bf16_t>(Z * D * SG);
+  w.dS = nullptr;
+  w.dST = nullptr;
+  w.PT = nullptr;
+  w.dOT = nullptr;
   w.dQ = bp.take<bf16_t>(Z * SG * D);
   w.dK = bp.take<bf16_t>(Z * Sp * D);
   w.dV = bp.take<bf16_t>(Z * Sp * D);
@@ -148,6 +152,7 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp)
   w.logits = bp.take<bf16_t>(R * V);
   w.row_loss = bp.take<float>(R);
   w.dxf = bp.take<float>(R * H);
+  w.dxf_part = bp.take<float>((long)LM_SPLITK * R * H);
   w.count = bp.take<float>(4);
   w.gscale = bp.take<float>(4);
   return w;
@@ -238,6 +243,7 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
   if (c->heads % c->kv_heads) return set_error("gemma3: heads %% kv_heads");
   if (Nv < 1) return set_error("gemma3: num_vision must be >= 1");
   if (ws_bytes < ptk_gemma3_workspace_bytes(c, B, T, Sp)) return set_error("gemma3: workspace too small");
+  if (c->vocab % (64 * LM_SPLITK)) return set_error("gemma3: vocab must be a multiple of %d", 64 * LM_SPLITK);
   const int H = c->hidden, I = c->inter, D = c->head_dim, Hq = c->heads, Hkv = c->kv_heads, G = Hq / Hkv;
   const int M = B * Sp, Dq = Hq * D, Dqkv = (Hq + 2 * Hkv) * D, R = B * T, V = c->vocab;
   const int Z = B * Hkv, SG = Sp * G, nl = c->layers;
@@ -265,7 +271,7 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
                               st));
     {  // causal / sliding-window GQA attention, flash; O token-major, LSE kept for the backward
       FlashArgs fa;
-      fa.Q = sv.Q; fa.K = sv.K; fa.V = sv.V; fa.O = w.O; fa.lse = sv.lse;
+      fa.Q = sv.Q; fa.K = sv.K; fa.V = sv.V; fa.O = sv.O; fa.lse = sv.lse;
       fa.rows = SG; fa.nkeys = Sp; fa.D = D;
       fa.ldq = D; fa.ldk = D; fa.ldo = D;
       fa.zin = Hkv; fa.zdiv = Hkv;
@@ -278,7 +284,7 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
       fa.scale = scale;
       CK(launch_attn_fwd(fa, Z, st));
     }
-    CK(launch_gemm(gemm(w.O, Dq, L.wo, Dq, sv.ao, H, M, H, Dq), ACT_NONE, OUT_BF16, 1, st));
+    CK(launch_gemm(gemm(sv.O, Dq, L.wo, Dq, sv.ao, H, M, H, Dq), ACT_NONE, OUT_BF16, 1, st));
     CK(launch_residual_norm_fwd(sv.ao, w.x[l], L.ln_post_attn, L.ln_pre_ff, sv.x2, w.xn, sv.rstd_ao, sv.rstd_pre, M,
                                 H, eps, st));
     {
@@ -300,7 +306,13 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
   CK(launch_count_valid(bt->labels, R, bt->loss_scale, w.gscale, w.count, st));
   CK(launch_ce_fwd_bwd(w.logits, V, R, V, bt->labels, w.row_loss, w.gscale, st));
   CK(launch_loss_reduce(w.row_loss, R, w.count, bt->loss, st));
-  CK(launch_gemm(gemm(w.logits, V, wt->embed_t, V, w.dxf, H, R, H, V), ACT_NONE, OUT_F32, 1, st));
+  {  // d(xf) = dlogits . E, K = vocab: split-K over LM_SPLITK slices (fp32 partials, ordered sum)
+    const int kc = V / LM_SPLITK;
+    GemmArgs g = gemm(w.logits, V, wt->embed_t, V, w.dxf_part, H, R, H, kc);
+    g.sA0 = kc; g.sB0 = kc; g.sC0 = (long)R * H;
+    CK(launch_gemm(g, ACT_NONE, OUT_F32, LM_SPLITK, st));
+    CK(launch_sum_partials(w.dxf_part, LM_SPLITK, (long)R * H, w.dxf, st));
+  }
   float* dR = bt->dx;
   CK(hipMemsetAsync(dR, 0, (size_t)M * H * 4, st) != hipSuccess);
   CK(launch_rmsnorm_bwd_scatter(w.x[nl], lossmap, wt->final_norm, w.rstd_f, w.dxf, dR, R, H, st));
@@ -328,40 +340,18 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
       g.cmap = RowMap{Sp, 0, (long)Hkv * Sp, 0};
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, Hkv, st));
     }
-    // attention backward: P recomputed (scores GEMM + masked softmax), then materialised dP/dS
-    {
-      GemmArgs g = gemm(sv.Q, D, sv.K, D, w.S, Sp, SG, Sp, D);
-      g.sA0 = (long)SG * D; g.sB0 = (long)Sp * D; g.sC0 = (long)SG * Sp;
-      g.alpha = scale;
-      CK(launch_gemm(g, ACT_NONE, OUT_F32, Z, st));
-      MaskSpec mk{SG, G, Hkv, 1, sliding ? c->sliding_window : 0, w.key_valid, Sp};
-      CK(launch_softmax_fwd(w.S, w.P, Z, SG, Sp, Sp, mk, st));
-    }
-    CK(launch_transpose(sv.K, D, (long)Sp * D, 0, 1, w.Kt, Sp, (long)D * Sp, 0, Z, Sp, D, Sp, st));
-    CK(launch_transpose(sv.Q, D, (long)SG * D, 0, 1, w.Qt, SG, (long)D * SG, 0, Z, SG, D, SG, st));
-    CK(launch_transpose(w.dO, D, (long)SG * D, 0, 1, w.dOT, SG, (long)D * SG, 0, Z, SG, D, SG, st));
-    CK(launch_transpose(w.P, Sp, (long)SG * Sp, 0, 1, w.PT, SG, (long)Sp * SG, 0, Z, SG, Sp, SG, st));
-    {  // dP = dO V^T
-      GemmArgs g = gemm(w.dO, D, sv.V, D, w.S, Sp, SG, Sp, D);
-      g.sA0 = (long)SG * D; g.sB0 = (long)Sp * D; g.sC0 = (long)SG * Sp;
-      CK(launch_gemm(g, ACT_NONE, OUT_F32, Z, st));
-    }
-    CK(launch_softmax_bwd(w.P, w.S, w.dS, Z * SG, Sp, Sp, scale, st));
-    CK(launch_transpose(w.dS, Sp, (long)SG * Sp, 0, 1, w.dST, SG, (long)Sp * SG, 0, Z, SG, Sp, SG, st));
-    {  // dQ = dS K
-      GemmArgs g = gemm(w.dS, Sp, w.Kt, Sp, w.dQ, D, SG, D, Sp);
-      g.sA0 = (long)SG * Sp; g.sB0 = (long)D * Sp; g.sC0 = (long)SG * D;
-      CK(launch_gemm(g, ACT_NONE, OUT_BF16, Z, st));
-    }
-    {  // dK = dS^T Q
-      GemmArgs g = gemm(w.dST, SG, w.Qt, SG, w.dK, D, Sp, D, SG);
-      g.sA0 = (long)Sp * SG; g.sB0 = (long)D * SG; g.sC0 = (long)Sp * D;
-      CK(launch_gemm(g, ACT_NONE, OUT_BF16, Z, st));
-    }
-    {  // dV = P^T dO
-      GemmArgs g = gemm(w.PT, SG, w.dOT, SG, w.dV, D, Sp, D, SG);
-      g.sA0 = (long)Sp * SG; g.sB0 = (long)D * SG; g.sC0 = (long)Sp * D;
-      CK(launch_gemm(g, ACT_NONE, OUT_BF16, Z, st));
+    {  // flash attention backward: delta = rowsum(dO*O), dK/dV per key block, dQ per query block
+      FlashBwdArgs fb;
+      fb.Q = sv.Q; fb.K = sv.K; fb.V = sv.V; fb.O = sv.O; fb.dO = w.dO; fb.lse = sv.lse; fb.delta = w.delta;
+      fb.dQ = w.dQ; fb.dK = w.dK; fb.dV = w.dV;
+      fb.rows = SG; fb.nkeys = Sp; fb.D = D;
+      fb.zin = Hkv; fb.zdiv = Hkv;
+      fb.ldo = D; fb.sO0 = (long)Sp * Hq * D; fb.sO1 = (long)G * D;
+      fb.omap = RowMap{G, 0, Hq, 0};
+      fb.qdiv = G; fb.causal = 1; fb.window = sliding ? c->sliding_window : 0;
+      fb.key_valid = w.key_valid;
+      fb.scale = scale;
+      CK(launch_attn_bwd(fb, Z, st));
     }
     CK(launch_qknorm_rope_bwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, sv.rstd_q, sv.rstd_k, w.dQ, w.dK, w.dV, w.dqkv,
                               st));

@@ -115,6 +115,28 @@ struct FlashArgs {
   float scale = 1.f;
 };
 int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st);
+// backward; Q, dO, dQ: [nz][rows][D]; K, V, dK, dV: [nz][nkeys][D]; lse, delta: [nz][rows];
+// O (forward output) addressed like FlashArgs::O (z split by zin, row map omap, stride ldo).
+struct FlashBwdArgs {
+  const bf16_t* Q = nullptr;
+  const bf16_t* K = nullptr;
+  const bf16_t* V = nullptr;
+  const bf16_t* O = nullptr;
+  const bf16_t* dO = nullptr;
+  const float* lse = nullptr;
+  float* delta = nullptr;          // workspace [nz][rows]
+  bf16_t* dQ = nullptr;
+  bf16_t* dK = nullptr;
+  bf16_t* dV = nullptr;
+  int rows = 0, nkeys = 0, D = 0;
+  int zin = 1, zdiv = 1;
+  long ldo = 0, sO0 = 0, sO1 = 0;
+  RowMap omap{0, 0, 0, 0};
+  int qdiv = 1, causal = 0, window = 0;
+  const int32_t* key_valid = nullptr;
+  float scale = 1.f;
+};
+int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st);
 
 // ---- misc (misc.hip) ----
 // batched 2-D transpose of bf16 [nz][rows][cols] (ld_in) -> [nz][cols][rows] (ld_out); zero-fills
@@ -137,6 +159,7 @@ int launch_sumsq_partial(const float* x, long n, float* partial, int nparts, hip
 int launch_clip_adamw(float* p, const float* g, float* m, float* v, long n, const float* partial,
                       int nparts, float grad_scale, float max_norm, float lr, float b1, float b2,
                       float eps, float wd, int step, float* norm_out, hipStream_t st);
+int launch_sum_partials(const float* part, int nsplit, long n, float* out, hipStream_t st);
 int launch_fill_normal_bf16(bf16_t* out, long n, uint64_t seed, float std, float mean, hipStream_t st);
 
 }  // namespace ptk

@@ -144,3 +144,23 @@ def flash_attn(Q, K, V, O, *, rows, nkeys, head_dim, ldq, ldk, ldo, batch, batch
     d.key_valid, d.scale = ptr(key_valid), scale
     check(L.lib().ptk_flash_attn_fwd(d, L.stream_ptr(Q.device)), "flash_attn_fwd")
     return O
+
+
+def flash_attn_bwd(Q, K, V, O, dO, lse, *, rows, nkeys, head_dim, batch, batch_inner=1, zdiv=1, ldo=None,
+                   sO=(0, 0), omap=(0, 0, 0, 0), qdiv=1, causal=False, window=0, key_valid=None, scale=1.0):
+    """Flash attention backward (ptk_flash_attn_bwd) -> (dQ, dK, dV) in the Q / K layouts."""
+    _require_cuda(Q, K, V, O, dO, lse)
+    dQ, dK, dV = torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)
+    delta = torch.empty(batch * rows, dtype=torch.float32, device=Q.device)
+    d = L.FlashBwdDesc()
+    d.Q, d.K, d.V, d.O, d.dO, d.lse, d.delta = ptr(Q), ptr(K), ptr(V), ptr(O), ptr(dO), ptr(lse), ptr(delta)
+    d.dQ, d.dK, d.dV = ptr(dQ), ptr(dK), ptr(dV)
+    d.rows, d.nkeys, d.head_dim = rows, nkeys, head_dim
+    d.batch, d.batch_inner, d.zdiv = batch, batch_inner, zdiv
+    d.ldo = head_dim if ldo is None else ldo
+    d.sO0, d.sO1 = sO
+    d.omap = L.RowMap(*omap)
+    d.qdiv, d.causal, d.window = qdiv, int(causal), window
+    d.key_valid, d.scale = ptr(key_valid), scale
+    check(L.lib().ptk_flash_attn_bwd(d, L.stream_ptr(Q.device)), "flash_attn_bwd")
+    return dQ, dK, dV

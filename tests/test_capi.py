@@ -44,6 +44,7 @@ STRUCTS = {
     "ptk_rowmap": ("RowMap", ["g", "skip", "gs", "off"]),
     "ptk_gemm_desc": ("GemmDesc", None),
     "ptk_flash_desc": ("FlashDesc", None),
+    "ptk_flash_bwd_desc": ("FlashBwdDesc", None),
     "ptk_siglip_config": ("SiglipConfigC", None),
     "ptk_siglip_layer": ("SiglipLayerC", None),
     "ptk_siglip_weights": ("SiglipWeightsC", None),

@@ -301,3 +301,45 @@ def test_flash_fwd_gemma_layout(gpu, Hkv, G, window):
     torch.testing.assert_close(O.float(), ref, rtol=2e-2, atol=2e-2)
     lg = lse.view(B, Hkv, S, G).permute(0, 1, 3, 2).reshape(B, Hq, S)
     torch.testing.assert_close(lg, lref, rtol=1e-3, atol=1e-3)
+
+
+@pytest.mark.parametrize("D,Hkv,G,window", [(256, 1, 4, 0), (256, 1, 4, 100), (256, 2, 2, 64), (64, 1, 2, 8)])
+def test_flash_bwd_vs_autograd(gpu, D, Hkv, G, window):
+    """dQ/dK/dV of softmax(scale QK^T + causal/window/key-pad mask) V vs torch autograd (fp32 math on the
+    same bf16 inputs).  Uses the forward kernel's O and LSE as the backward does."""
+    Kn, L = _k()
+    B, S = 2, 320
+    Hq = Hkv * G
+    Q = rnd(B * Hkv, S * G, D, dev=gpu, seed=51)
+    Kt = rnd(B * Hkv, S, D, dev=gpu, seed=52)
+    Vt = rnd(B * Hkv, S, D, dev=gpu, seed=53)
+    dO = rnd(B * Hkv, S * G, D, dev=gpu, seed=54)
+    kv = torch.ones(B, S, dtype=torch.int32, device=gpu)
+    kv[0, 200:215] = 0
+    kv[1, 290:] = 0
+    scale = D ** -0.5
+    O = torch.zeros(B * Hkv, S * G, D, dtype=torch.bfloat16, device=gpu)
+    lse = torch.zeros(B * Hkv, S * G, dtype=torch.float32, device=gpu)
+    common = dict(rows=S * G, nkeys=S, head_dim=D, batch=B * Hkv, batch_inner=Hkv, zdiv=Hkv, qdiv=G, causal=True,
+                  window=window, key_valid=kv, scale=scale)
+    Kn.flash_attn(Q, Kt, Vt, O, lse=lse, ldq=D, ldk=D, ldo=D,
+                  strides=(Hkv * S * G * D, S * G * D, Hkv * S * D, S * D, Hkv * S * G * D, S * G * D), **common)
+    dQ, dK, dV = Kn.flash_attn_bwd(Q, Kt, Vt, O, dO, lse, sO=(Hkv * S * G * D, S * G * D), **common)
+    # reference: rows (s, j) of each z, position s = r // G
+    q = Q.float().requires_grad_(True)
+    k = Kt.float().requires_grad_(True)
+    v = Vt.float().requires_grad_(True)
+    sc = (q @ k.transpose(-1, -2)) * scale
+    pos = torch.arange(S * G, device=gpu)[:, None] // G
+    kk = torch.arange(S, device=gpu)[None, :]
+    m = kk <= pos
+    if window:
+        m = m & (kk > pos - window)
+    m = m[None] & kv.bool().repeat_interleave(Hkv, 0)[:, None, :]
+    p = torch.softmax(sc.masked_fill(~m, float("-inf")), -1)
+    p = torch.where(m.any(-1, keepdim=True), p, torch.zeros_like(p))   # fully masked rows: P = 0 (kernel convention)
+    out = p @ v
+    out.backward(dO.float())
+    for got, ref, nm in ((dQ, q.grad, "dQ"), (dK, k.grad, "dK"), (dV, v.grad, "dV")):
+        err = (got.float() - ref).norm() / ref.norm()
+        assert err < 2e-2, (nm, float(err))
