@@ -363,7 +363,9 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
 }
 
 template <int D>
-__global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
+__global__ void __launch_bounds__(256, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
+  // 4 waves x 16 keys; one wave per SIMD so K/V fragments (B operands) and the dK^T/dV^T
+  // accumulators (128 fp32 per lane at D = 256) stay in the 512-entry register file.
   constexpr int CPR = D / 8;
   constexpr int TILE_BYTES = 64 * D * 2;     // 64 query rows of Q or dO
   constexpr int KS = D / 32;
@@ -372,10 +374,9 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int kw = wave & 3, qh = wave >> 2;   // 16 keys per kw; q sub-tiles {2qh, 2qh+1} of each chunk
   const long z = blockIdx.y;
   const int k0 = blockIdx.x * 64;
-  const int key = k0 + kw * 16 + c16;
+  const int key = k0 + wave * 16 + c16;
   const int key_c = min(key, a.nkeys - 1);
   const long b = z / a.zdiv;
   const bf16_t* Qz = a.Q + z * (long)a.rows * D;
@@ -390,7 +391,6 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
     }
   }
   const bool key_ok = key < a.nkeys && (!a.key_valid || a.key_valid[b * a.nkeys + key_c] != 0);
-  // query rows that can see this key block
   int r_lo = 0, r_hi = a.rows;
   if (a.causal) {
     r_lo = min(a.rows, k0 * a.qdiv);
@@ -401,7 +401,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
   const float sl2 = a.scale * L2E;
 
   constexpr int ROWS_PER_INST = 64 / CPR;
-  constexpr int INSTS = CPR / 8;
+  constexpr int INSTS = CPR / 4;              // per wave per tile (4 waves)
   auto stage = [&](int c, int buf) {
     char* qb = smem + buf * 2 * TILE_BYTES;
     char* ob = qb + TILE_BYTES;
@@ -423,6 +423,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
     dv[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     dk[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
   }
+  const int q4 = c16 >> 2, p4 = c16 & 3;
   if (c_lo < c_hi) stage(c_lo, 0);
   for (int c = c_lo; c < c_hi; ++c) {
     const int buf = (c - c_lo) & 1;
@@ -431,72 +432,58 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
     if (c + 1 < c_hi) stage(c + 1, buf ^ 1);
     const char* qb = smem + buf * 2 * TILE_BYTES;
     const char* ob = qb + TILE_BYTES;
-    bf16x8_t pf, dsf;
 #pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-      const int qt = 2 * qh + hh;
-      f32x4_t s = (f32x4_t){0.f, 0.f, 0.f, 0.f}, dp = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-      const int row = qt * 16 + c16;
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int ch = (ks * 4 + g) ^ swz_k<D>(row);
-        const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(qb + row * (D * 2) + ch * 16);
-        const bf16x8_t oa = *reinterpret_cast<const bf16x8_t*>(ob + row * (D * 2) + ch * 16);
-        s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ks], s, 0, 0, 0);
-        dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[ks], dp, 0, 0, 0);
-      }
-      // C layout: row = query 4g + j of sub-tile qt, column = this lane's key
-      const int qbase = c * 64 + qt * 16 + 4 * g;
-      const float4 l4 = *reinterpret_cast<const float4*>(a.lse + z * a.rows + min(qbase, a.rows - 4));
-      const float4 d4 = *reinterpret_cast<const float4*>(a.delta + z * a.rows + min(qbase, a.rows - 4));
-      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int q = qbase + j;
-        const int pos = q / a.qdiv;
-        bool ok = key_ok && q < a.rows;
-        if (a.causal) ok = ok && key <= pos;
-        if (a.window > 0) ok = ok && key > pos - a.window;
-        const float p = ok ? exp2f(s[j] * sl2 - lv[j] * L2E) : 0.f;
-        const bf16_t pb = f2bf(p);
-        pf[4 * hh + j] = (short)pb;
-        dsf[4 * hh + j] = (short)f2bf(bf2f(pb) * (dp[j] - dl[j]));
-      }
-    }
-    // dV^T += dO^T P, dK^T += Q^T dS over this wave's 32 query rows (k order = tr-read rows)
-    const int q4 = c16 >> 2, p4 = c16 & 3;
-#pragma unroll
-    for (int ds = 0; ds < DS; ++ds) {
-      bf16x8_t ot, qt_;
+    for (int kst = 0; kst < 2; ++kst) {          // two 32-query k-steps of the dV/dK products
+      bf16x8_t pf, dsf;
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
-        const int row = (2 * qh + hh) * 16 + 4 * g + q4;
-        const int ch = (2 * ds + (p4 >> 1)) ^ swz_k<D>(row);
-        const int off = row * (D * 2) + ch * 16 + 8 * (p4 & 1);
-        const s16x4_t ro = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(ob + off));
-        const s16x4_t rq = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(qb + off));
-        ot[4 * hh + 0] = ro[0]; ot[4 * hh + 1] = ro[1]; ot[4 * hh + 2] = ro[2]; ot[4 * hh + 3] = ro[3];
-        qt_[4 * hh + 0] = rq[0]; qt_[4 * hh + 1] = rq[1]; qt_[4 * hh + 2] = rq[2]; qt_[4 * hh + 3] = rq[3];
+        const int qt = 2 * kst + hh;
+        f32x4_t s = (f32x4_t){0.f, 0.f, 0.f, 0.f}, dp = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        const int row = qt * 16 + c16;
+#pragma unroll
+        for (int ks = 0; ks < KS; ++ks) {
+          const int ch = (ks * 4 + g) ^ swz_k<D>(row);
+          const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(qb + row * (D * 2) + ch * 16);
+          const bf16x8_t oa = *reinterpret_cast<const bf16x8_t*>(ob + row * (D * 2) + ch * 16);
+          s = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[ks], s, 0, 0, 0);
+          dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[ks], dp, 0, 0, 0);
+        }
+        const int qbase = c * 64 + qt * 16 + 4 * g;
+        const float4 l4 = *reinterpret_cast<const float4*>(a.lse + z * a.rows + min(qbase, a.rows - 4));
+        const float4 d4 = *reinterpret_cast<const float4*>(a.delta + z * a.rows + min(qbase, a.rows - 4));
+        const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int q = qbase + j;
+          const int pos = q / a.qdiv;
+          bool ok = key_ok && q < a.rows;
+          if (a.causal) ok = ok && key <= pos;
+          if (a.window > 0) ok = ok && key > pos - a.window;
+          const float p = ok ? exp2f(s[j] * sl2 - lv[j] * L2E) : 0.f;
+          const bf16_t pb = f2bf(p);
+          pf[4 * hh + j] = (short)pb;
+          dsf[4 * hh + j] = (short)f2bf(bf2f(pb) * (dp[j] - dl[j]));
+        }
       }
-      dv[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ot, pf, dv[ds], 0, 0, 0);
-      dk[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt_, dsf, dk[ds], 0, 0, 0);
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) {
+        bf16x8_t ot, qt_;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int row = (2 * kst + hh) * 16 + 4 * g + q4;
+          const int ch = (2 * ds + (p4 >> 1)) ^ swz_k<D>(row);
+          const int off = row * (D * 2) + ch * 16 + 8 * (p4 & 1);
+          const s16x4_t ro = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(ob + off));
+          const s16x4_t rq = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(qb + off));
+          ot[4 * hh + 0] = ro[0]; ot[4 * hh + 1] = ro[1]; ot[4 * hh + 2] = ro[2]; ot[4 * hh + 3] = ro[3];
+          qt_[4 * hh + 0] = rq[0]; qt_[4 * hh + 1] = rq[1]; qt_[4 * hh + 2] = rq[2]; qt_[4 * hh + 3] = rq[3];
+        }
+        dv[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ot, pf, dv[ds], 0, 0, 0);
+        dk[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt_, dsf, dk[ds], 0, 0, 0);
+      }
     }
   }
-  // combine the two query halves (waves kw and kw+4) through LDS, then store
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  float* red = reinterpret_cast<float*>(smem) + kw * (2 * DS * 4 * 64);
-  if (qh == 1) {
-#pragma unroll
-    for (int ds = 0; ds < DS; ++ds)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        red[((ds * 4 + j) * 64) + lane] = dv[ds][j];
-        red[((DS + ds) * 4 + j) * 64 + lane] = dk[ds][j];
-      }
-  }
-  __syncthreads();
-  if (qh == 1 || key >= a.nkeys) return;
+  if (key >= a.nkeys) return;
   bf16_t* dvp = a.dV + (z * a.nkeys + key) * (long)D + 4 * g;
   bf16_t* dkp = a.dK + (z * a.nkeys + key) * (long)D + 4 * g;
 #pragma unroll
@@ -504,8 +491,8 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
     u16x4_t uv, uk;
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
-      uv[j] = f2bf(dv[ds][j] + red[((ds * 4 + j) * 64) + lane]);
-      uk[j] = f2bf((dk[ds][j] + red[((DS + ds) * 4 + j) * 64 + lane]) * a.scale);
+      uv[j] = f2bf(dv[ds][j]);
+      uk[j] = f2bf(dk[ds][j] * a.scale);
     }
     *reinterpret_cast<u16x4_t*>(dvp + 16 * ds) = uv;
     *reinterpret_cast<u16x4_t*>(dkp + 16 * ds) = uk;
@@ -522,12 +509,12 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st) {
   switch (a.D) {
     case 64:
       hipLaunchKernelGGL(attn_delta_kernel<64>, gd, dim3(256), 0, st, a, nz);
-      hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, gk, dim3(512), 0, st, a);
+      hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, gk, dim3(256), 0, st, a);
       hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, gq, dim3(512), 0, st, a);
       break;
     case 256:
       hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, a, nz);
-      hipLaunchKernelGGL(attn_bwd_dkv_kernel<256>, gk, dim3(512), 0, st, a);
+      hipLaunchKernelGGL(attn_bwd_dkv_kernel<256>, gk, dim3(256), 0, st, a);
       hipLaunchKernelGGL(attn_bwd_dq_kernel<256>, gq, dim3(512), 0, st, a);
       break;
     default: return set_error("attn_bwd: head_dim %d unsupported (64, 256)", a.D);

@@ -387,3 +387,37 @@ int launch_sum_partials(const float* part, int nsplit, long n, float* out, hipSt
   return hipGetLastError() == hipSuccess ? 0 : set_error("sum_partials launch failed");
 }
 }  // namespace ptk
+
+namespace ptk {
+// GEGLU backward as a streaming pass (TF gemma3 :131-133 autograd, bf16 ops):
+//   dg = bf16(bf16(dh * u) * gelu_tanh'(g)),  du = bf16(dh * bf16(gelu_tanh(g)))
+// dh, g, u [M, I] bf16 -> dgu [M, 2I] bf16 in the interleaved gate/up layout (16-column groups).
+__global__ void __launch_bounds__(256) geglu_bwd_kernel(const bf16_t* __restrict__ dh, const bf16_t* __restrict__ g,
+                                                        const bf16_t* __restrict__ u, bf16_t* __restrict__ dgu,
+                                                        long n8, int I) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;   // one 8-element group
+  if (i >= n8) return;
+  const long e0 = i * 8;
+  const long r = e0 / I;
+  const int c = (int)(e0 - r * I);
+  const u16x8_t vd = *reinterpret_cast<const u16x8_t*>(dh + e0);
+  const u16x8_t vg = *reinterpret_cast<const u16x8_t*>(g + e0);
+  const u16x8_t vu = *reinterpret_cast<const u16x8_t*>(u + e0);
+  u16x8_t og, ou;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float d = bf2f(vd[k]), gg = bf2f(vg[k]), uu = bf2f(vu[k]);
+    og[k] = f2bf(bfround(d * uu) * gelu_tanh_grad(gg));
+    ou[k] = f2bf(d * bfround(gelu_tanh(gg)));
+  }
+  bf16_t* o = dgu + r * 2L * I + (c >> 4) * 32 + (c & 15);
+  *reinterpret_cast<u16x8_t*>(o) = og;
+  *reinterpret_cast<u16x8_t*>(o + 16) = ou;
+}
+int launch_geglu_bwd(const bf16_t* dh, const bf16_t* g, const bf16_t* u, bf16_t* dgu, long M, int I, hipStream_t st) {
+  if (I % 16) return set_error("geglu_bwd: intermediate %% 16");
+  const long n8 = M * I / 8;
+  hipLaunchKernelGGL(geglu_bwd_kernel, dim3((unsigned)((n8 + 255) / 256)), dim3(256), 0, st, dh, g, u, dgu, n8, I);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("geglu_bwd launch failed");
+}
+}  // namespace ptk

@@ -326,11 +326,9 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
     const float* sn = sliding ? wt->rope_sin_local : wt->rope_sin_global;
     // MLP half
     CK(launch_post_norm_bwd(dR, sv.dn, L.ln_post_ff, sv.rstd_dn, w.dao, M, H, st));
-    {
-      GemmArgs g = gemm(w.dao, H, L.wd_t, H, w.dgu, 2 * I, M, I, H);
-      g.aux_in = sv.g; g.aux_in2 = sv.u; g.ld_aux_in = I;
-      CK(launch_gemm(g, ACT_GEGLU_BWD, OUT_BF16, 1, st));
-    }
+    // dh = dd . Wd (plain GEMM at full MFMA rate), then the GEGLU backward as one streaming pass
+    CK(launch_gemm(gemm(w.dao, H, L.wd_t, H, w.h, I, M, I, H), ACT_NONE, OUT_BF16, 1, st));
+    CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, M, I, st));
     CK(launch_gemm(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), ACT_NONE, OUT_F32, 1, st));
     CK(launch_residual_norm_bwd(sv.x2, L.ln_pre_ff, sv.rstd_pre, w.dtmp, dR, sv.ao, L.ln_post_attn, sv.rstd_ao, w.dao,
                                 M, H, st));

@@ -160,6 +160,7 @@ int launch_clip_adamw(float* p, const float* g, float* m, float* v, long n, cons
                       int nparts, float grad_scale, float max_norm, float lr, float b1, float b2,
                       float eps, float wd, int step, float* norm_out, hipStream_t st);
 int launch_sum_partials(const float* part, int nsplit, long n, float* out, hipStream_t st);
+int launch_geglu_bwd(const bf16_t* dh, const bf16_t* g, const bf16_t* u, bf16_t* dgu, long M, int I, hipStream_t st);
 int launch_fill_normal_bf16(bf16_t* out, long n, uint64_t seed, float std, float mean, hipStream_t st);
 
 }  // namespace ptk
