@@ -143,6 +143,10 @@ def main():
     value = imgs / elapsed
     fpi = flops_per_image(cfg)["total"]
     geglu_ms = tot.value / max(cnt.value, 1)
+    traffic = None
+    pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic_geglu.json")
+    if os.path.exists(pmc) and args.config == "cfg2" and cfg.batch_size == 32:
+        traffic = json.load(open(pmc))["traffic_bytes_per_launch"]   # rocprofv3 --pmc passes (tools/pmc_traffic.py)
     achieved = geglu_gemm_flops(cfg) / (geglu_ms / 1e3) / 1e12
     line = {
         "metric": "Stage-1 images/sec/node (SigLIP-L-384 + Gemma3-1B, 576+128 tok)",
@@ -153,9 +157,10 @@ def main():
                                f"Gemma3-1B frozen fwd/bwd, {cfg.num_vision_tokens} vis + {cfg.text_len} text tokens",
                    "global_batch": world * cfg.batch_size, "per_gpu_batch": cfg.batch_size,
                    "seq_len": cfg.seq_len, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "gemm_nt_kernel<ACT_GEGLU> (Gemma3 gate|up projection)",
+        "roofline": {"bound": "mfma", "kernel": "gemm_big_kernel<ACT_GEGLU> (Gemma3 gate|up projection, 2*(B*S)*(2I)*H FLOP per launch)",
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
+                     "traffic_unit": "bytes/launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",
                      "launches": cnt.value, "avg_ms": round(geglu_ms, 4)},
         "step_mfma_frac": round(value * fpi / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
         "flop_per_image": fpi, "loss": round(float(loss), 5),

@@ -25,6 +25,8 @@ for step in "$@"; do
     benchfull) run benchfull 900 python bench.py ;;
     gemmbench) run gemmbench 300 python tools/gemm_bench.py ;;
     prof)    run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
+    pmcfetch) run pmcfetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --kernel-include-regex "gemm_big_kernel<3" --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcwrite) run pmcwrite 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --kernel-include-regex "gemm_big_kernel<3" --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
   esac
 done
