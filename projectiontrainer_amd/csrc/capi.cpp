@@ -88,8 +88,9 @@ int ptk_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream) {
   return launch_cast_f32_bf16(in, (bf16_t*)out, n, ST);
 }
 
-int ptk_gemm_force_small_tiles(int on) {
-  force_small_tiles(on);
+int ptk_gemm_force_small_tiles(int mode) {
+  if (mode < 0 || mode > 2) return set_error("gemm tile mode %d not in {0, 1, 2}", mode);
+  force_small_tiles(mode);
   return 0;
 }
 int ptk_gemm_timer_enable(int on) {

@@ -95,6 +95,60 @@ PTK_DEV void epi_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 v) {
   }
 }
 
+// 8 columns per lane, one 16-B store (bf16 output): the epilogue is store-issue bound
+// (one wave store instruction per ~140 cycles per CU regardless of width), so every
+// bf16 store moves 16 B.
+typedef __attribute__((ext_vector_type(8))) unsigned short u16x8_t;
+PTK_DEV void ldbf8(const bf16_t* p, float* v) {
+  const u16x8_t u = *reinterpret_cast<const u16x8_t*>(p);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) v[e] = bf2f(u[e]);
+}
+PTK_DEV void stbf8(bf16_t* p, const float* v) {
+  u16x8_t u;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
+  *reinterpret_cast<u16x8_t*>(p) = u;
+}
+
+template <int ACT>
+PTK_DEV void epi_vec8_bf16(const GemmArgs& p, char* Cz, long r, long c, float4 v0, float4 v1) {
+  // r < M; c..c+7 < N; c % 8 == 0; all leading dims multiples of 8
+  float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+  if (p.bias) {
+    const float4 b0 = ldf4(p.bias + c), b1 = ldf4(p.bias + c + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  if (p.rowadd) {
+    const float* ra = p.rowadd + (r % p.rowadd_period) * p.ld_rowadd + c;
+    const float4 b0 = ldf4(ra), b1 = ldf4(ra + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  if constexpr (ACT == ACT_GELU_TANH) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(bfround(v[e]));
+  } else if constexpr (ACT == ACT_GELU_ERF) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]);
+    if (p.aux) stbf8(p.aux + r * p.ld_aux + c, v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+  } else if constexpr (ACT == ACT_GELU_ERF_BWD) {
+    float a[8];
+    ldbf8(p.aux_in + r * p.ld_aux_in + c, a);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]) * gelu_erf_grad(a[e]);
+  }
+  const long cr = map_row(p.cmap, r);
+  if (cr < 0) return;
+  if (p.resid) {
+    const float* rp = p.resid + cr * p.ld_resid + c;
+    const float4 b0 = ldf4(rp), b1 = ldf4(rp + 4);
+    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
+  }
+  stbf8(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + c, v);
+}
+
 // scalar fallback for ragged column tails / unaligned leading dims
 template <int ACT, int OUT>
 PTK_DEV void epi_scalar(const GemmArgs& p, char* Cz, long r, long c, float v) {
@@ -137,6 +191,20 @@ PTK_DEV void geglu_vec4(const GemmArgs& p, char* Cz, long r, long hc, float4 g, 
   if (cr >= 0) stbf4(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + hc, h);
 }
 
+PTK_DEV void geglu_vec8(const GemmArgs& p, char* Cz, long r, long hc, const float* g, const float* u) {
+  float gg[8], uu[8], h[8];
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    gg[e] = bfround(g[e]);
+    uu[e] = bfround(u[e]);
+    h[e] = bfround(gelu_tanh(gg[e])) * uu[e];
+  }
+  if (p.aux) stbf8(p.aux + r * p.ld_aux + hc, gg);
+  if (p.aux2) stbf8(p.aux2 + r * p.ld_aux + hc, uu);
+  const long cr = map_row(p.cmap, r);
+  if (cr >= 0) stbf8(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + hc, h);
+}
+
 // GEGLU backward: GEMM output = dh [M, I]; writes dg, du into the interleaved [M, 2I] layout.
 PTK_DEV void geglu_bwd_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 dh) {
   const float4 g = ldbf4(p.aux_in + r * p.ld_aux_in + c);
@@ -173,17 +241,51 @@ PTK_DEV void epilogue(const GemmArgs& p, char* smem, int wave, int lane, f32x4_t
                       (!p.rowadd || (p.ld_rowadd & 3) == 0) && (!p.aux || (p.ld_aux & 3) == 0) &&
                       (!p.aux_in || (p.ld_aux_in & 3) == 0);
   if constexpr (ACT == ACT_GEGLU) {
-    // 8 lanes per row, each 4 h-columns; 8 rows per pass
-    const int rr = lane >> 3, cg = lane & 7, q = cg >> 2, cc = (cg & 3) * 4;
-    const long hc = col0 / 2 + q * 16 + cc;
+    const bool v8 = ((p.ldc | p.ld_aux) & 7) == 0;
+    if (v8) {
+      // 4 lanes per row, each 8 h-columns (one 16-B store per output); 16 rows per pass
+      const int rr = lane >> 2, cg = lane & 3, q = cg >> 1, cc = (cg & 1) * 8;
+      const long hc = col0 / 2 + q * 16 + cc;
+#pragma unroll
+      for (int it = 0; it < 4; ++it) {
+        const int lr = it * 16 + rr;
+        const long r = row0 + lr;
+        if (r >= p.M || 2 * hc >= p.N) continue;
+        const float* tg = T + lr * EPI_LD + q * 32 + cc;
+        float g[8], u[8];
+        *reinterpret_cast<float4*>(g) = *reinterpret_cast<const float4*>(tg);
+        *reinterpret_cast<float4*>(g + 4) = *reinterpret_cast<const float4*>(tg + 4);
+        *reinterpret_cast<float4*>(u) = *reinterpret_cast<const float4*>(tg + 16);
+        *reinterpret_cast<float4*>(u + 4) = *reinterpret_cast<const float4*>(tg + 20);
+        geglu_vec8(p, Cz, r, hc, g, u);
+      }
+    } else {
+      // 8 lanes per row, each 4 h-columns; 8 rows per pass
+      const int rr = lane >> 3, cg = lane & 7, q = cg >> 2, cc = (cg & 3) * 4;
+      const long hc = col0 / 2 + q * 16 + cc;
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int lr = it * 8 + rr;
+        const long r = row0 + lr;
+        if (r >= p.M || 2 * hc >= p.N) continue;
+        const float4 g = *reinterpret_cast<const float4*>(T + lr * EPI_LD + q * 32 + cc);
+        const float4 u = *reinterpret_cast<const float4*>(T + lr * EPI_LD + q * 32 + 16 + cc);
+        geglu_vec4(p, Cz, r, hc, g, u);
+      }
+    }
+  } else if (OUT == OUT_BF16 && ACT != ACT_GEGLU_BWD && vec_ok && ((p.ldc & 7) == 0) &&
+             (!p.aux || (p.ld_aux & 7) == 0) && (!p.aux_in || (p.ld_aux_in & 7) == 0) && col0 + 63 < p.N) {
+    // 8 lanes per row, each 8 columns (16-B stores); 8 rows per pass
+    const int rr = lane >> 3, c8 = (lane & 7) * 8;
+    const long c = col0 + c8;
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int lr = it * 8 + rr;
       const long r = row0 + lr;
-      if (r >= p.M || 2 * hc >= p.N) continue;
-      const float4 g = *reinterpret_cast<const float4*>(T + lr * EPI_LD + q * 32 + cc);
-      const float4 u = *reinterpret_cast<const float4*>(T + lr * EPI_LD + q * 32 + 16 + cc);
-      geglu_vec4(p, Cz, r, hc, g, u);
+      if (r >= p.M) continue;
+      const float4 v0 = *reinterpret_cast<const float4*>(T + lr * EPI_LD + c8);
+      const float4 v1 = *reinterpret_cast<const float4*>(T + lr * EPI_LD + c8 + 4);
+      epi_vec8_bf16<ACT>(p, Cz, r, c, v0, v1);
     }
   } else {
     // 16 lanes per row, each 4 columns; 4 rows per pass
@@ -317,9 +419,24 @@ constexpr int BIG = 256;
 constexpr int HALF_BYTES = 128 * BK * 2;   // 16 KiB
 constexpr int BUF_BYTES = 4 * HALF_BYTES;   // 64 KiB
 
+#ifdef PTK_STAMPS
+// diagnostic build only (make stamps): per-block s_memtime / s_memrealtime stamps of the 256x256 kernel
+__device__ unsigned long long g_stamps[1 << 15][6];
+__device__ int g_epi_mode;   // 0 normal, 1 no global stores, 2 no epilogue
+#define PTK_STAMP(i)                                                                  \
+  if (threadIdx.x == 0 && blockIdx.x < (1 << 15)) {                                   \
+    g_stamps[blockIdx.x][i] = __builtin_amdgcn_s_memtime();                           \
+    if (i == 0) g_stamps[blockIdx.x][5] = __builtin_amdgcn_s_memrealtime();           \
+    if (i == 3) g_stamps[blockIdx.x][4] = __builtin_amdgcn_s_memrealtime();           \
+  }
+#else
+#define PTK_STAMP(i)
+#endif
+
 template <int ACT, int OUT>
 __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[8 * EPI_WAVE_BYTES];   // 136 KiB >= 2 * BUF_BYTES
+  PTK_STAMP(0);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
 
@@ -379,6 +496,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
+  PTK_STAMP(1);
 
   bf16x8_t a[4][2], b0[2][2], b1[2][2];
   for (int t = 0; t < nt; ++t) {
@@ -465,6 +583,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
   }
+  PTK_STAMP(2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
 
@@ -473,15 +592,31 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
   f32x4_t (&top)[4][4] = *reinterpret_cast<f32x4_t(*)[4][4]>(&acc[0][0]);
   f32x4_t (&bot)[4][4] = *reinterpret_cast<f32x4_t(*)[4][4]>(&acc[4][0]);
   const long r0 = (long)bm * BIG + wr * 128, c0 = (long)bn * BIG + wc * 64;
+#ifdef PTK_STAMPS
+  const int em = g_epi_mode;
+  GemmArgs pe = p;
+  if (em == 1) pe.M = 0;   // every row skipped after staging
+  if (em != 2) {
+    epilogue<ACT, OUT>(pe, smem, wave, lane, top, r0, c0, Cz);
+    __builtin_amdgcn_wave_barrier();
+    epilogue<ACT, OUT>(pe, smem, wave, lane, bot, r0 + 64, c0, Cz);
+  }
+#else
   epilogue<ACT, OUT>(p, smem, wave, lane, top, r0, c0, Cz);
   __builtin_amdgcn_wave_barrier();
   epilogue<ACT, OUT>(p, smem, wave, lane, bot, r0 + 64, c0, Cz);
+#endif
+#ifdef PTK_STAMPS
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+#endif
+  PTK_STAMP(3);
 }
 
 // ---- optional live per-class timing (HIP events around launches; bench.py roofline)
 static bool g_timing = false;
-static bool g_force_small = false;   // tests: route every GEMM through the 128x128 kernel
-void force_small_tiles(int on) { g_force_small = on != 0; }
+static int g_force_tiles = 0;   // tests: 1 = every GEMM on 128x128, 2 = single-batch GEMMs on 256x256
+void force_small_tiles(int mode) { g_force_tiles = mode; }
 static std::vector<hipEvent_t> g_ev[8];
 static size_t g_ev_used[8];
 
@@ -531,7 +666,11 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   if (a.zin <= 0) return set_error("gemm: zin must be >= 1");
   const long ntile = (long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (ntile > 0x7fffffffL) return set_error("gemm: too many tiles");
-  const bool big = batch == 1 && a.M >= 1024 && a.N >= 512 && !g_force_small;
+  // 256x256 (one block per CU) only where the K loop amortises its lock-step epilogue: long K or
+  // wide N at K >= 1152.  Elsewhere two co-resident 128x128 blocks per CU overlap one block's
+  // epilogue with the other's MFMA and quantise better (tools/gemm_bench.py --all, r01).
+  const bool big = batch == 1 && g_force_tiles != 1 &&
+                   (g_force_tiles == 2 || (a.M >= 1024 && a.N >= 512 && (a.K >= 6144 || (a.N >= 6144 && a.K >= 1152))));
   if (big) {
     const long nb = (long)((a.M + BIG - 1) / BIG) * ((a.N + BIG - 1) / BIG);
     dim3 g2((unsigned)nb, 1, 1);
@@ -568,3 +707,12 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
 }
 
 }  // namespace ptk
+
+#ifdef PTK_STAMPS
+extern "C" int ptk_debug_epi_mode(int m) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(ptk::g_epi_mode), &m, sizeof(int), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+extern "C" int ptk_debug_stamps_read(void* host, size_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ptk::g_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -42,7 +42,7 @@ struct GemmArgs {
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
 // live GEMM timing per activation class (events recorded around each launch when enabled)
 void timer_enable(int on);
-void force_small_tiles(int on);
+void force_small_tiles(int mode);
 int timer_read(int cls, double* total_ms, int* count);
 
 // ---- row-wise normalisation (norm.hip) ----

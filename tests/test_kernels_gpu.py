@@ -196,11 +196,15 @@ def test_cross_entropy(gpu):
 @pytest.mark.parametrize("M,N,K", [(1024, 512, 64), (1024, 512, 128), (1100, 700, 192), (2048, 1152, 1152),
                                    (4096, 1536, 256)])
 def test_gemm_big_tile_path(gpu, M, N, K):
-    """256x256 8-wave kernel (M >= 1024, N >= 512): ragged M/N, 1..18 K-tiles, vs fp32."""
+    """256x256 8-wave kernel (forced): ragged M/N, 1..18 K-tiles, vs fp32."""
     Kn, L = _k()
     A, B = rnd(M, K, dev=gpu, seed=31), rnd(N, K, dev=gpu, seed=32)
     ref = A.float() @ B.float().T
-    C = Kn.gemm(A, B, out_dtype=torch.float32)
+    L.lib().ptk_gemm_force_small_tiles(2)
+    try:
+        C = Kn.gemm(A, B, out_dtype=torch.float32)
+    finally:
+        L.lib().ptk_gemm_force_small_tiles(0)
     torch.testing.assert_close(C, ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
 
 
@@ -215,8 +219,8 @@ def test_gemm_big_vs_small_all_epilogues(gpu):
     res = rnd(M, N, dev=gpu, dtype=torch.float32, seed=36)
     aux_in = rnd(M, N, dev=gpu, seed=37)
     outs = []
-    for small in (0, 1):
-        L.lib().ptk_gemm_force_small_tiles(small)
+    for mode in (2, 1):
+        L.lib().ptk_gemm_force_small_tiles(mode)
         try:
             o = {}
             C = res.clone()

@@ -48,11 +48,50 @@ def run(name, m, n, k, act, odt, reps=10):
     return {"name": name, "M": m, "N": n, "K": k, "ms": round(ms, 4), "TFLOPs": round(fl / ms / 1e9, 1)}
 
 
+ALL = [  # every single-batch GEMM of the cfg2 step: name, M, N, K, act, out
+    ("sig_patch", 18432, 1024, 768, L.ACT_NONE, torch.float32),
+    ("sig_qkv", 18432, 3072, 1024, L.ACT_NONE, torch.bfloat16),
+    ("sig_o", 18432, 1024, 1024, L.ACT_NONE, torch.float32),
+    ("sig_fc1", 18432, 4096, 1024, L.ACT_GELU_TANH, torch.bfloat16),
+    ("sig_fc2", 18432, 1024, 4096, L.ACT_NONE, torch.float32),
+    ("proj_fc1", 18432, 11520, 1024, L.ACT_GELU_ERF, torch.bfloat16),
+    ("proj_fc2", 18432, 1152, 11520, L.ACT_NONE, torch.float32),
+    ("g_qkv", M, 1536, 1152, L.ACT_NONE, torch.bfloat16),
+    ("g_o", M, 1152, 1024, L.ACT_NONE, torch.bfloat16),
+    ("g_gu", M, 13824, 1152, L.ACT_GEGLU, torch.bfloat16),
+    ("g_down", M, 1152, 6912, L.ACT_NONE, torch.bfloat16),
+    ("g_lm", 4096, 262144, 1152, L.ACT_NONE, torch.bfloat16),
+    ("g_dh", M, 6912, 1152, L.ACT_NONE, torch.bfloat16),
+    ("g_dgu", M, 1152, 13824, L.ACT_NONE, torch.float32),
+    ("g_dO", M, 1024, 1152, L.ACT_NONE, torch.bfloat16),
+    ("g_dqkv", M, 1152, 1536, L.ACT_NONE, torch.float32),
+    ("g_dao", M, 1152, 1024, L.ACT_NONE, torch.float32),
+]
+
+if __name__ == "__main__" and "--all" in sys.argv:
+    for s in ALL:
+        r = {}
+        for small in (0, 1, 0, 1):
+            L.lib().ptk_gemm_force_small_tiles(2 - small)
+            r[small] = run(*s)
+        print(json.dumps({"name": s[0], "M": s[1], "N": s[2], "K": s[3], "big_TF": r[0]["TFLOPs"],
+                          "small_TF": r[1]["TFLOPs"], "big_ms": r[0]["ms"], "small_ms": r[1]["ms"]}), flush=True)
+    sys.exit(0)
+
 if __name__ == "__main__":
     res = []
-    for rnd in range(2):
+    if "--small" in sys.argv:
+        L.lib().ptk_gemm_force_small_tiles(1)
+    for rnd in range(0 if "--sweep" in sys.argv else 2):
         for s in SHAPES:
             r = run(*s)
             if rnd == 1:
                 res.append(r)
+                print(json.dumps(r), flush=True)
+    if "--sweep" in sys.argv:
+        # fixed per-tile cost vs K-proportional cost (prologue/epilogue overhead)
+        for n in (13824, 4096):
+            for k in (256, 512, 1152, 2304, 4608):
+                r = run(f"sweep_n{n}", M, n, k, L.ACT_NONE, torch.bfloat16)
+                r["tiles"] = ((M + 255) // 256) * ((n + 255) // 256)
                 print(json.dumps(r), flush=True)
