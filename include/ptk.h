@@ -139,7 +139,12 @@ typedef struct {
   int qdiv, causal, window;
   const int32_t* key_valid;
   float scale;
+  /* optional scratch for head_dim 256: heavy causal key slabs are split over query pieces whose
+   * fp32 dK/dV partials live here (size: ptk_flash_bwd_workspace_bytes); NULL = no split. */
+  void* workspace;
+  int64_t workspace_bytes;
 } ptk_flash_bwd_desc;
+size_t ptk_flash_bwd_workspace_bytes(const ptk_flash_bwd_desc* d);
 int ptk_flash_attn_bwd(const ptk_flash_bwd_desc* d, void* stream);
 
 /* ------------------------------------------------------------------------ *

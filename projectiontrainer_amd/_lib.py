@@ -52,7 +52,7 @@ class FlashBwdDesc(C.Structure):
                 ("batch", c_int), ("batch_inner", c_int), ("zdiv", c_int),
                 ("ldo", c_int64), ("sO0", c_int64), ("sO1", c_int64), ("omap", RowMap),
                 ("qdiv", c_int), ("causal", c_int), ("window", c_int), ("key_valid", c_void_p),
-                ("scale", c_float)]
+                ("scale", c_float), ("workspace", c_void_p), ("workspace_bytes", c_int64)]
 
 
 class SiglipConfigC(C.Structure):
@@ -123,6 +123,7 @@ SIGNATURES = {
     "ptk_gemm_timer_read": (c_int, [c_int, C.POINTER(C.c_double), C.POINTER(c_int)]),
     "ptk_flash_attn_fwd": (c_int, [C.POINTER(FlashDesc), c_void_p]),
     "ptk_flash_attn_bwd": (c_int, [C.POINTER(FlashBwdDesc), c_void_p]),
+    "ptk_flash_bwd_workspace_bytes": (c_size_t, [C.POINTER(FlashBwdDesc)]),
     "ptk_siglip_workspace_bytes": (c_size_t, [C.POINTER(SiglipConfigC), c_int]),
     "ptk_siglip_fwd": (c_int, [C.POINTER(SiglipConfigC), C.POINTER(SiglipWeightsC), c_int, c_void_p, c_void_p,
                                c_void_p, c_size_t, c_void_p]),

@@ -117,8 +117,7 @@ int ptk_flash_attn_fwd(const ptk_flash_desc* d, void* stream) {
   return launch_attn_fwd(a, d->batch > 0 ? d->batch : 1, ST);
 }
 
-int ptk_flash_attn_bwd(const ptk_flash_bwd_desc* d, void* stream) {
-  if (!d) return set_error("flash_bwd: null desc");
+static FlashBwdArgs to_bwd_args(const ptk_flash_bwd_desc* d) {
   FlashBwdArgs a;
   a.Q = (const bf16_t*)d->Q; a.K = (const bf16_t*)d->K; a.V = (const bf16_t*)d->V; a.O = (const bf16_t*)d->O;
   a.dO = (const bf16_t*)d->dO; a.lse = d->lse; a.delta = d->delta;
@@ -128,7 +127,19 @@ int ptk_flash_attn_bwd(const ptk_flash_bwd_desc* d, void* stream) {
   a.ldo = d->ldo; a.sO0 = d->sO0; a.sO1 = d->sO1; a.omap = to_map(d->omap);
   a.qdiv = d->qdiv > 0 ? d->qdiv : 1; a.causal = d->causal; a.window = d->window;
   a.key_valid = d->key_valid; a.scale = d->scale;
-  return launch_attn_bwd(a, d->batch > 0 ? d->batch : 1, ST);
+  a.dkv_part = (float*)d->workspace;
+  a.dkv_part_bytes = d->workspace && d->workspace_bytes > 0 ? (size_t)d->workspace_bytes : 0;
+  return a;
+}
+
+size_t ptk_flash_bwd_workspace_bytes(const ptk_flash_bwd_desc* d) {
+  if (!d) return 0;
+  return attn_bwd_workspace_bytes(to_bwd_args(d), d->batch > 0 ? d->batch : 1);
+}
+
+int ptk_flash_attn_bwd(const ptk_flash_bwd_desc* d, void* stream) {
+  if (!d) return set_error("flash_bwd: null desc");
+  return launch_attn_bwd(to_bwd_args(d), d->batch > 0 ? d->batch : 1, ST);
 }
 
 // ---------------------------------------------------------------- projector

@@ -19,6 +19,7 @@
 // Writes O (bf16, row-remapped) and LSE = ln(sum exp(score)) per row (fp32)
 // for the backward.  Semantics: softmax(scale * Q K^T + mask) V, as
 // TF/models/siglip/modeling_siglip.py:289-300 and gemma3 :365-379 (sdpa).
+#include <algorithm>
 #include "common.h"
 #include "ptk_internal.h"
 
@@ -38,22 +39,51 @@ PTK_DEV int swz_k(int r) { return D == 256 ? (r & 15) : ((r >> 1) & 7); }     //
 template <int D>
 PTK_DEV int swz_v(int r) { return D == 256 ? 2 * (r & 7) : 2 * ((r >> 1) & 3); }  // ds_read_b64_tr_b16
 
+
+// s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a literal)
+PTK_DEV void vm_wait(int n) {
+  switch (n) {
+#define PTK_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
+    PTK_VMW(0) PTK_VMW(1) PTK_VMW(2) PTK_VMW(3) PTK_VMW(4) PTK_VMW(5) PTK_VMW(6) PTK_VMW(7)
+    PTK_VMW(8) PTK_VMW(9) PTK_VMW(10) PTK_VMW(11) PTK_VMW(12) PTK_VMW(13) PTK_VMW(14) PTK_VMW(15)
+    PTK_VMW(16) PTK_VMW(17) PTK_VMW(18) PTK_VMW(19) PTK_VMW(20)
+#undef PTK_VMW
+    default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
+  }
+}
+
+// K/V tiles of 32 keys in a 4-deep LDS ring (tile t+3 staged while tile t computes); every wave
+// issues the same number of LDS-DMA ops per tile (its share of K, V and, when present, 4 of the
+// tile's key_valid flags), so one counted vmcnt serves all waves.
+constexpr int FA_KT = 32, FA_NBUF = 4;
+template <int D>
+struct FaRing {
+  static constexpr int CPR = D / 8;                      // 16-B chunks per row
+  static constexpr int TILE = FA_KT * D * 2;             // one K or V tile
+  static constexpr int INST = FA_KT * CPR / 64;          // wave-instructions per tensor per tile
+  static constexpr int PER_WAVE = INST >= 8 ? INST / 8 : 1;   // per tensor per wave (8 waves)
+  static constexpr int KV_OFF = FA_NBUF * 2 * TILE;      // key_valid flags, 128 B per buffer
+  static constexpr int BYTES = KV_OFF + FA_NBUF * 128;
+};
+
 template <int D>
 __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
-  constexpr int CPR = D / 8;                 // 16-B chunks per row
-  constexpr int TILE_BYTES = 64 * D * 2;     // one K or V tile
+  using R = FaRing<D>;
   constexpr int KS = D / 32;                 // MFMA k-steps over the head dim
   constexpr int DS = D / 16;                 // 16-wide d sub-tiles
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];   // K0 V0 K1 V1
+  __shared__ __attribute__((aligned(16))) char smem[R::BYTES];   // (K, V) x4, key_valid x4
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const int z = blockIdx.y, z0 = z / a.zin, z1 = z - z0 * a.zin;
-  const int r0 = blockIdx.x * 128;
+  // heaviest (latest, for causal) row blocks first; z fastest
+  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
+  const int z = blockIdx.x % nz, z0 = z / a.zin, z1 = z - z0 * a.zin;
+  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;
   const bf16_t* Q = a.Q + z0 * a.sQ0 + z1 * a.sQ1;
   const bf16_t* K = a.K + z0 * a.sK0 + z1 * a.sK1;
   const bf16_t* V = a.V + z0 * a.sK0 + z1 * a.sK1;
   const long b = z / a.zdiv;
+  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
 
   // key range of the block (causal / window skip)
   const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
@@ -63,7 +93,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     k_hi = min(k_hi, pos_hi + 1);
     if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
   }
-  const int t_lo = k_lo / 64, t_hi = (k_hi + 63) / 64;
+  const int t_lo = k_lo / FA_KT, t_hi = (k_hi + FA_KT - 1) / FA_KT;
 
   // Q fragments: B operand of S^T = K Q^T, lane holds Q[row c16][8g + 32ks .. +7]
   const int qrow = r0 + wave * 16 + c16;
@@ -77,23 +107,32 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
   }
   const int qpos = qrow_c / a.qdiv;
 
-  // staging: wave-instruction i covers 64 chunks = (64 / CPR) rows of the tile
-  constexpr int ROWS_PER_INST = 64 / CPR;
-  constexpr int INSTS = 64 * CPR / 64 / 8;   // per wave per tile (K or V)
+  const int ops = (R::INST >= 8 ? 2 * R::PER_WAVE : 1) + (kvl ? 1 : 0);   // LDS-DMA ops per wave per tile
   auto stage = [&](int t, int buf) {
-    char* kb = smem + buf * 2 * TILE_BYTES;
-    char* vb = kb + TILE_BYTES;
+    char* kb = smem + buf * 2 * R::TILE;
+    char* vb = kb + R::TILE;
+    if constexpr (R::INST >= 8) {
 #pragma unroll
-    for (int j = 0; j < INSTS; ++j) {
-      const int inst = wave * INSTS + j;
-      const int row = inst * ROWS_PER_INST + lane / CPR;
-      const int pch = lane % CPR;
-      const int key = min(t * 64 + row, a.nkeys - 1);
-      const bf16_t* ks_ = K + (long)key * a.ldk + 8 * (pch ^ swz_k<D>(row));
-      const bf16_t* vs_ = V + (long)key * a.ldk + 8 * (pch ^ swz_v<D>(row));
-      fa_glds16(ks_, kb + inst * 1024);
-      fa_glds16(vs_, vb + inst * 1024);
+      for (int j = 0; j < R::PER_WAVE; ++j) {
+        const int inst = wave * R::PER_WAVE + j;
+        const int row = inst * (64 / R::CPR) + lane / R::CPR;
+        const int pch = lane % R::CPR;
+        const int key = min(t * FA_KT + row, a.nkeys - 1);
+        fa_glds16(K + (long)key * a.ldk + 8 * (pch ^ swz_k<D>(row)), kb + inst * 1024);
+        fa_glds16(V + (long)key * a.ldk + 8 * (pch ^ swz_v<D>(row)), vb + inst * 1024);
+      }
+    } else {   // fewer than 8 wave-instructions per tensor: waves split K / V
+      const int inst = wave & (R::INST - 1);
+      const int row = inst * (64 / R::CPR) + lane / R::CPR;
+      const int pch = lane % R::CPR;
+      const int key = min(t * FA_KT + row, a.nkeys - 1);
+      if (wave < R::INST)
+        fa_glds16(K + (long)key * a.ldk + 8 * (pch ^ swz_k<D>(row)), kb + inst * 1024);
+      else
+        fa_glds16(V + (long)key * a.ldk + 8 * (pch ^ swz_v<D>(row)), vb + inst * 1024);
     }
+    if (kvl && lane == 0)   // 4 flags per wave
+      fa_glds16(kvl + min(t * FA_KT + 4 * wave, a.nkeys - 4), smem + R::KV_OFF + buf * 128 + wave * 16);
   };
 
   f32x4_t o[DS];
@@ -102,19 +141,22 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
   float m_run = -INFINITY, l_run = 0.f;
   const float sl2 = a.scale * 1.4426950408889634f;   // scores in log2 units
 
-  if (t_lo < t_hi) stage(t_lo, 0);
-  for (int t = t_lo; t < t_hi; ++t) {
-    const int buf = (t - t_lo) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + 1 < t_hi) stage(t + 1, buf ^ 1);
-    const char* kb = smem + buf * 2 * TILE_BYTES;
-    const char* vb = kb + TILE_BYTES;
-
-    // ---- S^T = K Q^T : acc[ms] holds keys 16ms + 4g + j, query column c16
-    f32x4_t s[4];
 #pragma unroll
-    for (int ms = 0; ms < 4; ++ms) {
+  for (int i = 0; i < FA_NBUF - 1; ++i)
+    if (t_lo + i < t_hi) stage(t_lo + i, i);
+  for (int t = t_lo; t < t_hi; ++t) {
+    const int buf = (t - t_lo) & (FA_NBUF - 1);
+    vm_wait(ops * min(FA_NBUF - 2, t_hi - 1 - t));
+    __syncthreads();
+    if (t + FA_NBUF - 1 < t_hi) stage(t + FA_NBUF - 1, (buf + FA_NBUF - 1) & (FA_NBUF - 1));
+    const char* kb = smem + buf * 2 * R::TILE;
+    const char* vb = kb + R::TILE;
+    const int* kvs = reinterpret_cast<const int*>(smem + R::KV_OFF + buf * 128);
+
+    // ---- S^T = K Q^T : s[ms] holds keys 16ms + 4g + j, query column c16
+    f32x4_t s[2];
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms) {
       s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
       const int row = ms * 16 + c16;
 #pragma unroll
@@ -127,11 +169,11 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     // ---- mask + online softmax (log2 domain)
     float mt = -INFINITY;
 #pragma unroll
-    for (int ms = 0; ms < 4; ++ms) {
-      const int kbase = t * 64 + ms * 16 + 4 * g;
+    for (int ms = 0; ms < 2; ++ms) {
+      const int kbase = t * FA_KT + ms * 16 + 4 * g;
       int kv[4] = {1, 1, 1, 1};
-      if (a.key_valid) {
-        const int4 v4 = *reinterpret_cast<const int4*>(a.key_valid + b * a.nkeys + min(kbase, a.nkeys - 4));
+      if (kvl) {
+        const int4 v4 = *reinterpret_cast<const int4*>(kvs + ms * 16 + 4 * g);
         kv[0] = v4.x; kv[1] = v4.y; kv[2] = v4.z; kv[3] = v4.w;
       }
 #pragma unroll
@@ -149,16 +191,17 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
     const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m_run - m_new);
+    const float msub = (m_new == -INFINITY) ? 0.f : m_new;
     float rs = 0.f;
-    bf16x8_t pf[2];
+    bf16x8_t pf;
 #pragma unroll
-    for (int ms = 0; ms < 4; ++ms)
+    for (int ms = 0; ms < 2; ++ms)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float p = (s[ms][j] == -INFINITY) ? 0.f : exp2f(s[ms][j] - m_new);
+        const float p = exp2f(s[ms][j] - msub);   // exp2(-inf) = 0 for masked keys
         const bf16_t pb = f2bf(p);
         rs += bf2f(pb);
-        pf[ms >> 1][(ms & 1) * 4 + j] = (short)pb;
+        pf[ms * 4 + j] = (short)pb;
       }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
@@ -167,23 +210,20 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
 #pragma unroll
     for (int i = 0; i < DS; ++i) o[i] *= alpha;
 
-    // ---- O^T += V^T P^T : A = V^T (tr reads), k order = {16(2s)+4g+0..3, 16(2s+1)+4g+0..3}
+    // ---- O^T += V^T P^T : A = V^T (tr reads), k order = {4g+0..3, 16+4g+0..3}
     const int q4 = c16 >> 2, p4 = c16 & 3;
 #pragma unroll
     for (int ds = 0; ds < DS; ++ds) {
+      bf16x8_t vf;
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8_t vf;
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int row = (2 * st + hh) * 16 + 4 * g + q4;
-          const int ch = (2 * ds + (p4 >> 1)) ^ swz_v<D>(row);
-          const char* addr = vb + row * (D * 2) + ch * 16 + 8 * (p4 & 1);
-          const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
-          vf[4 * hh + 0] = r[0]; vf[4 * hh + 1] = r[1]; vf[4 * hh + 2] = r[2]; vf[4 * hh + 3] = r[3];
-        }
-        o[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[st], o[ds], 0, 0, 0);
+      for (int hh = 0; hh < 2; ++hh) {
+        const int row = hh * 16 + 4 * g + q4;
+        const int ch = (2 * ds + (p4 >> 1)) ^ swz_v<D>(row);
+        const char* addr = vb + row * (D * 2) + ch * 16 + 8 * (p4 & 1);
+        const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
+        vf[4 * hh + 0] = r[0]; vf[4 * hh + 1] = r[1]; vf[4 * hh + 2] = r[2]; vf[4 * hh + 3] = r[3];
       }
+      o[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[ds], 0, 0, 0);
     }
   }
 
@@ -233,26 +273,28 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(FlashBwdArgs a, int nz)
 
 template <int D>
 __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
-  constexpr int CPR = D / 8;
-  constexpr int TILE_BYTES = 64 * D * 2;
+  using R = FaRing<D>;
   constexpr int KS = D / 32;
   constexpr int DS = D / 16;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];   // K0 V0 K1 V1
+  __shared__ __attribute__((aligned(16))) char smem[R::BYTES];   // (K, V) x4, key_valid x4
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
-  const long z = blockIdx.y;
-  const int r0 = blockIdx.x * 128;
+  // heaviest (latest, for causal) row blocks first; z fastest
+  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
+  const long z = blockIdx.x % nz;
+  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;
   const bf16_t* K = a.K + z * (long)a.nkeys * D;
   const bf16_t* V = a.V + z * (long)a.nkeys * D;
   const long b = z / a.zdiv;
+  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
   const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
   int k_hi = a.nkeys, k_lo = 0;
   if (a.causal) {
     k_hi = min(k_hi, pos_hi + 1);
     if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
   }
-  const int t_lo = k_lo / 64, t_hi = (k_hi + 63) / 64;
+  const int t_lo = k_lo / FA_KT, t_hi = (k_hi + FA_KT - 1) / FA_KT;
 
   const int qrow = r0 + wave * 16 + c16;
   const int qrow_c = min(qrow, a.rows - 1);
@@ -269,38 +311,52 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
   const int qpos = qrow_c / a.qdiv;
   const float sl2 = a.scale * L2E;
 
-  constexpr int ROWS_PER_INST = 64 / CPR;
-  constexpr int INSTS = CPR / 8;
+  const int ops = (R::INST >= 8 ? 2 * R::PER_WAVE : 1) + (kvl ? 1 : 0);
   auto stage = [&](int t, int buf) {
-    char* kb = smem + buf * 2 * TILE_BYTES;
-    char* vb = kb + TILE_BYTES;
+    char* kb = smem + buf * 2 * R::TILE;
+    char* vb = kb + R::TILE;
+    if constexpr (R::INST >= 8) {
 #pragma unroll
-    for (int j = 0; j < INSTS; ++j) {
-      const int inst = wave * INSTS + j;
-      const int row = inst * ROWS_PER_INST + lane / CPR;
-      const int pch = lane % CPR;
-      const int key = min(t * 64 + row, a.nkeys - 1);
-      const int lch = pch ^ swz_k<D>(row);
-      fa_glds16(K + (long)key * D + 8 * lch, kb + inst * 1024);
-      fa_glds16(V + (long)key * D + 8 * lch, vb + inst * 1024);
+      for (int j = 0; j < R::PER_WAVE; ++j) {
+        const int inst = wave * R::PER_WAVE + j;
+        const int row = inst * (64 / R::CPR) + lane / R::CPR;
+        const int lch = (lane % R::CPR) ^ swz_k<D>(row);
+        const int key = min(t * FA_KT + row, a.nkeys - 1);
+        fa_glds16(K + (long)key * D + 8 * lch, kb + inst * 1024);
+        fa_glds16(V + (long)key * D + 8 * lch, vb + inst * 1024);
+      }
+    } else {
+      const int inst = wave & (R::INST - 1);
+      const int row = inst * (64 / R::CPR) + lane / R::CPR;
+      const int lch = (lane % R::CPR) ^ swz_k<D>(row);
+      const int key = min(t * FA_KT + row, a.nkeys - 1);
+      if (wave < R::INST)
+        fa_glds16(K + (long)key * D + 8 * lch, kb + inst * 1024);
+      else
+        fa_glds16(V + (long)key * D + 8 * lch, vb + inst * 1024);
     }
+    if (kvl && lane == 0)
+      fa_glds16(kvl + min(t * FA_KT + 4 * wave, a.nkeys - 4), smem + R::KV_OFF + buf * 128 + wave * 16);
   };
 
   f32x4_t acc[DS];
 #pragma unroll
   for (int i = 0; i < DS; ++i) acc[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 
-  if (t_lo < t_hi) stage(t_lo, 0);
-  for (int t = t_lo; t < t_hi; ++t) {
-    const int buf = (t - t_lo) & 1;
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
-    if (t + 1 < t_hi) stage(t + 1, buf ^ 1);
-    const char* kb = smem + buf * 2 * TILE_BYTES;
-    const char* vb = kb + TILE_BYTES;
-    f32x4_t s[4], dp[4];
 #pragma unroll
-    for (int ms = 0; ms < 4; ++ms) {
+  for (int i = 0; i < FA_NBUF - 1; ++i)
+    if (t_lo + i < t_hi) stage(t_lo + i, i);
+  for (int t = t_lo; t < t_hi; ++t) {
+    const int buf = (t - t_lo) & (FA_NBUF - 1);
+    vm_wait(ops * min(FA_NBUF - 2, t_hi - 1 - t));
+    __syncthreads();
+    if (t + FA_NBUF - 1 < t_hi) stage(t + FA_NBUF - 1, (buf + FA_NBUF - 1) & (FA_NBUF - 1));
+    const char* kb = smem + buf * 2 * R::TILE;
+    const char* vb = kb + R::TILE;
+    const int* kvs = reinterpret_cast<const int*>(smem + R::KV_OFF + buf * 128);
+    f32x4_t s[2], dp[2];
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms) {
       s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
       dp[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
       const int row = ms * 16 + c16;
@@ -313,13 +369,13 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
         dp[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[ks], dp[ms], 0, 0, 0);
       }
     }
-    bf16x8_t dsf[2];
+    bf16x8_t dsf;
 #pragma unroll
-    for (int ms = 0; ms < 4; ++ms) {
-      const int kbase = t * 64 + ms * 16 + 4 * g;
+    for (int ms = 0; ms < 2; ++ms) {
+      const int kbase = t * FA_KT + ms * 16 + 4 * g;
       int kv[4] = {1, 1, 1, 1};
-      if (a.key_valid) {
-        const int4 v4 = *reinterpret_cast<const int4*>(a.key_valid + b * a.nkeys + min(kbase, a.nkeys - 4));
+      if (kvl) {
+        const int4 v4 = *reinterpret_cast<const int4*>(kvs + ms * 16 + 4 * g);
         kv[0] = v4.x; kv[1] = v4.y; kv[2] = v4.z; kv[3] = v4.w;
       }
 #pragma unroll
@@ -328,27 +384,24 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
         bool ok = key < a.nkeys && kv[j] != 0;
         if (a.causal) ok = ok && key <= qpos;
         if (a.window > 0) ok = ok && key > qpos - a.window;
-        const float p = ok ? exp2f(s[ms][j] * sl2 - lse2) : 0.f;
+        const float p = exp2f(ok ? s[ms][j] * sl2 - lse2 : -INFINITY);
         const float d = bfround(p) * (dp[ms][j] - dlt);
-        dsf[ms >> 1][(ms & 1) * 4 + j] = (short)f2bf(d);
+        dsf[ms * 4 + j] = (short)f2bf(d);
       }
     }
     const int q4 = c16 >> 2, p4 = c16 & 3;
 #pragma unroll
     for (int ds = 0; ds < DS; ++ds) {
+      bf16x8_t kt;
 #pragma unroll
-      for (int st = 0; st < 2; ++st) {
-        bf16x8_t kt;
-#pragma unroll
-        for (int hh = 0; hh < 2; ++hh) {
-          const int row = (2 * st + hh) * 16 + 4 * g + q4;
-          const int ch = (2 * ds + (p4 >> 1)) ^ swz_k<D>(row);
-          const char* addr = kb + row * (D * 2) + ch * 16 + 8 * (p4 & 1);
-          const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
-          kt[4 * hh + 0] = r[0]; kt[4 * hh + 1] = r[1]; kt[4 * hh + 2] = r[2]; kt[4 * hh + 3] = r[3];
-        }
-        acc[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, dsf[st], acc[ds], 0, 0, 0);
+      for (int hh = 0; hh < 2; ++hh) {
+        const int row = hh * 16 + 4 * g + q4;
+        const int ch = (2 * ds + (p4 >> 1)) ^ swz_k<D>(row);
+        const char* addr = kb + row * (D * 2) + ch * 16 + 8 * (p4 & 1);
+        const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
+        kt[4 * hh + 0] = r[0]; kt[4 * hh + 1] = r[1]; kt[4 * hh + 2] = r[2]; kt[4 * hh + 3] = r[3];
       }
+      acc[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, dsf, acc[ds], 0, 0, 0);
     }
   }
   if (qrow >= a.rows) return;
@@ -370,7 +423,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
   constexpr int TILE_BYTES = 64 * D * 2;     // 64 query rows of Q or dO
   constexpr int KS = D / 32;
   constexpr int DS = D / 16;
-  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES];   // Q0 dO0 Q1 dO1
+  __shared__ __attribute__((aligned(16))) char smem[4 * TILE_BYTES + 2 * 512];   // Q0 dO0 Q1 dO1, (lse|delta) x2
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
@@ -415,6 +468,11 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
       fa_glds16(Qz + (long)qr * D + 8 * lch, qb + inst * 1024);
       fa_glds16(dOz + (long)qr * D + 8 * lch, ob + inst * 1024);
     }
+    // the chunk's 64 LSE and 64 delta values ride in the same LDS-DMA batch (rows % 64 == 0)
+    if (wave == 0 && lane < 32) {
+      const float* srcv = (lane < 16 ? a.lse : a.delta) + z * a.rows + c * 64 + 4 * (lane & 15);
+      fa_glds16(srcv, smem + 4 * TILE_BYTES + buf * 512);
+    }
   };
 
   f32x4_t dv[DS], dk[DS];
@@ -449,8 +507,9 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
           dp = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[ks], dp, 0, 0, 0);
         }
         const int qbase = c * 64 + qt * 16 + 4 * g;
-        const float4 l4 = *reinterpret_cast<const float4*>(a.lse + z * a.rows + min(qbase, a.rows - 4));
-        const float4 d4 = *reinterpret_cast<const float4*>(a.delta + z * a.rows + min(qbase, a.rows - 4));
+        const float* ld = reinterpret_cast<const float*>(smem + 4 * TILE_BYTES + buf * 512);
+        const float4 l4 = *reinterpret_cast<const float4*>(ld + qt * 16 + 4 * g);
+        const float4 d4 = *reinterpret_cast<const float4*>(ld + 64 + qt * 16 + 4 * g);
         const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
 #pragma unroll
         for (int j = 0; j < 4; ++j) {
@@ -499,12 +558,320 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
   }
 }
 
+
+// ---------------------------------------------------------------- dK/dV, head_dim 256
+// 4 waves x 32 keys = one 128-key slab per workgroup.  K/V fragments of the wave's 32 keys stay in
+// registers (B operands), dK^T/dV^T (256 fp32 per lane) accumulate in the AGPR half of the 512-entry
+// file (one wave per SIMD); 32-row Q/dO chunks (+ their LSE/delta) arrive by LDS-DMA, double-buffered.
+// Per chunk and wave: 128 MFMAs against 64 KB of LDS reads (half the bytes/MFMA of 16 keys/wave).
+// Causal slabs differ up to 11x in query rows, so a slab with more than `dkv_target` chunks is cut
+// into query pieces (~equal chunks); pieces of a split slab write fp32 partials that
+// attn_dkv_reduce_kernel sums in piece order (deterministic).  Blocks are ordered slab-major,
+// heaviest slabs first.
+constexpr int DKV_KEYS = 128, DKV_CH = 32;
+
+__host__ __device__ inline void dkv_slab_chunks(const FlashBwdArgs& a, int s, int& c_lo, int& c_hi) {
+  int r_lo = 0, r_hi = a.rows;
+  if (a.causal) {
+    r_lo = min(a.rows, s * DKV_KEYS * a.qdiv);
+    if (a.window > 0) r_hi = min(a.rows, (s * DKV_KEYS + DKV_KEYS + a.window - 1) * a.qdiv);
+  }
+  c_lo = r_lo / DKV_CH;
+  c_hi = max(c_lo, (r_hi + DKV_CH - 1) / DKV_CH);
+}
+__host__ __device__ inline int dkv_pieces(const FlashBwdArgs& a, int s) {
+  int lo, hi;
+  dkv_slab_chunks(a, s, lo, hi);
+  const int n = hi - lo;
+  return (a.dkv_target <= 0 || n <= a.dkv_target) ? 1 : (n + a.dkv_target - 1) / a.dkv_target;
+}
+
+__global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a) {
+  constexpr int D = 256, KS = D / 32, DS = D / 16;
+  constexpr int TILE = DKV_CH * D * 2;   // 16 KiB: 32 rows of Q or dO
+  constexpr int NBUF = 4;                 // ring depth: chunk c+3 is staged while chunk c computes
+  __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE + NBUF * 256];   // (Q, dO) x4, (lse|delta) x4
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int g = lane >> 4, c16 = lane & 15;
+  // ---- block -> (slab, piece, z)
+  const int nz = a.nz;
+  int L = blockIdx.x, s = 0, P = 1, base = 0;
+  for (;;) {
+    P = dkv_pieces(a, s);
+    if (L < P * nz) break;
+    L -= P * nz;
+    if (P > 1) base += P;
+    ++s;
+  }
+  const int piece = L / nz;
+  const long z = L - piece * nz;
+  int c0, c1;
+  {
+    int lo, hi;
+    dkv_slab_chunks(a, s, lo, hi);
+    const int n = hi - lo;
+    c0 = lo + (int)((long)piece * n / P);
+    c1 = lo + (int)((long)(piece + 1) * n / P);
+  }
+  const long b = z / a.zdiv;
+  const int kw = s * DKV_KEYS + wave * 32;   // the wave's first key
+
+  bf16x8_t kf[2][KS], vf[2][KS];
+  int key[2];
+  bool kok[2];
+#pragma unroll
+  for (int kg = 0; kg < 2; ++kg) {
+    key[kg] = kw + 16 * kg + c16;
+    const int kc = min(key[kg], a.nkeys - 1);
+    const long ko = (z * a.nkeys + kc) * (long)D + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[kg][ks] = *reinterpret_cast<const bf16x8_t*>(a.K + ko + 32 * ks);
+      vf[kg][ks] = *reinterpret_cast<const bf16x8_t*>(a.V + ko + 32 * ks);
+    }
+    kok[kg] = key[kg] < a.nkeys && (!a.key_valid || a.key_valid[b * a.nkeys + kc] != 0);
+  }
+  const bf16_t* Qz = a.Q + z * (long)a.rows * D;
+  const bf16_t* dOz = a.dO + z * (long)a.rows * D;
+  const float L2E = 1.4426950408889634f;
+  const float sl2 = a.scale * L2E;
+  const int qshift = (a.qdiv & (a.qdiv - 1)) == 0 ? __builtin_ctz(a.qdiv) : -1;
+
+  // staging: 32 rows x 32 16-B chunks per tensor = 16 wave-instructions, 4 per wave, plus one
+  // 64-B piece of the chunk's LSE|delta per wave (lanes 0-3): 9 LDS-DMA ops per wave per chunk,
+  // so one counted vmcnt serves every wave
+  auto stage = [&](int c, int buf) {
+    char* qb = smem + buf * 2 * TILE;
+    char* ob = qb + TILE;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int inst = wave * 4 + j;
+      const int row = inst * 2 + (lane >> 5);
+      const int lch = (lane & 31) ^ (row & 15);
+      const long src = (long)(c * DKV_CH + row) * D + 8 * lch;
+      fa_glds16(Qz + src, qb + inst * 1024);
+      fa_glds16(dOz + src, ob + inst * 1024);
+    }
+    if (lane < 4) {
+      const int item = wave * 4 + lane;   // 0-7 LSE, 8-15 delta (4 floats each)
+      const float* srcv = (item < 8 ? a.lse : a.delta) + z * a.rows + c * DKV_CH + 4 * (item & 7);
+      fa_glds16(srcv, smem + NBUF * 2 * TILE + buf * 256 + wave * 64);
+    }
+  };
+
+  f32x4_t dv[DS][2], dk[DS][2];
+#pragma unroll
+  for (int i = 0; i < DS; ++i)
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg) {
+      dv[i][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      dk[i][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    }
+  const int q4 = c16 >> 2, p4 = c16 & 3;
+#pragma unroll
+  for (int i = 0; i < NBUF - 1; ++i)
+    if (c0 + i < c1) stage(c0 + i, i);
+  for (int c = c0; c < c1; ++c) {
+    const int buf = (c - c0) & (NBUF - 1);
+    // chunk c landed; chunks c+1, c+2 may stay in flight (9 ops each)
+    const int ahead = min(NBUF - 2, c1 - 1 - c);
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();   // every wave's share landed; every wave is done reading chunk c-1's buffer
+    if (c + NBUF - 1 < c1) stage(c + NBUF - 1, (buf + NBUF - 1) & (NBUF - 1));
+    const char* qb = smem + buf * 2 * TILE;
+    const char* ob = qb + TILE;
+    const float* ld = reinterpret_cast<const float*>(smem + NBUF * 2 * TILE + buf * 256);
+
+    // ---- S = Q K^T, dP = dO V^T for 32 rows x 32 keys (key on the lane)
+    f32x4_t sc[2][2], dp[2][2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg) {
+        sc[qt][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        dp[qt][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const int row = qt * 16 + c16;
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int ch = (ks * 4 + g) ^ (row & 15);
+        const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(qb + row * (D * 2) + ch * 16);
+        const bf16x8_t oa = *reinterpret_cast<const bf16x8_t*>(ob + row * (D * 2) + ch * 16);
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          sc[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kg][ks], sc[qt][kg], 0, 0, 0);
+          dp[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[kg][ks], dp[qt][kg], 0, 0, 0);
+        }
+      }
+    }
+    // ---- P = exp(S*scale - LSE) (bf16), dS = P (dP - delta) (bf16); k order of the next products:
+    //      slot 4qt + j of lane group g <-> query row 16qt + 4g + j
+    bf16x8_t pf[2], dsf[2];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float4 l4 = *reinterpret_cast<const float4*>(ld + qt * 16 + 4 * g);
+      const float4 d4 = *reinterpret_cast<const float4*>(ld + 32 + qt * 16 + 4 * g);
+      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int qrow = c * DKV_CH + qt * 16 + 4 * g + j;
+        const int pos = qshift >= 0 ? (qrow >> qshift) : qrow / a.qdiv;
+#pragma unroll
+        for (int kg = 0; kg < 2; ++kg) {
+          bool ok = kok[kg];
+          if (a.causal) ok = ok && key[kg] <= pos;
+          if (a.window > 0) ok = ok && key[kg] > pos - a.window;
+          const float p = exp2f(ok ? sc[qt][kg][j] * sl2 - lv[j] * L2E : -INFINITY);   // branch-free mask
+          const bf16_t pb = f2bf(p);
+          pf[kg][4 * qt + j] = (short)pb;
+          dsf[kg][4 * qt + j] = (short)f2bf(bf2f(pb) * (dp[qt][kg][j] - dl[j]));
+        }
+      }
+    }
+    // ---- dV^T += dO^T P, dK^T += Q^T dS (A operands by transposed LDS reads)
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      bf16x8_t ot, qt_;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int row = hh * 16 + 4 * g + q4;
+        const int ch = (2 * ds + (p4 >> 1)) ^ (row & 15);
+        const int off = row * (D * 2) + ch * 16 + 8 * (p4 & 1);
+        const s16x4_t ro = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(ob + off));
+        const s16x4_t rq = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(qb + off));
+        ot[4 * hh + 0] = ro[0]; ot[4 * hh + 1] = ro[1]; ot[4 * hh + 2] = ro[2]; ot[4 * hh + 3] = ro[3];
+        qt_[4 * hh + 0] = rq[0]; qt_[4 * hh + 1] = rq[1]; qt_[4 * hh + 2] = rq[2]; qt_[4 * hh + 3] = rq[3];
+      }
+#pragma unroll
+      for (int kg = 0; kg < 2; ++kg) {
+        dv[ds][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ot, pf[kg], dv[ds][kg], 0, 0, 0);
+        dk[ds][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt_, dsf[kg], dk[ds][kg], 0, 0, 0);
+      }
+    }
+  }
+  // ---- outputs: lane holds dV^T[16ds + 4g + j][key]
+  if (P == 1) {
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg) {
+      if (key[kg] >= a.nkeys) continue;
+      bf16_t* dvp = a.dV + (z * a.nkeys + key[kg]) * (long)D + 4 * g;
+      bf16_t* dkp = a.dK + (z * a.nkeys + key[kg]) * (long)D + 4 * g;
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) {
+        u16x4_t uv, uk;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uv[j] = f2bf(dv[ds][kg][j]);
+          uk[j] = f2bf(dk[ds][kg][j] * a.scale);
+        }
+        *reinterpret_cast<u16x4_t*>(dvp + 16 * ds) = uv;
+        *reinterpret_cast<u16x4_t*>(dkp + 16 * ds) = uk;
+      }
+    }
+  } else {
+    // partial slot [base + piece][z]: [dK | dV][128 keys][D] fp32
+    float* part = a.dkv_part + ((long)(base + piece) * nz + z) * (2L * DKV_KEYS * D);
+#pragma unroll
+    for (int kg = 0; kg < 2; ++kg) {
+      const int kl = wave * 32 + 16 * kg + c16;
+      float* pk = part + (long)kl * D + 4 * g;
+      float* pv = pk + (long)DKV_KEYS * D;
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) {
+        *reinterpret_cast<float4*>(pk + 16 * ds) = make_float4(dk[ds][kg][0], dk[ds][kg][1], dk[ds][kg][2], dk[ds][kg][3]);
+        *reinterpret_cast<float4*>(pv + 16 * ds) = make_float4(dv[ds][kg][0], dv[ds][kg][1], dv[ds][kg][2], dv[ds][kg][3]);
+      }
+    }
+  }
+}
+
+// sums the partials of every split slab in piece order -> bf16 dK (x scale), dV
+__global__ void __launch_bounds__(256) attn_dkv_reduce_kernel(FlashBwdArgs a) {
+  constexpr int D = 256;
+  const int s = blockIdx.y;
+  const int P = dkv_pieces(a, s);
+  if (P == 1) return;
+  int base = 0;
+  for (int t = 0; t < s; ++t) {
+    const int pt = dkv_pieces(a, t);
+    if (pt > 1) base += pt;
+  }
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;   // float4 index in [nz][2][128][D/4]
+  const long per_z = 2L * DKV_KEYS * D / 4;
+  if (i >= (long)a.nz * per_z) return;
+  const long z = i / per_z;
+  const long r = i - z * per_z;
+  const int which = (int)(r / (DKV_KEYS * D / 4));        // 0 = dK, 1 = dV
+  const int kl = (int)((r / (D / 4)) % DKV_KEYS);
+  const int d4 = (int)(r % (D / 4));
+  const int key = s * DKV_KEYS + kl;
+  if (key >= a.nkeys) return;
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int pc = 0; pc < P; ++pc) {
+    const float4 v = reinterpret_cast<const float4*>(a.dkv_part + ((long)(base + pc) * a.nz + z) * (2L * DKV_KEYS * D))[r];
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  const float m = which == 0 ? a.scale : 1.f;
+  u16x4_t u;
+  u[0] = f2bf(acc.x * m); u[1] = f2bf(acc.y * m); u[2] = f2bf(acc.z * m); u[3] = f2bf(acc.w * m);
+  bf16_t* out = (which == 0 ? a.dK : a.dV) + (z * a.nkeys + key) * (long)D + 4 * d4;
+  *reinterpret_cast<u16x4_t*>(out) = u;
+}
+
+static int num_cus() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0, v = 0;
+    if (hipGetDevice(&dev) == hipSuccess &&
+        hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, dev) == hipSuccess && v > 0)
+      n = v;
+    else
+      n = 256;
+  }
+  return n;
+}
+
+// split plan: target chunks per piece = total chunks / CUs (at least 4)
+static void dkv_plan(FlashBwdArgs& a, int nz, int& nslab, long& npieces, long& nsplit) {
+  a.nz = nz;
+  nslab = (a.nkeys + DKV_KEYS - 1) / DKV_KEYS;
+  long total = 0;
+  for (int s = 0; s < nslab; ++s) {
+    int lo, hi;
+    a.dkv_target = 0;
+    dkv_slab_chunks(a, s, lo, hi);
+    total += hi - lo;
+  }
+  a.dkv_target = (int)std::max(4L, (total * nz + num_cus() - 1) / num_cus());
+  npieces = 0;
+  nsplit = 0;
+  for (int s = 0; s < nslab; ++s) {
+    const int P = dkv_pieces(a, s);
+    npieces += P;
+    if (P > 1) nsplit += P;
+  }
+}
+
+size_t attn_bwd_workspace_bytes(const FlashBwdArgs& a0, int nz) {
+  if (a0.D != 256 || a0.rows <= 0 || nz <= 0) return 0;
+  FlashBwdArgs a = a0;
+  int nslab;
+  long np, ns;
+  dkv_plan(a, nz, nslab, np, ns);
+  return (size_t)ns * nz * 2 * DKV_KEYS * 256 * sizeof(float);
+}
+
 int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st) {
   if (a.rows <= 0 || nz <= 0) return 0;
   if (a.rows % 64 || a.nkeys % 64) return set_error("attn_bwd: rows (%d) and keys (%d) must be multiples of 64",
                                                    a.rows, a.nkeys);
   if (a.ldo & 7) return set_error("attn_bwd: O stride must be a multiple of 8");
-  const dim3 gd((unsigned)((long)nz * a.rows / 4 + 1)), gq((unsigned)((a.rows + 127) / 128), (unsigned)nz),
+  const dim3 gd((unsigned)((long)nz * a.rows / 4 + 1)), gq((unsigned)((long)((a.rows + 127) / 128) * nz)),
       gk((unsigned)(a.nkeys / 64), (unsigned)nz);
   switch (a.D) {
     case 64:
@@ -512,11 +879,24 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st) {
       hipLaunchKernelGGL(attn_bwd_dkv_kernel<64>, gk, dim3(256), 0, st, a);
       hipLaunchKernelGGL(attn_bwd_dq_kernel<64>, gq, dim3(512), 0, st, a);
       break;
-    case 256:
-      hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, a, nz);
-      hipLaunchKernelGGL(attn_bwd_dkv_kernel<256>, gk, dim3(256), 0, st, a);
-      hipLaunchKernelGGL(attn_bwd_dq_kernel<256>, gq, dim3(512), 0, st, a);
+    case 256: {
+      FlashBwdArgs b = a;
+      int nslab;
+      long np, ns;
+      dkv_plan(b, nz, nslab, np, ns);
+      if (ns > 0 && (!b.dkv_part || b.dkv_part_bytes < (size_t)ns * nz * 2 * DKV_KEYS * 256 * sizeof(float))) {
+        b.dkv_target = 0;   // no workspace: every slab in one piece
+        np = nslab;
+        ns = 0;
+      }
+      hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
+      hipLaunchKernelGGL(attn_bwd_dkv256_kernel, dim3((unsigned)(np * nz)), dim3(256), 0, st, b);
+      if (ns > 0)
+        hipLaunchKernelGGL(attn_dkv_reduce_kernel, dim3((unsigned)((nz * 2L * DKV_KEYS * 64 + 255) / 256), (unsigned)nslab),
+                           dim3(256), 0, st, b);
+      hipLaunchKernelGGL(attn_bwd_dq_kernel<256>, gq, dim3(512), 0, st, b);
       break;
+    }
     default: return set_error("attn_bwd: head_dim %d unsupported (64, 256)", a.D);
   }
   return hipGetLastError() == hipSuccess ? 0 : set_error("attn_bwd launch failed");
@@ -527,7 +907,9 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
   if (a.nkeys < 4) return set_error("attn_fwd: nkeys must be >= 4");
   if ((a.ldq | a.ldk | a.ldo) & 7) return set_error("attn_fwd: row strides must be multiples of 8");
   if (a.key_valid && (a.nkeys & 3)) return set_error("attn_fwd: key_valid rows must be a multiple of 4");
-  dim3 grid((unsigned)((a.rows + 127) / 128), (unsigned)nz);
+  const long nblk = (long)((a.rows + 127) / 128) * nz;
+  if (nblk > 0x7fffffffL) return set_error("attn_fwd: too many blocks");
+  dim3 grid((unsigned)nblk);
   switch (a.D) {
     case 64: hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(512), 0, st, a); break;
     case 256: hipLaunchKernelGGL(attn_fwd_kernel<256>, grid, dim3(512), 0, st, a); break;

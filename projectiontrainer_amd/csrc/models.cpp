@@ -12,6 +12,7 @@
 //   Q [B,Hkv,S,G,D] (rows (s,j) contiguous), K/V [B,Hkv,S,D], scores/P
 //   [B*Hkv, S*G, S].  QK^T and P.V run on the MFMA GEMM; masks/softmax are
 //   row kernels.
+#include <algorithm>
 #include <math.h>
 #include <string.h>
 
@@ -94,6 +95,8 @@ struct GemmaWs {
   std::vector<GemmaLayerSave> L;
   bf16_t *P, *xn, *O, *h, *Vt, *Kt, *Qt, *dqkv, *dgu, *dao, *dO, *dS, *dST, *PT, *dOT, *dQ, *dK, *dV, *xf, *logits;
   float *S, *dtmp, *rstd_f, *row_loss, *dxf, *dxf_part, *count, *gscale, *delta;
+  float* dkv_part;          // split-query dK/dV partials of the attention backward
+  size_t dkv_part_bytes;
   int32_t* key_valid;
 };
 
@@ -135,6 +138,15 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp)
   w.Qt = nullptr;
   w.S = nullptr;
   w.delta = bp.take<float>(Z * SG);
+  {
+    FlashBwdArgs fa;
+    fa.rows = (int)SG; fa.nkeys = Sp; fa.D = (int)D; fa.qdiv = (int)G; fa.causal = 1;
+    size_t nb = attn_bwd_workspace_bytes(fa, (int)Z);
+    fa.window = c->sliding_window;
+    if (c->sliding_window > 0) nb = std::max(nb, attn_bwd_workspace_bytes(fa, (int)Z));
+    w.dkv_part_bytes = nb;
+    w.dkv_part = nb ? bp.take<float>((long)(nb / sizeof(float))) : nullptr;
+  }
   w.dqkv = bp.take<bf16_t>(M * Dqkv);
   w.dgu = bp.take<bf16_t>(M * 2 * I);
   w.dtmp = bp.take<float>(M * H);
@@ -349,6 +361,7 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
       fb.qdiv = G; fb.causal = 1; fb.window = sliding ? c->sliding_window : 0;
       fb.key_valid = w.key_valid;
       fb.scale = scale;
+      fb.dkv_part = w.dkv_part; fb.dkv_part_bytes = w.dkv_part_bytes;
       CK(launch_attn_bwd(fb, Z, st));
     }
     CK(launch_qknorm_rope_bwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, sv.rstd_q, sv.rstd_k, w.dQ, w.dK, w.dV, w.dqkv,

@@ -135,8 +135,15 @@ struct FlashBwdArgs {
   int qdiv = 1, causal = 0, window = 0;
   const int32_t* key_valid = nullptr;
   float scale = 1.f;
+  // D = 256 dK/dV split-query workspace (fp32 partials); null -> no split (correct, less balanced)
+  float* dkv_part = nullptr;
+  size_t dkv_part_bytes = 0;
+  // set by launch_attn_bwd
+  int dkv_target = 0, nz = 1;
 };
 int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st);
+// bytes of dkv_part for which launch_attn_bwd splits every heavy key slab (0 when it never splits)
+size_t attn_bwd_workspace_bytes(const FlashBwdArgs& a, int nz);
 
 // ---- misc (misc.hip) ----
 // batched 2-D transpose of bf16 [nz][rows][cols] (ld_in) -> [nz][cols][rows] (ld_out); zero-fills

@@ -147,8 +147,10 @@ def flash_attn(Q, K, V, O, *, rows, nkeys, head_dim, ldq, ldk, ldo, batch, batch
 
 
 def flash_attn_bwd(Q, K, V, O, dO, lse, *, rows, nkeys, head_dim, batch, batch_inner=1, zdiv=1, ldo=None,
-                   sO=(0, 0), omap=(0, 0, 0, 0), qdiv=1, causal=False, window=0, key_valid=None, scale=1.0):
-    """Flash attention backward (ptk_flash_attn_bwd) -> (dQ, dK, dV) in the Q / K layouts."""
+                   sO=(0, 0), omap=(0, 0, 0, 0), qdiv=1, causal=False, window=0, key_valid=None, scale=1.0,
+                   split=True):
+    """Flash attention backward (ptk_flash_attn_bwd) -> (dQ, dK, dV) in the Q / K layouts.
+    split=False passes no workspace (every key slab in one piece)."""
     _require_cuda(Q, K, V, O, dO, lse)
     dQ, dK, dV = torch.empty_like(Q), torch.empty_like(K), torch.empty_like(V)
     delta = torch.empty(batch * rows, dtype=torch.float32, device=Q.device)
@@ -162,5 +164,11 @@ def flash_attn_bwd(Q, K, V, O, dO, lse, *, rows, nkeys, head_dim, batch, batch_i
     d.omap = L.RowMap(*omap)
     d.qdiv, d.causal, d.window = qdiv, int(causal), window
     d.key_valid, d.scale = ptr(key_valid), scale
+    ws = None
+    if split:
+        nb = L.lib().ptk_flash_bwd_workspace_bytes(d)
+        if nb:
+            ws = torch.empty(nb, dtype=torch.uint8, device=Q.device)
+            d.workspace, d.workspace_bytes = ptr(ws), nb
     check(L.lib().ptk_flash_attn_bwd(d, L.stream_ptr(Q.device)), "flash_attn_bwd")
     return dQ, dK, dV

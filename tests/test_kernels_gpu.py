@@ -284,7 +284,7 @@ def test_flash_fwd_gemma_layout(gpu, Hkv, G, window):
     Vt = rnd(B, Hkv, S, hd, dev=gpu, seed=43)
     kv = torch.ones(B, S, dtype=torch.int32, device=gpu)
     kv[0, 200:215] = 0
-    kv[1, 290:] = 0
+    kv[1, S - 30:] = 0
     O = torch.zeros(B * S, Hq * hd, dtype=torch.bfloat16, device=gpu)
     lse = torch.zeros(B * Hkv, S * G, dtype=torch.float32, device=gpu)
     scale = 256 ** -0.5
@@ -307,12 +307,15 @@ def test_flash_fwd_gemma_layout(gpu, Hkv, G, window):
     torch.testing.assert_close(lg, lref, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("D,Hkv,G,window", [(256, 1, 4, 0), (256, 1, 4, 100), (256, 2, 2, 64), (64, 1, 2, 8)])
-def test_flash_bwd_vs_autograd(gpu, D, Hkv, G, window):
+@pytest.mark.parametrize("D,Hkv,G,window,S,split", [(256, 1, 4, 0, 320, True), (256, 1, 4, 0, 320, False),
+                                                     (256, 1, 4, 100, 320, True), (256, 2, 2, 64, 320, True),
+                                                     (256, 1, 4, 0, 704, True), (64, 1, 2, 8, 320, True)])
+def test_flash_bwd_vs_autograd(gpu, D, Hkv, G, window, S, split):
     """dQ/dK/dV of softmax(scale QK^T + causal/window/key-pad mask) V vs torch autograd (fp32 math on the
-    same bf16 inputs).  Uses the forward kernel's O and LSE as the backward does."""
+    same bf16 inputs).  Uses the forward kernel's O and LSE as the backward does.  split: heavy key slabs
+    cut into query pieces (fp32 partials + ordered reduce) vs one piece per slab; S 704 = the cfg2 length."""
     Kn, L = _k()
-    B, S = 2, 320
+    B = 2
     Hq = Hkv * G
     Q = rnd(B * Hkv, S * G, D, dev=gpu, seed=51)
     Kt = rnd(B * Hkv, S, D, dev=gpu, seed=52)
@@ -320,7 +323,7 @@ def test_flash_bwd_vs_autograd(gpu, D, Hkv, G, window):
     dO = rnd(B * Hkv, S * G, D, dev=gpu, seed=54)
     kv = torch.ones(B, S, dtype=torch.int32, device=gpu)
     kv[0, 200:215] = 0
-    kv[1, 290:] = 0
+    kv[1, S - 30:] = 0
     scale = D ** -0.5
     O = torch.zeros(B * Hkv, S * G, D, dtype=torch.bfloat16, device=gpu)
     lse = torch.zeros(B * Hkv, S * G, dtype=torch.float32, device=gpu)
@@ -328,7 +331,7 @@ def test_flash_bwd_vs_autograd(gpu, D, Hkv, G, window):
                   window=window, key_valid=kv, scale=scale)
     Kn.flash_attn(Q, Kt, Vt, O, lse=lse, ldq=D, ldk=D, ldo=D,
                   strides=(Hkv * S * G * D, S * G * D, Hkv * S * D, S * D, Hkv * S * G * D, S * G * D), **common)
-    dQ, dK, dV = Kn.flash_attn_bwd(Q, Kt, Vt, O, dO, lse, sO=(Hkv * S * G * D, S * G * D), **common)
+    dQ, dK, dV = Kn.flash_attn_bwd(Q, Kt, Vt, O, dO, lse, sO=(Hkv * S * G * D, S * G * D), split=split, **common)
     # reference: rows (s, j) of each z, position s = r // G
     q = Q.float().requires_grad_(True)
     k = Kt.float().requires_grad_(True)
