@@ -13,13 +13,8 @@ typedef __attribute__((ext_vector_type(8))) unsigned short u16x8_t;
 
 PTK_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 
-// round-to-nearest-even f32 -> bf16 (NaN stays NaN)
-PTK_DEV bf16_t f2bf(float f) {
-  uint32_t u = __float_as_uint(f);
-  if ((u & 0x7f800000u) == 0x7f800000u && (u & 0x007fffffu)) return (bf16_t)((u >> 16) | 0x40);
-  u += 0x7fffu + ((u >> 16) & 1u);
-  return (bf16_t)(u >> 16);
-}
+// round-to-nearest-even f32 -> bf16 (NaN stays NaN): one v_cvt_pk_bf16_f32 (adjacent pairs pack)
+PTK_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 PTK_DEV float bfround(float f) { return bf2f(f2bf(f)); }
 
 PTK_DEV float warp_sum(float v) {

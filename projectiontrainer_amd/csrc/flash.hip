@@ -106,6 +106,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * ks);
   }
   const int qpos = qrow_c / a.qdiv;
+  const int causal = a.causal != 0, nowin = a.window <= 0;
 
   const int ops = (R::INST >= 8 ? 2 * R::PER_WAVE : 1) + (kvl ? 1 : 0);   // LDS-DMA ops per wave per tile
   auto stage = [&](int t, int buf) {
@@ -179,9 +180,8 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int key = kbase + j;
-        bool ok = key < a.nkeys && kv[j] != 0;
-        if (a.causal) ok = ok && key <= qpos;
-        if (a.window > 0) ok = ok && key > qpos - a.window;
+        const int ok = (int)(key < a.nkeys) & (int)(kv[j] != 0) & ((int)(key <= qpos) | !causal) &
+                       ((int)(key > qpos - a.window) | nowin);
         const float v = ok ? s[ms][j] * sl2 : -INFINITY;
         s[ms][j] = v;
         mt = fmaxf(mt, v);
@@ -190,7 +190,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
-    const float alpha = (m_new == -INFINITY) ? 1.f : exp2f(m_run - m_new);
+    const float alpha = (m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m_run - m_new);
     const float msub = (m_new == -INFINITY) ? 0.f : m_new;
     float rs = 0.f;
     bf16x8_t pf;
@@ -198,7 +198,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     for (int ms = 0; ms < 2; ++ms)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float p = exp2f(s[ms][j] - msub);   // exp2(-inf) = 0 for masked keys
+        const float p = __builtin_amdgcn_exp2f(s[ms][j] - msub);   // exp2(-inf) = 0 for masked keys
         const bf16_t pb = f2bf(p);
         rs += bf2f(pb);
         pf[ms * 4 + j] = (short)pb;
@@ -310,6 +310,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
   const float dlt = a.delta[z * a.rows + qrow_c];
   const int qpos = qrow_c / a.qdiv;
   const float sl2 = a.scale * L2E;
+  const int causal = a.causal != 0, nowin = a.window <= 0;
 
   const int ops = (R::INST >= 8 ? 2 * R::PER_WAVE : 1) + (kvl ? 1 : 0);
   auto stage = [&](int t, int buf) {
@@ -381,10 +382,9 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int key = kbase + j;
-        bool ok = key < a.nkeys && kv[j] != 0;
-        if (a.causal) ok = ok && key <= qpos;
-        if (a.window > 0) ok = ok && key > qpos - a.window;
-        const float p = exp2f(ok ? s[ms][j] * sl2 - lse2 : -INFINITY);
+        const int ok = (int)(key < a.nkeys) & (int)(kv[j] != 0) & ((int)(key <= qpos) | !causal) &
+                       ((int)(key > qpos - a.window) | nowin);
+        const float p = __builtin_amdgcn_exp2f(ok ? s[ms][j] * sl2 - lse2 : -INFINITY);
         const float d = bfround(p) * (dp[ms][j] - dlt);
         dsf[ms * 4 + j] = (short)f2bf(d);
       }
@@ -518,7 +518,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
           bool ok = key_ok && q < a.rows;
           if (a.causal) ok = ok && key <= pos;
           if (a.window > 0) ok = ok && key > pos - a.window;
-          const float p = ok ? exp2f(s[j] * sl2 - lv[j] * L2E) : 0.f;
+          const float p = ok ? __builtin_amdgcn_exp2f(s[j] * sl2 - lv[j] * L2E) : 0.f;
           const bf16_t pb = f2bf(p);
           pf[4 * hh + j] = (short)pb;
           dsf[4 * hh + j] = (short)f2bf(bf2f(pb) * (dp[j] - dl[j]));
@@ -637,6 +637,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
   const float L2E = 1.4426950408889634f;
   const float sl2 = a.scale * L2E;
   const int qshift = (a.qdiv & (a.qdiv - 1)) == 0 ? __builtin_ctz(a.qdiv) : -1;
+  const int causal = a.causal != 0, nowin = a.window <= 0;
 
   // staging: 32 rows x 32 16-B chunks per tensor = 16 wave-instructions, 4 per wave, plus one
   // 64-B piece of the chunk's LSE|delta per wave (lanes 0-3): 9 LDS-DMA ops per wave per chunk,
@@ -723,10 +724,9 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
         const int pos = qshift >= 0 ? (qrow >> qshift) : qrow / a.qdiv;
 #pragma unroll
         for (int kg = 0; kg < 2; ++kg) {
-          bool ok = kok[kg];
-          if (a.causal) ok = ok && key[kg] <= pos;
-          if (a.window > 0) ok = ok && key[kg] > pos - a.window;
-          const float p = exp2f(ok ? sc[qt][kg][j] * sl2 - lv[j] * L2E : -INFINITY);   // branch-free mask
+          // branch-free mask (short-circuit && turns into exec-mask control flow per element)
+          const int ok = (int)kok[kg] & ((int)(key[kg] <= pos) | !causal) & ((int)(key[kg] > pos - a.window) | nowin);
+          const float p = __builtin_amdgcn_exp2f(ok ? sc[qt][kg][j] * sl2 - lv[j] * L2E : -INFINITY);
           const bf16_t pb = f2bf(p);
           pf[kg][4 * qt + j] = (short)pb;
           dsf[kg][4 * qt + j] = (short)f2bf(bf2f(pb) * (dp[qt][kg][j] - dl[j]));
