@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 from projectiontrainer_amd import _lib as L  # noqa: E402
 from projectiontrainer_amd import weights as W  # noqa: E402
 from projectiontrainer_amd.config import PRESETS  # noqa: E402
-from projectiontrainer_amd.flops import flops_per_image, geglu_gemm_flops  # noqa: E402
+from projectiontrainer_amd.flops import flops_per_image, geglu_step_flops  # noqa: E402
 from projectiontrainer_amd.stage1 import Stage1Engine  # noqa: E402
 
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md, chip table)
@@ -147,7 +147,8 @@ def main():
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic_geglu.json")
     if os.path.exists(pmc) and args.config == "cfg2" and cfg.batch_size == 32:
         traffic = json.load(open(pmc))["traffic_bytes_per_launch"]   # rocprofv3 --pmc passes (tools/pmc_traffic.py)
-    achieved = geglu_gemm_flops(cfg) / (geglu_ms / 1e3) / 1e12
+    # algorithmic FLOPs of every timed gate|up launch / their summed HIP-event time
+    achieved = geglu_step_flops(cfg) * args.steps / (tot.value / 1e3) / 1e12
     line = {
         "metric": "Stage-1 images/sec/node (SigLIP-L-384 + Gemma3-1B, 576+128 tok)",
         "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
@@ -157,7 +158,8 @@ def main():
                                f"Gemma3-1B frozen fwd/bwd, {cfg.num_vision_tokens} vis + {cfg.text_len} text tokens",
                    "global_batch": world * cfg.batch_size, "per_gpu_batch": cfg.batch_size,
                    "seq_len": cfg.seq_len, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "gemm_big_kernel<ACT_GEGLU> (Gemma3 gate|up projection, 2*(B*S)*(2I)*H FLOP per launch)",
+        "roofline": {"bound": "mfma", "kernel": "gemm_big_kernel<ACT_GEGLU> (Gemma3 gate|up projection: 2*(B*S)*(2I)*H FLOP per launch, "
+                               "last layer 2*(B*T)*(2I)*H)",
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",

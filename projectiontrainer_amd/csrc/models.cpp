@@ -271,6 +271,9 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
   w.x[0] = bt->x;
   CK(launch_rmsnorm_fwd(w.x[0], H, RowMap{0, 0, 0, 0}, wt->layers[0].ln_in, w.xn, w.L[0].rstd_in, M, H, eps, st));
 
+  // position Nv-1+t predicts token t: the only rows the loss reads from the last layer
+  const RowMap lossmap{T, 0, Sp, Nv - 1};
+
   // ---------------- forward
   for (int l = 0; l < nl; ++l) {
     const ptk_gemma3_layer& L = wt->layers[l];
@@ -299,20 +302,30 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
     CK(launch_gemm(gemm(sv.O, Dq, L.wo, Dq, sv.ao, H, M, H, Dq), ACT_NONE, OUT_BF16, 1, st));
     CK(launch_residual_norm_fwd(sv.ao, w.x[l], L.ln_post_attn, L.ln_pre_ff, sv.x2, w.xn, sv.rstd_ao, sv.rstd_pre, M,
                                 H, eps, st));
-    {
+    if (l + 1 < nl) {
       GemmArgs g = gemm(w.xn, H, L.wgu, H, w.h, I, M, 2 * I, H);
       g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
       CK(launch_gemm(g, ACT_GEGLU, OUT_BF16, 1, st));
+      CK(launch_gemm(gemm(w.h, I, L.wd, I, sv.dn, H, M, H, I), ACT_NONE, OUT_BF16, 1, st));
+    } else {
+      // last layer: only the loss rows reach the loss, so its MLP runs on those R rows (h, g, u compact);
+      // the other rows of dn are zero (their residual output is never read, their gradient is zero)
+      GemmArgs g = gemm(w.xn, H, L.wgu, H, w.h, I, R, 2 * I, H);
+      g.amap = lossmap;
+      g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
+      CK(launch_gemm(g, ACT_GEGLU, OUT_BF16, 1, st));
+      CK(hipMemsetAsync(sv.dn, 0, (size_t)M * H * sizeof(bf16_t), st) != hipSuccess);
+      GemmArgs g2 = gemm(w.h, I, L.wd, I, sv.dn, H, R, H, I);
+      g2.cmap = lossmap;
+      CK(launch_gemm(g2, ACT_NONE, OUT_BF16, 1, st));
     }
-    CK(launch_gemm(gemm(w.h, I, L.wd, I, sv.dn, H, M, H, I), ACT_NONE, OUT_BF16, 1, st));
     const float* wnext = (l + 1 < nl) ? wt->layers[l + 1].ln_in : nullptr;
     float* rnext = (l + 1 < nl) ? w.L[l + 1].rstd_in : nullptr;
     CK(launch_residual_norm_fwd(sv.dn, sv.x2, L.ln_post_ff, wnext, w.x[l + 1], w.xn, sv.rstd_dn, rnext, M, H, eps,
                                 st));
   }
 
-  // ---------------- loss (text-predicting rows only: position Nv-1+t predicts token t)
-  const RowMap lossmap{T, 0, Sp, Nv - 1};
+  // ---------------- loss (text-predicting rows only)
   CK(launch_rmsnorm_fwd(w.x[nl], H, lossmap, wt->final_norm, w.xf, w.rstd_f, R, H, eps, st));
   CK(launch_gemm(gemm(w.xf, H, wt->embed, H, w.logits, V, R, V, H), ACT_NONE, OUT_BF16, 1, st));
   CK(launch_count_valid(bt->labels, R, bt->loss_scale, w.gscale, w.count, st));
@@ -339,9 +352,20 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
     // MLP half
     CK(launch_post_norm_bwd(dR, sv.dn, L.ln_post_ff, sv.rstd_dn, w.dao, M, H, st));
     // dh = dd . Wd (plain GEMM at full MFMA rate), then the GEGLU backward as one streaming pass
-    CK(launch_gemm(gemm(w.dao, H, L.wd_t, H, w.h, I, M, I, H), ACT_NONE, OUT_BF16, 1, st));
-    CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, M, I, st));
-    CK(launch_gemm(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), ACT_NONE, OUT_F32, 1, st));
+    if (l + 1 < nl) {
+      CK(launch_gemm(gemm(w.dao, H, L.wd_t, H, w.h, I, M, I, H), ACT_NONE, OUT_BF16, 1, st));
+      CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, M, I, st));
+      CK(launch_gemm(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), ACT_NONE, OUT_F32, 1, st));
+    } else {   // last layer: MLP gradient is non-zero on the loss rows only (compact h, g, u, dgu)
+      GemmArgs g = gemm(w.dao, H, L.wd_t, H, w.h, I, R, I, H);
+      g.amap = lossmap;
+      CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
+      CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, R, I, st));
+      CK(hipMemsetAsync(w.dtmp, 0, (size_t)M * H * sizeof(float), st) != hipSuccess);
+      GemmArgs g2 = gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, R, H, 2 * I);
+      g2.cmap = lossmap;
+      CK(launch_gemm(g2, ACT_NONE, OUT_F32, 1, st));
+    }
     CK(launch_residual_norm_bwd(sv.x2, L.ln_pre_ff, sv.rstd_pre, w.dtmp, dR, sv.ao, L.ln_post_attn, sv.rstd_ao, w.dao,
                                 M, H, st));
     {  // dO (Q layout) = dao . Wo, one GEMM per kv head group of output columns

@@ -43,3 +43,11 @@ def geglu_gemm_flops(cfg: Stage1Config) -> float:
     """One Gemma3 gate|up projection launch (the step's largest kernel): 2·(B·S)·(2I)·H."""
     t = cfg.text
     return 2.0 * cfg.batch_size * cfg.seq_len * 2 * t.intermediate_size * t.hidden_size
+
+
+def geglu_step_flops(cfg: Stage1Config) -> float:
+    """Algorithmic FLOPs of all gate|up launches of one step: layers 0..L-2 on all B·S rows, the
+    last layer on the B·T loss rows only (its other rows never reach the loss: libptk skips them)."""
+    t = cfg.text
+    per_row = 2.0 * 2 * t.intermediate_size * t.hidden_size
+    return per_row * cfg.batch_size * (cfg.seq_len * (t.num_hidden_layers - 1) + cfg.text_len)
