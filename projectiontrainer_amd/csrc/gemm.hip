@@ -613,9 +613,185 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
   PTK_STAMP(3);
 }
 
+
+template <int ACT, int OUT>
+__global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * EPI_WAVE_BYTES];   // 136 KiB >= 2 * BUF_BYTES
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
+
+  const int nbm = (p.M + BIG - 1) / BIG, nbn = (p.N + BIG - 1) / BIG;
+  const int ntile = nbm * nbn;
+  int bid = blockIdx.x;
+  {
+    const int q = ntile >> 3, rr = ntile & 7, x = bid & 7;
+    bid = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (bid >> 3);
+  }
+  const int per_group = GROUP_M * nbn;
+  const int first_m = (bid / per_group) * GROUP_M;
+  const int gsz = min(nbm - first_m, GROUP_M);
+  const int bm = first_m + (bid % per_group) % gsz;
+  const int bn = (bid % per_group) / gsz;
+
+  const bf16_t* A = p.A;
+  const bf16_t* B = p.B;
+  // staging sources: half-tile h (0,1 = A halves, 2,3 = B halves), instruction j (0,1):
+  // lane writes LDS row (wave*16 + j*8 + (lane>>3)) of the half, chunk (lane&7)
+  const int sr = lane >> 3, sc = lane & 7;
+  const bf16_t* src[4][2];
+#pragma unroll
+  for (int h = 0; h < 4; ++h)
+#pragma unroll
+    for (int j = 0; j < 2; ++j) {
+      const int lr = wave * 16 + j * 8 + sr;               // row within the half-tile
+      const int lc = sc ^ ((lr >> 1) & 7);
+      if (h < 2) {
+        const long gm = min((long)bm * BIG + h * 128 + lr, (long)p.M - 1);
+        src[h][j] = A + map_row(p.amap, gm) * p.lda + lc * 8;
+      } else {
+        const long gn = min((long)bn * BIG + (h - 2) * 128 + lr, (long)p.N - 1);
+        src[h][j] = B + gn * p.ldb + lc * 8;
+      }
+    }
+  auto stage = [&](int h, int t) {
+    char* dst = smem + (t & 1) * BUF_BYTES + h * HALF_BYTES + wave * 16 * 128;
+    glds16(src[h][0] + (long)t * BK, dst);
+    glds16(src[h][1] + (long)t * BK, dst + 8 * 128);
+  };
+
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  const int frag_off = (lane & 15) * 128 + (((lane >> 4) ^ ((lane >> 1) & 7)) << 4);
+  const int nt = p.K / BK;
+  // prologue: K-tile 0 complete, B halves of K-tile 1 in flight
+  stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
+  if (nt > 1) {
+    stage(2, 1); stage(3, 1);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  __builtin_amdgcn_s_barrier();
+
+  // wave groups wr = 0 / wr = 1 run one barrier apart (half a phase): on every SIMD one wave of the
+  // pair issues its LDS reads while the other runs its MFMA cluster.  Each phase: reads + DMA issue,
+  // barrier, MFMA cluster, barrier.
+  if (__builtin_amdgcn_readfirstlane(wr) == 1) __builtin_amdgcn_s_barrier();
+  bf16x8_t a[4][2], b0[2][2], b1[2][2];
+  for (int t = 0; t < nt; ++t) {
+    const char* buf = smem + (t & 1) * BUF_BYTES;
+    const char* As = buf + wr * HALF_BYTES;
+    const char* Bs = buf + (2 + (wc >> 1)) * HALF_BYTES + (wc & 1) * 64 * 128;
+    // ---- phase 0: A(mh0), B(nh0), B(nh1) fragments; DMA A0(t+1)
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        b0[n][ks] = *reinterpret_cast<const bf16x8_t*>(Bs + (n * 16) * 128 + (frag_off ^ (ks << 6)));
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        a[i][ks] = *reinterpret_cast<const bf16x8_t*>(As + (i * 16) * 128 + (frag_off ^ (ks << 6)));
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        b1[n][ks] = *reinterpret_cast<const bf16x8_t*>(Bs + (32 + n * 16) * 128 + (frag_off ^ (ks << 6)));
+    if (t + 1 < nt) stage(0, t + 1);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");   // A(mh0), B(nh0) landed
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b0[n][ks], acc[i][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    // every read of tile t's B region is complete before any wave can reach phase 2's DMA into it
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 1: DMA A1(t+1); A(mh0) x B(nh1), A(mh1) re-read into a[i] as a[i] is consumed
+    if (t + 1 < nt) stage(1, t + 1);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          acc[i][2 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b1[n][ks], acc[i][2 + n], 0, 0, 0);
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks)
+        a[i][ks] = *reinterpret_cast<const bf16x8_t*>(As + (64 + i * 16) * 128 + (frag_off ^ (ks << 6)));
+    }
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 2: DMA B0(t+2) (B of tile t is in registers since phase 0); A(mh1) x B(nh0)
+    if (t + 2 < nt) stage(2, t + 2);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          acc[4 + i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b0[n][ks], acc[4 + i][n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+    // ---- phase 3: DMA B1(t+2); retire K-tile t+1 (B(t+2) stays in flight); A(mh1) x B(nh1)
+    if (t + 2 < nt) {
+      stage(3, t + 2);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int ks = 0; ks < 2; ++ks)
+          acc[4 + i][2 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b1[n][ks], acc[4 + i][2 + n], 0, 0, 0);
+    __builtin_amdgcn_s_setprio(0);
+    __builtin_amdgcn_s_barrier();
+  }
+  if (__builtin_amdgcn_readfirstlane(wr) == 0) __builtin_amdgcn_s_barrier();
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  char* Cz = reinterpret_cast<char*>(p.C);
+  // the wave's 128x64 tile as two 64x64 halves through its private LDS region
+  f32x4_t (&top)[4][4] = *reinterpret_cast<f32x4_t(*)[4][4]>(&acc[0][0]);
+  f32x4_t (&bot)[4][4] = *reinterpret_cast<f32x4_t(*)[4][4]>(&acc[4][0]);
+  const long r0 = (long)bm * BIG + wr * 128, c0 = (long)bn * BIG + wc * 64;
+  epilogue<ACT, OUT>(p, smem, wave, lane, top, r0, c0, Cz);
+  __builtin_amdgcn_wave_barrier();
+  epilogue<ACT, OUT>(p, smem, wave, lane, bot, r0 + 64, c0, Cz);
+
+}
+
+
+
 // ---- optional live per-class timing (HIP events around launches; bench.py roofline)
 static bool g_timing = false;
-static int g_force_tiles = 0;   // tests: 1 = every GEMM on 128x128, 2 = single-batch GEMMs on 256x256
+static int g_force_tiles = 0;   // tests: 1 = every GEMM on 128x128, 2 / 4 = single-batch GEMMs on 256x256 / staggered 256x256
 void force_small_tiles(int mode) { g_force_tiles = mode; }
 static std::vector<hipEvent_t> g_ev[8];
 static size_t g_ev_used[8];
@@ -669,8 +845,32 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // 256x256 (one block per CU) only where the K loop amortises its lock-step epilogue: long K or
   // wide N at K >= 1152.  Elsewhere two co-resident 128x128 blocks per CU overlap one block's
   // epilogue with the other's MFMA and quantise better (tools/gemm_bench.py --all, r01).
-  const bool big = batch == 1 && g_force_tiles != 1 &&
-                   (g_force_tiles == 2 || (a.M >= 1024 && a.N >= 512 && (a.K >= 6144 || (a.N >= 6144 && a.K >= 1152))));
+  // long K: the barrier-staggered 256x256 variant (+6-7 % at K >= 4096, tools/gemm_bench.py --all)
+  const bool big_shape = a.M >= 1024 && a.N >= 512 && (a.K >= 6144 || (a.N >= 6144 && a.K >= 1152));
+  if (batch == 1 && (g_force_tiles == 4 || (g_force_tiles == 0 && big_shape && a.K >= 4096))) {
+    const long nb = (long)((a.M + BIG - 1) / BIG) * ((a.N + BIG - 1) / BIG);
+    dim3 g4((unsigned)nb, 1, 1);
+#define PTK_BIG2_CASE(ACT_, OUT_)                                                               \
+    if (act == ACT_ && out == OUT_) {                                                           \
+      hipEvent_t e0 = nullptr, e1 = nullptr;                                                    \
+      if (g_timing) { e0 = next_event(act); e1 = next_event(act); }                             \
+      if (e0) (void)hipEventRecord(e0, st);                                                     \
+      hipLaunchKernelGGL((gemm_big2_kernel<ACT_, OUT_>), g4, dim3(512), 0, st, a);              \
+      if (e1) (void)hipEventRecord(e1, st);                                                     \
+      return hipGetLastError() == hipSuccess ? 0 : set_error("gemm launch failed");            \
+    }
+    PTK_BIG2_CASE(ACT_NONE, OUT_BF16)
+    PTK_BIG2_CASE(ACT_NONE, OUT_F32)
+    PTK_BIG2_CASE(ACT_NONE, OUT_F32_BFR)
+    PTK_BIG2_CASE(ACT_GELU_TANH, OUT_BF16)
+    PTK_BIG2_CASE(ACT_GELU_ERF, OUT_BF16)
+    PTK_BIG2_CASE(ACT_GEGLU, OUT_BF16)
+    PTK_BIG2_CASE(ACT_GELU_ERF_BWD, OUT_BF16)
+    PTK_BIG2_CASE(ACT_GEGLU_BWD, OUT_BF16)
+#undef PTK_BIG2_CASE
+    return set_error("gemm: unsupported (act=%d, out=%d)", act, out);
+  }
+  const bool big = batch == 1 && g_force_tiles != 1 && (g_force_tiles == 2 || big_shape);
   if (big) {
     const long nb = (long)((a.M + BIG - 1) / BIG) * ((a.N + BIG - 1) / BIG);
     dim3 g2((unsigned)nb, 1, 1);

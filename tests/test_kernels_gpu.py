@@ -193,14 +193,16 @@ def test_cross_entropy(gpu):
     torch.testing.assert_close(lg.float(), x.grad, rtol=1e-2, atol=1e-6)
 
 
+@pytest.mark.parametrize("mode", [2, 4])
 @pytest.mark.parametrize("M,N,K", [(1024, 512, 64), (1024, 512, 128), (1100, 700, 192), (2048, 1152, 1152),
-                                   (4096, 1536, 256)])
-def test_gemm_big_tile_path(gpu, M, N, K):
-    """256x256 8-wave kernel (forced): ragged M/N, 1..18 K-tiles, vs fp32."""
+                                   (4096, 1536, 256), (300, 200, 64)])
+def test_gemm_big_tile_path(gpu, M, N, K, mode):
+    """256x256 8-wave kernel (mode 2) and its barrier-staggered variant (mode 4), forced: ragged M/N,
+    1..18 K-tiles, vs fp32."""
     Kn, L = _k()
     A, B = rnd(M, K, dev=gpu, seed=31), rnd(N, K, dev=gpu, seed=32)
     ref = A.float() @ B.float().T
-    L.lib().ptk_gemm_force_small_tiles(2)
+    L.lib().ptk_gemm_force_small_tiles(mode)
     try:
         C = Kn.gemm(A, B, out_dtype=torch.float32)
     finally:
@@ -208,9 +210,10 @@ def test_gemm_big_tile_path(gpu, M, N, K):
     torch.testing.assert_close(C, ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
 
 
-def test_gemm_big_vs_small_all_epilogues(gpu):
-    """Every epilogue through the 256x256 path equals the 128x128 path bit-for-bit
-    (same fp32 accumulation order per K-tile is not guaranteed, so compare at 1e-5)."""
+@pytest.mark.parametrize("mode", [2, 4])
+def test_gemm_big_vs_small_all_epilogues(gpu, mode):
+    """Every epilogue through the 256x256 (mode 2) / staggered 256x256 (mode 4) path matches the 128x128 path
+    (fp32 accumulation order differs, so compare at bf16-level tolerance)."""
     Kn, L = _k()
     from projectiontrainer_amd.gemma3 import interleave_gate_up
     M, N, K = 1300, 768, 320
@@ -219,8 +222,8 @@ def test_gemm_big_vs_small_all_epilogues(gpu):
     res = rnd(M, N, dev=gpu, dtype=torch.float32, seed=36)
     aux_in = rnd(M, N, dev=gpu, seed=37)
     outs = []
-    for mode in (2, 1):
-        L.lib().ptk_gemm_force_small_tiles(mode)
+    for md in (mode, 1):
+        L.lib().ptk_gemm_force_small_tiles(md)
         try:
             o = {}
             C = res.clone()

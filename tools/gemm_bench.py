@@ -23,6 +23,7 @@ SHAPES = [  # name, M, N, K, act, out dtype
     ("lm_head", 4096, 262144, 1152, L.ACT_NONE, torch.bfloat16),
     ("square_8192", 8192, 8192, 8192, L.ACT_NONE, torch.bfloat16),
 ]
+SQUARE = [("sq4096", 4096, 4096, 4096, L.ACT_NONE, torch.bfloat16), ("sq8192", 8192, 8192, 8192, L.ACT_NONE, torch.bfloat16)]
 
 
 def run(name, m, n, k, act, odt, reps=10):
@@ -69,13 +70,16 @@ ALL = [  # every single-batch GEMM of the cfg2 step: name, M, N, K, act, out
 ]
 
 if __name__ == "__main__" and "--all" in sys.argv:
-    for s in ALL:
+    for s in ALL + SQUARE:
         r = {}
-        for small in (0, 1, 0, 1):
-            L.lib().ptk_gemm_force_small_tiles(2 - small)
-            r[small] = run(*s)
-        print(json.dumps({"name": s[0], "M": s[1], "N": s[2], "K": s[3], "big_TF": r[0]["TFLOPs"],
-                          "small_TF": r[1]["TFLOPs"], "big_ms": r[0]["ms"], "small_ms": r[1]["ms"]}), flush=True)
+        for mode in (2, 1, 4, 2, 1, 4):   # second round kept (warm)
+            L.lib().ptk_gemm_force_small_tiles(mode)
+            r[mode] = run(*s)
+        L.lib().ptk_gemm_force_small_tiles(0)
+        r[0] = run(*s)
+        print(json.dumps({"name": s[0], "M": s[1], "N": s[2], "K": s[3], "big_TF": r[2]["TFLOPs"],
+                          "small_TF": r[1]["TFLOPs"], "big2_TF": r[4]["TFLOPs"], "auto_TF": r[0]["TFLOPs"]}),
+              flush=True)
     sys.exit(0)
 
 if __name__ == "__main__":
