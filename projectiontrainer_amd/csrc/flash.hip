@@ -38,6 +38,12 @@ template <int D>
 PTK_DEV int swz_k(int r) { return D == 256 ? (r & 15) : ((r >> 1) & 7); }     // ds_read_b128 row reads
 template <int D>
 PTK_DEV int swz_v(int r) { return D == 256 ? 2 * (r & 7) : 2 * ((r >> 1) & 3); }  // ds_read_b64_tr_b16
+// d 256 tiles read both by rows (ds_read_b128, 16 rows x one chunk) and transposed (ds_read_b64_tr_b16,
+// 8 rows x two adjacent chunks per 32-lane half): even values for rows 0-7, odd for 8-15 keeps both
+// patterns conflict-free (r & 15 alone leaves the transposed reads 2-way conflicted)
+PTK_DEV int swz_rt(int r) { return ((r & 7) << 1) | ((r >> 3) & 1); }
+template <int D>
+PTK_DEV int swz_kt(int r) { return D == 256 ? swz_rt(r) : swz_k<D>(r); }
 
 
 // s_waitcnt vmcnt(n) for a wave-uniform runtime n (the immediate must be a literal)
@@ -55,22 +61,29 @@ PTK_DEV void vm_wait(int n) {
 // K/V tiles of 32 keys in a 4-deep LDS ring (tile t+3 staged while tile t computes); every wave
 // issues the same number of LDS-DMA ops per tile (its share of K, V and, when present, 4 of the
 // tile's key_valid flags), so one counted vmcnt serves all waves.
-constexpr int FA_KT = 32, FA_NBUF = 4;
-template <int D>
+constexpr int FA_NBUF = 4;
+template <int D, int KT>
 struct FaRing {
   static constexpr int CPR = D / 8;                      // 16-B chunks per row
-  static constexpr int TILE = FA_KT * D * 2;             // one K or V tile
-  static constexpr int INST = FA_KT * CPR / 64;          // wave-instructions per tensor per tile
+  static constexpr int TILE = KT * D * 2;                // one K or V tile
+  static constexpr int INST = KT * CPR / 64;             // wave-instructions per tensor per tile
   static constexpr int PER_WAVE = INST >= 8 ? INST / 8 : 1;   // per tensor per wave (8 waves)
-  static constexpr int KV_OFF = FA_NBUF * 2 * TILE;      // key_valid flags, 128 B per buffer
-  static constexpr int BYTES = KV_OFF + FA_NBUF * 128;
+  static constexpr int KV_LANES = KT / 32;               // 16-B key_valid pieces per wave per tile
+  static constexpr int KV_OFF = FA_NBUF * 2 * TILE;      // key_valid flags, KT*4 B per buffer
+  static constexpr int BYTES = KV_OFF + FA_NBUF * KT * 4;
 };
+// key tile per head dim: d 256 keeps 32 keys (4 x 32 KiB ring); d 64 amortises the per-tile softmax,
+// barrier and DMA issue over 64 keys
+template <int D>
+constexpr int fa_kt() { return D == 256 ? 32 : 64; }
 
 template <int D>
 __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
-  using R = FaRing<D>;
+  constexpr int KT = fa_kt<D>();
+  using R = FaRing<D, KT>;
   constexpr int KS = D / 32;                 // MFMA k-steps over the head dim
   constexpr int DS = D / 16;                 // 16-wide d sub-tiles
+  constexpr int MS = KT / 16, ST = KT / 32;  // 16-key score sub-tiles, 32-key P.V k-steps
   __shared__ __attribute__((aligned(16))) char smem[R::BYTES];   // (K, V) x4, key_valid x4
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -93,7 +106,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     k_hi = min(k_hi, pos_hi + 1);
     if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
   }
-  const int t_lo = k_lo / FA_KT, t_hi = (k_hi + FA_KT - 1) / FA_KT;
+  const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
 
   // Q fragments: B operand of S^T = K Q^T, lane holds Q[row c16][8g + 32ks .. +7]
   const int qrow = r0 + wave * 16 + c16;
@@ -107,6 +120,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
   }
   const int qpos = qrow_c / a.qdiv;
   const int causal = a.causal != 0, nowin = a.window <= 0;
+  const bool unmasked = !kvl && !causal && nowin;
 
   const int ops = (R::INST >= 8 ? 2 * R::PER_WAVE : 1) + (kvl ? 1 : 0);   // LDS-DMA ops per wave per tile
   auto stage = [&](int t, int buf) {
@@ -118,7 +132,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
         const int inst = wave * R::PER_WAVE + j;
         const int row = inst * (64 / R::CPR) + lane / R::CPR;
         const int pch = lane % R::CPR;
-        const int key = min(t * FA_KT + row, a.nkeys - 1);
+        const int key = min(t * KT + row, a.nkeys - 1);
         fa_glds16(K + (long)key * a.ldk + 8 * (pch ^ swz_k<D>(row)), kb + inst * 1024);
         fa_glds16(V + (long)key * a.ldk + 8 * (pch ^ swz_v<D>(row)), vb + inst * 1024);
       }
@@ -126,14 +140,15 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
       const int inst = wave & (R::INST - 1);
       const int row = inst * (64 / R::CPR) + lane / R::CPR;
       const int pch = lane % R::CPR;
-      const int key = min(t * FA_KT + row, a.nkeys - 1);
+      const int key = min(t * KT + row, a.nkeys - 1);
       if (wave < R::INST)
         fa_glds16(K + (long)key * a.ldk + 8 * (pch ^ swz_k<D>(row)), kb + inst * 1024);
       else
         fa_glds16(V + (long)key * a.ldk + 8 * (pch ^ swz_v<D>(row)), vb + inst * 1024);
     }
-    if (kvl && lane == 0)   // 4 flags per wave
-      fa_glds16(kvl + min(t * FA_KT + 4 * wave, a.nkeys - 4), smem + R::KV_OFF + buf * 128 + wave * 16);
+    if (kvl && lane < R::KV_LANES)   // 4 flags per lane
+      fa_glds16(kvl + min(t * KT + 4 * (wave * R::KV_LANES + lane), a.nkeys - 4),
+                smem + R::KV_OFF + buf * (KT * 4) + wave * (R::KV_LANES * 16));
   };
 
   f32x4_t o[DS];
@@ -152,12 +167,12 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     if (t + FA_NBUF - 1 < t_hi) stage(t + FA_NBUF - 1, (buf + FA_NBUF - 1) & (FA_NBUF - 1));
     const char* kb = smem + buf * 2 * R::TILE;
     const char* vb = kb + R::TILE;
-    const int* kvs = reinterpret_cast<const int*>(smem + R::KV_OFF + buf * 128);
+    const int* kvs = reinterpret_cast<const int*>(smem + R::KV_OFF + buf * (KT * 4));
 
     // ---- S^T = K Q^T : s[ms] holds keys 16ms + 4g + j, query column c16
-    f32x4_t s[2];
+    f32x4_t s[MS];
 #pragma unroll
-    for (int ms = 0; ms < 2; ++ms) {
+    for (int ms = 0; ms < MS; ++ms) {
       s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
       const int row = ms * 16 + c16;
 #pragma unroll
@@ -169,22 +184,32 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     }
     // ---- mask + online softmax (log2 domain)
     float mt = -INFINITY;
+    if (unmasked && (t + 1) * KT <= a.nkeys) {   // full tile, no mask at all (SigLIP)
 #pragma unroll
-    for (int ms = 0; ms < 2; ++ms) {
-      const int kbase = t * FA_KT + ms * 16 + 4 * g;
-      int kv[4] = {1, 1, 1, 1};
-      if (kvl) {
-        const int4 v4 = *reinterpret_cast<const int4*>(kvs + ms * 16 + 4 * g);
-        kv[0] = v4.x; kv[1] = v4.y; kv[2] = v4.z; kv[3] = v4.w;
-      }
+      for (int ms = 0; ms < MS; ++ms)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int key = kbase + j;
-        const int ok = (int)(key < a.nkeys) & (int)(kv[j] != 0) & ((int)(key <= qpos) | !causal) &
-                       ((int)(key > qpos - a.window) | nowin);
-        const float v = ok ? s[ms][j] * sl2 : -INFINITY;
-        s[ms][j] = v;
-        mt = fmaxf(mt, v);
+        for (int j = 0; j < 4; ++j) {
+          s[ms][j] *= sl2;
+          mt = fmaxf(mt, s[ms][j]);
+        }
+    } else {
+#pragma unroll
+      for (int ms = 0; ms < MS; ++ms) {
+        const int kbase = t * KT + ms * 16 + 4 * g;
+        int kv[4] = {1, 1, 1, 1};
+        if (kvl) {
+          const int4 v4 = *reinterpret_cast<const int4*>(kvs + ms * 16 + 4 * g);
+          kv[0] = v4.x; kv[1] = v4.y; kv[2] = v4.z; kv[3] = v4.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int key = kbase + j;
+          const int ok = (int)(key < a.nkeys) & (int)(kv[j] != 0) & ((int)(key <= qpos) | !causal) &
+                         ((int)(key > qpos - a.window) | nowin);
+          const float v = ok ? s[ms][j] * sl2 : -INFINITY;
+          s[ms][j] = v;
+          mt = fmaxf(mt, v);
+        }
       }
     }
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
@@ -193,37 +218,42 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     const float alpha = (m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m_run - m_new);
     const float msub = (m_new == -INFINITY) ? 0.f : m_new;
     float rs = 0.f;
-    bf16x8_t pf;
+    bf16x8_t pf[ST];
 #pragma unroll
-    for (int ms = 0; ms < 2; ++ms)
+    for (int ms = 0; ms < MS; ++ms)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const float p = __builtin_amdgcn_exp2f(s[ms][j] - msub);   // exp2(-inf) = 0 for masked keys
         const bf16_t pb = f2bf(p);
         rs += bf2f(pb);
-        pf[ms * 4 + j] = (short)pb;
+        pf[ms >> 1][(ms & 1) * 4 + j] = (short)pb;
       }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
     l_run = l_run * alpha + rs;
     m_run = m_new;
+    if (__any(alpha != 1.f)) {   // no row's running max moved: nothing to rescale (common after a few tiles)
 #pragma unroll
-    for (int i = 0; i < DS; ++i) o[i] *= alpha;
+      for (int i = 0; i < DS; ++i) o[i] *= alpha;
+    }
 
-    // ---- O^T += V^T P^T : A = V^T (tr reads), k order = {4g+0..3, 16+4g+0..3}
+    // ---- O^T += V^T P^T : A = V^T (tr reads), k order of step st = {32st+4g+0..3, 32st+16+4g+0..3}
     const int q4 = c16 >> 2, p4 = c16 & 3;
 #pragma unroll
     for (int ds = 0; ds < DS; ++ds) {
-      bf16x8_t vf;
 #pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const int row = hh * 16 + 4 * g + q4;
-        const int ch = (2 * ds + (p4 >> 1)) ^ swz_v<D>(row);
-        const char* addr = vb + row * (D * 2) + ch * 16 + 8 * (p4 & 1);
-        const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
-        vf[4 * hh + 0] = r[0]; vf[4 * hh + 1] = r[1]; vf[4 * hh + 2] = r[2]; vf[4 * hh + 3] = r[3];
+      for (int st = 0; st < ST; ++st) {
+        bf16x8_t vf;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const int row = (2 * st + hh) * 16 + 4 * g + q4;
+          const int ch = (2 * ds + (p4 >> 1)) ^ swz_v<D>(row);
+          const char* addr = vb + row * (D * 2) + ch * 16 + 8 * (p4 & 1);
+          const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
+          vf[4 * hh + 0] = r[0]; vf[4 * hh + 1] = r[1]; vf[4 * hh + 2] = r[2]; vf[4 * hh + 3] = r[3];
+        }
+        o[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[st], o[ds], 0, 0, 0);
       }
-      o[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[ds], 0, 0, 0);
     }
   }
 
@@ -273,7 +303,8 @@ __global__ void __launch_bounds__(256) attn_delta_kernel(FlashBwdArgs a, int nz)
 
 template <int D>
 __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
-  using R = FaRing<D>;
+  constexpr int FA_KT = 32;
+  using R = FaRing<D, FA_KT>;
   constexpr int KS = D / 32;
   constexpr int DS = D / 16;
   __shared__ __attribute__((aligned(16))) char smem[R::BYTES];   // (K, V) x4, key_valid x4
@@ -321,7 +352,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
       for (int j = 0; j < R::PER_WAVE; ++j) {
         const int inst = wave * R::PER_WAVE + j;
         const int row = inst * (64 / R::CPR) + lane / R::CPR;
-        const int lch = (lane % R::CPR) ^ swz_k<D>(row);
+        const int lch = (lane % R::CPR) ^ swz_kt<D>(row);
         const int key = min(t * FA_KT + row, a.nkeys - 1);
         fa_glds16(K + (long)key * D + 8 * lch, kb + inst * 1024);
         fa_glds16(V + (long)key * D + 8 * lch, vb + inst * 1024);
@@ -329,7 +360,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
     } else {
       const int inst = wave & (R::INST - 1);
       const int row = inst * (64 / R::CPR) + lane / R::CPR;
-      const int lch = (lane % R::CPR) ^ swz_k<D>(row);
+      const int lch = (lane % R::CPR) ^ swz_kt<D>(row);
       const int key = min(t * FA_KT + row, a.nkeys - 1);
       if (wave < R::INST)
         fa_glds16(K + (long)key * D + 8 * lch, kb + inst * 1024);
@@ -354,7 +385,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
     if (t + FA_NBUF - 1 < t_hi) stage(t + FA_NBUF - 1, (buf + FA_NBUF - 1) & (FA_NBUF - 1));
     const char* kb = smem + buf * 2 * R::TILE;
     const char* vb = kb + R::TILE;
-    const int* kvs = reinterpret_cast<const int*>(smem + R::KV_OFF + buf * 128);
+    const int* kvs = reinterpret_cast<const int*>(smem + R::KV_OFF + buf * (FA_KT * 4));
     f32x4_t s[2], dp[2];
 #pragma unroll
     for (int ms = 0; ms < 2; ++ms) {
@@ -363,7 +394,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
       const int row = ms * 16 + c16;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const int ch = (ks * 4 + g) ^ swz_k<D>(row);
+        const int ch = (ks * 4 + g) ^ swz_kt<D>(row);
         const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + row * (D * 2) + ch * 16);
         const bf16x8_t vf = *reinterpret_cast<const bf16x8_t*>(vb + row * (D * 2) + ch * 16);
         s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
@@ -396,7 +427,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int row = hh * 16 + 4 * g + q4;
-        const int ch = (2 * ds + (p4 >> 1)) ^ swz_k<D>(row);
+        const int ch = (2 * ds + (p4 >> 1)) ^ swz_kt<D>(row);
         const char* addr = kb + row * (D * 2) + ch * 16 + 8 * (p4 & 1);
         const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
         kt[4 * hh + 0] = r[0]; kt[4 * hh + 1] = r[1]; kt[4 * hh + 2] = r[2]; kt[4 * hh + 3] = r[3];
@@ -586,8 +617,12 @@ __host__ __device__ inline int dkv_pieces(const FlashBwdArgs& a, int s) {
   return (a.dkv_target <= 0 || n <= a.dkv_target) ? 1 : (n + a.dkv_target - 1) / a.dkv_target;
 }
 
-__global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a) {
+template <int KPW>   // keys per wave: 32 (4 waves, one per SIMD) or 16 (8 waves, two per SIMD)
+__global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a) {
   constexpr int D = 256, KS = D / 32, DS = D / 16;
+  constexpr int KG = KPW / 16, NW = DKV_KEYS / KPW;   // 16-key groups per wave, waves
+  constexpr int IPW = 16 / NW;                        // staging wave-instructions per tensor per wave
+  constexpr int OPS = 2 * IPW + 1;                    // LDS-DMA ops per wave per chunk
   constexpr int TILE = DKV_CH * D * 2;   // 16 KiB: 32 rows of Q or dO
   constexpr int NBUF = 4;                 // ring depth: chunk c+3 is staged while chunk c computes
   __shared__ __attribute__((aligned(16))) char smem[NBUF * 2 * TILE + NBUF * 256];   // (Q, dO) x4, (lse|delta) x4
@@ -615,13 +650,13 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
     c1 = lo + (int)((long)(piece + 1) * n / P);
   }
   const long b = z / a.zdiv;
-  const int kw = s * DKV_KEYS + wave * 32;   // the wave's first key
+  const int kw = s * DKV_KEYS + wave * KPW;   // the wave's first key
 
-  bf16x8_t kf[2][KS], vf[2][KS];
-  int key[2];
-  bool kok[2];
+  bf16x8_t kf[KG][KS], vf[KG][KS];
+  int key[KG];
+  bool kok[KG];
 #pragma unroll
-  for (int kg = 0; kg < 2; ++kg) {
+  for (int kg = 0; kg < KG; ++kg) {
     key[kg] = kw + 16 * kg + c16;
     const int kc = min(key[kg], a.nkeys - 1);
     const long ko = (z * a.nkeys + kc) * (long)D + 8 * g;
@@ -639,33 +674,33 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
   const int qshift = (a.qdiv & (a.qdiv - 1)) == 0 ? __builtin_ctz(a.qdiv) : -1;
   const int causal = a.causal != 0, nowin = a.window <= 0;
 
-  // staging: 32 rows x 32 16-B chunks per tensor = 16 wave-instructions, 4 per wave, plus one
-  // 64-B piece of the chunk's LSE|delta per wave (lanes 0-3): 9 LDS-DMA ops per wave per chunk,
-  // so one counted vmcnt serves every wave
+  // staging: 32 rows x 32 16-B chunks per tensor = 16 wave-instructions (IPW per wave), plus the
+  // chunk's LSE|delta (256 B) spread over all waves: OPS LDS-DMA ops per wave per chunk, so one
+  // counted vmcnt serves every wave
   auto stage = [&](int c, int buf) {
     char* qb = smem + buf * 2 * TILE;
     char* ob = qb + TILE;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int inst = wave * 4 + j;
+    for (int j = 0; j < IPW; ++j) {
+      const int inst = wave * IPW + j;
       const int row = inst * 2 + (lane >> 5);
-      const int lch = (lane & 31) ^ (row & 15);
+      const int lch = (lane & 31) ^ swz_rt(row);
       const long src = (long)(c * DKV_CH + row) * D + 8 * lch;
       fa_glds16(Qz + src, qb + inst * 1024);
       fa_glds16(dOz + src, ob + inst * 1024);
     }
-    if (lane < 4) {
-      const int item = wave * 4 + lane;   // 0-7 LSE, 8-15 delta (4 floats each)
+    if (lane < 16 / NW) {
+      const int item = wave * (16 / NW) + lane;   // 0-7 LSE, 8-15 delta (4 floats each)
       const float* srcv = (item < 8 ? a.lse : a.delta) + z * a.rows + c * DKV_CH + 4 * (item & 7);
-      fa_glds16(srcv, smem + NBUF * 2 * TILE + buf * 256 + wave * 64);
+      fa_glds16(srcv, smem + NBUF * 2 * TILE + buf * 256 + wave * (256 / NW));
     }
   };
 
-  f32x4_t dv[DS][2], dk[DS][2];
+  f32x4_t dv[DS][KG], dk[DS][KG];
 #pragma unroll
   for (int i = 0; i < DS; ++i)
 #pragma unroll
-    for (int kg = 0; kg < 2; ++kg) {
+    for (int kg = 0; kg < KG; ++kg) {
       dv[i][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
       dk[i][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
     }
@@ -677,21 +712,30 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
     const int buf = (c - c0) & (NBUF - 1);
     // chunk c landed; chunks c+1, c+2 may stay in flight (9 ops each)
     const int ahead = min(NBUF - 2, c1 - 1 - c);
-    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();   // every wave's share landed; every wave is done reading chunk c-1's buffer
+    if (ahead >= 2) {
+      if constexpr (OPS == 9) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(10)" ::: "memory");
+    } else if (ahead == 1) {
+      if constexpr (OPS == 9) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(5)" ::: "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    // raw barrier: __syncthreads() here compiles to vmcnt(0) + barrier and would drain the ring.
+    // Every wave's share of chunk c landed (counted wait above); its reads of chunk c-1's buffer
+    // were consumed by MFMAs before this point.
+    __builtin_amdgcn_s_barrier();
     if (c + NBUF - 1 < c1) stage(c + NBUF - 1, (buf + NBUF - 1) & (NBUF - 1));
     const char* qb = smem + buf * 2 * TILE;
     const char* ob = qb + TILE;
     const float* ld = reinterpret_cast<const float*>(smem + NBUF * 2 * TILE + buf * 256);
 
     // ---- S = Q K^T, dP = dO V^T for 32 rows x 32 keys (key on the lane)
-    f32x4_t sc[2][2], dp[2][2];
+    f32x4_t sc[2][KG], dp[2][KG];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt)
 #pragma unroll
-      for (int kg = 0; kg < 2; ++kg) {
+      for (int kg = 0; kg < KG; ++kg) {
         sc[qt][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
         dp[qt][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
       }
@@ -700,11 +744,11 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
       const int row = qt * 16 + c16;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
-        const int ch = (ks * 4 + g) ^ (row & 15);
+        const int ch = (ks * 4 + g) ^ swz_rt(row);
         const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(qb + row * (D * 2) + ch * 16);
         const bf16x8_t oa = *reinterpret_cast<const bf16x8_t*>(ob + row * (D * 2) + ch * 16);
 #pragma unroll
-        for (int kg = 0; kg < 2; ++kg) {
+        for (int kg = 0; kg < KG; ++kg) {
           sc[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kg][ks], sc[qt][kg], 0, 0, 0);
           dp[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[kg][ks], dp[qt][kg], 0, 0, 0);
         }
@@ -712,7 +756,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
     }
     // ---- P = exp(S*scale - LSE) (bf16), dS = P (dP - delta) (bf16); k order of the next products:
     //      slot 4qt + j of lane group g <-> query row 16qt + 4g + j
-    bf16x8_t pf[2], dsf[2];
+    bf16x8_t pf[KG], dsf[KG];
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const float4 l4 = *reinterpret_cast<const float4*>(ld + qt * 16 + 4 * g);
@@ -723,7 +767,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
         const int qrow = c * DKV_CH + qt * 16 + 4 * g + j;
         const int pos = qshift >= 0 ? (qrow >> qshift) : qrow / a.qdiv;
 #pragma unroll
-        for (int kg = 0; kg < 2; ++kg) {
+        for (int kg = 0; kg < KG; ++kg) {
           // branch-free mask (short-circuit && turns into exec-mask control flow per element)
           const int ok = (int)kok[kg] & ((int)(key[kg] <= pos) | !causal) & ((int)(key[kg] > pos - a.window) | nowin);
           const float p = __builtin_amdgcn_exp2f(ok ? sc[qt][kg][j] * sl2 - lv[j] * L2E : -INFINITY);
@@ -740,7 +784,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int row = hh * 16 + 4 * g + q4;
-        const int ch = (2 * ds + (p4 >> 1)) ^ (row & 15);
+        const int ch = (2 * ds + (p4 >> 1)) ^ swz_rt(row);
         const int off = row * (D * 2) + ch * 16 + 8 * (p4 & 1);
         const s16x4_t ro = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(ob + off));
         const s16x4_t rq = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(qb + off));
@@ -748,7 +792,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
         qt_[4 * hh + 0] = rq[0]; qt_[4 * hh + 1] = rq[1]; qt_[4 * hh + 2] = rq[2]; qt_[4 * hh + 3] = rq[3];
       }
 #pragma unroll
-      for (int kg = 0; kg < 2; ++kg) {
+      for (int kg = 0; kg < KG; ++kg) {
         dv[ds][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ot, pf[kg], dv[ds][kg], 0, 0, 0);
         dk[ds][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt_, dsf[kg], dk[ds][kg], 0, 0, 0);
       }
@@ -757,7 +801,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
   // ---- outputs: lane holds dV^T[16ds + 4g + j][key]
   if (P == 1) {
 #pragma unroll
-    for (int kg = 0; kg < 2; ++kg) {
+    for (int kg = 0; kg < KG; ++kg) {
       if (key[kg] >= a.nkeys) continue;
       bf16_t* dvp = a.dV + (z * a.nkeys + key[kg]) * (long)D + 4 * g;
       bf16_t* dkp = a.dK + (z * a.nkeys + key[kg]) * (long)D + 4 * g;
@@ -777,8 +821,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a)
     // partial slot [base + piece][z]: [dK | dV][128 keys][D] fp32
     float* part = a.dkv_part + ((long)(base + piece) * nz + z) * (2L * DKV_KEYS * D);
 #pragma unroll
-    for (int kg = 0; kg < 2; ++kg) {
-      const int kl = wave * 32 + 16 * kg + c16;
+    for (int kg = 0; kg < KG; ++kg) {
+      const int kl = wave * KPW + 16 * kg + c16;
       float* pk = part + (long)kl * D + 4 * g;
       float* pv = pk + (long)DKV_KEYS * D;
 #pragma unroll
@@ -890,7 +934,9 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st) {
         ns = 0;
       }
       hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
-      hipLaunchKernelGGL(attn_bwd_dkv256_kernel, dim3((unsigned)(np * nz)), dim3(256), 0, st, b);
+      // 32 keys per wave (one wave per SIMD) measured 209 us vs 252 us for 16 keys per wave (two per
+      // SIMD, which spills the precomputed transposed-read addresses) at cfg2
+      hipLaunchKernelGGL(attn_bwd_dkv256_kernel<32>, dim3((unsigned)(np * nz)), dim3(256), 0, st, b);
       if (ns > 0)
         hipLaunchKernelGGL(attn_dkv_reduce_kernel, dim3((unsigned)((nz * 2L * DKV_KEYS * 64 + 255) / 256), (unsigned)nslab),
                            dim3(256), 0, st, b);
