@@ -22,6 +22,7 @@
 #include "common.h"
 #include "ptk_internal.h"
 
+#include <algorithm>
 #include <vector>
 
 namespace ptk {
@@ -223,6 +224,25 @@ PTK_DEV void geglu_bwd_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 
   stbf4(C + 16, du);
 }
 
+// 8-wide GEGLU backward: 16-B loads of g, u and 16-B stores of dg, du (8 columns stay inside one
+// 16-column interleave group)
+PTK_DEV void geglu_bwd_vec8(const GemmArgs& p, char* Cz, long r, long c, const float* dh) {
+  float g[8], u[8], dg[8], du[8];
+  ldbf8(p.aux_in + r * p.ld_aux_in + c, g);
+  ldbf8(p.aux_in2 + r * p.ld_aux_in + c, u);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float d = bfround(dh[e]);
+    dg[e] = bfround(d * u[e]) * gelu_tanh_grad(g[e]);
+    du[e] = d * bfround(gelu_tanh(g[e]));
+  }
+  const long cr = map_row(p.cmap, r);
+  if (cr < 0) return;
+  bf16_t* C = reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + (c >> 4) * 32 + (c & 15);
+  stbf8(C, dg);
+  stbf8(C + 16, du);
+}
+
 template <int ACT, int OUT>
 PTK_DEV void epilogue(const GemmArgs& p, char* smem, int wave, int lane, f32x4_t (&acc)[4][4], long row0,
                       long col0, char* Cz) {
@@ -272,6 +292,20 @@ PTK_DEV void epilogue(const GemmArgs& p, char* smem, int wave, int lane, f32x4_t
         const float4 u = *reinterpret_cast<const float4*>(T + lr * EPI_LD + q * 32 + 16 + cc);
         geglu_vec4(p, Cz, r, hc, g, u);
       }
+    }
+  } else if (ACT == ACT_GEGLU_BWD && ((p.ldc | p.ld_aux_in) & 7) == 0 && col0 + 63 < p.N) {
+    // 8 lanes per row, each 8 columns; 8 rows per pass
+    const int rr = lane >> 3, c8 = (lane & 7) * 8;
+    const long c = col0 + c8;
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {
+      const int lr = it * 8 + rr;
+      const long r = row0 + lr;
+      if (r >= p.M) continue;
+      float v[8];
+      *reinterpret_cast<float4*>(v) = *reinterpret_cast<const float4*>(T + lr * EPI_LD + c8);
+      *reinterpret_cast<float4*>(v + 4) = *reinterpret_cast<const float4*>(T + lr * EPI_LD + c8 + 4);
+      geglu_bwd_vec8(p, Cz, r, c, v);
     }
   } else if (OUT == OUT_BF16 && ACT != ACT_GEGLU_BWD && vec_ok && ((p.ldc & 7) == 0) &&
              (!p.aux || (p.ld_aux & 7) == 0) && (!p.aux_in || (p.ld_aux_in & 7) == 0) && col0 + 63 < p.N) {
@@ -612,6 +646,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
 #endif
   PTK_STAMP(3);
 }
+
 
 
 template <int ACT, int OUT>

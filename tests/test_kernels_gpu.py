@@ -195,7 +195,7 @@ def test_cross_entropy(gpu):
 
 @pytest.mark.parametrize("mode", [2, 4])
 @pytest.mark.parametrize("M,N,K", [(1024, 512, 64), (1024, 512, 128), (1100, 700, 192), (2048, 1152, 1152),
-                                   (4096, 1536, 256), (300, 200, 64)])
+                                   (4096, 1536, 256), (300, 200, 64), (4096, 4096, 576), (8448, 2304, 1152)])
 def test_gemm_big_tile_path(gpu, M, N, K, mode):
     """256x256 8-wave kernel (mode 2) and its barrier-staggered variant (mode 4), forced: ragged M/N,
     1..18 K-tiles, vs fp32."""

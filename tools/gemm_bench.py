@@ -63,6 +63,7 @@ ALL = [  # every single-batch GEMM of the cfg2 step: name, M, N, K, act, out
     ("g_down", M, 1152, 6912, L.ACT_NONE, torch.bfloat16),
     ("g_lm", 4096, 262144, 1152, L.ACT_NONE, torch.bfloat16),
     ("g_dh", M, 6912, 1152, L.ACT_NONE, torch.bfloat16),
+    ("g_dh_geglu_bwd", M, 6912, 1152, L.ACT_GEGLU_BWD, torch.bfloat16),
     ("g_dgu", M, 1152, 13824, L.ACT_NONE, torch.float32),
     ("g_dO", M, 1024, 1152, L.ACT_NONE, torch.bfloat16),
     ("g_dqkv", M, 1152, 1536, L.ACT_NONE, torch.float32),
