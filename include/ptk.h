@@ -103,7 +103,8 @@ int ptk_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float std, float m
  * synchronises those events and returns the summed kernel time and count. */
 int ptk_gemm_timer_enable(int on);
 /* Tile-path test hook: 0 = shape heuristic, 1 = every GEMM on the 128x128 kernel,
-   2 / 4 = every single-batch GEMM on the 256x256 / barrier-staggered 256x256 kernel. */
+   2 / 4 = every single-batch GEMM on the 256x256 / barrier-staggered 256x256 kernel,
+   8 = every single-batch GEMM the persistent 4-wave 256x256 kernel supports on it. */
 int ptk_gemm_force_small_tiles(int mode);
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
 

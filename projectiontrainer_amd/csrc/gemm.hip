@@ -21,6 +21,7 @@
 // GROUP_M-row groups (L2 reuse of A row-panels and B column-panels).
 #include "common.h"
 #include "ptk_internal.h"
+#include "gemm_epi.h"
 
 #include <algorithm>
 #include <vector>
@@ -36,211 +37,6 @@ typedef __attribute__((address_space(3))) void* lptr_t;
 
 PTK_DEV void glds16(const void* src, void* lds) {
   __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 16, 0, 0);
-}
-
-// ---------------------------------------------------------------- epilogue
-// The wave's 64x64 fp32 accumulator tile is staged through LDS ([64][68] f32,
-// 17 KiB per wave) and re-read row-contiguously, so every global access of the
-// epilogue (bias, row-add, residual, aux in/out, C) is a 8/16-byte vector and
-// consecutive lanes touch consecutive addresses.
-constexpr int EPI_LD = 68;                       // floats per staged row (64 + 4 pad)
-constexpr int EPI_WAVE_BYTES = 64 * EPI_LD * 4;  // 17408
-
-PTK_DEV float4 ldf4(const float* p) { return *reinterpret_cast<const float4*>(p); }
-PTK_DEV float4 ldbf4(const bf16_t* p) {
-  u16x4_t u = *reinterpret_cast<const u16x4_t*>(p);
-  return make_float4(bf2f(u[0]), bf2f(u[1]), bf2f(u[2]), bf2f(u[3]));
-}
-PTK_DEV void stbf4(bf16_t* p, float4 v) {
-  u16x4_t u;
-  u[0] = f2bf(v.x); u[1] = f2bf(v.y); u[2] = f2bf(v.z); u[3] = f2bf(v.w);
-  *reinterpret_cast<u16x4_t*>(p) = u;
-}
-PTK_DEV float& el(float4& v, int e) { return reinterpret_cast<float*>(&v)[e]; }
-PTK_DEV float el(const float4& v, int e) { return reinterpret_cast<const float*>(&v)[e]; }
-
-template <int ACT, int OUT>
-PTK_DEV void epi_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 v) {
-  // r < M; c..c+3 < N (checked by caller); c % 4 == 0
-  if (p.bias) { float4 b = ldf4(p.bias + c); v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w; }
-  if (p.rowadd) {
-    float4 b = ldf4(p.rowadd + (r % p.rowadd_period) * p.ld_rowadd + c);
-    v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
-  }
-  if constexpr (ACT == ACT_GELU_TANH) {
-#pragma unroll
-    for (int e = 0; e < 4; ++e) el(v, e) = gelu_tanh(bfround(el(v, e)));
-  } else if constexpr (ACT == ACT_GELU_ERF) {
-    // pre-activation kept (bf16) for the backward: Stage1/projectors.py:17-18
-#pragma unroll
-    for (int e = 0; e < 4; ++e) el(v, e) = bfround(el(v, e));
-    if (p.aux) stbf4(p.aux + r * p.ld_aux + c, v);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) el(v, e) = gelu_erf(el(v, e));
-  } else if constexpr (ACT == ACT_GELU_ERF_BWD) {
-    float4 a = ldbf4(p.aux_in + r * p.ld_aux_in + c);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) el(v, e) = bfround(el(v, e)) * gelu_erf_grad(el(a, e));
-  }
-  const long cr = map_row(p.cmap, r);
-  if (cr < 0) return;
-  if (p.resid) {
-    float4 b = ldf4(p.resid + cr * p.ld_resid + c);
-    v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
-  }
-  if constexpr (OUT == OUT_BF16) {
-    stbf4(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + c, v);
-  } else {
-    if constexpr (OUT == OUT_F32_BFR) v = make_float4(bfround(v.x), bfround(v.y), bfround(v.z), bfround(v.w));
-    *reinterpret_cast<float4*>(reinterpret_cast<float*>(Cz) + cr * p.ldc + c) = v;
-  }
-}
-
-// 8 columns per lane, one 16-B store (bf16 output): the epilogue is store-issue bound
-// (one wave store instruction per ~140 cycles per CU regardless of width), so every
-// bf16 store moves 16 B.
-typedef __attribute__((ext_vector_type(8))) unsigned short u16x8_t;
-PTK_DEV void ldbf8(const bf16_t* p, float* v) {
-  const u16x8_t u = *reinterpret_cast<const u16x8_t*>(p);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) v[e] = bf2f(u[e]);
-}
-PTK_DEV void stbf8(bf16_t* p, const float* v) {
-  u16x8_t u;
-#pragma unroll
-  for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
-  *reinterpret_cast<u16x8_t*>(p) = u;
-}
-
-template <int ACT>
-PTK_DEV void epi_vec8_bf16(const GemmArgs& p, char* Cz, long r, long c, float4 v0, float4 v1) {
-  // r < M; c..c+7 < N; c % 8 == 0; all leading dims multiples of 8
-  float v[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
-  if (p.bias) {
-    const float4 b0 = ldf4(p.bias + c), b1 = ldf4(p.bias + c + 4);
-    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-  }
-  if (p.rowadd) {
-    const float* ra = p.rowadd + (r % p.rowadd_period) * p.ld_rowadd + c;
-    const float4 b0 = ldf4(ra), b1 = ldf4(ra + 4);
-    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-  }
-  if constexpr (ACT == ACT_GELU_TANH) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(bfround(v[e]));
-  } else if constexpr (ACT == ACT_GELU_ERF) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]);
-    if (p.aux) stbf8(p.aux + r * p.ld_aux + c, v);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
-  } else if constexpr (ACT == ACT_GELU_ERF_BWD) {
-    float a[8];
-    ldbf8(p.aux_in + r * p.ld_aux_in + c, a);
-#pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]) * gelu_erf_grad(a[e]);
-  }
-  const long cr = map_row(p.cmap, r);
-  if (cr < 0) return;
-  if (p.resid) {
-    const float* rp = p.resid + cr * p.ld_resid + c;
-    const float4 b0 = ldf4(rp), b1 = ldf4(rp + 4);
-    v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
-  }
-  stbf8(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + c, v);
-}
-
-// scalar fallback for ragged column tails / unaligned leading dims
-template <int ACT, int OUT>
-PTK_DEV void epi_scalar(const GemmArgs& p, char* Cz, long r, long c, float v) {
-  if (p.bias) v += p.bias[c];
-  if (p.rowadd) v += p.rowadd[(r % p.rowadd_period) * p.ld_rowadd + c];
-  if constexpr (ACT == ACT_GELU_TANH) {
-    v = gelu_tanh(bfround(v));
-  } else if constexpr (ACT == ACT_GELU_ERF) {
-    float a = bfround(v);
-    if (p.aux) p.aux[r * p.ld_aux + c] = f2bf(a);
-    v = gelu_erf(a);
-  } else if constexpr (ACT == ACT_GELU_ERF_BWD) {
-    v = bfround(v) * gelu_erf_grad(bf2f(p.aux_in[r * p.ld_aux_in + c]));
-  }
-  const long cr = map_row(p.cmap, r);
-  if (cr < 0) return;
-  if (p.resid) v += p.resid[cr * p.ld_resid + c];
-  if constexpr (OUT == OUT_BF16) {
-    reinterpret_cast<bf16_t*>(Cz)[cr * p.ldc + c] = f2bf(v);
-  } else if constexpr (OUT == OUT_F32) {
-    reinterpret_cast<float*>(Cz)[cr * p.ldc + c] = v;
-  } else {
-    reinterpret_cast<float*>(Cz)[cr * p.ldc + c] = bfround(v);
-  }
-}
-
-// GEGLU: GEMM cols [32q, 32q+16) = gate[16q..], [32q+16, 32q+32) = up[16q..] (interleaved
-// weights); writes h = bf16(gelu_tanh(g)) * u and the bf16 g, u side outputs (TF gemma3 :131-133).
-PTK_DEV void geglu_vec4(const GemmArgs& p, char* Cz, long r, long hc, float4 g, float4 u) {
-  float4 h;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    el(g, e) = bfround(el(g, e));
-    el(u, e) = bfround(el(u, e));
-    el(h, e) = bfround(gelu_tanh(el(g, e))) * el(u, e);
-  }
-  if (p.aux) stbf4(p.aux + r * p.ld_aux + hc, g);
-  if (p.aux2) stbf4(p.aux2 + r * p.ld_aux + hc, u);
-  const long cr = map_row(p.cmap, r);
-  if (cr >= 0) stbf4(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + hc, h);
-}
-
-PTK_DEV void geglu_vec8(const GemmArgs& p, char* Cz, long r, long hc, const float* g, const float* u) {
-  float gg[8], uu[8], h[8];
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    gg[e] = bfround(g[e]);
-    uu[e] = bfround(u[e]);
-    h[e] = bfround(gelu_tanh(gg[e])) * uu[e];
-  }
-  if (p.aux) stbf8(p.aux + r * p.ld_aux + hc, gg);
-  if (p.aux2) stbf8(p.aux2 + r * p.ld_aux + hc, uu);
-  const long cr = map_row(p.cmap, r);
-  if (cr >= 0) stbf8(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + hc, h);
-}
-
-// GEGLU backward: GEMM output = dh [M, I]; writes dg, du into the interleaved [M, 2I] layout.
-PTK_DEV void geglu_bwd_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 dh) {
-  const float4 g = ldbf4(p.aux_in + r * p.ld_aux_in + c);
-  const float4 u = ldbf4(p.aux_in2 + r * p.ld_aux_in + c);
-  float4 dg, du;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float d = bfround(el(dh, e));
-    el(dg, e) = bfround(d * el(u, e)) * gelu_tanh_grad(el(g, e));
-    el(du, e) = d * bfround(gelu_tanh(el(g, e)));
-  }
-  const long cr = map_row(p.cmap, r);
-  if (cr < 0) return;
-  bf16_t* C = reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + (c >> 4) * 32 + (c & 15);
-  stbf4(C, dg);
-  stbf4(C + 16, du);
-}
-
-// 8-wide GEGLU backward: 16-B loads of g, u and 16-B stores of dg, du (8 columns stay inside one
-// 16-column interleave group)
-PTK_DEV void geglu_bwd_vec8(const GemmArgs& p, char* Cz, long r, long c, const float* dh) {
-  float g[8], u[8], dg[8], du[8];
-  ldbf8(p.aux_in + r * p.ld_aux_in + c, g);
-  ldbf8(p.aux_in2 + r * p.ld_aux_in + c, u);
-#pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float d = bfround(dh[e]);
-    dg[e] = bfround(d * u[e]) * gelu_tanh_grad(g[e]);
-    du[e] = d * bfround(gelu_tanh(g[e]));
-  }
-  const long cr = map_row(p.cmap, r);
-  if (cr < 0) return;
-  bf16_t* C = reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + (c >> 4) * 32 + (c & 15);
-  stbf8(C, dg);
-  stbf8(C + 16, du);
 }
 
 template <int ACT, int OUT>
@@ -882,6 +678,14 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // epilogue with the other's MFMA and quantise better (tools/gemm_bench.py --all, r01).
   // long K: the barrier-staggered 256x256 variant (+6-7 % at K >= 4096, tools/gemm_bench.py --all)
   const bool big_shape = a.M >= 1024 && a.N >= 512 && (a.K >= 6144 || (a.N >= 6144 && a.K >= 1152));
+  if (batch == 1 && g_force_tiles == 8 && w4_supported(a, act, out)) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (g_timing) { e0 = next_event(act); e1 = next_event(act); }
+    if (e0) (void)hipEventRecord(e0, st);
+    const int rc = launch_gemm_w4(a, act, out, st, 0);
+    if (e1) (void)hipEventRecord(e1, st);
+    return rc;
+  }
   if (batch == 1 && (g_force_tiles == 4 || (g_force_tiles == 0 && big_shape && a.K >= 4096))) {
     const long nb = (long)((a.M + BIG - 1) / BIG) * ((a.N + BIG - 1) / BIG);
     dim3 g4((unsigned)nb, 1, 1);

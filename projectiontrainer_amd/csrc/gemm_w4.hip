@@ -1,0 +1,443 @@
+// Persistent 256x256-tile bf16 GEMM for gfx950: 4 waves, one per SIMD, 128x128 fp32 accumulator
+// tile per wave (256 accumulator registers: the kernel runs at one wave per SIMD with the full
+// 512-register file).
+//
+//   C[M,N] = epi( alpha * A[M,K] . B[N,K]^T )        (same contract as gemm_nt_kernel, batch 1)
+//
+// Why this shape: the Stage-1 step's projections are K = 1024..1536 deep, so a
+// 256x256 tile runs only 16..24 K-tiles and the per-tile prologue (first DMA round trip) and
+// epilogue (128 KiB of stores per CU, staged through LDS in gemm_big_kernel) cost as much as a
+// third of the main loop.  Here
+//   * one wave per SIMD software-pipelines its own LDS reads: the 16 ds_read_b128 fragments of
+//     k-step s+1 are issued while the 64 MFMAs of k-step s run; one barrier per 64-deep K-tile;
+//   * the global->LDS stream (buffer_load ... lds, 16 per wave per K-tile, OOB rows read as zero)
+//     runs two K-tiles ahead and continues straight into the workgroup's NEXT tile, so the next
+//     tile's first K-tiles land while this tile's epilogue runs;
+//   * the epilogue stores straight from the accumulators: the MFMA operands are swapped (C^T
+//     orientation) so each lane holds 4 consecutive columns of one row, and one
+//     v_permlane16_swap per dword pairs two 16-column MFMA tiles into 8 consecutive columns, i.e.
+//     one 16-B store per lane (no LDS staging, no barrier);
+//   * every store the epilogue must make is issued unconditionally (invalid rows go to a sink),
+//     so the next tile's first wait can leave exactly that many stores in flight (vmcnt(NST)).
+// Tiles are dealt round-robin over the persistent workgroups; the workgroups that share an XCD
+// (b % 8) take consecutive tiles of the grouped (GROUP_M = 8) order, so a round's A row panels and
+// B column panels are shared through that XCD's L2.
+#include "common.h"
+#include "ptk_internal.h"
+#include "gemm_epi.h"
+
+#include <algorithm>
+
+#ifndef PTK_W4_ABLATE
+#define PTK_W4_ABLATE 0   // diagnostic builds only: 1 = no DMA in the K loop, 2 = no fragment reads,
+                          // 3 = the DMA re-reads one L2-resident K-tile, 4 = no K-loop barrier,
+                          // 5 = no K-loop vmcnt wait
+#endif
+
+namespace ptk {
+
+namespace {
+constexpr int W4 = 256;                  // output tile edge
+constexpr int W4_KT = 64;                // K-tile depth
+constexpr int W4_OPB = W4 * W4_KT * 2;   // one operand's K-tile image: 256 rows x 128 B = 32 KiB
+constexpr int W4_BUF = 2 * W4_OPB;       // A + B per pipeline buffer
+constexpr uint32_t W4_OOB = 0x80000000u; // voffset beyond every buffer's num_records -> zeros
+typedef __attribute__((address_space(3))) void* lds_ptr_t;
+
+__device__ char g_w4_sink[64 * 64];      // store target of rows/columns outside C (64 B per lane)
+
+// RowMap in 32-bit arithmetic (every row index of the step fits an int; 64-bit division is a
+// software routine on gfx950)
+PTK_DEV int map_row32(const RowMap& m, int r) {
+  if (m.g == 0) return r + (int)m.off;
+  const int q = (int)((unsigned)r / (unsigned)m.g), s = r - q * m.g;
+  if (s < m.skip) return -1;
+  return q * (int)m.gs + s + (int)m.off;
+}
+
+PTK_DEV void add8(float* v, const float* s) {
+  const float4 a = *reinterpret_cast<const float4*>(s), b = *reinterpret_cast<const float4*>(s + 4);
+  v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
+}
+
+// 8 consecutive columns [c, c+8) of row r (c % 8 == 0, c < N); rows r >= M and unmapped rows
+// store into the sink so the store count per wave is fixed
+template <int ACT, int OUT>
+PTK_DEV void w4_epi8(const GemmArgs& p, long r, long c_, float* v, char* sink) {
+  const bool rv = r < p.M && c_ < p.N;     // N % 8 == 0: c < N covers all 8 columns
+  const long rl = rv ? r : 0, c = rv ? c_ : 0;
+  if (p.bias) add8(v, p.bias + c);
+  if (p.rowadd) add8(v, p.rowadd + (long)((unsigned)rl % (unsigned)p.rowadd_period) * p.ld_rowadd + c);
+  if constexpr (ACT == ACT_GELU_TANH) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(bfround(v[e]));
+  } else if constexpr (ACT == ACT_GELU_ERF) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]);
+    if (p.aux) stbf8(rv ? p.aux + r * p.ld_aux + c : reinterpret_cast<bf16_t*>(sink), v);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
+  } else if constexpr (ACT == ACT_GELU_ERF_BWD) {
+    float a[8];
+    ldbf8(p.aux_in + rl * p.ld_aux_in + c, a);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]) * gelu_erf_grad(a[e]);
+  }
+  const long cr = rv ? map_row32(p.cmap, (int)r) : -1;
+  if (p.resid) add8(v, p.resid + (cr >= 0 ? cr : 0) * p.ld_resid + c);
+  if constexpr (OUT == OUT_BF16) {
+    stbf8(cr >= 0 ? reinterpret_cast<bf16_t*>(p.C) + cr * p.ldc + c : reinterpret_cast<bf16_t*>(sink), v);
+  } else {
+    if constexpr (OUT == OUT_F32_BFR) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]);
+    }
+    float* d = cr >= 0 ? reinterpret_cast<float*>(p.C) + cr * p.ldc + c : reinterpret_cast<float*>(sink);
+    *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
+    *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
+  }
+}
+
+// unconditional stores per wave per tile (the vmcnt the next tile's first wait leaves in flight)
+template <int ACT, int OUT>
+constexpr int w4_nstore() {
+  if (ACT == ACT_GEGLU) return 16;
+  if (ACT == ACT_GEGLU_BWD) return 63;   // 64, capped at the 6-bit vmcnt field (a smaller count is safe)
+  return OUT == OUT_BF16 ? 32 : 63;
+}
+
+// row block I of the wave's tile: lane holds C[row0 + 16I + (lane&15)][col0 + 16j + 4(lane>>4) + e]
+// (one function per row block so every accumulator index is a compile-time constant)
+template <int ACT, int OUT, int I>
+PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, int lane, char* sink) {
+  // pin the accumulator reads to this row block (otherwise hipcc reads all 256 up front and spills)
+#pragma unroll
+  for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
+  const int q = lane >> 4;
+  const int cb = 16 * (q & 1) + 8 * (q >> 1);
+  const long r = row0 + 16 * I + (lane & 15);
+  if constexpr (ACT == ACT_GEGLU) {
+    // GEMM columns: 16-wide gate / up groups alternate (interleaved weights); tiles 4pp, 4pp+2 are
+    // gate and 4pp+1, 4pp+3 up for h columns [col0/2 + 32pp, +32)
+#pragma unroll
+    for (int pp = 0; pp < 2; ++pp) {
+      f32x4_t g0 = a[4 * pp] * p.alpha, g1 = a[4 * pp + 2] * p.alpha;
+      f32x4_t u0 = a[4 * pp + 1] * p.alpha, u1 = a[4 * pp + 3] * p.alpha;
+      swap16(g0, g1);
+      swap16(u0, u1);
+      float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+      float u[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+      float h[8];
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        g[e] = bfround(g[e]);
+        u[e] = bfround(u[e]);
+        h[e] = bfround(gelu_tanh(g[e])) * u[e];
+      }
+      const long hc = col0 / 2 + 32 * pp + cb;
+      const bool rv = r < p.M && 2 * hc < p.N;
+      bf16_t* sk = reinterpret_cast<bf16_t*>(sink);
+      if (p.aux) stbf8(rv ? p.aux + r * p.ld_aux + hc : sk, g);
+      if (p.aux2) stbf8(rv ? p.aux2 + r * p.ld_aux + hc : sk, u);
+      const long cr = rv ? map_row32(p.cmap, (int)r) : -1;
+      stbf8(cr >= 0 ? reinterpret_cast<bf16_t*>(p.C) + cr * p.ldc + hc : sk, h);
+    }
+  } else {
+#pragma unroll
+    for (int pp = 0; pp < 4; ++pp) {
+      f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
+      swap16(x, y);
+      float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+      w4_epi8<ACT, OUT>(p, r, col0 + 32 * pp + cb, v, sink);
+    }
+  }
+}
+
+template <int ACT, int OUT>
+PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][8], long row0, long col0, int lane) {
+  char* sink = g_w4_sink + lane * 64;
+  w4_rows<ACT, OUT, 0>(p, acc[0], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 1>(p, acc[1], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 2>(p, acc[2], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 3>(p, acc[3], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 4>(p, acc[4], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 5>(p, acc[5], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 6>(p, acc[6], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 7>(p, acc[7], row0, col0, lane, sink);
+}
+
+PTK_DEV void w4_tile_coords(int t, int nbm, int nbn, int& bm, int& bn) {
+  const int per_group = 8 * nbn;
+  const int first_m = (t / per_group) * 8;
+  const int gsz = min(nbm - first_m, 8);
+  bm = first_m + (t % per_group) % gsz;
+  bn = (t % per_group) / gsz;
+}
+}  // namespace
+
+// ---- main-loop primitives as inline asm: hipcc neither reorders volatile asm statements nor splits
+// the AGPR accumulators, so the instruction stream below is exactly the source order.  Waits are
+// explicit (hipcc does not count asm memory operations): lgkmcnt(0) before a fragment's first MFMA,
+// vmcnt before the barrier that publishes an LDS-DMA K-tile.
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
+
+#define W4_MFMA(ACC, FB, FA) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(ACC) : "v"(FB), "v"(FA))
+#define W4_MFMA0(ACC, FB, FA) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(ACC) : "v"(FB), "v"(FA))
+#define W4_DSREAD(DST, ADDR, OFF) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(DST) : "v"(ADDR), "i"(OFF))
+// one 1-KiB LDS-DMA piece: M0 = wave-uniform LDS destination.  hipcc emits no M0 use of its own in
+// these kernels (no LDS-DMA builtins, gfx950 ds_* do not read M0), so M0 is not saved / restored.
+#define W4_DMA(RSRC, VOFF, SOFF, LDS)                                                                      \
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen lds"                   \
+               :: "v"(VOFF), "s"(LDS), "s"(RSRC), "s"(SOFF) : "memory")
+
+PTK_DEV u32x4_t w4_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t a = (uint64_t)base;
+  u32x4_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)a);
+  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));   // stride 0: raw buffer
+  r[2] = __builtin_amdgcn_readfirstlane(bytes);                  // num_records (bytes)
+  r[3] = 0x00020000u;
+  return r;
+}
+PTK_DEV uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_ptr_t)p; }
+
+template <int ACT, int OUT>
+__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
+  __shared__ __attribute__((aligned(16))) char smem[2 * W4_BUF];   // 128 KiB: two K-tile buffers
+  const int lane = threadIdx.x & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int wr = wave >> 1, wc = wave & 1;
+  const int nbm = (p.M + W4 - 1) / W4, nbn = (p.N + W4 - 1) / W4;
+  const int ntile = nbm * nbn;
+  const int G = gridDim.x;
+  int loc;
+  {
+    const int b = blockIdx.x, q = G >> 3, rr = G & 7, x = b & 7;
+    loc = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
+  }
+  if (loc >= ntile) return;
+  const int nt = p.K / W4_KT;
+  const int total_kt = ((ntile - loc + G - 1) / G) * nt;
+
+  // A rows past M / B rows past N fall outside num_records and read as zero
+  const u32x4_t rsa = w4_rsrc(p.A, a_bytes), rsb = w4_rsrc(p.B, b_bytes);
+
+  // ---- global -> LDS stream.  Lane i of DMA piece j writes LDS row wave*64 + 8j + (i>>3), 16-B
+  // chunk i&7, fetching logical chunk (i&7) ^ ((row>>1)&7) (XOR swizzle on the source address, LDS
+  // image lane-linear) so the fragment reads are bank-conflict free.  The per-lane part of the
+  // source offset is fixed; the tile's row panel and the K-tile go into the scalar offset.
+  uint32_t offa[8], offb[8];
+#pragma unroll
+  for (int j = 0; j < 8; ++j) {
+    const int lr = wave * 64 + 8 * j + (lane >> 3);
+    const int lc = (lane & 7) ^ ((lr >> 1) & 7);
+    offa[j] = (uint32_t)lr * (uint32_t)p.lda * 2u + lc * 16;
+    offb[j] = (uint32_t)lr * (uint32_t)p.ldb * 2u + lc * 16;
+  }
+  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave * 64 * 128;
+  // DMA cursor: tile dt, K-tile dkt, scalar offsets of its row panels.  Past the workgroup's last
+  // K-tile the cursor stays put and the stream re-loads that K-tile into the free buffer (never
+  // read), so every k-step issues the same instructions.
+  int dt = loc, dkt = 0, dcount = 0;
+  uint32_t dsa = 0, dsb = 0;
+  auto dma_tile = [&](int t) {
+    int bm, bn;
+    w4_tile_coords(t, nbm, nbn, bm, bn);
+    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * W4 + (int)p.amap.off) * (uint32_t)p.lda * 2u);
+    dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * W4) * (uint32_t)p.ldb * 2u);
+  };
+  auto dma_advance = [&]() {
+    if (++dcount < total_kt) {
+      if (++dkt == nt) {
+        dkt = 0;
+        dt += G;
+        dma_tile(dt);
+      }
+    }
+  };
+
+  // ---- fragments: A rows wr*128 + 16i + (lane&15), B rows wc*128 + 16j + (lane&15); logical
+  // 16-B chunk 4ks + (lane>>4) of the 128-B row
+  const int frag_off = (lane & 15) * 128 + (((lane >> 4) ^ ((lane >> 1) & 7)) << 4);
+  const uint32_t frag_a = lds_addr(smem) + wr * 128 * 128 + frag_off;            // buffer 0, ks 0
+  const uint32_t frag_b = lds_addr(smem) + W4_OPB + wc * 128 * 128 + frag_off;
+  bf16x8_t fa0[8], fb0[8], fa1[8], fb1[8];
+  f32x4_t acc[8][8];
+
+// MFMA group q (0..15) of a k-step: 4 MFMAs of row block i = q/2, column blocks 4(q&1)..+3
+#define W4_GROUP(FA, FB, Q, FIRST)                                                  \
+  do {                                                                              \
+    _Pragma("unroll") for (int jj = 0; jj < 4; ++jj) {                              \
+      if (FIRST) W4_MFMA0(acc[(Q) >> 1][4 * ((Q) & 1) + jj], FB[4 * ((Q) & 1) + jj], FA[(Q) >> 1]); \
+      else W4_MFMA(acc[(Q) >> 1][4 * ((Q) & 1) + jj], FB[4 * ((Q) & 1) + jj], FA[(Q) >> 1]);       \
+    }                                                                               \
+  } while (0)
+// fragment read q (0..15) of the next k-step: q < 8 -> A row block q, else B column block q-8
+#define W4_READ(FA, FB, BA, BB, Q)                                                  \
+  do {                                                                              \
+    if ((Q) < 8) W4_DSREAD(FA[(Q) & 7], BA, ((Q) & 7) * 2048);                      \
+    else W4_DSREAD(FB[(Q) & 7], BB, ((Q) & 7) * 2048);                              \
+  } while (0)
+// every destination of the last 16 reads is pinned after the wait (no copy before the data lands)
+#define W4_PIN(FA, FB)                                                                              \
+  do {                                                                                              \
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");                                              \
+    asm volatile("" : "+v"(FA[0]), "+v"(FA[1]), "+v"(FA[2]), "+v"(FA[3]), "+v"(FA[4]), "+v"(FA[5]),  \
+                 "+v"(FA[6]), "+v"(FA[7]));                                                         \
+    asm volatile("" : "+v"(FB[0]), "+v"(FB[1]), "+v"(FB[2]), "+v"(FB[3]), "+v"(FB[4]), "+v"(FB[5]),  \
+                 "+v"(FB[6]), "+v"(FB[7]));                                                         \
+  } while (0)
+
+  // k-step 2kt (ks 0): 16 groups of 4 MFMAs on FA/FB; the 16 reads of (kt, ks 1) go out two per group
+  // in the first half, so they have landed when the step ends (its lgkmcnt(0) costs nothing)
+  auto step_a = [&](const bf16x8_t (&FA)[8], const bf16x8_t (&FB)[8], bf16x8_t (&NA)[8], bf16x8_t (&NB)[8],
+                    uint32_t ba, uint32_t bb, bool first) {
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+#if PTK_W4_ABLATE != 2
+      if (q < 8) {
+        W4_READ(NA, NB, ba, bb, 2 * q);
+        W4_READ(NA, NB, ba, bb, 2 * q + 1);
+      }
+#endif
+      if (first) W4_GROUP(FA, FB, q, true); else W4_GROUP(FA, FB, q, false);
+    }
+  };
+  // k-step 2kt+1 (ks 1): the 16 LDS-DMA pieces of K-tile g+2 go out two per group in the first half
+  // (latency slack until the next K-tile's barrier), the 16 reads of the next K-tile's ks 0 one per
+  // group in groups 0..7 and two per group in groups 8..11
+  auto step_b = [&](const bf16x8_t (&FA)[8], const bf16x8_t (&FB)[8], bf16x8_t (&NA)[8], bf16x8_t (&NB)[8],
+                    uint32_t ba, uint32_t bb, int buf) {
+    const uint32_t da = lds0 + buf * W4_BUF, db = da + W4_OPB;
+#if PTK_W4_ABLATE == 3
+    const uint32_t sa = dsa, sb = dsb;   // always K-tile 0 of the tile: L2-resident (timing only)
+#else
+    const uint32_t sa = dsa + dkt * (W4_KT * 2), sb = dsb + dkt * (W4_KT * 2);
+#endif
+#pragma unroll
+    for (int q = 0; q < 16; ++q) {
+#if PTK_W4_ABLATE != 1
+      if (q < 8) {
+        W4_DMA(rsa, offa[q], sa, da + q * 1024);
+        W4_DMA(rsb, offb[q], sb, db + q * 1024);
+      }
+#endif
+#if PTK_W4_ABLATE != 2
+      if (q < 8) {
+        W4_READ(NA, NB, ba, bb, q);
+      } else if (q < 12) {
+        W4_READ(NA, NB, ba, bb, 8 + 2 * (q - 8));
+        W4_READ(NA, NB, ba, bb, 9 + 2 * (q - 8));
+      }
+#endif
+      W4_GROUP(FA, FB, q, false);
+    }
+  };
+
+  // ---- prologue: K-tiles 0 and 1, fragments of k-step 0
+  dma_tile(dt);
+#pragma unroll
+  for (int b = 0; b < 2; ++b) {
+    const uint32_t da = lds0 + b * W4_BUF, db = da + W4_OPB;
+    const uint32_t sa = dsa + dkt * (W4_KT * 2), sb = dsb + dkt * (W4_KT * 2);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      W4_DMA(rsa, offa[j], sa, da + j * 1024);
+      W4_DMA(rsb, offb[j], sb, db + j * 1024);
+    }
+    dma_advance();
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int q = 0; q < 16; ++q) W4_READ(fa0, fb0, frag_a, frag_b, q);
+  W4_PIN(fa0, fb0);
+
+  constexpr int NST = w4_nstore<ACT, OUT>();
+  int t = loc, kt = 0;
+  for (int g = 0; g < total_kt; ++g) {
+    const int buf = g & 1;
+    step_a(fa0, fb0, fa1, fb1, (frag_a + buf * W4_BUF) ^ 64, (frag_b + buf * W4_BUF) ^ 64, kt == 0);
+    W4_PIN(fa1, fb1);
+    // K-tile g+1 must have landed (own DMA, then everyone's via the barrier); after the barrier
+    // every read of buffer g&1 is done, so K-tile g+2 may overwrite it
+#if PTK_W4_ABLATE != 5
+    if (kt == 0) {
+      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NST) : "memory");   // previous tile's stores may fly
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+#endif
+#if PTK_W4_ABLATE != 4
+    __builtin_amdgcn_s_barrier();
+#endif
+    step_b(fa1, fb1, fa0, fb0, frag_a + (buf ^ 1) * W4_BUF, frag_b + (buf ^ 1) * W4_BUF, buf);
+    W4_PIN(fa0, fb0);
+    dma_advance();
+    if (kt == nt - 1) {
+      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");   // MFMA D -> accumulator read wait states
+      int bm, bn;
+      w4_tile_coords(t, nbm, nbn, bm, bn);
+      w4_epilogue<ACT, OUT>(p, acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128, lane);
+      t += G;
+      kt = 0;
+    } else {
+      ++kt;
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup exits
+#undef W4_GROUP
+#undef W4_READ
+#undef W4_PIN
+}
+
+// the W4 path needs: batch 1, 16-B aligned rows of every operand it touches 8 columns at a time,
+// N % 8 == 0, byte extents of A and B below 2^31 (32-bit buffer offsets)
+bool w4_supported(const GemmArgs& a, int act, int out) {
+  if (a.N % 8 || a.K % W4_KT) return false;
+  if ((a.ldc % 8) || (a.resid && a.ld_resid % 4) || (a.rowadd && a.ld_rowadd % 4)) return false;
+  if ((a.aux || a.aux2) && a.ld_aux % 8) return false;
+  if ((a.aux_in || a.aux_in2) && a.ld_aux_in % 8) return false;
+  if (((uintptr_t)a.C | (uintptr_t)a.bias | (uintptr_t)a.resid | (uintptr_t)a.rowadd | (uintptr_t)a.aux |
+       (uintptr_t)a.aux2 | (uintptr_t)a.aux_in | (uintptr_t)a.aux_in2) & 15)
+    return false;
+  if (act == ACT_GEGLU && (a.N % 32)) return false;
+  if (act == ACT_GEGLU_BWD) return false;   // the streaming geglu_bwd pass after a plain GEMM is faster
+  if (act == ACT_GELU_ERF_BWD && !a.aux_in) return false;
+  if (out != OUT_BF16 && (act != ACT_NONE)) return false;
+  if (a.amap.g != 0) return false;   // gathered A rows: not an affine row panel
+  const double abytes = (double)(a.M + a.amap.off) * a.lda * 2, bbytes = (double)a.N * a.ldb * 2;
+  return abytes < 2147483000.0 && bbytes < 2147483000.0;
+}
+
+static int g_num_cu = 0;
+
+int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid) {
+  if (!g_num_cu) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&g_num_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cu <= 0)
+      g_num_cu = 256;
+  }
+  const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
+  long grid = std::min<long>(ntile, max_grid > 0 ? max_grid : g_num_cu);
+  const long arows = a.M + a.amap.off;
+  const uint32_t ab = (uint32_t)std::min<double>((double)arows * a.lda * 2, 2147483000.0);
+  const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
+#define PTK_W4_CASE(ACT_, OUT_)                                                                   \
+  if (act == ACT_ && out == OUT_) {                                                               \
+    hipLaunchKernelGGL((gemm_w4_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb); \
+    return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_w4 launch failed");              \
+  }
+  PTK_W4_CASE(ACT_NONE, OUT_BF16)
+  PTK_W4_CASE(ACT_NONE, OUT_F32)
+  PTK_W4_CASE(ACT_NONE, OUT_F32_BFR)
+  PTK_W4_CASE(ACT_GELU_TANH, OUT_BF16)
+  PTK_W4_CASE(ACT_GELU_ERF, OUT_BF16)
+  PTK_W4_CASE(ACT_GEGLU, OUT_BF16)
+  PTK_W4_CASE(ACT_GELU_ERF_BWD, OUT_BF16)
+#undef PTK_W4_CASE
+  return set_error("gemm_w4: unsupported (act=%d, out=%d)", act, out);
+}
+
+}  // namespace ptk

@@ -40,6 +40,9 @@ struct GemmArgs {
 };
 
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
+// persistent 256x256 4-wave GEMM (gemm_w4.hip): batch 1 only; w4_supported says whether a shape qualifies
+bool w4_supported(const GemmArgs& a, int act, int out);
+int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid);
 // live GEMM timing per activation class (events recorded around each launch when enabled)
 void timer_enable(int on);
 void force_small_tiles(int mode);

@@ -73,17 +73,18 @@ ALL = [  # every single-batch GEMM of the cfg2 step: name, M, N, K, act, out
 if __name__ == "__main__" and "--all" in sys.argv:
     for s in ALL + SQUARE:
         r = {}
-        for mode in (2, 1, 4, 2, 1, 4):   # second round kept (warm)
+        for mode in (2, 1, 4, 8, 2, 1, 4, 8):   # second round kept (warm)
             L.lib().ptk_gemm_force_small_tiles(mode)
             r[mode] = run(*s)
         L.lib().ptk_gemm_force_small_tiles(0)
         r[0] = run(*s)
         print(json.dumps({"name": s[0], "M": s[1], "N": s[2], "K": s[3], "big_TF": r[2]["TFLOPs"],
-                          "small_TF": r[1]["TFLOPs"], "big2_TF": r[4]["TFLOPs"], "auto_TF": r[0]["TFLOPs"]}),
+                          "small_TF": r[1]["TFLOPs"], "big2_TF": r[4]["TFLOPs"], "w4_TF": r[8]["TFLOPs"],
+                          "auto_TF": r[0]["TFLOPs"]}),
               flush=True)
     sys.exit(0)
 
-if __name__ == "__main__":
+if __name__ == "__main__" and "--blas" not in sys.argv:
     res = []
     if "--small" in sys.argv:
         L.lib().ptk_gemm_force_small_tiles(1)
@@ -100,3 +101,28 @@ if __name__ == "__main__":
                 r = run(f"sweep_n{n}", M, n, k, L.ACT_NONE, torch.bfloat16)
                 r["tiles"] = ((M + 255) // 256) * ((n + 255) // 256)
                 print(json.dumps(r), flush=True)
+
+
+def run_blas(name, m, n, k, reps=10):
+    """torch.matmul (hipBLASLt) on the same shape, plain bf16 output: calibration only."""
+    A = torch.randn(m, k, device=dev).to(torch.bfloat16)
+    B = (torch.randn(n, k, device=dev) * 0.05).to(torch.bfloat16)
+    C = torch.empty(m, n, device=dev, dtype=torch.bfloat16)
+    torch.matmul(A, B.t(), out=C)
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        torch.matmul(A, B.t(), out=C)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return round(2.0 * m * n * k / ms / 1e9, 1)
+
+
+if __name__ == "__main__" and "--blas" in sys.argv:
+    for s in ALL + SQUARE:
+        ours = [run(*s) for _ in range(2)][-1]["TFLOPs"]
+        blas = [run_blas(*s[:4]) for _ in range(2)][-1]
+        print(json.dumps({"name": s[0], "M": s[1], "N": s[2], "K": s[3], "ptk_TF": ours, "hipblaslt_TF": blas}),
+              flush=True)
