@@ -35,8 +35,11 @@ static_assert(4 * 64 * 68 * 4 >= 2 * STAGE_BYTES, "epilogue staging must cover t
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
+#ifndef PTK_GLDS_AUX
+#define PTK_GLDS_AUX 0   // cache-policy bits of the LDS-DMA staging loads (diagnostic builds vary it)
+#endif
 PTK_DEV void glds16(const void* src, void* lds) {
-  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 16, 0, 0);
+  __builtin_amdgcn_global_load_lds((gptr_t)src, (lptr_t)lds, 16, 0, PTK_GLDS_AUX);
 }
 
 template <int ACT, int OUT>
@@ -263,6 +266,22 @@ __device__ int g_epi_mode;   // 0 normal, 1 no global stores, 2 no epilogue
 #define PTK_STAMP(i)
 #endif
 
+// diagnostic ablations of the 256x256 kernel's K loop (timing only, wrong results): 1 = no LDS-DMA,
+// 4 = no barriers
+#ifndef PTK_BIG_ABLATE
+#define PTK_BIG_ABLATE 0
+#endif
+#if PTK_BIG_ABLATE == 4
+#define PTK_BIG_BAR() ((void)0)
+#else
+#define PTK_BIG_BAR() __builtin_amdgcn_s_barrier()
+#endif
+#if PTK_BIG_ABLATE == 1
+#define PTK_BIG_STAGE(h, t) ((void)0)
+#else
+#define PTK_BIG_STAGE(h, t) stage(h, t)
+#endif
+
 template <int ACT, int OUT>
 __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
   __shared__ __attribute__((aligned(16))) char smem[8 * EPI_WAVE_BYTES];   // 136 KiB >= 2 * BUF_BYTES
@@ -349,7 +368,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
         b1[n][ks] = *reinterpret_cast<const bf16x8_t*>(Bs + (32 + n * 16) * 128 + (frag_off ^ (ks << 6)));
-    if (t + 1 < nt) stage(0, t + 1);
+    if (t + 1 < nt) PTK_BIG_STAGE(0, t + 1);
     asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");   // A(mh0), B(nh0) landed; B(nh1) may be in flight
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -361,9 +380,9 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
         for (int ks = 0; ks < 2; ++ks)
           acc[i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b0[n][ks], acc[i][n], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
+    PTK_BIG_BAR();
     // ---- phase 1: A(mh0) x B(nh1); A(mh1) is re-read into a[i] as soon as a[i] is consumed
-    if (t + 1 < nt) stage(1, t + 1);
+    if (t + 1 < nt) PTK_BIG_STAGE(1, t + 1);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -379,9 +398,9 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
         a[i][ks] = *reinterpret_cast<const bf16x8_t*>(As + (64 + i * 16) * 128 + (frag_off ^ (ks << 6)));
     }
     __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
+    PTK_BIG_BAR();
     // ---- phase 2: A(mh1) x B(nh0)
-    if (t + 2 < nt) stage(2, t + 2);
+    if (t + 2 < nt) PTK_BIG_STAGE(2, t + 2);
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
     __builtin_amdgcn_s_setprio(1);
@@ -393,10 +412,10 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
         for (int ks = 0; ks < 2; ++ks)
           acc[4 + i][n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b0[n][ks], acc[4 + i][n], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
+    PTK_BIG_BAR();
     // ---- phase 3: A(mh1) x B(nh1); retire K-tile t+1 (B(t+2) stays in flight)
     if (t + 2 < nt) {
-      stage(3, t + 2);
+      PTK_BIG_STAGE(3, t + 2);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -411,7 +430,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
         for (int ks = 0; ks < 2; ++ks)
           acc[4 + i][2 + n] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][ks], b1[n][ks], acc[4 + i][2 + n], 0, 0, 0);
     __builtin_amdgcn_s_setprio(0);
-    __builtin_amdgcn_s_barrier();
+    PTK_BIG_BAR();
   }
   PTK_STAMP(2);
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
