@@ -7,6 +7,8 @@ import os
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "libptk.so")
+if os.environ.get("PTK_LIB"):   # A/B timing of a diagnostic build (tools/); never set by tests or the driver
+    LIB_PATH = os.path.join(os.path.dirname(_HERE), os.environ["PTK_LIB"])
 
 c_void_p, c_int, c_int64, c_float, c_size_t, c_uint64 = C.c_void_p, C.c_int, C.c_int64, C.c_float, C.c_size_t, C.c_uint64
 c_float_p = C.POINTER(C.c_float)

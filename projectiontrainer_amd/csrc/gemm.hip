@@ -57,6 +57,7 @@ PTK_DEV void epilogue(const GemmArgs& p, char* smem, int wave, int lane, f32x4_t
   __builtin_amdgcn_s_waitcnt(0xc07f);   // lgkmcnt(0): own LDS writes done (wave-private region)
   __builtin_amdgcn_wave_barrier();
   const bool vec_ok = ((p.ldc & 3) == 0) && (!p.resid || (p.ld_resid & 3) == 0) &&
+                      (!p.resid16 || (p.ld_resid16 & 7) == 0) &&
                       (!p.rowadd || (p.ld_rowadd & 3) == 0) && (!p.aux || (p.ld_aux & 3) == 0) &&
                       (!p.aux_in || (p.ld_aux_in & 3) == 0);
   if constexpr (ACT == ACT_GEGLU) {

@@ -31,6 +31,7 @@ template <int ACT, int OUT>
 PTK_DEV void epi_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 v) {
   // r < M; c..c+3 < N (checked by caller); c % 4 == 0
   if (p.bias) { float4 b = ldf4(p.bias + c); v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w; }
+  if (p.bf16_linear) v = make_float4(bfround(v.x), bfround(v.y), bfround(v.z), bfround(v.w));
   if (p.rowadd) {
     float4 b = ldf4(p.rowadd + (r % p.rowadd_period) * p.ld_rowadd + c);
     v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
@@ -54,6 +55,10 @@ PTK_DEV void epi_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 v) {
   if (cr < 0) return;
   if (p.resid) {
     float4 b = ldf4(p.resid + cr * p.ld_resid + c);
+    v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
+  }
+  if (p.resid16) {
+    float4 b = ldbf4(p.resid16 + cr * p.ld_resid16 + c);
     v.x += b.x; v.y += b.y; v.z += b.z; v.w += b.w;
   }
   if constexpr (OUT == OUT_BF16) {
@@ -88,6 +93,10 @@ PTK_DEV void epi_vec8_bf16(const GemmArgs& p, char* Cz, long r, long c, float4 v
     const float4 b0 = ldf4(p.bias + c), b1 = ldf4(p.bias + c + 4);
     v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
   }
+  if (p.bf16_linear) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]);
+  }
   if (p.rowadd) {
     const float* ra = p.rowadd + (r % p.rowadd_period) * p.ld_rowadd + c;
     const float4 b0 = ldf4(ra), b1 = ldf4(ra + 4);
@@ -115,6 +124,12 @@ PTK_DEV void epi_vec8_bf16(const GemmArgs& p, char* Cz, long r, long c, float4 v
     const float4 b0 = ldf4(rp), b1 = ldf4(rp + 4);
     v[0] += b0.x; v[1] += b0.y; v[2] += b0.z; v[3] += b0.w; v[4] += b1.x; v[5] += b1.y; v[6] += b1.z; v[7] += b1.w;
   }
+  if (p.resid16) {
+    float rr[8];
+    ldbf8(p.resid16 + cr * p.ld_resid16 + c, rr);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += rr[e];
+  }
   stbf8(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + c, v);
 }
 
@@ -122,6 +137,7 @@ PTK_DEV void epi_vec8_bf16(const GemmArgs& p, char* Cz, long r, long c, float4 v
 template <int ACT, int OUT>
 PTK_DEV void epi_scalar(const GemmArgs& p, char* Cz, long r, long c, float v) {
   if (p.bias) v += p.bias[c];
+  if (p.bf16_linear) v = bfround(v);
   if (p.rowadd) v += p.rowadd[(r % p.rowadd_period) * p.ld_rowadd + c];
   if constexpr (ACT == ACT_GELU_TANH) {
     v = gelu_tanh(bfround(v));
@@ -135,6 +151,7 @@ PTK_DEV void epi_scalar(const GemmArgs& p, char* Cz, long r, long c, float v) {
   const long cr = map_row(p.cmap, r);
   if (cr < 0) return;
   if (p.resid) v += p.resid[cr * p.ld_resid + c];
+  if (p.resid16) v += bf2f(p.resid16[cr * p.ld_resid16 + c]);
   if constexpr (OUT == OUT_BF16) {
     reinterpret_cast<bf16_t*>(Cz)[cr * p.ldc + c] = f2bf(v);
   } else if constexpr (OUT == OUT_F32) {

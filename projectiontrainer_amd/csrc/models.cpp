@@ -64,8 +64,7 @@ GemmArgs gemm(const void* A, long lda, const void* B, long ldb, void* C, long ld
 
 // ------------------------------------------------------------------ SigLIP
 struct SiglipWs {
-  bf16_t *patches, *a, *qkv, *vt, *P, *o, *mlp;
-  float *h, *S;
+  bf16_t *patches, *h, *a, *qkv, *o, *mlp;
 };
 
 SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
@@ -73,12 +72,9 @@ SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
   const long Np = (Nn + 63) / 64 * 64, M = B * Nn, H = c->heads, hd = D / H, Kp = (long)c->channels * P * P;
   SiglipWs w;
   w.patches = bp.take<bf16_t>(M * Kp);
-  w.h = bp.take<float>(M * D);
+  w.h = bp.take<bf16_t>(M * D);   // bf16 residual stream: the reference tower runs in pure bf16
   w.a = bp.take<bf16_t>(M * D);
   w.qkv = bp.take<bf16_t>(M * 3 * D);
-  w.vt = nullptr;
-  w.S = nullptr;
-  w.P = nullptr;
   w.o = bp.take<bf16_t>(M * D);
   w.mlp = bp.take<bf16_t>(M * I);
   return w;
@@ -192,17 +188,18 @@ int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int
   Bump bp(ws);
   SiglipWs w = siglip_layout(bp, c, B);
 
-  // K1 patch embed: im2col + GEMM (+bias +pos) -> fp32 residual stream
+  // K1 patch embed: im2col + GEMM; bf16(conv + bias) + pos -> bf16 residual stream (modeling_siglip.py:175-186)
   CK(launch_im2col((const bf16_t*)pixels, w.patches, B, c->channels, c->image_size, c->image_size, P, st));
   {
     GemmArgs g = gemm(w.patches, Kp, wt->patch_w, Kp, w.h, D, M, D, Kp);
     g.bias = wt->patch_b;
+    g.bf16_linear = 1;
     g.rowadd = wt->pos; g.rowadd_period = Nn; g.ld_rowadd = D;
-    CK(launch_gemm(g, ACT_NONE, OUT_F32, 1, st));
+    CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
   }
   for (int l = 0; l < c->layers; ++l) {
     const ptk_siglip_layer& L = wt->layers[l];
-    CK(launch_layernorm(w.h, L.ln1_w, L.ln1_b, w.a, M, D, c->eps, st));
+    CK(launch_layernorm_bf16(w.h, L.ln1_w, L.ln1_b, w.a, M, D, c->eps, st));
     {  // fused q|k|v projection
       GemmArgs g = gemm(w.a, D, L.wqkv, D, w.qkv, 3 * D, M, 3 * D, D);
       g.bias = L.bqkv;
@@ -219,24 +216,24 @@ int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int
       fa.scale = 1.0f / sqrtf((float)hd);
       CK(launch_attn_fwd(fa, B * Hh, st));
     }
-    {  // out_proj + bias + residual
+    {  // h = bf16(h + bf16(out_proj + bias))   (modeling_siglip.py:343-346, bf16 module)
       GemmArgs g = gemm(w.o, D, L.wo, D, w.h, D, M, D, D);
-      g.bias = L.bo; g.resid = w.h; g.ld_resid = D;
-      CK(launch_gemm(g, ACT_NONE, OUT_F32, 1, st));
+      g.bias = L.bo; g.bf16_linear = 1; g.resid16 = w.h; g.ld_resid16 = D;
+      CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
     }
-    CK(launch_layernorm(w.h, L.ln2_w, L.ln2_b, w.a, M, D, c->eps, st));
+    CK(launch_layernorm_bf16(w.h, L.ln2_w, L.ln2_b, w.a, M, D, c->eps, st));
     {
       GemmArgs g = gemm(w.a, D, L.w1, D, w.mlp, I, M, I, D);
       g.bias = L.b1;
       CK(launch_gemm(g, ACT_GELU_TANH, OUT_BF16, 1, st));
     }
-    {
+    {  // h = bf16(h + bf16(fc2 + bias))
       GemmArgs g = gemm(w.mlp, I, L.w2, I, w.h, D, M, D, I);
-      g.bias = L.b2; g.resid = w.h; g.ld_resid = D;
-      CK(launch_gemm(g, ACT_NONE, OUT_F32, 1, st));
+      g.bias = L.b2; g.bf16_linear = 1; g.resid16 = w.h; g.ld_resid16 = D;
+      CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
     }
   }
-  CK(launch_layernorm(w.h, wt->post_w, wt->post_b, (bf16_t*)out, M, D, c->eps, st));
+  CK(launch_layernorm_bf16(w.h, wt->post_w, wt->post_b, (bf16_t*)out, M, D, c->eps, st));
   return 0;
 }
 

@@ -38,14 +38,18 @@ PTK_DEV float4 scl4(float4 a, float s) { return make_float4(a.x * s, a.y * s, a.
 #define FOR_V for (int v = 0; v < MAXV; ++v) if (lane * 4 + v * 256 < cols)
 #define COL (lane * 4 + v * 256)
 
-__global__ void __launch_bounds__(256) layernorm_kernel(const float* __restrict__ x, const float* __restrict__ w,
+PTK_DEV float4 ldx4(const float* p) { return ld4(p); }
+PTK_DEV float4 ldx4(const bf16_t* p) { return ld4bf(p); }
+
+template <typename T>
+__global__ void __launch_bounds__(256) layernorm_kernel(const T* __restrict__ x, const float* __restrict__ w,
                                                         const float* __restrict__ b, bf16_t* __restrict__ y,
                                                         long rows, int cols, float eps) {
   ROW_SETUP
   float4 r[MAXV];
   float s = 0.f;
 #pragma unroll
-  FOR_V { r[v] = ld4(x + row * cols + COL); s += r[v].x + r[v].y + r[v].z + r[v].w; }
+  FOR_V { r[v] = ldx4(x + row * cols + COL); s += r[v].x + r[v].y + r[v].z + r[v].w; }
   const float mean = warp_sum(s) / cols;
   float q = 0.f;
 #pragma unroll
@@ -188,8 +192,15 @@ int launch_layernorm(const float* x, const float* w, const float* b, bf16_t* y, 
                      hipStream_t st) {
   if (check_cols(cols)) return -1;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(layernorm_kernel, NORM_GRID, x, w, b, y, (long)rows, cols, eps);
+  hipLaunchKernelGGL(layernorm_kernel<float>, NORM_GRID, x, w, b, y, (long)rows, cols, eps);
   RET_LAUNCH("layernorm");
+}
+int launch_layernorm_bf16(const bf16_t* x, const float* w, const float* b, bf16_t* y, int rows, int cols, float eps,
+                          hipStream_t st) {
+  if (check_cols(cols)) return -1;
+  if (rows <= 0) return 0;
+  hipLaunchKernelGGL(layernorm_kernel<bf16_t>, NORM_GRID, x, w, b, y, (long)rows, cols, eps);
+  RET_LAUNCH("layernorm_bf16");
 }
 int launch_rmsnorm_fwd(const float* x, long ldx, RowMap xmap, const float* w, bf16_t* y, float* rstd, int rows,
                        int cols, float eps, hipStream_t st) {

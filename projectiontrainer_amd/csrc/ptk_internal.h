@@ -29,6 +29,11 @@ struct GemmArgs {
   long ld_rowadd = 0;
   const float* resid = nullptr;                  // resid[mapped r * ld + c] (may alias C)
   long ld_resid = 0;
+  // bf16 residual stream (SigLIP runs in pure bf16): the linear output (alpha*acc + bias)
+  // is rounded to bf16 first, then row-add / resid16 are added and the sum is rounded again
+  const bf16_t* resid16 = nullptr;               // resid16[mapped r * ld + c] (may alias C), OUT_BF16 only
+  long ld_resid16 = 0;
+  int bf16_linear = 0;                           // round alpha*acc + bias to bf16 before row-add / resid16
   bf16_t* aux = nullptr;                         // activation side outputs [M, *]
   bf16_t* aux2 = nullptr;
   long ld_aux = 0;
@@ -49,9 +54,11 @@ void force_small_tiles(int mode);
 int timer_read(int cls, double* total_ms, int* count);
 
 // ---- row-wise normalisation (norm.hip) ----
-// SigLIP LayerNorm: y(bf16) = LN(x f32 or bf16) * w + b
+// SigLIP LayerNorm: y(bf16) = LN(x) * w + b, fp32 statistics (x f32 or bf16)
 int launch_layernorm(const float* x, const float* w, const float* b, bf16_t* y, int rows, int cols,
                      float eps, hipStream_t st);
+int launch_layernorm_bf16(const bf16_t* x, const float* w, const float* b, bf16_t* y, int rows, int cols,
+                          float eps, hipStream_t st);
 // RMSNorm (Gemma3, scale 1+w) of x (f32) -> y bf16, rstd f32; optional row gather map
 int launch_rmsnorm_fwd(const float* x, long ldx, RowMap xmap, const float* w, bf16_t* y, float* rstd,
                        int rows, int cols, float eps, hipStream_t st);

@@ -139,3 +139,27 @@ def test_architecture_scale_vs_oracle(gpu):
     for k, g in zip(["model.0.weight", "model.0.bias", "model.2.weight", "model.2.bias"], eng.proj.grads()):
         gc, rc = g.cpu(), out["grads"][k]
         assert cosine(gc, rc) >= 0.995 and rel_l2(gc, rc) <= 6e-2, (k, cosine(gc, rc), rel_l2(gc, rc))
+
+
+@pytest.mark.slow
+def test_siglip_full_depth_vs_oracle(gpu):
+    """All 24 SigLIP-L/16-384 layers (bf16 residual stream, as the reference's pure-bf16 tower)
+    vs the fp32 CPU oracle: last_hidden_state rel-L2 and per-patch cosine."""
+    from oracle import stage1_ref as R
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.siglip import SiglipVisionTower
+    cfg = PRESETS["cfg2"].replace(batch_size=1)
+    vp = W.siglip_vision_params(cfg.vision, seed=11)
+    px, _, _ = W.synthetic_batch(cfg, seed=12)
+    vt = SiglipVisionTower(cfg.vision, vp, gpu)
+    out = vt(torch.from_numpy(px).to(gpu)).float().cpu()
+    torch.cuda.synchronize()
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    with torch.no_grad():
+        ref = R.siglip_vision_forward({k: torch.as_tensor(v) for k, v in vp.items()}, cfg.vision,
+                                      torch.from_numpy(px).bfloat16().float())
+    ref = ref.reshape(out.shape)
+    assert rel_l2(out, ref) <= 3e-2, rel_l2(out, ref)
+    cos = torch.nn.functional.cosine_similarity(out.reshape(-1, out.shape[-1]), ref.reshape(-1, ref.shape[-1]), dim=-1)
+    assert cos.min() >= 0.99, cos.min()
