@@ -20,6 +20,9 @@
 // for the backward.  Semantics: softmax(scale * Q K^T + mask) V, as
 // TF/models/siglip/modeling_siglip.py:289-300 and gemma3 :365-379 (sdpa).
 #include <algorithm>
+#include <functional>
+#include <queue>
+#include <vector>
 #include "common.h"
 #include "ptk_internal.h"
 
@@ -631,16 +634,15 @@ __global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel
   const int g = lane >> 4, c16 = lane & 15;
   // ---- block -> (slab, piece, z)
   const int nz = a.nz;
-  int L = blockIdx.x, s = 0, P = 1, base = 0;
-  for (;;) {
-    P = dkv_pieces(a, s);
-    if (L < P * nz) break;
-    L -= P * nz;
-    if (P > 1) base += P;
-    ++s;
+  const int item = blockIdx.x / nz;
+  const long z = blockIdx.x - (long)item * nz;
+  const int s = a.dkv_item_slab[item], piece = a.dkv_item_piece[item];
+  const int P = dkv_pieces(a, s);
+  int base = 0;   // partial slots are numbered slab-major over the split slabs
+  for (int s2 = 0; s2 < s; ++s2) {
+    const int P2 = dkv_pieces(a, s2);
+    if (P2 > 1) base += P2;
   }
-  const int piece = L / nz;
-  const long z = L - piece * nz;
   int c0, c1;
   {
     int lo, hi;
@@ -880,7 +882,38 @@ static int num_cus() {
   return n;
 }
 
-// split plan: target chunks per piece = total chunks / CUs (at least 4)
+// Split plan.  Each block (one slab piece of one z) costs its query chunks plus a fixed overhead
+// (K/V fragment loads, ring fill, dK/dV stores; ~1.5 chunks) and, for a piece of a split slab, the
+// fp32 partial store (~1 chunk).  Blocks are dispatched heaviest first (LPT) onto num_cus() CUs
+// (one block per CU: 129 KiB LDS); the target piece size is the candidate whose simulated makespan
+// is smallest (causal slabs differ up to 11x, so one-piece-per-CU targets leave a third of the
+// machine idle in the tail).
+static double dkv_makespan(FlashBwdArgs& a, int nz, int nslab, int target, int ncu) {
+  a.dkv_target = target;
+  std::vector<double> cost;
+  for (int s = 0; s < nslab; ++s) {
+    int lo, hi;
+    dkv_slab_chunks(a, s, lo, hi);
+    const int n = hi - lo, P = dkv_pieces(a, s);
+    for (int p = 0; p < P; ++p) {
+      const int c = (int)((long)(p + 1) * n / P - (long)p * n / P);
+      cost.push_back(c + 1.5 + (P > 1 ? 1.0 : 0.0));
+    }
+  }
+  std::sort(cost.begin(), cost.end(), std::greater<double>());
+  std::priority_queue<double, std::vector<double>, std::greater<double>> cu;
+  for (int i = 0; i < ncu; ++i) cu.push(0.0);
+  double span = 0.0;
+  for (double c : cost)
+    for (int z = 0; z < nz; ++z) {
+      const double t = cu.top() + c;
+      cu.pop();
+      cu.push(t);
+      span = std::max(span, t);
+    }
+  return span;
+}
+
 static void dkv_plan(FlashBwdArgs& a, int nz, int& nslab, long& npieces, long& nsplit) {
   a.nz = nz;
   nslab = (a.nkeys + DKV_KEYS - 1) / DKV_KEYS;
@@ -891,13 +924,40 @@ static void dkv_plan(FlashBwdArgs& a, int nz, int& nslab, long& npieces, long& n
     dkv_slab_chunks(a, s, lo, hi);
     total += hi - lo;
   }
-  a.dkv_target = (int)std::max(4L, (total * nz + num_cus() - 1) / num_cus());
+  const int ncu = num_cus();
+  const int base = (int)std::max(4L, (total * nz + ncu - 1) / ncu);
+  int best = base;
+  double best_span = dkv_makespan(a, nz, nslab, base, ncu);
+  for (int k = 9; k >= 3; --k) {   // targets base * k / 12 (3/4 .. 1/4)
+    const int t = std::max(4, base * k / 12);
+    long items = 0;
+    a.dkv_target = t;
+    for (int s = 0; s < nslab; ++s) items += dkv_pieces(a, s);
+    if (items > 128) break;
+    const double sp = dkv_makespan(a, nz, nslab, t, ncu);
+    if (sp < best_span - 1e-9) { best_span = sp; best = t; }
+  }
+  a.dkv_target = best;
+  // items (slab, piece) heaviest first; ties keep slab order
+  std::vector<std::pair<int, int>> it;   // (-chunks, slab * 256 + piece)
   npieces = 0;
   nsplit = 0;
   for (int s = 0; s < nslab; ++s) {
-    const int P = dkv_pieces(a, s);
+    int lo, hi;
+    dkv_slab_chunks(a, s, lo, hi);
+    const int n = hi - lo, P = dkv_pieces(a, s);
     npieces += P;
     if (P > 1) nsplit += P;
+    for (int p = 0; p < P; ++p)
+      it.push_back({-(int)((long)(p + 1) * n / P - (long)p * n / P), s * 256 + p});
+  }
+  std::stable_sort(it.begin(), it.end(), [](const std::pair<int, int>& x, const std::pair<int, int>& y) {
+    return x.first < y.first;
+  });
+  a.dkv_items = (int)it.size();
+  for (size_t i = 0; i < it.size() && i < 128; ++i) {
+    a.dkv_item_slab[i] = (unsigned char)(it[i].second >> 8);
+    a.dkv_item_piece[i] = (unsigned char)(it[i].second & 255);
   }
 }
 
@@ -929,10 +989,13 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st) {
       long np, ns;
       dkv_plan(b, nz, nslab, np, ns);
       if (ns > 0 && (!b.dkv_part || b.dkv_part_bytes < (size_t)ns * nz * 2 * DKV_KEYS * 256 * sizeof(float))) {
-        b.dkv_target = 0;   // no workspace: every slab in one piece
+        b.dkv_target = 0;   // no workspace: every slab in one piece, heaviest (lowest) slabs first
         np = nslab;
         ns = 0;
+        b.dkv_items = nslab;
+        for (int s = 0; s < nslab && s < 128; ++s) { b.dkv_item_slab[s] = (unsigned char)s; b.dkv_item_piece[s] = 0; }
       }
+      if (b.dkv_items > 128 || nslab > 255) return set_error("attn_bwd: %d dK/dV work items (max 128)", b.dkv_items);
       hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
       // 32 keys per wave (one wave per SIMD) measured 209 us vs 252 us for 16 keys per wave (two per
       // SIMD, which spills the precomputed transposed-read addresses) at cfg2

@@ -150,6 +150,10 @@ struct FlashBwdArgs {
   size_t dkv_part_bytes = 0;
   // set by launch_attn_bwd
   int dkv_target = 0, nz = 1;
+  // dK/dV work items (slab, query piece) in dispatch order, heaviest first (LPT): block b runs item
+  // b / nz for z = b % nz
+  int dkv_items = 0;
+  unsigned char dkv_item_slab[128], dkv_item_piece[128];
 };
 int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st);
 // bytes of dkv_part for which launch_attn_bwd splits every heavy key slab (0 when it never splits)
