@@ -124,6 +124,9 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
   const int qpos = qrow_c / a.qdiv;
   const int causal = a.causal != 0, nowin = a.window <= 0;
   const bool unmasked = !kvl && !causal && nowin;
+  // query positions of this wave's 16 rows (interior-tile test)
+  const int wpos_lo = min(r0 + wave * 16, a.rows - 1) / a.qdiv;
+  const int wpos_hi = min(r0 + wave * 16 + 15, a.rows - 1) / a.qdiv;
 
   const int ops = (R::INST >= 8 ? 2 * R::PER_WAVE : 1) + (kvl ? 1 : 0);   // LDS-DMA ops per wave per tile
   auto stage = [&](int t, int buf) {
@@ -185,16 +188,18 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
         s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
       }
     }
-    // ---- mask + online softmax (log2 domain)
+    // ---- mask + online softmax.  Running max in raw score units; p = exp2(s*c - m*c) is one FMA and
+    // one v_exp (c = scale*log2 e > 0 keeps the argmax).  A tile every key of which is visible to every
+    // row of this wave (all keys valid, below the causal diagonal, inside the window) skips the mask.
     float mt = -INFINITY;
-    if (unmasked && (t + 1) * KT <= a.nkeys) {   // full tile, no mask at all (SigLIP)
+    bool interior = (t + 1) * KT <= a.nkeys && (unmasked || ((!causal || t * KT + KT - 1 <= wpos_lo) &&
+                                                             (nowin || t * KT > wpos_hi - a.window)));
+    if (interior && kvl) interior = __all(lane >= KT || kvs[lane] != 0);
+    if (interior) {
 #pragma unroll
       for (int ms = 0; ms < MS; ++ms)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          s[ms][j] *= sl2;
-          mt = fmaxf(mt, s[ms][j]);
-        }
+        for (int j = 0; j < 4; ++j) mt = fmaxf(mt, s[ms][j]);
     } else {
 #pragma unroll
       for (int ms = 0; ms < MS; ++ms) {
@@ -209,7 +214,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
           const int key = kbase + j;
           const int ok = (int)(key < a.nkeys) & (int)(kv[j] != 0) & ((int)(key <= qpos) | !causal) &
                          ((int)(key > qpos - a.window) | nowin);
-          const float v = ok ? s[ms][j] * sl2 : -INFINITY;
+          const float v = ok ? s[ms][j] : -INFINITY;
           s[ms][j] = v;
           mt = fmaxf(mt, v);
         }
@@ -218,18 +223,17 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
     mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
     const float m_new = fmaxf(m_run, mt);
-    const float alpha = (m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f(m_run - m_new);
-    const float msub = (m_new == -INFINITY) ? 0.f : m_new;
+    const float alpha = (m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f((m_run - m_new) * sl2);
+    const float mc = (m_new == -INFINITY) ? 0.f : m_new * sl2;
     float rs = 0.f;
     bf16x8_t pf[ST];
 #pragma unroll
     for (int ms = 0; ms < MS; ++ms)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const float p = __builtin_amdgcn_exp2f(s[ms][j] - msub);   // exp2(-inf) = 0 for masked keys
-        const bf16_t pb = f2bf(p);
-        rs += bf2f(pb);
-        pf[ms >> 1][(ms & 1) * 4 + j] = (short)pb;
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[ms][j], sl2, -mc));   // exp2(-inf) = 0 for masked keys
+        rs += p;   // fp32 row sum (P itself enters P.V in bf16)
+        pf[ms >> 1][(ms & 1) * 4 + j] = (short)f2bf(p);
       }
     rs += __shfl_xor(rs, 16, 64);
     rs += __shfl_xor(rs, 32, 64);
@@ -272,7 +276,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     u[2] = f2bf(o[ds][2] * inv); u[3] = f2bf(o[ds][3] * inv);
     *reinterpret_cast<u16x4_t*>(op + 16 * ds) = u;
   }
-  if (a.lse && g == 0) a.lse[(long)z * a.rows + qrow] = (m_run + log2f(l_run)) * 0.6931471805599453f;
+  if (a.lse && g == 0) a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_run)) * 0.6931471805599453f;
 }
 
 // ============================================================================ backward
@@ -345,6 +349,8 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
   const int qpos = qrow_c / a.qdiv;
   const float sl2 = a.scale * L2E;
   const int causal = a.causal != 0, nowin = a.window <= 0;
+  const int wpos_lo = min(r0 + wave * 16, a.rows - 1) / a.qdiv;
+  const int wpos_hi = min(r0 + wave * 16 + 15, a.rows - 1) / a.qdiv;
 
   const int ops = (R::INST >= 8 ? 2 * R::PER_WAVE : 1) + (kvl ? 1 : 0);
   auto stage = [&](int t, int buf) {
@@ -405,22 +411,35 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
       }
     }
     bf16x8_t dsf;
+    // tile visible to every row of the wave (valid keys, below the diagonal, inside the window): no mask
+    bool interior = (t + 1) * FA_KT <= a.nkeys && (!causal || t * FA_KT + FA_KT - 1 <= wpos_lo) &&
+                    (nowin || t * FA_KT > wpos_hi - a.window);
+    if (interior && kvl) interior = __all(lane >= FA_KT || kvs[lane] != 0);
+    if (interior) {
 #pragma unroll
-    for (int ms = 0; ms < 2; ++ms) {
-      const int kbase = t * FA_KT + ms * 16 + 4 * g;
-      int kv[4] = {1, 1, 1, 1};
-      if (kvl) {
-        const int4 v4 = *reinterpret_cast<const int4*>(kvs + ms * 16 + 4 * g);
-        kv[0] = v4.x; kv[1] = v4.y; kv[2] = v4.z; kv[3] = v4.w;
-      }
+      for (int ms = 0; ms < 2; ++ms)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int key = kbase + j;
-        const int ok = (int)(key < a.nkeys) & (int)(kv[j] != 0) & ((int)(key <= qpos) | !causal) &
-                       ((int)(key > qpos - a.window) | nowin);
-        const float p = __builtin_amdgcn_exp2f(ok ? s[ms][j] * sl2 - lse2 : -INFINITY);
-        const float d = bfround(p) * (dp[ms][j] - dlt);
-        dsf[ms * 4 + j] = (short)f2bf(d);
+        for (int j = 0; j < 4; ++j) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[ms][j], sl2, -lse2));
+          dsf[ms * 4 + j] = (short)f2bf(bfround(p) * (dp[ms][j] - dlt));
+        }
+    } else {
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms) {
+        const int kbase = t * FA_KT + ms * 16 + 4 * g;
+        int kv[4] = {1, 1, 1, 1};
+        if (kvl) {
+          const int4 v4 = *reinterpret_cast<const int4*>(kvs + ms * 16 + 4 * g);
+          kv[0] = v4.x; kv[1] = v4.y; kv[2] = v4.z; kv[3] = v4.w;
+        }
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int key = kbase + j;
+          const int ok = (int)(key < a.nkeys) & (int)(kv[j] != 0) & ((int)(key <= qpos) | !causal) &
+                         ((int)(key > qpos - a.window) | nowin);
+          const float p = __builtin_amdgcn_exp2f(ok ? fmaf(s[ms][j], sl2, -lse2) : -INFINITY);
+          dsf[ms * 4 + j] = (short)f2bf(bfround(p) * (dp[ms][j] - dlt));
+        }
       }
     }
     const int q4 = c16 >> 2, p4 = c16 & 3;
@@ -675,6 +694,10 @@ __global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel
   const float sl2 = a.scale * L2E;
   const int qshift = (a.qdiv & (a.qdiv - 1)) == 0 ? __builtin_ctz(a.qdiv) : -1;
   const int causal = a.causal != 0, nowin = a.window <= 0;
+  bool kall = true;
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) kall = kall && kok[kg];
+  const bool wkall = __all(kall);   // every key of the wave valid
 
   // staging: 32 rows x 32 16-B chunks per tensor = 16 wave-instructions (IPW per wave), plus the
   // chunk's LSE|delta (256 B) spread over all waves: OPS LDS-DMA ops per wave per chunk, so one
@@ -759,23 +782,37 @@ __global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel
     // ---- P = exp(S*scale - LSE) (bf16), dS = P (dP - delta) (bf16); k order of the next products:
     //      slot 4qt + j of lane group g <-> query row 16qt + 4g + j
     bf16x8_t pf[KG], dsf[KG];
+    // chunk rows all see all of the wave's keys (valid, below the diagonal, inside the window): no mask
+    const int cpos_lo = (c * DKV_CH) / a.qdiv, cpos_hi = (c * DKV_CH + DKV_CH - 1) / a.qdiv;
+    const bool interior = wkall && (!causal || kw + KPW - 1 <= cpos_lo) && (nowin || kw > cpos_hi - a.window);
 #pragma unroll
     for (int qt = 0; qt < 2; ++qt) {
       const float4 l4 = *reinterpret_cast<const float4*>(ld + qt * 16 + 4 * g);
       const float4 d4 = *reinterpret_cast<const float4*>(ld + 32 + qt * 16 + 4 * g);
-      const float lv[4] = {l4.x, l4.y, l4.z, l4.w}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+      const float lv[4] = {l4.x * L2E, l4.y * L2E, l4.z * L2E, l4.w * L2E}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+      if (interior) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int qrow = c * DKV_CH + qt * 16 + 4 * g + j;
-        const int pos = qshift >= 0 ? (qrow >> qshift) : qrow / a.qdiv;
+        for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int kg = 0; kg < KG; ++kg) {
-          // branch-free mask (short-circuit && turns into exec-mask control flow per element)
-          const int ok = (int)kok[kg] & ((int)(key[kg] <= pos) | !causal) & ((int)(key[kg] > pos - a.window) | nowin);
-          const float p = __builtin_amdgcn_exp2f(ok ? sc[qt][kg][j] * sl2 - lv[j] * L2E : -INFINITY);
-          const bf16_t pb = f2bf(p);
-          pf[kg][4 * qt + j] = (short)pb;
-          dsf[kg][4 * qt + j] = (short)f2bf(bf2f(pb) * (dp[qt][kg][j] - dl[j]));
+          for (int kg = 0; kg < KG; ++kg) {
+            const bf16_t pb = f2bf(__builtin_amdgcn_exp2f(fmaf(sc[qt][kg][j], sl2, -lv[j])));
+            pf[kg][4 * qt + j] = (short)pb;
+            dsf[kg][4 * qt + j] = (short)f2bf(bf2f(pb) * (dp[qt][kg][j] - dl[j]));
+          }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int qrow = c * DKV_CH + qt * 16 + 4 * g + j;
+          const int pos = qshift >= 0 ? (qrow >> qshift) : qrow / a.qdiv;
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg) {
+            // branch-free mask (short-circuit && turns into exec-mask control flow per element)
+            const int ok = (int)kok[kg] & ((int)(key[kg] <= pos) | !causal) & ((int)(key[kg] > pos - a.window) | nowin);
+            const float p = __builtin_amdgcn_exp2f(ok ? fmaf(sc[qt][kg][j], sl2, -lv[j]) : -INFINITY);
+            const bf16_t pb = f2bf(p);
+            pf[kg][4 * qt + j] = (short)pb;
+            dsf[kg][4 * qt + j] = (short)f2bf(bf2f(pb) * (dp[qt][kg][j] - dl[j]));
+          }
         }
       }
     }
