@@ -51,7 +51,7 @@ __global__ void __launch_bounds__(256) qknorm_rope_fwd_kernel(const bf16_t* __re
 #pragma unroll
   for (int e = 0; e < EPL; ++e) xn[e] = bfround(x[e] * rs * (1.f + w[lane * EPL + e]));
 #pragma unroll
-  for (int e = 0; e < EPL; ++e) part[e] = __shfl_xor(xn[e], 32, 64);
+  for (int e = 0; e < EPL; ++e) part[e] = xor32_get(xn[e]);
   const int fi = (lane & 31) * EPL;   // frequency index (cos[i] == cos[i + D/2])
   const float sgn = lane < 32 ? -1.f : 1.f;
   bf16_t* dst;
@@ -117,7 +117,7 @@ __global__ void __launch_bounds__(256) qknorm_rope_bwd_kernel(
     ds[e] = g * sin_t[(long)s * (D / 2) + fi + e];
   }
 #pragma unroll
-  for (int e = 0; e < EPL; ++e) part[e] = __shfl_xor(ds[e], 32, 64);
+  for (int e = 0; e < EPL; ++e) part[e] = xor32_get(ds[e]);
   // rot^T(v)_i = v_{i+D/2} (i < D/2), -v_{i-D/2} (i >= D/2)
   const float sgn = lane < 32 ? 1.f : -1.f;
   const bf16_t* xs = qkv + m * (long)nh * D + (long)h * D + lane * EPL;

@@ -17,16 +17,53 @@ PTK_DEV float bf2f(bf16_t h) { return __uint_as_float(((uint32_t)h) << 16); }
 PTK_DEV bf16_t f2bf(float f) { return __builtin_bit_cast(bf16_t, (__bf16)f); }
 PTK_DEV float bfround(float f) { return bf2f(f2bf(f)); }
 
-PTK_DEV float warp_sum(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+// lane ^ 32 / lane ^ 16 exchanges without the LDS crossbar (__shfl_xor lowers to ds_bpermute for
+// these): v_permlane32_swap / v_permlane16_swap of a register with itself returns the partner's value
+// in one of the two results and the lane's own in the other, so op(r0, r1) is the butterfly step
+PTK_DEV float xor32_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+PTK_DEV float xor16_sum(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(r[0]) + __uint_as_float(r[1]);
+}
+PTK_DEV float xor32_max(float v) {
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+PTK_DEV float xor16_max(float v) {
+  const auto r = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
+}
+
+PTK_DEV float xor32_get(float v) {   // the value of lane ^ 32
+  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
+}
+
+// within a 16-lane row: DPP butterflies (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror);
+// after each step every lane of the group holds the group's result
+template <int CTRL>
+PTK_DEV float dpp(float v) {
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+PTK_DEV float row_sum16(float v) {
+  v += dpp<0xB1>(v);
+  v += dpp<0x4E>(v);
+  v += dpp<0x141>(v);
+  v += dpp<0x140>(v);
   return v;
 }
-PTK_DEV float warp_max(float v) {
-#pragma unroll
-  for (int o = 32; o > 0; o >>= 1) v = fmaxf(v, __shfl_xor(v, o, 64));
+PTK_DEV float row_max16(float v) {
+  v = fmaxf(v, dpp<0xB1>(v));
+  v = fmaxf(v, dpp<0x4E>(v));
+  v = fmaxf(v, dpp<0x141>(v));
+  v = fmaxf(v, dpp<0x140>(v));
   return v;
 }
+PTK_DEV float warp_sum(float v) { return xor32_sum(xor16_sum(row_sum16(v))); }
+PTK_DEV float warp_max(float v) { return xor32_max(xor16_max(row_max16(v))); }
 
 // block-wide sum for blockDim.x == NT (multiple of 64); `red` holds NT/64 floats
 template <int NT>

@@ -220,8 +220,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
         }
       }
     }
-    mt = fmaxf(mt, __shfl_xor(mt, 16, 64));
-    mt = fmaxf(mt, __shfl_xor(mt, 32, 64));
+    mt = xor32_max(xor16_max(mt));
     const float m_new = fmaxf(m_run, mt);
     const float alpha = (m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f((m_run - m_new) * sl2);
     const float mc = (m_new == -INFINITY) ? 0.f : m_new * sl2;
@@ -235,8 +234,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
         rs += p;   // fp32 row sum (P itself enters P.V in bf16)
         pf[ms >> 1][(ms & 1) * 4 + j] = (short)f2bf(p);
       }
-    rs += __shfl_xor(rs, 16, 64);
-    rs += __shfl_xor(rs, 32, 64);
+    rs = xor32_sum(xor16_sum(rs));
     l_run = l_run * alpha + rs;
     m_run = m_new;
     if (__any(alpha != 1.f)) {   // no row's running max moved: nothing to rescale (common after a few tiles)
