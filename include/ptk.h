@@ -88,6 +88,18 @@ int ptk_rmsnorm(const float* x, const float* w, void* y, float* rstd, int rows, 
 int ptk_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const float* dn, const float* dacc,
                     float* dx, int rows, int cols, void* stream);
 /* Masked softmax over the last dim (scores f32 -> P bf16), see ptk_internal MaskSpec. */
+/* Gemma3 q/k RMSNorm (scale 1+w) + RoPE (rotate-half) of the fused qkv projection rows, scattered to the
+ * attention layouts Q [B,Hkv,S,G,D], K/V [B,Hkv,S,D]; rstd per (row, q head) / (row, kv head).
+ * Replaces modeling_gemma3.py:356-360 (q_norm / k_norm / apply_rotary_pos_emb). qkv: bf16 [B*S, (Hq+2Hkv)*D],
+ * cos/sin: f32 [S, D/2]. */
+int ptk_qknorm_rope_fwd(const void* qkv, const float* q_norm_w, const float* k_norm_w, const float* cos_t,
+                        const float* sin_t, int batch, int seq, int heads, int kv_heads, int head_dim, float eps,
+                        void* Q, void* K, void* V, float* rstd_q, float* rstd_k, void* stream);
+/* Backward of ptk_qknorm_rope_fwd: d(qkv) bf16 [B*S, (Hq+2Hkv)*D] from dQ, dK, dV (attention layouts). */
+int ptk_qknorm_rope_bwd(const void* qkv, const float* q_norm_w, const float* k_norm_w, const float* cos_t,
+                        const float* sin_t, int batch, int seq, int heads, int kv_heads, int head_dim,
+                        const float* rstd_q, const float* rstd_k, const void* dQ, const void* dK, const void* dV,
+                        void* dqkv, void* stream);
 int ptk_softmax(const float* S, void* P, int nz, int rows, int cols, int64_t ld, int rows_per_batch, int qdiv,
                 int zdiv, int causal, int window, const int32_t* key_valid, int key_len, void* stream);
 /* Fused cross-entropy forward+backward on bf16 logits (TF/loss/loss_utils.py:49-67):

@@ -113,6 +113,8 @@ SIGNATURES = {
     "ptk_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
     "ptk_rmsnorm": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
     "ptk_rmsnorm_bwd": (c_int, [c_void_p] * 6 + [c_int, c_int, c_void_p]),
+    "ptk_qknorm_rope_fwd": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_float] + [c_void_p] * 6),
+    "ptk_qknorm_rope_bwd": (c_int, [c_void_p] * 5 + [c_int] * 5 + [c_void_p] * 7),
     "ptk_softmax": (c_int, [c_void_p, c_void_p, c_int, c_int, c_int, c_int64, c_int, c_int, c_int, c_int,
                             c_int, c_void_p, c_int, c_void_p]),
     "ptk_cross_entropy": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),

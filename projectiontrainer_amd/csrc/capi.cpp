@@ -66,6 +66,21 @@ int ptk_rmsnorm_bwd(const float* x, const float* w, const float* rstd, const flo
   return launch_rmsnorm_bwd_f32(x, w, rstd, dn, dacc, dx, rows, cols, ST);
 }
 
+int ptk_qknorm_rope_fwd(const void* qkv, const float* q_norm_w, const float* k_norm_w, const float* cos_t,
+                        const float* sin_t, int batch, int seq, int heads, int kv_heads, int head_dim, float eps,
+                        void* Q, void* K, void* V, float* rstd_q, float* rstd_k, void* stream) {
+  const AttnShape sh{batch, seq, heads, kv_heads, head_dim};
+  return launch_qknorm_rope_fwd((const bf16_t*)qkv, q_norm_w, k_norm_w, cos_t, sin_t, sh, eps, (bf16_t*)Q,
+                                (bf16_t*)K, (bf16_t*)V, rstd_q, rstd_k, ST);
+}
+int ptk_qknorm_rope_bwd(const void* qkv, const float* q_norm_w, const float* k_norm_w, const float* cos_t,
+                        const float* sin_t, int batch, int seq, int heads, int kv_heads, int head_dim,
+                        const float* rstd_q, const float* rstd_k, const void* dQ, const void* dK, const void* dV,
+                        void* dqkv, void* stream) {
+  const AttnShape sh{batch, seq, heads, kv_heads, head_dim};
+  return launch_qknorm_rope_bwd((const bf16_t*)qkv, q_norm_w, k_norm_w, cos_t, sin_t, sh, rstd_q, rstd_k,
+                                (const bf16_t*)dQ, (const bf16_t*)dK, (const bf16_t*)dV, (bf16_t*)dqkv, ST);
+}
 int ptk_softmax(const float* S, void* P, int nz, int rows, int cols, int64_t ld, int rows_per_batch, int qdiv,
                 int zdiv, int causal, int window, const int32_t* key_valid, int key_len, void* stream) {
   MaskSpec m{rows_per_batch > 0 ? rows_per_batch : rows, qdiv > 0 ? qdiv : 1, zdiv > 0 ? zdiv : 1, causal, window,

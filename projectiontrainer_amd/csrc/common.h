@@ -37,10 +37,8 @@ PTK_DEV float xor16_max(float v) {
   return fmaxf(__uint_as_float(r[0]), __uint_as_float(r[1]));
 }
 
-PTK_DEV float xor32_get(float v) {   // the value of lane ^ 32
-  const auto r = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
-  return __uint_as_float((threadIdx.x & 32) ? r[0] : r[1]);
-}
+// the value of lane ^ 32 (ds_bpermute; only used by HBM-bound kernels)
+PTK_DEV float xor32_get(float v) { return __shfl_xor(v, 32, 64); }
 
 // within a 16-lane row: DPP butterflies (quad_perm [1,0,3,2], [2,3,0,1], row_half_mirror, row_mirror);
 // after each step every lane of the group holds the group's result

@@ -85,6 +85,31 @@ def rmsnorm_bwd(x, w, rstd, dn, dacc=None):
     return dx
 
 
+def qknorm_rope(qkv, q_w, k_w, cos_t, sin_t, *, batch, seq, heads, kv_heads, head_dim, eps):
+    """Gemma3 q/k RMSNorm + RoPE (ptk_qknorm_rope_fwd) -> Q [B,Hkv,S,G,D], K, V [B,Hkv,S,D], rstd_q, rstd_k."""
+    _require_cuda(qkv)
+    dev, G = qkv.device, heads // kv_heads
+    Q = torch.empty(batch, kv_heads, seq, G, head_dim, dtype=torch.bfloat16, device=dev)
+    K = torch.empty(batch, kv_heads, seq, head_dim, dtype=torch.bfloat16, device=dev)
+    V = torch.empty_like(K)
+    rq = torch.empty(batch * seq, heads, dtype=torch.float32, device=dev)
+    rk = torch.empty(batch * seq, kv_heads, dtype=torch.float32, device=dev)
+    check(L.lib().ptk_qknorm_rope_fwd(ptr(qkv), ptr(q_w), ptr(k_w), ptr(cos_t), ptr(sin_t), batch, seq, heads, kv_heads,
+                                      head_dim, eps, ptr(Q), ptr(K), ptr(V), ptr(rq), ptr(rk), L.stream_ptr(dev)),
+          "qknorm_rope_fwd")
+    return Q, K, V, rq, rk
+
+
+def qknorm_rope_bwd(qkv, q_w, k_w, cos_t, sin_t, rq, rk, dQ, dK, dV, *, batch, seq, heads, kv_heads, head_dim):
+    """Backward of qknorm_rope (ptk_qknorm_rope_bwd) -> d(qkv) bf16 [B*S, (Hq+2Hkv)*D]."""
+    _require_cuda(qkv)
+    dqkv = torch.empty_like(qkv)
+    check(L.lib().ptk_qknorm_rope_bwd(ptr(qkv), ptr(q_w), ptr(k_w), ptr(cos_t), ptr(sin_t), batch, seq, heads,
+                                      kv_heads, head_dim, ptr(rq), ptr(rk), ptr(dQ), ptr(dK), ptr(dV), ptr(dqkv),
+                                      L.stream_ptr(qkv.device)), "qknorm_rope_bwd")
+    return dqkv
+
+
 def softmax(S, *, nz, rows, cols, rows_per_batch=0, qdiv=1, zdiv=1, causal=False, window=0, key_valid=None,
             key_len=None):
     P = torch.empty(S.shape, dtype=torch.bfloat16, device=S.device)

@@ -363,3 +363,47 @@ def test_flash_bwd_vs_autograd(gpu, D, Hkv, G, window, S, split):
     for got, ref, nm in ((dQ, q.grad, "dQ"), (dK, k.grad, "dK"), (dV, v.grad, "dV")):
         err = (got.float() - ref).norm() / ref.norm()
         assert err < 2e-2, (nm, float(err))
+
+
+def _qknorm_rope_ref(qkv, qw, kw, cos_h, sin_h, B, S, Hq, Hkv, D, eps):
+    """fp32 restatement of Gemma3 q_norm / k_norm (RMSNorm, scale 1+w) + rotate-half RoPE
+    (TF/models/gemma3/modeling_gemma3.py:136-150, :356-360)."""
+    x = qkv.float().view(B, S, Hq + 2 * Hkv, D)
+    q, k, v = x[:, :, :Hq], x[:, :, Hq:Hq + Hkv], x[:, :, Hq + Hkv:]
+    rms = lambda t, w: t * torch.rsqrt(t.pow(2).mean(-1, keepdim=True) + eps) * (1 + w)
+    cos = torch.cat([cos_h, cos_h], -1)[None, :, None, :]
+    sin = torch.cat([sin_h, sin_h], -1)[None, :, None, :]
+    rot = lambda t: torch.cat([-t[..., D // 2:], t[..., :D // 2]], -1)
+    q, k = rms(q, qw), rms(k, kw)
+    return q * cos + rot(q) * sin, k * cos + rot(k) * sin, v
+
+
+@pytest.mark.parametrize("Hq,Hkv,D", [(4, 1, 256), (8, 4, 256), (2, 1, 64)])
+def test_qknorm_rope_fwd_bwd(gpu, Hq, Hkv, D):
+    """q/k RMSNorm + RoPE forward (layout scatter) and backward vs torch fp32 autograd."""
+    Kn, L = _k()
+    B, S, eps, G = 2, 96, 1e-6, Hq // Hkv
+    qkv = rnd(B * S, (Hq + 2 * Hkv) * D, dev=gpu, seed=41, scale=2.0)
+    qw = rnd(D, dev=gpu, dtype=torch.float32, seed=42, scale=0.3)
+    kw = rnd(D, dev=gpu, dtype=torch.float32, seed=43, scale=0.3)
+    inv = 1.0 / (10000.0 ** (torch.arange(0, D, 2, device=gpu, dtype=torch.float32) / D))
+    ang = torch.arange(S, device=gpu, dtype=torch.float32)[:, None] * inv[None]
+    cos_h, sin_h = ang.cos().contiguous(), ang.sin().contiguous()
+    Q, K, V, rq, rk = Kn.qknorm_rope(qkv, qw, kw, cos_h, sin_h, batch=B, seq=S, heads=Hq, kv_heads=Hkv,
+                                     head_dim=D, eps=eps)
+    x = qkv.float().requires_grad_(True)
+    qr, kr, vr = _qknorm_rope_ref(x, qw, kw, cos_h, sin_h, B, S, Hq, Hkv, D, eps)
+    # kernel layouts: Q [B,Hkv,S,G,D], K/V [B,Hkv,S,D]
+    Qr = qr.view(B, S, Hkv, G, D).permute(0, 2, 1, 3, 4)
+    Kr, Vr = kr.permute(0, 2, 1, 3), vr.permute(0, 2, 1, 3)
+    torch.testing.assert_close(Q.float(), Qr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(K.float(), Kr, rtol=2e-2, atol=2e-2)
+    torch.testing.assert_close(V.float(), Vr, rtol=0, atol=0)
+    dQ, dK, dV = rnd(*Q.shape, dev=gpu, seed=44), rnd(*K.shape, dev=gpu, seed=45), rnd(*V.shape, dev=gpu, seed=46)
+    (Qr * dQ.float()).sum().add((Kr * dK.float()).sum()).add((Vr * dV.float()).sum()).backward()
+    dqkv = Kn.qknorm_rope_bwd(qkv, qw, kw, cos_h, sin_h, rq, rk, dQ, dK, dV, batch=B, seq=S, heads=Hq,
+                              kv_heads=Hkv, head_dim=D)
+    ref = x.grad
+    cos = torch.nn.functional.cosine_similarity(dqkv.float().flatten(), ref.flatten(), dim=0)
+    assert cos > 0.999, cos
+    torch.testing.assert_close(dqkv.float(), ref, rtol=3e-2, atol=3e-2)
