@@ -347,7 +347,9 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
     const float* cs = sliding ? wt->rope_cos_local : wt->rope_cos_global;
     const float* sn = sliding ? wt->rope_sin_local : wt->rope_sin_global;
     // MLP half
-    CK(launch_post_norm_bwd(dR, sv.dn, L.ln_post_ff, sv.rstd_dn, w.dao, M, H, st));
+    // post-ff norm backward: for layers below the last it ran fused into the previous iteration's
+    // input-norm backward (one pass over dR instead of two)
+    if (l == nl - 1) CK(launch_post_norm_bwd(dR, sv.dn, L.ln_post_ff, sv.rstd_dn, w.dao, M, H, st));
     // dh = dd . Wd (plain GEMM at full MFMA rate), then the GEGLU backward as one streaming pass
     if (l + 1 < nl) {
       CK(launch_gemm(gemm(w.dao, H, L.wd_t, H, w.h, I, M, I, H), ACT_NONE, OUT_BF16, 1, st));
@@ -388,7 +390,15 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
     CK(launch_qknorm_rope_bwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, sv.rstd_q, sv.rstd_k, w.dQ, w.dK, w.dV, w.dqkv,
                               st));
     CK(launch_gemm(gemm(w.dqkv, Dqkv, L.wqkv_t, Dqkv, w.dtmp, H, M, H, Dqkv), ACT_NONE, OUT_F32, 1, st));
-    CK(launch_rmsnorm_bwd_f32(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, dR, M, H, st));
+    if (l > 0) {
+      // dR += rms_bwd(x_l, ln_in, dtmp), then layer l-1's post-ff norm backward on the new dR -> dao
+      const ptk_gemma3_layer& Lp = wt->layers[l - 1];
+      const GemmaLayerSave& sp = w.L[l - 1];
+      CK(launch_residual_norm_bwd(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, sp.dn, Lp.ln_post_ff, sp.rstd_dn, w.dao,
+                                  M, H, st));
+    } else {
+      CK(launch_rmsnorm_bwd_f32(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, dR, M, H, st));
+    }
   }
   return 0;
 }
