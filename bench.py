@@ -121,7 +121,7 @@ def main():
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    L.lib().ptk_gemm_timer_enable(1)
+    L.lib().ptk_gemm_timer_enable((1 << 8) | (1 << L.ACT_GEGLU))   # events around the gate|up launches only
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(args.steps):

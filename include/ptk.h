@@ -113,7 +113,7 @@ int ptk_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float std, float m
 /* Live GEMM timing: when enabled, HIP events are recorded on the launch stream
  * around every GEMM launch, grouped by epilogue class (PTK_ACT_*).  read()
  * synchronises those events and returns the summed kernel time and count. */
-int ptk_gemm_timer_enable(int on);
+int ptk_gemm_timer_enable(int on);   /* 0 off, 1 every class, (1 << 8) | class mask: only those classes */
 /* Tile-path test hook: 0 = shape heuristic, 1 = every GEMM on the 128x128 kernel,
    2 / 4 = every single-batch GEMM on the 256x256 / barrier-staggered 256x256 kernel,
    8 = every single-batch GEMM the persistent 4-wave 256x256 kernel supports on it. */

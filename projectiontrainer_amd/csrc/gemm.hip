@@ -642,13 +642,16 @@ __global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
 
 // ---- optional live per-class timing (HIP events around launches; bench.py roofline)
 static bool g_timing = false;
+static int g_timing_mask = 0;   // activation classes whose launches are timed
 static int g_force_tiles = 0;   // tests: 1 = every GEMM on 128x128, 2 / 4 = single-batch GEMMs on 256x256 / staggered 256x256
 void force_small_tiles(int mode) { g_force_tiles = mode; }
 static std::vector<hipEvent_t> g_ev[8];
 static size_t g_ev_used[8];
 
 void timer_enable(int on) {
+  // on: 0 = off, 1 = every class, otherwise (1 << 8) | mask of classes (only those launches get events)
   g_timing = on != 0;
+  g_timing_mask = on == 1 ? 0xff : (on & 0xff);
   if (g_timing)
     for (int c = 0; c < 8; ++c) g_ev_used[c] = 0;   // a new measurement window starts
 }
@@ -678,7 +681,7 @@ int timer_read(int cls, double* total_ms, int* count) {
 #define PTK_GEMM_CASE(ACT_, OUT_)                                                              \
   if (act == ACT_ && out == OUT_) {                                                            \
     hipEvent_t e0 = nullptr, e1 = nullptr;                                                     \
-    if (g_timing) { e0 = next_event(act); e1 = next_event(act); }                              \
+    if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }                              \
     if (e0) (void)hipEventRecord(e0, st);                                                          \
     hipLaunchKernelGGL((gemm_nt_kernel<ACT_, OUT_>), grid, dim3(256), 0, st, a);              \
     if (e1) (void)hipEventRecord(e1, st);                                                          \
@@ -700,7 +703,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   const bool big_shape = a.M >= 1024 && a.N >= 512 && (a.K >= 6144 || (a.N >= 6144 && a.K >= 1152));
   if (batch == 1 && g_force_tiles == 8 && w4_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (g_timing) { e0 = next_event(act); e1 = next_event(act); }
+    if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);
     const int rc = launch_gemm_w4(a, act, out, st, 0);
     if (e1) (void)hipEventRecord(e1, st);
@@ -712,7 +715,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
 #define PTK_BIG2_CASE(ACT_, OUT_)                                                               \
     if (act == ACT_ && out == OUT_) {                                                           \
       hipEvent_t e0 = nullptr, e1 = nullptr;                                                    \
-      if (g_timing) { e0 = next_event(act); e1 = next_event(act); }                             \
+      if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }                             \
       if (e0) (void)hipEventRecord(e0, st);                                                     \
       hipLaunchKernelGGL((gemm_big2_kernel<ACT_, OUT_>), g4, dim3(512), 0, st, a);              \
       if (e1) (void)hipEventRecord(e1, st);                                                     \
@@ -736,7 +739,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
 #define PTK_BIG_CASE(ACT_, OUT_)                                                                \
     if (act == ACT_ && out == OUT_) {                                                           \
       hipEvent_t e0 = nullptr, e1 = nullptr;                                                    \
-      if (g_timing) { e0 = next_event(act); e1 = next_event(act); }                             \
+      if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }                             \
       if (e0) (void)hipEventRecord(e0, st);                                                     \
       hipLaunchKernelGGL((gemm_big_kernel<ACT_, OUT_>), g2, dim3(512), 0, st, a);               \
       if (e1) (void)hipEventRecord(e1, st);                                                     \
