@@ -35,18 +35,17 @@ PTK_DEV float4 scl4(float4 a, float s) { return make_float4(a.x * s, a.y * s, a.
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6); \
   if (row >= rows) return;
 
-#define FOR_V for (int v = 0; v < MAXV; ++v) if (lane * 4 + v * 256 < cols)
+#define FOR_V for (int v = 0; v < NV; ++v) if (lane * 4 + v * 256 < cols)
 #define COL (lane * 4 + v * 256)
 
 PTK_DEV float4 ldx4(const float* p) { return ld4(p); }
 PTK_DEV float4 ldx4(const bf16_t* p) { return ld4bf(p); }
 
-template <typename T>
-__global__ void __launch_bounds__(256) layernorm_kernel(const T* __restrict__ x, const float* __restrict__ w,
-                                                        const float* __restrict__ b, bf16_t* __restrict__ y,
-                                                        long rows, int cols, float eps) {
+template <typename T, int NV>
+PTK_DEV void layernorm_body(const T* __restrict__ x, const float* __restrict__ w, const float* __restrict__ b,
+                            bf16_t* __restrict__ y, long rows, int cols, float eps) {
   ROW_SETUP
-  float4 r[MAXV];
+  float4 r[NV];
   float s = 0.f;
 #pragma unroll
   FOR_V { r[v] = ldx4(x + row * cols + COL); s += r[v].x + r[v].y + r[v].z + r[v].w; }
@@ -63,13 +62,27 @@ __global__ void __launch_bounds__(256) layernorm_kernel(const T* __restrict__ x,
   FOR_V { st4bf(y + row * cols + COL, add4(mul4(scl4(r[v], rstd), ld4(w + COL)), ld4(b + COL))); }
 }
 
+template <int NV>
+__global__ void __launch_bounds__(256) layernorm_f32(const float* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ b, bf16_t* __restrict__ y, long rows,
+                                                     int cols, float eps) {
+  layernorm_body<float, NV>(x, w, b, y, rows, cols, eps);
+}
+template <int NV>
+__global__ void __launch_bounds__(256) layernorm_b16(const bf16_t* __restrict__ x, const float* __restrict__ w,
+                                                     const float* __restrict__ b, bf16_t* __restrict__ y, long rows,
+                                                     int cols, float eps) {
+  layernorm_body<bf16_t, NV>(x, w, b, y, rows, cols, eps);
+}
+
+template <int NV>
 __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const float* __restrict__ x, long ldx, RowMap xmap,
                                                           const float* __restrict__ w, bf16_t* __restrict__ y,
                                                           float* __restrict__ rstd_out, long rows, int cols,
                                                           float eps) {
   ROW_SETUP
   const float* xr = x + map_row(xmap, row) * ldx;
-  float4 r[MAXV];
+  float4 r[NV];
   float q = 0.f;
 #pragma unroll
   FOR_V { r[v] = ld4(xr + COL); q += dot4(r[v], r[v]); }
@@ -79,12 +92,13 @@ __global__ void __launch_bounds__(256) rmsnorm_fwd_kernel(const float* __restric
   FOR_V { st4bf(y + row * cols + COL, mul4(scl4(r[v], rs), onep(ld4(w + COL)))); }
 }
 
+template <int NV>
 __global__ void __launch_bounds__(256) residual_norm_fwd_kernel(
     const bf16_t* __restrict__ t, const float* __restrict__ xi, const float* __restrict__ w_post,
     const float* __restrict__ w_next, float* __restrict__ xo, bf16_t* __restrict__ n,
     float* __restrict__ rstd_t, float* __restrict__ rstd_x, long rows, int cols, float eps) {
   ROW_SETUP
-  float4 r[MAXV];
+  float4 r[NV];
   float q = 0.f;
 #pragma unroll
   FOR_V { r[v] = ld4bf(t + row * cols + COL); q += dot4(r[v], r[v]); }
@@ -119,11 +133,12 @@ __global__ void __launch_bounds__(256) residual_norm_fwd_kernel(
     }                                                                         \
   }
 
+template <int NV>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                               const float* __restrict__ rstd, const float* __restrict__ dn,
                                                               const float* dacc, float* dx, long rows, int cols) {
   ROW_SETUP
-  float4 xv[MAXV], dv[MAXV];
+  float4 xv[NV], dv[NV];
 #pragma unroll
   FOR_V { xv[v] = ld4(x + row * cols + COL); dv[v] = ld4(dn + row * cols + COL); }
   const float rs = rstd[row];
@@ -133,6 +148,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_f32_kernel(const float* __res
   })
 }
 
+template <int NV>
 __global__ void __launch_bounds__(256) rmsnorm_bwd_scatter_kernel(const float* __restrict__ x, RowMap xmap,
                                                                   const float* __restrict__ w,
                                                                   const float* __restrict__ rstd,
@@ -140,7 +156,7 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_scatter_kernel(const float* _
                                                                   long rows, int cols) {
   ROW_SETUP
   const long xr = map_row(xmap, row);
-  float4 xv[MAXV], dv[MAXV];
+  float4 xv[NV], dv[NV];
 #pragma unroll
   FOR_V { xv[v] = ld4(x + xr * cols + COL); dv[v] = ld4(dn + row * cols + COL); }
   const float rs = rstd[row];
@@ -149,37 +165,64 @@ __global__ void __launch_bounds__(256) rmsnorm_bwd_scatter_kernel(const float* _
 
 // grad through a post-norm whose output (bf16) was added to the residual:
 // dy = bf16(dR); dt = bf16(rms_bwd(t, w, rstd_t, dy))
+template <int NV>
 PTK_DEV void post_norm_bwd_row(const float* dR, const bf16_t* t, const float* w, float rs, bf16_t* dt, int lane,
                                int cols) {
-  float4 xv[MAXV], dv[MAXV];
+  float4 xv[NV], dv[NV];
 #pragma unroll
   FOR_V { xv[v] = ld4bf(t + COL); dv[v] = bfr4(ld4(dR + COL)); }
   RMS_BWD_BODY(xv, dv, rs, { st4bf(dt + COL, dxv); })
 }
 
+template <int NV>
 __global__ void __launch_bounds__(256) residual_norm_bwd_kernel(
     const float* __restrict__ x2, const float* __restrict__ w_pre, const float* __restrict__ rstd_pre,
     const float* __restrict__ dn, float* __restrict__ dR, const bf16_t* __restrict__ t,
     const float* __restrict__ w_post, const float* __restrict__ rstd_t, bf16_t* __restrict__ dt, long rows,
     int cols) {
   ROW_SETUP
+  float4 nd[NV];   // the updated dR row stays in registers for the post-norm pass
   {
     const float* w = w_pre;
-    float4 xv[MAXV], dv[MAXV];
+    float4 xv[NV], dv[NV];
 #pragma unroll
     FOR_V { xv[v] = ld4(x2 + row * cols + COL); dv[v] = ld4(dn + row * cols + COL); }
     const float rs = rstd_pre[row];
-    RMS_BWD_BODY(xv, dv, rs, { st4(dR + row * cols + COL, add4(ld4(dR + row * cols + COL), dxv)); })
+    RMS_BWD_BODY(xv, dv, rs, {
+      nd[v] = add4(ld4(dR + row * cols + COL), dxv);
+      st4(dR + row * cols + COL, nd[v]);
+    })
   }
-  post_norm_bwd_row(dR + row * cols, t + row * cols, w_post, rstd_t[row], dt + row * cols, lane, cols);
+  {
+    const float* w = w_post;
+    const float rs = rstd_t[row];
+    float4 xv[NV], dv[NV];
+#pragma unroll
+    FOR_V { xv[v] = ld4bf(t + row * cols + COL); dv[v] = bfr4(nd[v]); }
+    RMS_BWD_BODY(xv, dv, rs, { st4bf(dt + row * cols + COL, dxv); })
+  }
 }
 
+template <int NV>
 __global__ void __launch_bounds__(256) post_norm_bwd_kernel(const float* __restrict__ dR, const bf16_t* __restrict__ t,
                                                             const float* __restrict__ w, const float* __restrict__ rstd_t,
                                                             bf16_t* __restrict__ dt, long rows, int cols) {
   ROW_SETUP
-  post_norm_bwd_row(dR + row * cols, t + row * cols, w, rstd_t[row], dt + row * cols, lane, cols);
+  post_norm_bwd_row<NV>(dR + row * cols, t + row * cols, w, rstd_t[row], dt + row * cols, lane, cols);
 }
+
+// float4 registers per lane for a row of `cols` (one wave per row): kernels are instantiated per count
+// so the row arrays take only the registers they need (occupancy of these HBM-bound kernels)
+#define NORM_DISPATCH(KERNEL, ...)                                                                  \
+  do {                                                                                              \
+    const int nv_ = (cols + 255) / 256;                                                             \
+    if (nv_ <= 1) hipLaunchKernelGGL(KERNEL<1>, NORM_GRID, __VA_ARGS__);                            \
+    else if (nv_ <= 2) hipLaunchKernelGGL(KERNEL<2>, NORM_GRID, __VA_ARGS__);                       \
+    else if (nv_ <= 4) hipLaunchKernelGGL(KERNEL<4>, NORM_GRID, __VA_ARGS__);                       \
+    else if (nv_ <= 5) hipLaunchKernelGGL(KERNEL<5>, NORM_GRID, __VA_ARGS__);                       \
+    else if (nv_ <= 8) hipLaunchKernelGGL(KERNEL<8>, NORM_GRID, __VA_ARGS__);                       \
+    else hipLaunchKernelGGL(KERNEL<MAXV>, NORM_GRID, __VA_ARGS__);                                  \
+  } while (0)
 
 static int check_cols(int cols) {
   if (cols <= 0 || cols % 4 || cols > 256 * MAXV) return set_error("norm: cols=%d unsupported", cols);
@@ -192,21 +235,21 @@ int launch_layernorm(const float* x, const float* w, const float* b, bf16_t* y, 
                      hipStream_t st) {
   if (check_cols(cols)) return -1;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(layernorm_kernel<float>, NORM_GRID, x, w, b, y, (long)rows, cols, eps);
+  NORM_DISPATCH(layernorm_f32, x, w, b, y, (long)rows, cols, eps);
   RET_LAUNCH("layernorm");
 }
 int launch_layernorm_bf16(const bf16_t* x, const float* w, const float* b, bf16_t* y, int rows, int cols, float eps,
                           hipStream_t st) {
   if (check_cols(cols)) return -1;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(layernorm_kernel<bf16_t>, NORM_GRID, x, w, b, y, (long)rows, cols, eps);
+  NORM_DISPATCH(layernorm_b16, x, w, b, y, (long)rows, cols, eps);
   RET_LAUNCH("layernorm_bf16");
 }
 int launch_rmsnorm_fwd(const float* x, long ldx, RowMap xmap, const float* w, bf16_t* y, float* rstd, int rows,
                        int cols, float eps, hipStream_t st) {
   if (check_cols(cols)) return -1;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(rmsnorm_fwd_kernel, NORM_GRID, x, ldx, xmap, w, y, rstd, (long)rows, cols, eps);
+  NORM_DISPATCH(rmsnorm_fwd_kernel, x, ldx, xmap, w, y, rstd, (long)rows, cols, eps);
   RET_LAUNCH("rmsnorm_fwd");
 }
 int launch_residual_norm_fwd(const bf16_t* t, const float* xi, const float* w_post, const float* w_next, float* xo,
@@ -214,7 +257,7 @@ int launch_residual_norm_fwd(const bf16_t* t, const float* xi, const float* w_po
                              hipStream_t st) {
   if (check_cols(cols)) return -1;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(residual_norm_fwd_kernel, NORM_GRID, t, xi, w_post, w_next, xo, n, rstd_t, rstd_x,
+  NORM_DISPATCH(residual_norm_fwd_kernel, t, xi, w_post, w_next, xo, n, rstd_t, rstd_x,
                      (long)rows, cols, eps);
   RET_LAUNCH("residual_norm_fwd");
 }
@@ -222,14 +265,14 @@ int launch_rmsnorm_bwd_f32(const float* x, const float* w, const float* rstd, co
                            float* dx, int rows, int cols, hipStream_t st) {
   if (check_cols(cols)) return -1;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(rmsnorm_bwd_f32_kernel, NORM_GRID, x, w, rstd, dn, dacc, dx, (long)rows, cols);
+  NORM_DISPATCH(rmsnorm_bwd_f32_kernel, x, w, rstd, dn, dacc, dx, (long)rows, cols);
   RET_LAUNCH("rmsnorm_bwd");
 }
 int launch_rmsnorm_bwd_scatter(const float* x, RowMap xmap, const float* w, const float* rstd, const float* dn,
                                float* dR, int rows, int cols, hipStream_t st) {
   if (check_cols(cols)) return -1;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(rmsnorm_bwd_scatter_kernel, NORM_GRID, x, xmap, w, rstd, dn, dR, (long)rows, cols);
+  NORM_DISPATCH(rmsnorm_bwd_scatter_kernel, x, xmap, w, rstd, dn, dR, (long)rows, cols);
   RET_LAUNCH("rmsnorm_bwd_scatter");
 }
 int launch_residual_norm_bwd(const float* x2, const float* w_pre, const float* rstd_pre, const float* dn, float* dR,
@@ -237,7 +280,7 @@ int launch_residual_norm_bwd(const float* x2, const float* w_pre, const float* r
                              int cols, hipStream_t st) {
   if (check_cols(cols)) return -1;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(residual_norm_bwd_kernel, NORM_GRID, x2, w_pre, rstd_pre, dn, dR, t, w_post, rstd_t, dt,
+  NORM_DISPATCH(residual_norm_bwd_kernel, x2, w_pre, rstd_pre, dn, dR, t, w_post, rstd_t, dt,
                      (long)rows, cols);
   RET_LAUNCH("residual_norm_bwd");
 }
@@ -245,7 +288,7 @@ int launch_post_norm_bwd(const float* dR, const bf16_t* t, const float* w, const
                          int rows, int cols, hipStream_t st) {
   if (check_cols(cols)) return -1;
   if (rows <= 0) return 0;
-  hipLaunchKernelGGL(post_norm_bwd_kernel, NORM_GRID, dR, t, w, rstd_t, dt, (long)rows, cols);
+  NORM_DISPATCH(post_norm_bwd_kernel, dR, t, w, rstd_t, dt, (long)rows, cols);
   RET_LAUNCH("post_norm_bwd");
 }
 
