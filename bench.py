@@ -149,13 +149,16 @@ def main():
         traffic = json.load(open(pmc))["traffic_bytes_per_launch"]   # rocprofv3 --pmc passes (tools/pmc_traffic.py)
     # algorithmic FLOPs of every timed gate|up launch / their summed HIP-event time
     achieved = geglu_step_flops(cfg) * args.steps / (tot.value / 1e3) / 1e12
+    lm_name = {2560: "Gemma3-4B", 1152: "Gemma3-1B"}.get(cfg.text.hidden_size, f"Gemma3(h{cfg.text.hidden_size})")
+    metric = ("Stage-1 images/sec/node (SigLIP-L-384 + Gemma3-1B, 576+128 tok)" if args.config == "cfg2" else
+              f"Stage-1 images/sec/node ({args.config}: SigLIP + {lm_name}, {cfg.vision.num_patches}+{cfg.text_len} tok)")
     line = {
-        "metric": "Stage-1 images/sec/node (SigLIP-L-384 + Gemma3-1B, 576+128 tok)",
+        "metric": metric,
         "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
         "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
         "config": {"workload": f"{args.config}: SigLIP-ViT-L/16-384 frozen fwd + MLP projector fwd/bwd + "
-                               f"Gemma3-1B frozen fwd/bwd, {cfg.num_vision_tokens} vis + {cfg.text_len} text tokens",
+                               f"{lm_name} frozen fwd/bwd, {cfg.num_vision_tokens} vis + {cfg.text_len} text tokens",
                    "global_batch": world * cfg.batch_size, "per_gpu_batch": cfg.batch_size,
                    "seq_len": cfg.seq_len, "parallelism": f"dp{world}"},
         "roofline": {"bound": "mfma", "kernel": "gemm_big_kernel<ACT_GEGLU> (Gemma3 gate|up projection: 2*(B*S)*(2I)*H FLOP per launch, "

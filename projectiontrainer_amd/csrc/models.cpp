@@ -160,7 +160,7 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp)
   w.logits = bp.take<bf16_t>(R * V);
   w.row_loss = bp.take<float>(R);
   w.dxf = bp.take<float>(R * H);
-  w.dxf_part = bp.take<float>((long)LM_SPLITK * R * H);
+  w.dxf_part = bp.take<float>((long)(LM_SPLITK + 1) * R * H);   // + one slot for a vocab remainder
   w.count = bp.take<float>(4);
   w.gscale = bp.take<float>(4);
   return w;
@@ -252,7 +252,7 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
   if (c->heads % c->kv_heads) return set_error("gemma3: heads %% kv_heads");
   if (Nv < 1) return set_error("gemma3: num_vision must be >= 1");
   if (ws_bytes < ptk_gemma3_workspace_bytes(c, B, T, Sp)) return set_error("gemma3: workspace too small");
-  if (c->vocab % (64 * LM_SPLITK)) return set_error("gemma3: vocab must be a multiple of %d", 64 * LM_SPLITK);
+  if (c->vocab % 64 || c->vocab < 64 * LM_SPLITK) return set_error("gemma3: vocab must be a multiple of 64 and >= %d", 64 * LM_SPLITK);
   const int H = c->hidden, I = c->inter, D = c->head_dim, Hq = c->heads, Hkv = c->kv_heads, G = Hq / Hkv;
   const int M = B * Sp, Dq = Hq * D, Dqkv = (Hq + 2 * Hkv) * D, R = B * T, V = c->vocab;
   const int Z = B * Hkv, SG = Sp * G, nl = c->layers;
@@ -328,12 +328,19 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
   CK(launch_count_valid(bt->labels, R, bt->loss_scale, w.gscale, w.count, st));
   CK(launch_ce_fwd_bwd(w.logits, V, R, V, bt->labels, w.row_loss, w.gscale, st));
   CK(launch_loss_reduce(w.row_loss, R, w.count, bt->loss, st));
-  {  // d(xf) = dlogits . E, K = vocab: split-K over LM_SPLITK slices (fp32 partials, ordered sum)
-    const int kc = V / LM_SPLITK;
+  {  // d(xf) = dlogits . E, K = vocab: split-K over LM_SPLITK equal slices (fp32 partials, ordered sum);
+     // a vocab that is not a multiple of 64 * LM_SPLITK (Gemma3-4B: 262 208 = 4 097 x 64) leaves a
+     // remainder slice, computed into one more partial
+    const int kc = V / (64 * LM_SPLITK) * 64, rem = V - LM_SPLITK * kc;
     GemmArgs g = gemm(w.logits, V, wt->embed_t, V, w.dxf_part, H, R, H, kc);
     g.sA0 = kc; g.sB0 = kc; g.sC0 = (long)R * H;
     CK(launch_gemm(g, ACT_NONE, OUT_F32, LM_SPLITK, st));
-    CK(launch_sum_partials(w.dxf_part, LM_SPLITK, (long)R * H, w.dxf, st));
+    if (rem) {
+      const long o = (long)LM_SPLITK * kc;
+      CK(launch_gemm(gemm(w.logits + o, V, (const bf16_t*)wt->embed_t + o, V, w.dxf_part + (long)LM_SPLITK * R * H, H, R, H, rem),
+                     ACT_NONE, OUT_F32, 1, st));
+    }
+    CK(launch_sum_partials(w.dxf_part, LM_SPLITK + (rem ? 1 : 0), (long)R * H, w.dxf, st));
   }
   float* dR = bt->dx;
   CK(hipMemsetAsync(dR, 0, (size_t)M * H * 4, st) != hipSuccess);
@@ -350,7 +357,8 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
     // post-ff norm backward: for layers below the last it ran fused into the previous iteration's
     // input-norm backward (one pass over dR instead of two)
     if (l == nl - 1) CK(launch_post_norm_bwd(dR, sv.dn, L.ln_post_ff, sv.rstd_dn, w.dao, M, H, st));
-    // dh = dd . Wd (plain GEMM at full MFMA rate), then the GEGLU backward as one streaming pass
+    // dh = dd . Wd (plain GEMM at full MFMA rate), then the GEGLU backward as one streaming pass (measured:
+    // the same step time as the GEGLU backward fused into this GEMM's epilogue, which reads g, u per tile)
     if (l + 1 < nl) {
       CK(launch_gemm(gemm(w.dao, H, L.wd_t, H, w.h, I, M, I, H), ACT_NONE, OUT_BF16, 1, st));
       CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, M, I, st));
