@@ -272,6 +272,41 @@ int ptk_clip_adamw(float* params, const float* grads, float* exp_avg, float* exp
                    float grad_scale, float max_norm, float lr, float beta1, float beta2, float eps,
                    float weight_decay, int step, float* partial, float* norm_out, void* stream);
 
+/* ------------------------------------------------------------------------ *
+ * Host data step: image resize + normalise.              *
+ * Replaces, per image, `Image.open(p).convert('RGB').resize((S, S))` and    *
+ * `processor(images=image).pixel_values` of XrayTextPairDataset.__getitem__ *
+ * (Stage1/train_projection_stage1.py:97-99) plus the trainer's cast to the  *
+ * tower dtype (Stage1/projector_trainer.py:158-171): JPEG decode stays on   *
+ * the host, the bicubic resample (Pillow Resample.c semantics, bit-exact)   *
+ * and the rescale/normalise run on the GPU.                                 *
+ * ------------------------------------------------------------------------ */
+
+/* Host-only (no GPU): taps per output of a Pillow-compatible antialiased bicubic resample
+ * in_size -> out_size (Resample.c precompute_coeffs: ceil(2 * max(in/out, 1)) * 2 + 1). */
+int ptk_resize_ksize(int in_size, int out_size);
+/* Host-only: fixed-point weights (Resample.c precompute_coeffs + normalize_coeffs_8bpc):
+ * bounds [out][2] = (first source index, tap count), coeffs [out][ksize] int32 at 22 fraction bits.
+ * Returns ksize, or < 0 on error. */
+int ptk_resize_coeffs(int in_size, int out_size, int32_t* bounds, int32_t* coeffs);
+
+typedef struct ptk_image_desc {
+  int64_t src_off;    /* byte offset of the image in src: h rows of w * c bytes, packed */
+  int32_t h, w, c;    /* source size; c = 1 (greyscale: .convert('RGB') replicates it) or 3 */
+  int32_t kh, kv;     /* taps of the horizontal / vertical pass (ptk_resize_ksize) */
+  int32_t pad_;
+  int64_t coef_off;   /* int32 offset in coefs: bounds_h [S][2], k_h [S][kh], bounds_v [S][2], k_v [S][kv] */
+  int64_t tmp_off;    /* byte offset of the image's [h][S][c] uint8 intermediate in tmp */
+} ptk_image_desc;
+
+/* Every image i of n: out[i][ch] = lut[ch][resize_v(resize_h(src_i))] as [3][S][S] planar, bf16
+ * (out_f32 = 0) or f32 (out_f32 = 1); lut: [3][256] of the output type in device memory.  desc, coefs, src, tmp
+ * are device pointers; max_h / max_row_bytes bound every image's h / w * c (grid and LDS sizing,
+ * max_row_bytes <= 65536). */
+int ptk_image_preprocess(const uint8_t* src, const int32_t* coefs, const ptk_image_desc* desc, int n, int max_h,
+                         int max_row_bytes, int out_size, const void* lut, int out_f32, uint8_t* tmp, void* out,
+                         void* stream);
+
 #ifdef __cplusplus
 }
 #endif

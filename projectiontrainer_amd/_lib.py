@@ -105,6 +105,12 @@ class Gemma3BatchC(C.Structure):
                 ("loss_scale", c_float), ("loss", c_void_p)]
 
 
+class ImageDesc(C.Structure):
+    _fields_ = [("src_off", c_int64), ("h", C.c_int32), ("w", C.c_int32), ("c", C.c_int32),
+                ("kh", C.c_int32), ("kv", C.c_int32), ("pad_", C.c_int32),
+                ("coef_off", c_int64), ("tmp_off", c_int64)]
+
+
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
     "ptk_abi_version": (c_int, []),
@@ -139,6 +145,10 @@ SIGNATURES = {
     "ptk_gemma3_workspace_bytes": (c_size_t, [C.POINTER(Gemma3ConfigC), c_int, c_int, c_int]),
     "ptk_gemma3_loss_fwd_bwd": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC),
                                         C.POINTER(Gemma3BatchC), c_void_p, c_size_t, c_void_p]),
+    "ptk_resize_ksize": (c_int, [c_int, c_int]),
+    "ptk_resize_coeffs": (c_int, [c_int, c_int, c_void_p, c_void_p]),
+    "ptk_image_preprocess": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
+                                     c_void_p, c_void_p, c_void_p]),
     "ptk_clip_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                                c_float, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_void_p]),
 }

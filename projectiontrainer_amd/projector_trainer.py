@@ -46,7 +46,7 @@ class ProjectionTrainerStage1:
                  train_dataset, val_dataset=None, output_dir="./trained_projection_stage1", batch_size=8,
                  learning_rate=1e-4, weight_decay=0.01, num_epochs=10, gradient_accumulation_steps=1,
                  warmup_ratio=0.0, wandb_project="xray_projection_training", save_every_n_epochs=0,
-                 log_fn=None, seed=0):
+                 log_fn=None, seed=0, num_workers=8):
         if accelerator is None:
             accelerator = D.DistState(gradient_accumulation_steps)
         elif not isinstance(accelerator, D.DistState):
@@ -59,6 +59,8 @@ class ProjectionTrainerStage1:
         self.processor, self.tokenizer = processor, tokenizer
         self.log_fn = log_fn
         self.seed = seed
+        self.num_workers = num_workers   # decode threads for image datasets (the reference: 2 DataLoader workers, :60)
+        self._pre = None
         if acc.is_main_process:
             os.makedirs(output_dir, exist_ok=True)
 
@@ -90,10 +92,23 @@ class ProjectionTrainerStage1:
     # ------------------------------------------------------------------ data
     def _batches(self, dataset, epoch, shuffle=True):
         acc = self.accelerator
-        for idx in D.shard_batches(len(dataset), self.batch_size, acc.process_index, acc.num_processes, epoch,
-                                   self.seed, shuffle):
-            b = _collate([dataset[int(i)] for i in idx])
+        index_batches = [[int(i) for i in idx] for idx in
+                         D.shard_batches(len(dataset), self.batch_size, acc.process_index, acc.num_processes, epoch,
+                                         self.seed, shuffle)]
+        if getattr(dataset, "yields_images", False):
+            # decoded-image dataset (data.XrayTextPairDataset): workers decode, the GPU resizes/normalises
+            yield from self._image_batches(dataset, index_batches)
+            return
+        for idx in index_batches:
+            b = _collate([dataset[i] for i in idx])
             yield {k: v.to(self.device, non_blocking=True) for k, v in b.items()}
+
+    def _image_batches(self, dataset, index_batches):
+        from .data import ImagePreprocessor, ThreadedImageLoader
+        if self._pre is None:
+            self._pre = ImagePreprocessor(self.vision_encoder.cfg.image_size, self.device, processor=self.processor,
+                                          dtype=torch.bfloat16)
+        yield from ThreadedImageLoader(dataset, index_batches, self._pre, threads=self.num_workers)
 
     def _log(self, d, step):
         if self.accelerator.is_main_process:

@@ -53,6 +53,7 @@ STRUCTS = {
     "ptk_gemma3_layer": ("Gemma3LayerC", None),
     "ptk_gemma3_weights": ("Gemma3WeightsC", None),
     "ptk_gemma3_batch": ("Gemma3BatchC", None),
+    "ptk_image_desc": ("ImageDesc", None),
 }
 
 

@@ -76,3 +76,60 @@ def test_trainer_with_hf_models_matches_reference(gpu):
             ref, g = d[f"s{last}_param.{k}@rows16"], got[::16]
         assert np.max(np.abs(g - ref)) <= 2.5 * lr_sum + 1e-6, k
         assert np.median(np.abs(g - ref)) <= 0.05 * meta["lr"], k
+
+
+def test_trainer_on_decoding_dataset_matches_pixel_dataset(gpu, tmp_path):
+    """The reference's data contract end to end: JPEG files + JSON through data.XrayTextPairDataset
+    (2 decode workers, GPU resize/normalise) train exactly like a dataset that yields the pixel_values
+    the reference's __getitem__ makes (Pillow resize + SiglipImageProcessor, fp32)."""
+    from PIL import Image
+    import transformers
+    from projectiontrainer_amd.data import XrayTextPairDataset
+    from projectiontrainer_amd.dist import DistState
+    from projectiontrainer_amd.projector_trainer import ProjectionTrainerStage1
+    from projectiontrainer_amd.projectors import MLPProjector
+    name = "tiny"
+    d, meta = G.load(name)
+    cfg, sig, llm, pp = hf_models(name)
+    S, T = cfg.vision.image_size, cfg.text_len
+    rng = np.random.default_rng(0)
+    samples = []
+    for i in range(2 * cfg.batch_size):
+        h, w = int(rng.integers(S // 2, 4 * S)), int(rng.integers(S // 2, 4 * S))
+        im = rng.integers(0, 256, (h, w) if i % 2 else (h, w, 3), dtype=np.uint8)
+        Image.fromarray(im, "L" if i % 2 else "RGB").save(tmp_path / f"{i}.jpg", quality=90)
+        samples.append({"image": f"{i}.jpg", "normal_caption": f"finding {i} " * (1 + i % 5)})
+    (tmp_path / "s.json").write_text(json.dumps(samples))
+
+    class Tok:
+        pad_token_id, eos_token_id = 0, 1
+
+        def __call__(self, text, max_length, padding, truncation, return_tensors):
+            ids = [2] + [3 + (ord(ch) % 200) for ch in text][: max_length - 1]
+            return types.SimpleNamespace(input_ids=torch.tensor([[0] * (max_length - len(ids)) + ids]))
+
+    proc = transformers.SiglipImageProcessor(size={"height": S, "width": S})
+    ds = XrayTextPairDataset(str(tmp_path), str(tmp_path / "s.json"), proc, Tok(), S, max_length=T)
+    ref_items = []
+    for i, s in enumerate(samples):
+        image = Image.open(tmp_path / s["image"]).convert("RGB").resize((S, S))
+        px = torch.from_numpy(proc(images=image, return_tensors="np")["pixel_values"][0])
+        ids, labels = ds.tokenize(s["normal_caption"])
+        ref_items.append({"pixel_values": px, "token_ids": ids, "labels": labels})
+
+    def run(data, out):
+        proj = MLPProjector(cfg.vision.hidden_size, cfg.text.hidden_size)
+        proj.load_state_dict({k: torch.from_numpy(v) for k, v in pp.items()})
+        logs = []
+        tr = ProjectionTrainerStage1(DistState(1), sig, llm, proj, proc, Tok(), data, None, output_dir=str(out),
+                                     batch_size=cfg.batch_size, learning_rate=1e-3, num_epochs=1,
+                                     log_fn=lambda dd, s: logs.append(dd))
+        tr.train()
+        return [x["train/batch_loss"] for x in logs if "train/batch_loss" in x], tr.projection_layer
+
+    l_img, p_img = run(ds, tmp_path / "o1")
+    l_ref, p_ref = run(ref_items, tmp_path / "o2")
+    assert len(l_img) == len(l_ref) == 2
+    assert l_img == l_ref, (l_img, l_ref)
+    for a, b in zip(p_img.state_dict().values(), p_ref.state_dict().values()):
+        assert torch.equal(a, b)
