@@ -9,8 +9,11 @@
 
 namespace ptk {
 
-// One wave per (token m, head h) of the fused qkv row.  EPL = head_dim / 64
-// contiguous elements per lane; RoPE partner i +- D/2 sits in lane ^ 32.
+// One wave per token m: every head of its fused qkv row (q heads, k heads, v heads), four heads'
+// loads in flight at a time, the token's cos/sin and the q/k norm weights loaded once.  EPL =
+// head_dim / 64 contiguous elements per lane; the RoPE partner i +- D/2 sits in lane ^ 32.
+constexpr int QKR_HB = 4;   // heads per load batch
+
 template <int EPL>
 __global__ void __launch_bounds__(256) qknorm_rope_fwd_kernel(const bf16_t* __restrict__ qkv,
                                                               const float* __restrict__ qw,
@@ -23,51 +26,64 @@ __global__ void __launch_bounds__(256) qknorm_rope_fwd_kernel(const bf16_t* __re
   constexpr int D = EPL * 64;
   const int lane = threadIdx.x & 63;
   const int nh = sh.Hq + 2 * sh.Hkv;
-  const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const long M = (long)sh.B * sh.S;
-  if (gw >= M * nh) return;
-  const long m = gw / nh;
-  const int h = (int)(gw - m * nh);
+  const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= (long)sh.B * sh.S) return;
   const int b = (int)(m / sh.S), s = (int)(m - (long)b * sh.S);
   const int G = sh.Hq / sh.Hkv;
-  const bf16_t* src = qkv + m * (long)nh * D + (long)h * D + lane * EPL;
-  float x[EPL];
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) x[e] = bf2f(src[e]);
-  if (h >= sh.Hq + sh.Hkv) {   // v head: relayout only
-    const int kvh = h - sh.Hq - sh.Hkv;
-    bf16_t* dst = V + (((long)b * sh.Hkv + kvh) * sh.S + s) * D + lane * EPL;
-#pragma unroll
-    for (int e = 0; e < EPL; ++e) dst[e] = src[e];
-    return;
-  }
-  const bool isq = h < sh.Hq;
-  const float* w = isq ? qw : kw;
-  float ss = 0.f;
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) ss += x[e] * x[e];
-  const float rs = rsqrtf(warp_sum(ss) / D + eps);
-  float xn[EPL], part[EPL];
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) xn[e] = bfround(x[e] * rs * (1.f + w[lane * EPL + e]));
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) part[e] = xor32_get(xn[e]);
   const int fi = (lane & 31) * EPL;   // frequency index (cos[i] == cos[i + D/2])
-  const float sgn = lane < 32 ? -1.f : 1.f;
-  bf16_t* dst;
-  if (isq) {
-    const int kvh = h / G, j = h - kvh * G;
-    dst = Q + ((((long)b * sh.Hkv + kvh) * sh.S + s) * G + j) * D + lane * EPL;
-    if (lane == 0) rstd_q[m * sh.Hq + h] = rs;
-  } else {
-    const int kvh = h - sh.Hq;
-    dst = K + (((long)b * sh.Hkv + kvh) * sh.S + s) * D + lane * EPL;
-    if (lane == 0) rstd_k[m * sh.Hkv + kvh] = rs;
-  }
+  float cs[EPL], sn[EPL], wq[EPL], wk[EPL];
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
-    const float c = cos_t[(long)s * (D / 2) + fi + e], sn = sin_t[(long)s * (D / 2) + fi + e];
-    dst[e] = f2bf(xn[e] * c + sgn * part[e] * sn);
+    cs[e] = cos_t[(long)s * (D / 2) + fi + e];
+    sn[e] = sin_t[(long)s * (D / 2) + fi + e];
+    wq[e] = 1.f + qw[lane * EPL + e];
+    wk[e] = 1.f + kw[lane * EPL + e];
+  }
+  const float sgn = lane < 32 ? -1.f : 1.f;
+  const bf16_t* row = qkv + m * (long)nh * D + lane * EPL;
+  for (int h0 = 0; h0 < nh; h0 += QKR_HB) {
+    bf16_t raw[QKR_HB][EPL];
+#pragma unroll
+    for (int i = 0; i < QKR_HB; ++i)
+      if (h0 + i < nh)
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) raw[i][e] = row[(long)(h0 + i) * D + e];
+#pragma unroll
+    for (int i = 0; i < QKR_HB; ++i) {
+      const int h = h0 + i;
+      if (h >= nh) break;
+      if (h >= sh.Hq + sh.Hkv) {   // v head: relayout only
+        bf16_t* dst = V + (((long)b * sh.Hkv + (h - sh.Hq - sh.Hkv)) * sh.S + s) * D + lane * EPL;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) dst[e] = raw[i][e];
+        continue;
+      }
+      const bool isq = h < sh.Hq;
+      float x[EPL], ss = 0.f;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        x[e] = bf2f(raw[i][e]);
+        ss += x[e] * x[e];
+      }
+      const float rs = rsqrtf(warp_sum(ss) / D + eps);
+      float xn[EPL], part[EPL];
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) xn[e] = bfround(x[e] * rs * (isq ? wq[e] : wk[e]));
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) part[e] = xor32_get(xn[e]);
+      bf16_t* dst;
+      if (isq) {
+        const int kvh = h / G, j = h - kvh * G;
+        dst = Q + ((((long)b * sh.Hkv + kvh) * sh.S + s) * G + j) * D + lane * EPL;
+        if (lane == 0) rstd_q[m * sh.Hq + h] = rs;
+      } else {
+        const int kvh = h - sh.Hq;
+        dst = K + (((long)b * sh.Hkv + kvh) * sh.S + s) * D + lane * EPL;
+        if (lane == 0) rstd_k[m * sh.Hkv + kvh] = rs;
+      }
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) dst[e] = f2bf(xn[e] * cs[e] + sgn * part[e] * sn[e]);
+    }
   }
 }
 
@@ -80,59 +96,84 @@ __global__ void __launch_bounds__(256) qknorm_rope_bwd_kernel(
   constexpr int D = EPL * 64;
   const int lane = threadIdx.x & 63;
   const int nh = sh.Hq + 2 * sh.Hkv;
-  const long gw = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  const long M = (long)sh.B * sh.S;
-  if (gw >= M * nh) return;
-  const long m = gw / nh;
-  const int h = (int)(gw - m * nh);
+  const long m = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (m >= (long)sh.B * sh.S) return;
   const int b = (int)(m / sh.S), s = (int)(m - (long)b * sh.S);
   const int G = sh.Hq / sh.Hkv;
-  bf16_t* out = dqkv + m * (long)nh * D + (long)h * D + lane * EPL;
-  if (h >= sh.Hq + sh.Hkv) {
-    const int kvh = h - sh.Hq - sh.Hkv;
-    const bf16_t* src = dV + (((long)b * sh.Hkv + kvh) * sh.S + s) * D + lane * EPL;
-#pragma unroll
-    for (int e = 0; e < EPL; ++e) out[e] = src[e];
-    return;
-  }
-  const bool isq = h < sh.Hq;
-  const float* w = isq ? qw : kw;
-  const bf16_t* dy;
-  float rs;
-  if (isq) {
-    const int kvh = h / G, j = h - kvh * G;
-    dy = dQ + ((((long)b * sh.Hkv + kvh) * sh.S + s) * G + j) * D + lane * EPL;
-    rs = rstd_q[m * sh.Hq + h];
-  } else {
-    const int kvh = h - sh.Hq;
-    dy = dK + (((long)b * sh.Hkv + kvh) * sh.S + s) * D + lane * EPL;
-    rs = rstd_k[m * sh.Hkv + kvh];
-  }
   const int fi = (lane & 31) * EPL;
-  float ds[EPL], dc[EPL], part[EPL];
+  float cs[EPL], sn[EPL], wq[EPL], wk[EPL];
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
-    const float g = bf2f(dy[e]);
-    dc[e] = g * cos_t[(long)s * (D / 2) + fi + e];
-    ds[e] = g * sin_t[(long)s * (D / 2) + fi + e];
+    cs[e] = cos_t[(long)s * (D / 2) + fi + e];
+    sn[e] = sin_t[(long)s * (D / 2) + fi + e];
+    wq[e] = 1.f + qw[lane * EPL + e];
+    wk[e] = 1.f + kw[lane * EPL + e];
   }
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) part[e] = xor32_get(ds[e]);
   // rot^T(v)_i = v_{i+D/2} (i < D/2), -v_{i-D/2} (i >= D/2)
   const float sgn = lane < 32 ? 1.f : -1.f;
-  const bf16_t* xs = qkv + m * (long)nh * D + (long)h * D + lane * EPL;
-  float x[EPL], dxn[EPL];
-  float sdot = 0.f;
+  const bf16_t* xrow = qkv + m * (long)nh * D + lane * EPL;
+  bf16_t* orow = dqkv + m * (long)nh * D + lane * EPL;
+  for (int h0 = 0; h0 < nh; h0 += QKR_HB) {
+    bf16_t gy[QKR_HB][EPL], xr[QKR_HB][EPL];
+    float rsv[QKR_HB];
 #pragma unroll
-  for (int e = 0; e < EPL; ++e) {
-    x[e] = bf2f(xs[e]);
-    dxn[e] = bfround(dc[e] + sgn * part[e]) * (1.f + w[lane * EPL + e]);
-    sdot += dxn[e] * x[e];
+    for (int i = 0; i < QKR_HB; ++i) {
+      const int h = h0 + i;
+      if (h >= nh) break;
+      const bf16_t* dy;
+      if (h < sh.Hq) {
+        const int kvh = h / G, j = h - kvh * G;
+        dy = dQ + ((((long)b * sh.Hkv + kvh) * sh.S + s) * G + j) * D + lane * EPL;
+        rsv[i] = rstd_q[m * sh.Hq + h];
+      } else if (h < sh.Hq + sh.Hkv) {
+        const int kvh = h - sh.Hq;
+        dy = dK + (((long)b * sh.Hkv + kvh) * sh.S + s) * D + lane * EPL;
+        rsv[i] = rstd_k[m * sh.Hkv + kvh];
+      } else {
+        dy = dV + (((long)b * sh.Hkv + (h - sh.Hq - sh.Hkv)) * sh.S + s) * D + lane * EPL;
+        rsv[i] = 0.f;
+      }
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) gy[i][e] = dy[e];
+      if (h < sh.Hq + sh.Hkv)
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) xr[i][e] = xrow[(long)h * D + e];
+    }
+#pragma unroll
+    for (int i = 0; i < QKR_HB; ++i) {
+      const int h = h0 + i;
+      if (h >= nh) break;
+      bf16_t* out = orow + (long)h * D;
+      if (h >= sh.Hq + sh.Hkv) {
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) out[e] = gy[i][e];
+        continue;
+      }
+      const bool isq = h < sh.Hq;
+      const float rs = rsv[i];
+      float ds[EPL], dc[EPL], part[EPL];
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        const float g = bf2f(gy[i][e]);
+        dc[e] = g * cs[e];
+        ds[e] = g * sn[e];
+      }
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) part[e] = xor32_get(ds[e]);
+      float x[EPL], dxn[EPL];
+      float sdot = 0.f;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) {
+        x[e] = bf2f(xr[i][e]);
+        dxn[e] = bfround(dc[e] + sgn * part[e]) * (isq ? wq[e] : wk[e]);
+        sdot += dxn[e] * x[e];
+      }
+      sdot = warp_sum(sdot);
+      const float c3 = rs * rs * rs * sdot / D;
+#pragma unroll
+      for (int e = 0; e < EPL; ++e) out[e] = f2bf(rs * dxn[e] - c3 * x[e]);
+    }
   }
-  sdot = warp_sum(sdot);
-  const float c3 = rs * rs * rs * sdot / D;
-#pragma unroll
-  for (int e = 0; e < EPL; ++e) out[e] = f2bf(rs * dxn[e] - c3 * x[e]);
 }
 
 constexpr int SMAXV = 8;   // float4 per lane -> cols <= 2048
@@ -236,7 +277,7 @@ int launch_qknorm_rope_fwd(const bf16_t* qkv, const float* qw, const float* kw, 
                            const float* sin_t, AttnShape s, float eps, bf16_t* Q, bf16_t* K, bf16_t* V,
                            float* rstd_q, float* rstd_k, hipStream_t st) {
   if (s.Hq % s.Hkv) return set_error("qknorm_rope: Hq %% Hkv != 0");
-  const long waves = (long)s.B * s.S * (s.Hq + 2 * s.Hkv);
+  const long waves = (long)s.B * s.S;   // one wave per token
   dim3 grid((unsigned)((waves + 3) / 4));
   QKR_DISPATCH(qknorm_rope_fwd_kernel, qkv, qw, kw, cos_t, sin_t, s, eps, Q, K, V, rstd_q, rstd_k)
   return hipGetLastError() == hipSuccess ? 0 : set_error("qknorm_rope_fwd launch failed");
@@ -245,7 +286,7 @@ int launch_qknorm_rope_bwd(const bf16_t* qkv, const float* qw, const float* kw, 
                            const float* sin_t, AttnShape s, const float* rstd_q, const float* rstd_k,
                            const bf16_t* dQ, const bf16_t* dK, const bf16_t* dV, bf16_t* dqkv, hipStream_t st) {
   if (s.Hq % s.Hkv) return set_error("qknorm_rope: Hq %% Hkv != 0");
-  const long waves = (long)s.B * s.S * (s.Hq + 2 * s.Hkv);
+  const long waves = (long)s.B * s.S;   // one wave per token
   dim3 grid((unsigned)((waves + 3) / 4));
   QKR_DISPATCH(qknorm_rope_bwd_kernel, qkv, qw, kw, cos_t, sin_t, s, rstd_q, rstd_k, dQ, dK, dV, dqkv)
   return hipGetLastError() == hipSuccess ? 0 : set_error("qknorm_rope_bwd launch failed");

@@ -166,11 +166,15 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
 #pragma unroll
   for (int i = 0; i < FA_NBUF - 1; ++i)
     if (t_lo + i < t_hi) stage(t_lo + i, i);
+  // waves whose 16 rows all lie past the last row (the half-empty last block when rows % 128 = 64, e.g.
+  // SigLIP's 576 patches) only stage and keep the barriers; their SIMD time goes to the co-resident block
+  const bool idle = r0 + wave * 16 >= a.rows;
   for (int t = t_lo; t < t_hi; ++t) {
     const int buf = (t - t_lo) & (FA_NBUF - 1);
     vm_wait(ops * min(FA_NBUF - 2, t_hi - 1 - t));
     __syncthreads();
     if (t + FA_NBUF - 1 < t_hi) stage(t + FA_NBUF - 1, (buf + FA_NBUF - 1) & (FA_NBUF - 1));
+    if (idle) continue;
     const char* kb = smem + buf * 2 * R::TILE;
     const char* vb = kb + R::TILE;
     const int* kvs = reinterpret_cast<const int*>(smem + R::KV_OFF + buf * (KT * 4));

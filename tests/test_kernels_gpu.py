@@ -268,7 +268,7 @@ def _attn_ref(q, k, v, mask, scale):
     return (p / l) @ v.float(), (m + torch.log(l)).squeeze(-1)
 
 
-@pytest.mark.parametrize("N", [576, 196, 16])
+@pytest.mark.parametrize("N", [576, 288, 196, 16])
 def test_flash_fwd_siglip_layout(gpu, N):
     """Non-causal, head_dim 64, Q/K/V read in place from the fused [B*N, 3D] qkv buffer."""
     Kn, L = _k()
