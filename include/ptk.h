@@ -75,7 +75,13 @@ typedef struct {
   int64_t ld_aux_in;
   ptk_rowmap amap;
   ptk_rowmap cmap;
+  /* optional stream-K scratch (NULL: off): sk_workspace >= ptk_gemm_sk_workspace_bytes(), sk_flags >=
+   * ptk_gemm_sk_flag_count() int32 zeroed once before first use (each use leaves them zero) */
+  void* sk_workspace;
+  int32_t* sk_flags;
 } ptk_gemm_desc;
+size_t ptk_gemm_sk_workspace_bytes(void);
+int ptk_gemm_sk_flag_count(void);
 int ptk_gemm(const ptk_gemm_desc* d, void* stream);
 
 /* LayerNorm (SigLIP, modeling_siglip.py:329): x f32 [rows,cols] -> y bf16. */
@@ -117,7 +123,8 @@ int ptk_gemm_timer_enable(int on);   /* 0 off, 1 every class, (1 << 8) | class m
 /* Tile-path test hook: 0 = shape heuristic, 1 = every GEMM on the 128x128 kernel,
    2 / 4 = every single-batch GEMM on the 256x256 / barrier-staggered 256x256 kernel,
    8 = every single-batch GEMM the persistent 4-wave 256x256 kernel supports on it. */
-int ptk_gemm_force_small_tiles(int mode);
+int ptk_gemm_force_small_tiles(int mode);   /* tests: 0 auto, 1 128x128, 2 256x256, 4 staggered 256x256,
+                                              8 persistent 4-wave, 16 stream-K (needs desc scratch) */
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
 
 /* Flash attention forward: O = softmax(scale * Q K^T + mask) V per z, bf16 in/out,

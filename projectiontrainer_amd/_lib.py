@@ -33,7 +33,7 @@ class GemmDesc(C.Structure):
                 ("ld_rowadd", c_int64), ("resid", c_void_p), ("ld_resid", c_int64),
                 ("aux", c_void_p), ("aux2", c_void_p), ("ld_aux", c_int64),
                 ("aux_in", c_void_p), ("aux_in2", c_void_p), ("ld_aux_in", c_int64),
-                ("amap", RowMap), ("cmap", RowMap)]
+                ("amap", RowMap), ("cmap", RowMap), ("sk_workspace", c_void_p), ("sk_flags", c_void_p)]
 
 
 class FlashDesc(C.Structure):
@@ -130,6 +130,8 @@ SIGNATURES = {
     "ptk_fill_normal_bf16": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_void_p]),
     "ptk_gemm_timer_enable": (c_int, [c_int]),
     "ptk_gemm_force_small_tiles": (c_int, [c_int]),
+    "ptk_gemm_sk_workspace_bytes": (c_size_t, []),
+    "ptk_gemm_sk_flag_count": (c_int, []),
     "ptk_gemm_timer_read": (c_int, [c_int, C.POINTER(C.c_double), C.POINTER(c_int)]),
     "ptk_flash_attn_fwd": (c_int, [C.POINTER(FlashDesc), c_void_p]),
     "ptk_flash_attn_bwd": (c_int, [C.POINTER(FlashBwdDesc), c_void_p]),
@@ -168,6 +170,8 @@ def lib():
             raise PtkError(f"libptk.so not found at {LIB_PATH}: run `python -c 'import __graft_entry__ as g; g.build()'`")
         L = C.CDLL(LIB_PATH)
         for name, (res, args) in SIGNATURES.items():
+            if os.environ.get("PTK_LIB") and not hasattr(L, name):
+                continue   # an older diagnostic build may predate an entry point
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
         if L.ptk_abi_version() != 1:

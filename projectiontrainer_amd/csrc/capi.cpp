@@ -33,6 +33,7 @@ GemmArgs to_args(const ptk_gemm_desc* d) {
   a.aux = (bf16_t*)d->aux; a.aux2 = (bf16_t*)d->aux2; a.ld_aux = d->ld_aux;
   a.aux_in = (const bf16_t*)d->aux_in; a.aux_in2 = (const bf16_t*)d->aux_in2; a.ld_aux_in = d->ld_aux_in;
   a.amap = to_map(d->amap); a.cmap = to_map(d->cmap);
+  a.sk_part = (float*)d->sk_workspace; a.sk_flags = (int*)d->sk_flags;
   return a;
 }
 
@@ -103,9 +104,12 @@ int ptk_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream) {
   return launch_cast_f32_bf16(in, (bf16_t*)out, n, ST);
 }
 
+size_t ptk_gemm_sk_workspace_bytes(void) { return (size_t)SK_MAX_BLOCKS * SK_SLAB_FLOATS * sizeof(float); }
+int ptk_gemm_sk_flag_count(void) { return SK_MAX_BLOCKS; }
+
 int ptk_gemm_force_small_tiles(int mode) {
-  if (mode != 0 && mode != 1 && mode != 2 && mode != 4 && mode != 8)
-    return set_error("gemm tile mode %d not in {0, 1, 2, 4, 8}", mode);
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 4 && mode != 8 && mode != 16)
+    return set_error("gemm tile mode %d not in {0, 1, 2, 4, 8, 16}", mode);
   force_small_tiles(mode);
   return 0;
 }

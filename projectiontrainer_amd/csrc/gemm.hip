@@ -465,25 +465,14 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
 
 
 
-template <int ACT, int OUT>
-__global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[8 * EPI_WAVE_BYTES];   // 136 KiB >= 2 * BUF_BYTES
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+// K-tiles [k0, k1) of the 256x256 tile (bm, bn) into acc (zeroed by the caller), wave groups wr = 0 / 1
+// one barrier apart (half a phase): on every SIMD one wave of the pair issues its LDS reads while the
+// other runs its MFMA cluster.  Each phase: reads + DMA issue, barrier, MFMA cluster, barrier.  Ends with
+// every DMA retired and a workgroup barrier (the LDS is free for the epilogue).
+PTK_DEV void big2_kloop(const GemmArgs& p, char* smem, int bm, int bn, int k0, int k1, f32x4_t (&acc)[8][4],
+                        int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
   const int wr = wave >> 2, wc = wave & 3;
-
-  const int nbm = (p.M + BIG - 1) / BIG, nbn = (p.N + BIG - 1) / BIG;
-  const int ntile = nbm * nbn;
-  int bid = blockIdx.x;
-  {
-    const int q = ntile >> 3, rr = ntile & 7, x = bid & 7;
-    bid = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (bid >> 3);
-  }
-  const int per_group = GROUP_M * nbn;
-  const int first_m = (bid / per_group) * GROUP_M;
-  const int gsz = min(nbm - first_m, GROUP_M);
-  const int bm = first_m + (bid % per_group) % gsz;
-  const int bn = (bid % per_group) / gsz;
-
   const bf16_t* A = p.A;
   const bf16_t* B = p.B;
   // staging sources: half-tile h (0,1 = A halves, 2,3 = B halves), instruction j (0,1):
@@ -505,36 +494,26 @@ __global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
       }
     }
   auto stage = [&](int h, int t) {
-    char* dst = smem + (t & 1) * BUF_BYTES + h * HALF_BYTES + wave * 16 * 128;
+    char* dst = smem + ((t - k0) & 1) * BUF_BYTES + h * HALF_BYTES + wave * 16 * 128;
     glds16(src[h][0] + (long)t * BK, dst);
     glds16(src[h][1] + (long)t * BK, dst + 8 * 128);
   };
 
-  f32x4_t acc[8][4];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
   const int frag_off = (lane & 15) * 128 + (((lane >> 4) ^ ((lane >> 1) & 7)) << 4);
-  const int nt = p.K / BK;
-  // prologue: K-tile 0 complete, B halves of K-tile 1 in flight
-  stage(0, 0); stage(1, 0); stage(2, 0); stage(3, 0);
-  if (nt > 1) {
-    stage(2, 1); stage(3, 1);
+  // prologue: K-tile k0 complete, B halves of K-tile k0+1 in flight
+  stage(0, k0); stage(1, k0); stage(2, k0); stage(3, k0);
+  if (k1 - k0 > 1) {
+    stage(2, k0 + 1); stage(3, k0 + 1);
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
   } else {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   __builtin_amdgcn_s_barrier();
 
-  // wave groups wr = 0 / wr = 1 run one barrier apart (half a phase): on every SIMD one wave of the
-  // pair issues its LDS reads while the other runs its MFMA cluster.  Each phase: reads + DMA issue,
-  // barrier, MFMA cluster, barrier.
   if (__builtin_amdgcn_readfirstlane(wr) == 1) __builtin_amdgcn_s_barrier();
   bf16x8_t a[4][2], b0[2][2], b1[2][2];
-  for (int t = 0; t < nt; ++t) {
-    const char* buf = smem + (t & 1) * BUF_BYTES;
+  for (int t = k0; t < k1; ++t) {
+    const char* buf = smem + ((t - k0) & 1) * BUF_BYTES;
     const char* As = buf + wr * HALF_BYTES;
     const char* Bs = buf + (2 + (wc >> 1)) * HALF_BYTES + (wc & 1) * 64 * 128;
     // ---- phase 0: A(mh0), B(nh0), B(nh1) fragments; DMA A0(t+1)
@@ -553,7 +532,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
 #pragma unroll
       for (int ks = 0; ks < 2; ++ks)
         b1[n][ks] = *reinterpret_cast<const bf16x8_t*>(Bs + (32 + n * 16) * 128 + (frag_off ^ (ks << 6)));
-    if (t + 1 < nt) stage(0, t + 1);
+    if (t + 1 < k1) stage(0, t + 1);
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(4)" ::: "memory");   // A(mh0), B(nh0) landed
     __builtin_amdgcn_sched_barrier(0);
@@ -570,7 +549,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_s_barrier();
     // ---- phase 1: DMA A1(t+1); A(mh0) x B(nh1), A(mh1) re-read into a[i] as a[i] is consumed
-    if (t + 1 < nt) stage(1, t + 1);
+    if (t + 1 < k1) stage(1, t + 1);
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -589,7 +568,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
     // ---- phase 2: DMA B0(t+2) (B of tile t is in registers since phase 0); A(mh1) x B(nh0)
-    if (t + 2 < nt) stage(2, t + 2);
+    if (t + 2 < k1) stage(2, t + 2);
     __builtin_amdgcn_s_barrier();
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_sched_barrier(0);
@@ -604,7 +583,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
     __builtin_amdgcn_s_setprio(0);
     __builtin_amdgcn_s_barrier();
     // ---- phase 3: DMA B1(t+2); retire K-tile t+1 (B(t+2) stays in flight); A(mh1) x B(nh1)
-    if (t + 2 < nt) {
+    if (t + 2 < k1) {
       stage(3, t + 2);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     } else {
@@ -626,7 +605,28 @@ __global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
   if (__builtin_amdgcn_readfirstlane(wr) == 0) __builtin_amdgcn_s_barrier();
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
+}
 
+// tile index -> (bm, bn): GROUP_M-row groups (A row-panels and B column-panels reused through L2)
+PTK_DEV void big_tile_coords(const GemmArgs& p, int tile, int& bm, int& bn) {
+  const int nbm = (p.M + BIG - 1) / BIG, nbn = (p.N + BIG - 1) / BIG;
+  const int per_group = GROUP_M * nbn;
+  const int first_m = (tile / per_group) * GROUP_M;
+  const int gsz = min(nbm - first_m, GROUP_M);
+  bm = first_m + (tile % per_group) % gsz;
+  bn = (tile % per_group) / gsz;
+}
+
+// blocks b, b+8, ... share an XCD: give them consecutive indices (bijective over n)
+PTK_DEV int xcd_remap(int b, int n) {
+  const int q = n >> 3, rr = n & 7, x = b & 7;
+  return (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
+}
+
+template <int ACT, int OUT>
+PTK_DEV void big_epilogue(const GemmArgs& p, char* smem, int bm, int bn, f32x4_t (&acc)[8][4], int tid) {
+  const int lane = tid & 63, wave = tid >> 6;
+  const int wr = wave >> 2, wc = wave & 3;
   char* Cz = reinterpret_cast<char*>(p.C);
   // the wave's 128x64 tile as two 64x64 halves through its private LDS region
   f32x4_t (&top)[4][4] = *reinterpret_cast<f32x4_t(*)[4][4]>(&acc[0][0]);
@@ -635,15 +635,125 @@ __global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
   epilogue<ACT, OUT>(p, smem, wave, lane, top, r0, c0, Cz);
   __builtin_amdgcn_wave_barrier();
   epilogue<ACT, OUT>(p, smem, wave, lane, bot, r0 + 64, c0, Cz);
-
 }
 
+template <int ACT, int OUT>
+__global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * EPI_WAVE_BYTES];   // 136 KiB >= 2 * BUF_BYTES
+  const int nbm = (p.M + BIG - 1) / BIG, nbn = (p.N + BIG - 1) / BIG;
+  int bm, bn;
+  big_tile_coords(p, xcd_remap(blockIdx.x, nbm * nbn), bm, bn);
+  f32x4_t acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  big2_kloop(p, smem, bm, bn, 0, p.K / BK, acc, threadIdx.x);
+  big_epilogue<ACT, OUT>(p, smem, bm, bn, acc, threadIdx.x);
+}
 
+// ---------------------------------------------------------------- stream-K over the 256x256 tiles
+// A tile grid that quantises badly onto the CUs (Gemma3's N = 1152 projections: 440 tiles = 1.72
+// waves of 256 CUs) runs as a persistent grid of G blocks, block v owning the K-tile iterations
+// [v*T/G, (v+1)*T/G) of the T = tiles x K-tiles iteration space (every range >= one tile's K loop, so a
+// tile is split between at most two neighbouring blocks).  Block v's range starts with the tail of a
+// tile whose head block v-1 computes LAST: the tail block writes its fp32 partial (256 KiB slab, MFMA
+// register order, 1 KiB per wave instruction), publishes it (agent-scope release + flag), and the head
+// block, finishing its range, acquires it, adds it to its registers and runs the fused epilogue.  The
+// head never waits on a block that could be waiting on it (block v depends only on v+1's FIRST segment).
+template <int ACT, int OUT>
+__global__ void __launch_bounds__(512, 1) gemm_sk_kernel(GemmArgs p) {
+  __shared__ __attribute__((aligned(16))) char smem[8 * EPI_WAVE_BYTES];
+  const int tid = threadIdx.x;
+  const int G = gridDim.x;
+  // segment control in scalar registers (32-bit: the launcher bounds tiles x K-tiles below 2^31)
+  const int v = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, G));   // consecutive v share an XCD
+  const int nt = __builtin_amdgcn_readfirstlane(p.K / BK);
+  const int ntile = __builtin_amdgcn_readfirstlane(((p.M + BIG - 1) / BIG) * ((p.N + BIG - 1) / BIG));
+  const long total = (long)ntile * nt;
+  const int g0 = __builtin_amdgcn_readfirstlane((int)((long)v * total / G));
+  const int g1 = __builtin_amdgcn_readfirstlane((int)((long)(v + 1) * total / G));
+  f32x4_t acc[8][4];
+  for (int g = g0; g < g1;) {
+    const int tile = __builtin_amdgcn_readfirstlane(g / nt);
+    const int k0 = __builtin_amdgcn_readfirstlane(g - tile * nt);
+    const int k1 = __builtin_amdgcn_readfirstlane(min(nt, k0 + (g1 - g)));
+    g += k1 - k0;
+    int bm, bn;
+    big_tile_coords(p, tile, bm, bn);
+    bm = __builtin_amdgcn_readfirstlane(bm);
+    bn = __builtin_amdgcn_readfirstlane(bn);
+    // an opaque copy of the thread index per segment: keeps the per-lane address arithmetic of the
+    // K loop and the epilogue inside the segment (hoisted out of this loop it stays live through the
+    // MFMA loop and spills)
+    int ltid = tid;
+    asm volatile("" : "+v"(ltid));
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    big2_kloop(p, smem, bm, bn, k0, k1, acc, ltid);
+    if (k0 > 0) {
+      // tail of a tile whose head is block v-1's last segment: publish the partial in slot v-1
+      float4* slab = reinterpret_cast<float4*>(p.sk_part + (long)(v - 1) * SK_SLAB_FLOATS) + ltid * 1 + (ltid >> 6) * 31 * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          slab[(i * 4 + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p.sk_flags + (v - 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      continue;   // k1 == nt: the head block finishes this tile
+    }
+    if (k1 < nt) {
+      // head of a tile whose tail is block v+1's first segment: take its partial
+      if (tid == 0) {
+        while (__hip_atomic_load(p.sk_flags + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+          __builtin_amdgcn_s_sleep(4);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        __hip_atomic_store(p.sk_flags + v, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next launch
+      }
+      __syncthreads();
+      const float4* slab = reinterpret_cast<const float4*>(p.sk_part + (long)v * SK_SLAB_FLOATS) + ltid + (ltid >> 6) * 31 * 64;
+#pragma unroll
+      for (int i = 0; i < 8; ++i) {
+        float4 t[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) t[j] = slab[(i * 4 + j) * 64];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          acc[i][j][0] += t[j].x; acc[i][j][1] += t[j].y; acc[i][j][2] += t[j].z; acc[i][j][3] += t[j].w;
+        }
+        __builtin_amdgcn_sched_barrier(0);   // four slab loads in flight at a time (register pressure)
+      }
+    }
+    big_epilogue<ACT, OUT>(p, smem, bm, bn, acc, ltid);
+    __syncthreads();   // epilogue staging done before the next segment's DMA reuses the LDS
+  }
+}
+
+static int g_num_cu = 0;
+static int num_cus() {
+  if (!g_num_cu) {
+    int dev = 0;
+    hipDeviceProp_t prop;
+    if (hipGetDevice(&dev) != hipSuccess || hipGetDeviceProperties(&prop, dev) != hipSuccess) return 256;
+    g_num_cu = prop.multiProcessorCount;
+  }
+  return g_num_cu;
+}
 
 // ---- optional live per-class timing (HIP events around launches; bench.py roofline)
 static bool g_timing = false;
 static int g_timing_mask = 0;   // activation classes whose launches are timed
-static int g_force_tiles = 0;   // tests: 1 = every GEMM on 128x128, 2 / 4 = single-batch GEMMs on 256x256 / staggered 256x256
+static int g_force_tiles = 0;   // tests: 1 = every GEMM on 128x128, 2 / 4 = single-batch GEMMs on 256x256 / staggered 256x256,
+                                // 8 = persistent 4-wave kernel, 16 = stream-K wherever scratch is given and tiles > CUs
 void force_small_tiles(int mode) { g_force_tiles = mode; }
 static std::vector<hipEvent_t> g_ev[8];
 static size_t g_ev_used[8];
@@ -708,6 +818,35 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
     const int rc = launch_gemm_w4(a, act, out, st, 0);
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
+  }
+  // stream-K (forced mode 16 only): measured on the step's N = 1152 projections (440 tiles = 1.72 waves of
+  // 256 CUs) it balances the CUs but runs each K-tile ~1.5x slower — blocks enter their tiles at
+  // different K offsets, so neighbouring tiles no longer stream the same A/B panels through L2 in
+  // lock-step and the launch becomes bound by L2-miss traffic (g_dgu 643 -> 832 us)
+  if (batch == 1 && a.sk_part && a.sk_flags && g_force_tiles == 16) {
+    const int nbig = ((a.M + BIG - 1) / BIG) * ((a.N + BIG - 1) / BIG);
+    const int G = std::min(num_cus(), SK_MAX_BLOCKS);
+    if (nbig > G && (long)nbig * (a.K / BK) < 0x7fffffffL) {
+#define PTK_SK_CASE(ACT_, OUT_)                                                                 \
+      if (act == ACT_ && out == OUT_) {                                                         \
+        hipEvent_t e0 = nullptr, e1 = nullptr;                                                  \
+        if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); } \
+        if (e0) (void)hipEventRecord(e0, st);                                                   \
+        hipLaunchKernelGGL((gemm_sk_kernel<ACT_, OUT_>), dim3(G), dim3(512), 0, st, a);         \
+        if (e1) (void)hipEventRecord(e1, st);                                                   \
+        return hipGetLastError() == hipSuccess ? 0 : set_error("gemm launch failed");          \
+      }
+      PTK_SK_CASE(ACT_NONE, OUT_BF16)
+      PTK_SK_CASE(ACT_NONE, OUT_F32)
+      PTK_SK_CASE(ACT_NONE, OUT_F32_BFR)
+      PTK_SK_CASE(ACT_GELU_TANH, OUT_BF16)
+      PTK_SK_CASE(ACT_GELU_ERF, OUT_BF16)
+      PTK_SK_CASE(ACT_GEGLU, OUT_BF16)
+      PTK_SK_CASE(ACT_GELU_ERF_BWD, OUT_BF16)
+      PTK_SK_CASE(ACT_GEGLU_BWD, OUT_BF16)
+#undef PTK_SK_CASE
+      return set_error("gemm: unsupported (act=%d, out=%d)", act, out);
+    }
   }
   if (batch == 1 && (g_force_tiles == 4 || (g_force_tiles == 0 && big_shape && a.K >= 4096))) {
     const long nb = (long)((a.M + BIG - 1) / BIG) * ((a.N + BIG - 1) / BIG);

@@ -42,7 +42,14 @@ struct GemmArgs {
   long ld_aux_in = 0;
   RowMap amap{0, 0, 0, 0};                       // A row remap (gather)
   RowMap cmap{0, 0, 0, 0};                       // C row remap (scatter / skip)
+  // stream-K scratch (launch_gemm may then balance a poorly quantised tile grid over the CUs):
+  // sk_part >= SK_MAX_BLOCKS * 256 KiB, sk_flags >= SK_MAX_BLOCKS ints, zero before the first use
+  // (every split tile's consumer resets its flag)
+  float* sk_part = nullptr;
+  int* sk_flags = nullptr;
 };
+constexpr int SK_MAX_BLOCKS = 512;
+constexpr long SK_SLAB_FLOATS = 256L * 256;
 
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
 // persistent 256x256 4-wave GEMM (gemm_w4.hip): batch 1 only; w4_supported says whether a shape qualifies
