@@ -14,6 +14,15 @@ The body of `for batch in progress_bar:` (Stage1/projector_trainer.py:152-245):
 
 All buffers are allocated once per (batch, text_len); a step issues no host
 synchronisation, so the loss is returned as a device tensor.
+
+Vision prefetch: the SigLIP tower is frozen, so the vision features of the NEXT
+batch do not depend on this step's update.  `step(..., next_pixel_values=...)`
+runs the next batch's SigLIP forward on a side stream as soon as this step's
+projector forward has consumed its own features; it overlaps the Gemma3
+forward/backward (filling the CUs its GEMM tail waves and HBM-bound passes
+leave idle), and the next step waits only on its event.  Vision features and
+pixels are double-buffered; a buffer is reused only after the projector
+backward that reads it has run.
 """
 from __future__ import annotations
 
@@ -57,6 +66,8 @@ class Stage1Engine:
         self.grad_norm = torch.zeros(1, dtype=torch.float32, device=self.device)
         self._shape = None
         self.last_lr = learning_rate * cosine_lambda(0, warmup_steps, total_steps)
+        self.vstream = None        # side stream of the vision prefetch
+        self._prefetched = None    # event: the current buffer's features were computed ahead
 
     def _buffers(self, B, T):
         if self._shape == (B, T):
@@ -67,8 +78,13 @@ class Stage1Engine:
         Sp = Gemma3CausalLM.seq_pad(S)
         dev, bf = self.device, torch.bfloat16
         self.N, self.Sp = N, Sp
-        self.px = torch.empty((B, vc.num_channels, vc.image_size, vc.image_size), dtype=bf, device=dev)
-        self.vis = torch.empty((B * N, Dv), dtype=bf, device=dev)
+        self.px_bufs = [torch.empty((B, vc.num_channels, vc.image_size, vc.image_size), dtype=bf, device=dev)
+                        for _ in range(2)]
+        self.vis_bufs = [torch.empty((B * N, Dv), dtype=bf, device=dev) for _ in range(2)]
+        self._cur = 0
+        self._released = [None, None]   # event per buffer: the projector backward reading it has run
+        self._prefetched = None
+        self.px, self.vis = self.px_bufs[0], self.vis_bufs[0]
         self.a = torch.empty((B * N, I), dtype=bf, device=dev)
         self.h = torch.empty((B * N, I), dtype=bf, device=dev)
         self.x = torch.empty((B * Sp, Dl), dtype=torch.float32, device=dev)
@@ -81,23 +97,61 @@ class Stage1Engine:
         self._shape = (B, T)
 
     # ---------------------------------------------------------------- pieces
-    def forward_backward(self, pixel_values, token_ids, labels):
-        """Everything up to (and including) the projector grads; returns loss (device [1])."""
+    def _vision(self, pixel_values, i):
+        """pixels -> bf16 px_bufs[i] -> SigLIP features vis_bufs[i], on the current stream."""
+        px = self.px_bufs[i]
+        if pixel_values.dtype == torch.bfloat16:
+            px.copy_(pixel_values)
+        else:
+            K.cast_bf16(pixel_values.contiguous(), px)
+        self.vision.forward_into(px, self.vis_bufs[i])
+
+    def forward_backward(self, pixel_values, token_ids, labels, next_pixel_values=None):
+        """Everything up to (and including) the projector grads; returns loss (device [1]).
+        next_pixel_values: the following step's pixels, whose SigLIP forward then runs on the side stream
+        during this step's Gemma3 forward/backward (that step must pass the same pixels)."""
         B, T = token_ids.shape
         self._buffers(B, T)
-        if pixel_values.dtype == torch.bfloat16:
-            self.px.copy_(pixel_values)
+        main = torch.cuda.current_stream(self.device)
+        i = self._cur
+        if self._prefetched is not None:
+            main.wait_event(self._prefetched)
+            self._prefetched = None
         else:
-            K.cast_bf16(pixel_values.contiguous(), self.px)
-        self.vision.forward_into(self.px, self.vis)
+            self._vision(pixel_values, i)
+        self.px, self.vis = self.px_bufs[i], self.vis_bufs[i]
         # projector rows (b, i) -> LLM rows b*Sp + i - 1; patch 0 dropped (projector_trainer.py:173)
         self.proj.fwd_into(self.vis, self.a, self.h, self.x, out_map=(self.N, 1, self.Sp, -1), round_bf16=True)
+        if next_pixel_values is not None:
+            j = 1 - i
+            consumed = torch.cuda.Event()
+            consumed.record(main)   # SigLIP workspace and this step's features consumed by the projector
+            if self.vstream is None:
+                self.vstream = torch.cuda.Stream(self.device)
+            self.vstream.wait_event(consumed)
+            if self._released[j] is not None:
+                self.vstream.wait_event(self._released[j])
+            next_pixel_values.record_stream(self.vstream)
+            with torch.cuda.stream(self.vstream):
+                self._vision(next_pixel_values, j)
+                ready = torch.cuda.Event()
+                ready.record(self.vstream)
+            self._prefetched = ready
+            self._cur = j
         self.llm.loss_and_input_grad(self.x, self.dx, token_ids, labels, self.N - 1,
                                      1.0 / float(self.gas * self.gas), self.loss)
         L.check(L.lib().ptk_gather_vision_grad(self.dx.data_ptr(), B, self.N, self.Sp, self.llm.cfg.hidden_size,
                                                self.dy.data_ptr(), L.stream_ptr(self.device)), "gather_vision_grad")
         self.proj.bwd_into(self.vis, self.a, self.h, self.dy, self.proj_ws)
+        rel = torch.cuda.Event()
+        rel.record(main)
+        self._released[i] = rel
         return self.loss
+
+    def join_prefetch(self):
+        """Make the current stream wait for an outstanding vision prefetch (end of a timed region)."""
+        if self._prefetched is not None:
+            torch.cuda.current_stream(self.device).wait_event(self._prefetched)
 
     def optimizer_step(self):
         """DDP all-reduce (sum; 1/W folded into the update), clip + AdamW, schedule."""
@@ -115,8 +169,8 @@ class Stage1Engine:
         self.last_lr = lr
         return lr
 
-    def step(self, pixel_values, token_ids, labels):
-        loss = self.forward_backward(pixel_values, token_ids, labels)
+    def step(self, pixel_values, token_ids, labels, next_pixel_values=None):
+        loss = self.forward_backward(pixel_values, token_ids, labels, next_pixel_values)
         self.optimizer_step()
         return loss
 

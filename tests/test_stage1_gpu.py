@@ -166,3 +166,27 @@ def test_siglip_full_depth_vs_oracle(gpu):
     assert rel_l2(out, ref) <= 3e-2, rel_l2(out, ref)
     cos = torch.nn.functional.cosine_similarity(out.reshape(-1, out.shape[-1]), ref.reshape(-1, ref.shape[-1]), dim=-1)
     assert cos.min() >= 0.99, cos.min()
+
+
+def test_vision_prefetch_is_exact(gpu):
+    """Steps that prefetch the next batch's SigLIP forward on the side stream give bit-identical losses,
+    grads and parameters to steps that run it inline (three steps, three different batches)."""
+    name = "tiny"
+    d, meta = G.load(name)
+    batches = []
+    for s in range(3):
+        px, ids, labels = G.batch(d, s % meta["steps"])
+        px = torch.from_numpy(px).to(gpu) * (1.0 + 0.1 * s)   # three distinct pixel batches
+        batches.append((px.clamp(-1, 1), torch.from_numpy(ids).to(gpu), torch.from_numpy(labels).to(gpu)))
+    runs = []
+    for prefetch in (False, True):
+        cfg, eng = build_engine(name, gpu, 1, meta["lr"], 10)
+        losses = []
+        for s, (px, ids, labels) in enumerate(batches):
+            nxt = batches[s + 1][0] if prefetch and s + 1 < len(batches) else None
+            losses.append(float(eng.step(px, ids, labels, next_pixel_values=nxt)))
+        eng.join_prefetch()
+        torch.cuda.synchronize()
+        runs.append((losses, eng.proj.flat.detach().clone(), eng.proj.flat_grad.detach().clone()))
+    assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
+    assert torch.equal(runs[0][1], runs[1][1]) and torch.equal(runs[0][2], runs[1][2])
