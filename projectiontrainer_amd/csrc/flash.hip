@@ -42,9 +42,12 @@ PTK_DEV int swz_k(int r) { return D == 256 ? (r & 15) : ((r >> 1) & 7); }     //
 template <int D>
 PTK_DEV int swz_v(int r) { return D == 256 ? 2 * (r & 7) : 2 * ((r >> 1) & 3); }  // ds_read_b64_tr_b16
 // d 256 tiles read both by rows (ds_read_b128, 16 rows x one chunk) and transposed (ds_read_b64_tr_b16,
-// 8 rows x two adjacent chunks per 32-lane half): even values for rows 0-7, odd for 8-15 keeps both
-// patterns conflict-free (r & 15 alone leaves the transposed reads 2-way conflicted)
-PTK_DEV int swz_rt(int r) { return ((r & 7) << 1) | ((r >> 3) & 1); }
+// 8 rows x two adjacent chunks per 32-lane half).  With the b128 lane groups {0-3,12-15,20-27},
+// {4-11,16-19,28-31}, ... (MI355X_MICROARCH.md, LDS table) a row swizzle f keeps the row reads
+// conflict-free iff f(r) and f(r ^ 8) ^ 1 never collide, and the transposed reads iff f(r) >> 1 is
+// distinct over each octet of rows: f(r) = 2 (r & 7) meets both.  (The former ((r & 7) << 1) | (r >> 3)
+// met the second only: 2-way conflicts on every row read, 32-40 % of the backward kernels' LDS cycles.)
+PTK_DEV int swz_rt(int r) { return (r & 7) << 1; }
 template <int D>
 PTK_DEV int swz_kt(int r) { return D == 256 ? swz_rt(r) : swz_k<D>(r); }
 
@@ -80,21 +83,27 @@ struct FaRing {
 template <int D>
 constexpr int fa_kt() { return D == 256 ? 32 : 64; }
 
-template <int D>
+// QG query groups of 16 rows per wave (block = 8 waves x 16 QG rows): with QG = 2 every K fragment
+// (ds_read_b128) and V^T fragment (ds_read_b64_tr_b16) read from LDS feeds two MFMAs, halving the LDS
+// traffic per FLOP — at head_dim 256 the 16-row form reads as many LDS bytes per tile as its MFMAs
+// take cycles (8 waves x 32 KiB per 32-key tile)
+template <int D, int QG>
 __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
   constexpr int KT = fa_kt<D>();
   using R = FaRing<D, KT>;
   constexpr int KS = D / 32;                 // MFMA k-steps over the head dim
   constexpr int DS = D / 16;                 // 16-wide d sub-tiles
   constexpr int MS = KT / 16, ST = KT / 32;  // 16-key score sub-tiles, 32-key P.V k-steps
+  constexpr int BR = 128 * QG;               // query rows per block
+  constexpr int WR = 16 * QG;                // query rows per wave
   __shared__ __attribute__((aligned(16))) char smem[R::BYTES];   // (K, V) x4, key_valid x4
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int g = lane >> 4, c16 = lane & 15;
   // heaviest (latest, for causal) row blocks first; z fastest
-  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
+  const int nqb = (a.rows + BR - 1) / BR, nz = gridDim.x / nqb;
   const int z = blockIdx.x % nz, z0 = z / a.zin, z1 = z - z0 * a.zin;
-  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;
+  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * BR;
   const bf16_t* Q = a.Q + z0 * a.sQ0 + z1 * a.sQ1;
   const bf16_t* K = a.K + z0 * a.sK0 + z1 * a.sK1;
   const bf16_t* V = a.V + z0 * a.sK0 + z1 * a.sK1;
@@ -102,7 +111,7 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
   const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
 
   // key range of the block (causal / window skip)
-  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
+  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + BR - 1, a.rows - 1) / a.qdiv;
   int k_hi = a.nkeys;
   int k_lo = 0;
   if (a.causal) {
@@ -111,22 +120,25 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
   }
   const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
 
-  // Q fragments: B operand of S^T = K Q^T, lane holds Q[row c16][8g + 32ks .. +7]
-  const int qrow = r0 + wave * 16 + c16;
-  const int qrow_c = min(qrow, a.rows - 1);
-  bf16x8_t qf[KS];
-  {
+  // Q fragments: B operand of S^T = K Q^T, lane holds Q[row c16 of group qg][8g + 32ks .. +7]
+  const int wrow0 = r0 + wave * WR;
+  int qrow[QG], qpos[QG];
+  bf16x8_t qf[QG][KS];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) {
+    qrow[qg] = wrow0 + qg * 16 + c16;
+    const int qrow_c = min(qrow[qg], a.rows - 1);
+    qpos[qg] = qrow_c / a.qdiv;
     const long qa = map_row(a.qmap, qrow_c);
     const bf16_t* qp = Q + qa * a.ldq + 8 * g;
 #pragma unroll
-    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * ks);
+    for (int ks = 0; ks < KS; ++ks) qf[qg][ks] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * ks);
   }
-  const int qpos = qrow_c / a.qdiv;
   const int causal = a.causal != 0, nowin = a.window <= 0;
   const bool unmasked = !kvl && !causal && nowin;
-  // query positions of this wave's 16 rows (interior-tile test)
-  const int wpos_lo = min(r0 + wave * 16, a.rows - 1) / a.qdiv;
-  const int wpos_hi = min(r0 + wave * 16 + 15, a.rows - 1) / a.qdiv;
+  // query positions of this wave's rows (interior-tile test)
+  const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
+  const int wpos_hi = min(wrow0 + WR - 1, a.rows - 1) / a.qdiv;
 
   const int ops = (R::INST >= 8 ? 2 * R::PER_WAVE : 1) + (kvl ? 1 : 0);   // LDS-DMA ops per wave per tile
   auto stage = [&](int t, int buf) {
@@ -157,18 +169,22 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
                 smem + R::KV_OFF + buf * (KT * 4) + wave * (R::KV_LANES * 16));
   };
 
-  f32x4_t o[DS];
+  f32x4_t o[QG][DS];
 #pragma unroll
-  for (int i = 0; i < DS; ++i) o[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
+  for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+    for (int i = 0; i < DS; ++i) o[qg][i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float m_run[QG], l_run[QG];
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg) { m_run[qg] = -INFINITY; l_run[qg] = 0.f; }
   const float sl2 = a.scale * 1.4426950408889634f;   // scores in log2 units
 
 #pragma unroll
   for (int i = 0; i < FA_NBUF - 1; ++i)
     if (t_lo + i < t_hi) stage(t_lo + i, i);
-  // waves whose 16 rows all lie past the last row (the half-empty last block when rows % 128 = 64, e.g.
+  // waves whose rows all lie past the last row (the half-empty last block when rows % 128 = 64, e.g.
   // SigLIP's 576 patches) only stage and keep the barriers; their SIMD time goes to the co-resident block
-  const bool idle = r0 + wave * 16 >= a.rows;
+  const bool idle = wrow0 >= a.rows;
   for (int t = t_lo; t < t_hi; ++t) {
     const int buf = (t - t_lo) & (FA_NBUF - 1);
     vm_wait(ops * min(FA_NBUF - 2, t_hi - 1 - t));
@@ -179,71 +195,82 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     const char* vb = kb + R::TILE;
     const int* kvs = reinterpret_cast<const int*>(smem + R::KV_OFF + buf * (KT * 4));
 
-    // ---- S^T = K Q^T : s[ms] holds keys 16ms + 4g + j, query column c16
-    f32x4_t s[MS];
+    // ---- S^T = K Q^T : s[qg][ms] holds keys 16ms + 4g + j, query column c16 of group qg
+    f32x4_t s[QG][MS];
 #pragma unroll
     for (int ms = 0; ms < MS; ++ms) {
-      s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int qg = 0; qg < QG; ++qg) s[qg][ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
       const int row = ms * 16 + c16;
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
         const int ch = (ks * 4 + g) ^ swz_k<D>(row);
         const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + row * (D * 2) + ch * 16);
-        s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg)
+          s[qg][ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[qg][ks], s[qg][ms], 0, 0, 0);
       }
     }
     // ---- mask + online softmax.  Running max in raw score units; p = exp2(s*c - m*c) is one FMA and
     // one v_exp (c = scale*log2 e > 0 keeps the argmax).  A tile every key of which is visible to every
     // row of this wave (all keys valid, below the causal diagonal, inside the window) skips the mask.
-    float mt = -INFINITY;
     bool interior = (t + 1) * KT <= a.nkeys && (unmasked || ((!causal || t * KT + KT - 1 <= wpos_lo) &&
                                                              (nowin || t * KT > wpos_hi - a.window)));
     if (interior && kvl) interior = __all(lane >= KT || kvs[lane] != 0);
-    if (interior) {
+    bf16x8_t pf[QG][ST];
+    float alpha[QG];
+    bool rescale = false;
+#pragma unroll
+    for (int qg = 0; qg < QG; ++qg) {
+      float mt = -INFINITY;
+      if (interior) {
+#pragma unroll
+        for (int ms = 0; ms < MS; ++ms)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) mt = fmaxf(mt, s[qg][ms][j]);
+      } else {
+#pragma unroll
+        for (int ms = 0; ms < MS; ++ms) {
+          const int kbase = t * KT + ms * 16 + 4 * g;
+          int kv[4] = {1, 1, 1, 1};
+          if (kvl) {
+            const int4 v4 = *reinterpret_cast<const int4*>(kvs + ms * 16 + 4 * g);
+            kv[0] = v4.x; kv[1] = v4.y; kv[2] = v4.z; kv[3] = v4.w;
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int key = kbase + j;
+            const int ok = (int)(key < a.nkeys) & (int)(kv[j] != 0) & ((int)(key <= qpos[qg]) | !causal) &
+                           ((int)(key > qpos[qg] - a.window) | nowin);
+            const float v = ok ? s[qg][ms][j] : -INFINITY;
+            s[qg][ms][j] = v;
+            mt = fmaxf(mt, v);
+          }
+        }
+      }
+      mt = xor32_max(xor16_max(mt));
+      const float m_new = fmaxf(m_run[qg], mt);
+      alpha[qg] = (m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f((m_run[qg] - m_new) * sl2);
+      const float mc = (m_new == -INFINITY) ? 0.f : m_new * sl2;
+      float rs = 0.f;
 #pragma unroll
       for (int ms = 0; ms < MS; ++ms)
 #pragma unroll
-        for (int j = 0; j < 4; ++j) mt = fmaxf(mt, s[ms][j]);
-    } else {
-#pragma unroll
-      for (int ms = 0; ms < MS; ++ms) {
-        const int kbase = t * KT + ms * 16 + 4 * g;
-        int kv[4] = {1, 1, 1, 1};
-        if (kvl) {
-          const int4 v4 = *reinterpret_cast<const int4*>(kvs + ms * 16 + 4 * g);
-          kv[0] = v4.x; kv[1] = v4.y; kv[2] = v4.z; kv[3] = v4.w;
-        }
-#pragma unroll
         for (int j = 0; j < 4; ++j) {
-          const int key = kbase + j;
-          const int ok = (int)(key < a.nkeys) & (int)(kv[j] != 0) & ((int)(key <= qpos) | !causal) &
-                         ((int)(key > qpos - a.window) | nowin);
-          const float v = ok ? s[ms][j] : -INFINITY;
-          s[ms][j] = v;
-          mt = fmaxf(mt, v);
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[qg][ms][j], sl2, -mc));   // exp2(-inf) = 0 for masked keys
+          rs += p;   // fp32 row sum (P itself enters P.V in bf16)
+          pf[qg][ms >> 1][(ms & 1) * 4 + j] = (short)f2bf(p);
         }
-      }
+      rs = xor32_sum(xor16_sum(rs));
+      l_run[qg] = l_run[qg] * alpha[qg] + rs;
+      m_run[qg] = m_new;
+      rescale = rescale || alpha[qg] != 1.f;
     }
-    mt = xor32_max(xor16_max(mt));
-    const float m_new = fmaxf(m_run, mt);
-    const float alpha = (m_new == -INFINITY) ? 1.f : __builtin_amdgcn_exp2f((m_run - m_new) * sl2);
-    const float mc = (m_new == -INFINITY) ? 0.f : m_new * sl2;
-    float rs = 0.f;
-    bf16x8_t pf[ST];
+    if (__any(rescale)) {   // no row's running max moved: nothing to rescale (common after a few tiles)
 #pragma unroll
-    for (int ms = 0; ms < MS; ++ms)
+      for (int qg = 0; qg < QG; ++qg)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[ms][j], sl2, -mc));   // exp2(-inf) = 0 for masked keys
-        rs += p;   // fp32 row sum (P itself enters P.V in bf16)
-        pf[ms >> 1][(ms & 1) * 4 + j] = (short)f2bf(p);
-      }
-    rs = xor32_sum(xor16_sum(rs));
-    l_run = l_run * alpha + rs;
-    m_run = m_new;
-    if (__any(alpha != 1.f)) {   // no row's running max moved: nothing to rescale (common after a few tiles)
-#pragma unroll
-      for (int i = 0; i < DS; ++i) o[i] *= alpha;
+        for (int i = 0; i < DS; ++i) o[qg][i] *= alpha[qg];
     }
 
     // ---- O^T += V^T P^T : A = V^T (tr reads), k order of step st = {32st+4g+0..3, 32st+16+4g+0..3}
@@ -261,24 +288,30 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
           const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
           vf[4 * hh + 0] = r[0]; vf[4 * hh + 1] = r[1]; vf[4 * hh + 2] = r[2]; vf[4 * hh + 3] = r[3];
         }
-        o[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[st], o[ds], 0, 0, 0);
+#pragma unroll
+        for (int qg = 0; qg < QG; ++qg)
+          o[qg][ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[qg][st], o[qg][ds], 0, 0, 0);
       }
     }
   }
 
   // ---- epilogue: O[q][d] = O^T[d][q] / l ; lane holds d = 16ds + 4g + j for query c16
-  if (qrow >= a.rows) return;
-  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-  const long orow = map_row(a.omap, qrow);
-  bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + orow * a.ldo + 4 * g;
 #pragma unroll
-  for (int ds = 0; ds < DS; ++ds) {
-    u16x4_t u;
-    u[0] = f2bf(o[ds][0] * inv); u[1] = f2bf(o[ds][1] * inv);
-    u[2] = f2bf(o[ds][2] * inv); u[3] = f2bf(o[ds][3] * inv);
-    *reinterpret_cast<u16x4_t*>(op + 16 * ds) = u;
+  for (int qg = 0; qg < QG; ++qg) {
+    if (qrow[qg] >= a.rows) continue;
+    const float inv = l_run[qg] > 0.f ? 1.f / l_run[qg] : 0.f;
+    const long orow = map_row(a.omap, qrow[qg]);
+    bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + orow * a.ldo + 4 * g;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      u16x4_t u;
+      u[0] = f2bf(o[qg][ds][0] * inv); u[1] = f2bf(o[qg][ds][1] * inv);
+      u[2] = f2bf(o[qg][ds][2] * inv); u[3] = f2bf(o[qg][ds][3] * inv);
+      *reinterpret_cast<u16x4_t*>(op + 16 * ds) = u;
+    }
+    if (a.lse && g == 0)
+      a.lse[(long)z * a.rows + qrow[qg]] = (m_run[qg] * sl2 + log2f(l_run[qg])) * 0.6931471805599453f;
   }
-  if (a.lse && g == 0) a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_run)) * 0.6931471805599453f;
 }
 
 // ============================================================================ backward
@@ -1059,8 +1092,10 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
   if (nblk > 0x7fffffffL) return set_error("attn_fwd: too many blocks");
   dim3 grid((unsigned)nblk);
   switch (a.D) {
-    case 64: hipLaunchKernelGGL(attn_fwd_kernel<64>, grid, dim3(512), 0, st, a); break;
-    case 256: hipLaunchKernelGGL(attn_fwd_kernel<256>, grid, dim3(512), 0, st, a); break;
+    case 64: hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(512), 0, st, a); break;
+    // QG = 2 (256-row blocks) measured slower on the Gemma3 step: 352 blocks of double work on 256 CUs
+    // quantise worse than 704 (110 vs 78 us per layer), and it spills
+    case 256: hipLaunchKernelGGL((attn_fwd_kernel<256, 1>), grid, dim3(512), 0, st, a); break;
     default: return set_error("attn_fwd: head_dim %d unsupported (64, 256)", a.D);
   }
   return hipGetLastError() == hipSuccess ? 0 : set_error("attn_fwd launch failed");
