@@ -327,20 +327,33 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
 //   z-batch, so dK/dV sum over the group for free.
 template <int D>
 __global__ void __launch_bounds__(256) attn_delta_kernel(FlashBwdArgs a, int nz) {
-  constexpr int EPL = D / 64;
+  // DELTA_RPW rows per wave, every row's loads issued before the first reduction (latency-bound otherwise:
+  // one 512-B row pair per wave)
+  constexpr int EPL = D / 64, RPW = 4;
   const int lane = threadIdx.x & 63;
-  const long gr = (long)blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (gr >= (long)nz * a.rows) return;
-  const long z = gr / a.rows;
-  const int r = (int)(gr - z * a.rows);
-  const int z0 = (int)(z / a.zin), z1 = (int)(z - (long)z0 * a.zin);
-  const bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, r) * a.ldo + lane * EPL;
-  const bf16_t* dp = a.dO + gr * D + lane * EPL;
-  float s = 0.f;
+  const long gr0 = ((long)blockIdx.x * 4 + (threadIdx.x >> 6)) * RPW;
+  const long total = (long)nz * a.rows;
+  if (gr0 >= total) return;
+  bf16_t ov[RPW][EPL], dv[RPW][EPL];
 #pragma unroll
-  for (int e = 0; e < EPL; ++e) s += bf2f(op[e]) * bf2f(dp[e]);
-  s = warp_sum(s);
-  if (lane == 0) a.delta[gr] = s;
+  for (int i = 0; i < RPW; ++i) {
+    const long gr = min(gr0 + i, total - 1);
+    const long z = gr / a.rows;
+    const int r = (int)(gr - z * a.rows);
+    const int z0 = (int)(z / a.zin), z1 = (int)(z - (long)z0 * a.zin);
+    const bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, r) * a.ldo + lane * EPL;
+    const bf16_t* dp = a.dO + gr * D + lane * EPL;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) { ov[i][e] = op[e]; dv[i][e] = dp[e]; }
+  }
+#pragma unroll
+  for (int i = 0; i < RPW; ++i) {
+    float s = 0.f;
+#pragma unroll
+    for (int e = 0; e < EPL; ++e) s += bf2f(ov[i][e]) * bf2f(dv[i][e]);
+    s = warp_sum(s);
+    if (lane == 0 && gr0 + i < total) a.delta[gr0 + i] = s;
+  }
 }
 
 template <int D>
@@ -1047,7 +1060,7 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st) {
   if (a.rows % 64 || a.nkeys % 64) return set_error("attn_bwd: rows (%d) and keys (%d) must be multiples of 64",
                                                    a.rows, a.nkeys);
   if (a.ldo & 7) return set_error("attn_bwd: O stride must be a multiple of 8");
-  const dim3 gd((unsigned)((long)nz * a.rows / 4 + 1)), gq((unsigned)((long)((a.rows + 127) / 128) * nz)),
+  const dim3 gd((unsigned)(((long)nz * a.rows + 15) / 16)), gq((unsigned)((long)((a.rows + 127) / 128) * nz)),
       gk((unsigned)(a.nkeys / 64), (unsigned)nz);
   switch (a.D) {
     case 64:
