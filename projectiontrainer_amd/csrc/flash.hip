@@ -750,6 +750,8 @@ __global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel
   // staging: 32 rows x 32 16-B chunks per tensor = 16 wave-instructions (IPW per wave), plus the
   // chunk's LSE|delta (256 B) spread over all waves: OPS LDS-DMA ops per wave per chunk, so one
   // counted vmcnt serves every wave
+  const float* lse_base = a.lse;
+  const float* delta_base = a.delta;
   auto stage = [&](int c, int buf) {
     char* qb = smem + buf * 2 * TILE;
     char* ob = qb + TILE;
@@ -764,7 +766,11 @@ __global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel
     }
     if (lane < 16 / NW) {
       const int item = wave * (16 / NW) + lane;   // 0-7 LSE, 8-15 delta (4 floats each)
-      const float* srcv = (item < 8 ? a.lse : a.delta) + z * a.rows + c * DKV_CH + 4 * (item & 7);
+      // select between the two (uniform) base pointers arithmetically: a per-lane `? :` on the kernel
+      // argument fields compiles to a load of the pointer from the kernarg segment, whose vmcnt(0) wait
+      // drained the whole DMA ring every chunk
+      const long off = z * a.rows + c * DKV_CH + 4 * (item & 7);
+      const float* srcv = (item < 8 ? lse_base : delta_base) + off;
       fa_glds16(srcv, smem + NBUF * 2 * TILE + buf * 256 + wave * (256 / NW));
     }
   };
