@@ -169,7 +169,7 @@ def main():
                                f"{lm_name} frozen fwd/bwd, {cfg.num_vision_tokens} vis + {cfg.text_len} text tokens",
                    "global_batch": world * cfg.batch_size, "per_gpu_batch": cfg.batch_size,
                    "seq_len": cfg.seq_len, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "gemm_big_kernel<ACT_GEGLU> (Gemma3 gate|up projection: 2*(B*S)*(2I)*H FLOP per launch, "
+        "roofline": {"bound": "mfma", "kernel": "gemm_w4_kernel<ACT_GEGLU> (Gemma3 gate|up projection: 2*(B*S)*(2I)*H FLOP per launch, "
                                "last layer 2*(B*T)*(2I)*H)",
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,

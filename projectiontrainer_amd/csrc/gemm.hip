@@ -35,6 +35,14 @@ static_assert(4 * 64 * 68 * 4 >= 2 * STAGE_BYTES, "epilogue staging must cover t
 typedef const __attribute__((address_space(1))) void* gptr_t;
 typedef __attribute__((address_space(3))) void* lptr_t;
 
+// diagnostic: PTK_NO_SRC_SWZ builds stage the 256x256 kernels' tiles without the XOR source swizzle
+// (wrong results, timing only: does a lane-permuted DMA source cost issue time?)
+#ifdef PTK_NO_SRC_SWZ
+#define PTK_SRC_SWZ(c, r) (c)
+#else
+#define PTK_SRC_SWZ(c, r) ((c) ^ (((r) >> 1) & 7))
+#endif
+
 #ifndef PTK_GLDS_AUX
 #define PTK_GLDS_AUX 0   // cache-policy bits of the LDS-DMA staging loads (diagnostic builds vary it)
 #endif
@@ -314,7 +322,7 @@ __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int lr = wave * 16 + j * 8 + sr;               // row within the half-tile
-      const int lc = sc ^ ((lr >> 1) & 7);
+      const int lc = PTK_SRC_SWZ(sc, lr);
       if (h < 2) {
         const long gm = min((long)bm * BIG + h * 128 + lr, (long)p.M - 1);
         src[h][j] = A + map_row(p.amap, gm) * p.lda + lc * 8;
@@ -484,7 +492,7 @@ PTK_DEV void big2_kloop(const GemmArgs& p, char* smem, int bm, int bn, int k0, i
 #pragma unroll
     for (int j = 0; j < 2; ++j) {
       const int lr = wave * 16 + j * 8 + sr;               // row within the half-tile
-      const int lc = sc ^ ((lr >> 1) & 7);
+      const int lc = PTK_SRC_SWZ(sc, lr);
       if (h < 2) {
         const long gm = min((long)bm * BIG + h * 128 + lr, (long)p.M - 1);
         src[h][j] = A + map_row(p.amap, gm) * p.lda + lc * 8;
@@ -811,7 +819,16 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // epilogue with the other's MFMA and quantise better (tools/gemm_bench.py --all, r01).
   // long K: the barrier-staggered 256x256 variant (+6-7 % at K >= 4096, tools/gemm_bench.py --all)
   const bool big_shape = a.M >= 1024 && a.N >= 512 && (a.K >= 6144 || (a.N >= 6144 && a.K >= 1152));
-  if (batch == 1 && g_force_tiles == 8 && w4_supported(a, act, out)) {
+  // persistent 4-wave 256x256 kernel (gemm_w4.hip) where it measured ahead of the 8-wave kernels
+  // (tools/gemm_bench.py --all, same box): the GEGLU gate|up projection (+4 %), plain bf16 projections
+  // with N > 2048 at K <= 2048 (SigLIP qkv +3.5 %, Gemma dh +1.6 %) and N <= 2048 at K 4096..8192
+  // (Gemma down +2.4 %); not the vocab-wide lm_head, the N = 1152 fp32 K = 13824 d(gate|up) or the
+  // 128x128-quantised shapes
+  const bool w4_auto = g_force_tiles == 0 && a.M >= 8192 && a.N <= 16384 &&
+                       (act == ACT_GEGLU ||
+                        (act == ACT_NONE && out == OUT_BF16 &&
+                         ((a.N > 2048 && a.K <= 2048) || (a.N <= 2048 && a.K >= 4096 && a.K <= 8192))));
+  if (batch == 1 && (g_force_tiles == 8 || w4_auto) && w4_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);

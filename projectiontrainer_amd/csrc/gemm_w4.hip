@@ -303,9 +303,8 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
       if (first) W4_GROUP(FA, FB, q, true); else W4_GROUP(FA, FB, q, false);
     }
   };
-  // k-step 2kt+1 (ks 1): the 16 LDS-DMA pieces of K-tile g+2 go out two per group in the first half
-  // (latency slack until the next K-tile's barrier), the 16 reads of the next K-tile's ks 0 one per
-  // group in groups 0..7 and two per group in groups 8..11
+  // k-step 2kt+1 (ks 1): the 16 LDS-DMA pieces of K-tile g+2 go out one per group, the 16 reads of
+  // the next K-tile's ks 0 one per group in groups 0..7 and two per group in groups 8..11
   auto step_b = [&](const bf16x8_t (&FA)[8], const bf16x8_t (&FB)[8], bf16x8_t (&NA)[8], bf16x8_t (&NB)[8],
                     uint32_t ba, uint32_t bb, int buf) {
     const uint32_t da = lds0 + buf * W4_BUF, db = da + W4_OPB;
@@ -317,10 +316,11 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
 #if PTK_W4_ABLATE != 1
-      if (q < 8) {
-        W4_DMA(rsa, offa[q], sa, da + q * 1024);
-        W4_DMA(rsb, offb[q], sb, db + q * 1024);
-      }
+      // one LDS-DMA piece per group of 4 MFMAs: a piece's issue cost (tens of cycles) fits in the MFMA
+      // gaps; two per group in the first half (the former schedule) left the SIMD stalled on issue
+      // (+6-7 % at 8192^3 and the step's K = 1152 shapes)
+      if (q & 1) W4_DMA(rsb, offb[q >> 1], sb, db + (q >> 1) * 1024);
+      else W4_DMA(rsa, offa[q >> 1], sa, da + (q >> 1) * 1024);
 #endif
 #if PTK_W4_ABLATE != 2
       if (q < 8) {

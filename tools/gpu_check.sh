@@ -25,8 +25,8 @@ for step in "$@"; do
     benchfull) run benchfull 900 python bench.py ;;
     gemmbench) run gemmbench 300 python tools/gemm_bench.py ;;
     prof)    run prof 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 5 --warmup 2 --no-cpu-baseline ;;
-    pmcfetch) run pmcfetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --kernel-include-regex "gemm_big_kernel<3" --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
-    pmcwrite) run pmcwrite 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --kernel-include-regex "gemm_big_kernel<3" --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcfetch) run pmcfetch 600 rocprofv3 --kernel-trace --pmc FETCH_SIZE --kernel-include-regex "gemm_(big|w4)_kernel<3" --output-format csv -d gpurun_out/pmc_fetch -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcwrite) run pmcwrite 600 rocprofv3 --kernel-trace --pmc WRITE_SIZE --kernel-include-regex "gemm_(big|w4)_kernel<3" --output-format csv -d gpurun_out/pmc_write -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     counters) run counters 120 rocprofv3 -L ;;
     pmcdkv) run pmcdkv 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU --kernel-include-regex "dkv256" --output-format csv -d gpurun_out/pmc_dkv -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
