@@ -9,16 +9,15 @@
 // epilogue (128 KiB of stores per CU, staged through LDS in gemm_big_kernel) cost as much as a
 // third of the main loop.  Here
 //   * one wave per SIMD software-pipelines its own LDS reads: the 16 ds_read_b128 fragments of
-//     k-step s+1 are issued while the 64 MFMAs of k-step s run; one barrier per 64-deep K-tile;
-//   * the global->LDS stream (buffer_load ... lds, 16 per wave per K-tile, OOB rows read as zero)
-//     runs two K-tiles ahead and continues straight into the workgroup's NEXT tile, so the next
-//     tile's first K-tiles land while this tile's epilogue runs;
+//     k-step s+1 are issued while the 64 MFMAs of k-step s run;
+//   * LDS is a ring of five 32-deep k-step slots (160 KiB); the global->LDS stream (buffer_load ...
+//     lds, 8 pieces per wave per k-step, one every 8 MFMAs, OOB rows read as zero) runs four
+//     k-steps ahead and continues straight into the workgroup's NEXT tile, so the next tile's first
+//     k-steps land while this tile's epilogue runs; one wait + barrier per pair of k-steps;
 //   * the epilogue stores straight from the accumulators: the MFMA operands are swapped (C^T
 //     orientation) so each lane holds 4 consecutive columns of one row, and one
 //     v_permlane16_swap per dword pairs two 16-column MFMA tiles into 8 consecutive columns, i.e.
-//     one 16-B store per lane (no LDS staging, no barrier);
-//   * every store the epilogue must make is issued unconditionally (invalid rows go to a sink),
-//     so the next tile's first wait can leave exactly that many stores in flight (vmcnt(NST)).
+//     one 16-B store per lane (no LDS staging, no barrier); invalid rows store to a sink.
 // Tiles are dealt round-robin over the persistent workgroups; the workgroups that share an XCD
 // (b % 8) take consecutive tiles of the grouped (GROUP_M = 8) order, so a round's A row panels and
 // B column panels are shared through that XCD's L2.
@@ -27,6 +26,7 @@
 #include "gemm_epi.h"
 
 #include <algorithm>
+#include <type_traits>
 
 #ifndef PTK_W4_ABLATE
 #define PTK_W4_ABLATE 0   // diagnostic builds only: 1 = no DMA in the K loop, 2 = no fragment reads,
@@ -38,9 +38,11 @@ namespace ptk {
 
 namespace {
 constexpr int W4 = 256;                  // output tile edge
-constexpr int W4_KT = 64;                // K-tile depth
-constexpr int W4_OPB = W4 * W4_KT * 2;   // one operand's K-tile image: 256 rows x 128 B = 32 KiB
-constexpr int W4_BUF = 2 * W4_OPB;       // A + B per pipeline buffer
+constexpr int W4_KT = 64;                // K granularity of the path (a pair of k-steps per barrier)
+constexpr int W4_KS = 32;                // k-step depth: one MFMA 16x16x32 deep, one ring slot
+constexpr int W4_SOPB = W4 * W4_KS * 2;  // one operand's k-step image: 256 rows x 64 B = 16 KiB
+constexpr int W4_SLOT = 2 * W4_SOPB;     // A + B per ring slot
+constexpr int W4_NSLOT = 5;              // ring depth: 5 x 32 KiB = the CU's 160 KiB of LDS
 constexpr uint32_t W4_OOB = 0x80000000u; // voffset beyond every buffer's num_records -> zeros
 typedef __attribute__((address_space(3))) void* lds_ptr_t;
 
@@ -96,14 +98,6 @@ PTK_DEV void w4_epi8(const GemmArgs& p, long r, long c_, float* v, char* sink) {
     *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
   }
-}
-
-// unconditional stores per wave per tile (the vmcnt the next tile's first wait leaves in flight)
-template <int ACT, int OUT>
-constexpr int w4_nstore() {
-  if (ACT == ACT_GEGLU) return 16;
-  if (ACT == ACT_GEGLU_BWD) return 63;   // 64, capped at the 6-bit vmcnt field (a smaller count is safe)
-  return OUT == OUT_BF16 ? 32 : 63;
 }
 
 // row block I of the wave's tile: lane holds C[row0 + 16I + (lane&15)][col0 + 16j + 4(lane>>4) + e]
@@ -203,7 +197,7 @@ PTK_DEV uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_ptr_
 
 template <int ACT, int OUT>
 __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * W4_BUF];   // 128 KiB: two K-tile buffers
+  __shared__ __attribute__((aligned(16))) char smem[W4_NSLOT * W4_SLOT];   // 160 KiB: the k-step ring
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wr = wave >> 1, wc = wave & 1;
@@ -216,29 +210,32 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
     loc = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
   }
   if (loc >= ntile) return;
-  const int nt = p.K / W4_KT;
-  const int total_kt = ((ntile - loc + G - 1) / G) * nt;
+  const int nt = p.K / W4_KT;                              // 64-deep K-tiles per output tile
+  const int nks = 2 * nt;                                  // 32-deep k-steps per output tile
+  const int total_ks = ((ntile - loc + G - 1) / G) * nks;
 
   // A rows past M / B rows past N fall outside num_records and read as zero
   const u32x4_t rsa = w4_rsrc(p.A, a_bytes), rsb = w4_rsrc(p.B, b_bytes);
 
-  // ---- global -> LDS stream.  Lane i of DMA piece j writes LDS row wave*64 + 8j + (i>>3), 16-B
-  // chunk i&7, fetching logical chunk (i&7) ^ ((row>>1)&7) (XOR swizzle on the source address, LDS
-  // image lane-linear) so the fragment reads are bank-conflict free.  The per-lane part of the
-  // source offset is fixed; the tile's row panel and the K-tile go into the scalar offset.
-  uint32_t offa[8], offb[8];
+  // ---- global -> LDS stream, one ring slot (32 KiB: A and B, 256 rows x 64 B each) per k-step.
+  // Wave w fills rows 64w..64w+63 of both operands: 4 + 4 pieces of 16 rows x 64 B.  Lane i of a
+  // piece writes LDS row 16j + (i>>2), 16-B chunk i&3 (LDS image lane-linear) and fetches logical
+  // chunk (i&3) ^ ((row>>1)&2): the XOR swizzle on the source address makes the fragment reads
+  // bank-conflict free (every ds_read_b128 lane group covers the 64 banks once).
+  uint32_t offa[4], offb[4];
 #pragma unroll
-  for (int j = 0; j < 8; ++j) {
-    const int lr = wave * 64 + 8 * j + (lane >> 3);
-    const int lc = (lane & 7) ^ ((lr >> 1) & 7);
+  for (int j = 0; j < 4; ++j) {
+    const int lr = wave * 64 + 16 * j + (lane >> 2);
+    const int lc = (lane & 3) ^ ((lane >> 3) & 2);
     offa[j] = (uint32_t)lr * (uint32_t)p.lda * 2u + lc * 16;
     offb[j] = (uint32_t)lr * (uint32_t)p.ldb * 2u + lc * 16;
   }
-  const uint32_t lds0 = __builtin_amdgcn_readfirstlane(lds_addr(smem)) + wave * 64 * 128;
-  // DMA cursor: tile dt, K-tile dkt, scalar offsets of its row panels.  Past the workgroup's last
-  // K-tile the cursor stays put and the stream re-loads that K-tile into the free buffer (never
-  // read), so every k-step issues the same instructions.
-  int dt = loc, dkt = 0, dcount = 0;
+  const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem));
+  const uint32_t lds_dma = lds_base + wave * 64 * 64;      // this wave's rows in a slot
+  // DMA cursor: tile dt, k-step dks, scalar offsets of its row panels.  Past the workgroup's last
+  // k-step the cursor stays put and the stream re-loads that k-step into a free slot (never read),
+  // so every k-step issues the same instructions.
+  int dt = loc, dks = 0, dcount = 0;
   uint32_t dsa = 0, dsb = 0;
   auto dma_tile = [&](int t) {
     int bm, bn;
@@ -247,20 +244,21 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
     dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * W4) * (uint32_t)p.ldb * 2u);
   };
   auto dma_advance = [&]() {
-    if (++dcount < total_kt) {
-      if (++dkt == nt) {
-        dkt = 0;
+    if (++dcount < total_ks) {
+      if (++dks == nks) {
+        dks = 0;
         dt += G;
         dma_tile(dt);
       }
     }
   };
+  auto slot_next = [](uint32_t s) { s += W4_SLOT; return s == W4_NSLOT * W4_SLOT ? 0u : s; };
 
-  // ---- fragments: A rows wr*128 + 16i + (lane&15), B rows wc*128 + 16j + (lane&15); logical
-  // 16-B chunk 4ks + (lane>>4) of the 128-B row
-  const int frag_off = (lane & 15) * 128 + (((lane >> 4) ^ ((lane >> 1) & 7)) << 4);
-  const uint32_t frag_a = lds_addr(smem) + wr * 128 * 128 + frag_off;            // buffer 0, ks 0
-  const uint32_t frag_b = lds_addr(smem) + W4_OPB + wc * 128 * 128 + frag_off;
+  // ---- fragments: A rows wr*128 + 16i + (lane&15), B rows wc*128 + 16j + (lane&15); logical 16-B
+  // chunk lane>>4 of the slot's 64-B row
+  const int frag_off = (lane & 15) * 64 + (((lane >> 4) ^ ((lane >> 1) & 2)) << 4);
+  const uint32_t frag_a = lds_addr(smem) + wr * 128 * 64 + frag_off;
+  const uint32_t frag_b = lds_addr(smem) + W4_SOPB + wc * 128 * 64 + frag_off;
   bf16x8_t fa0[8], fb0[8], fa1[8], fb1[8];
   f32x4_t acc[8][8];
 
@@ -275,8 +273,8 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 // fragment read q (0..15) of the next k-step: q < 8 -> A row block q, else B column block q-8
 #define W4_READ(FA, FB, BA, BB, Q)                                                  \
   do {                                                                              \
-    if ((Q) < 8) W4_DSREAD(FA[(Q) & 7], BA, ((Q) & 7) * 2048);                      \
-    else W4_DSREAD(FB[(Q) & 7], BB, ((Q) & 7) * 2048);                              \
+    if ((Q) < 8) W4_DSREAD(FA[(Q) & 7], BA, ((Q) & 7) * 1024);                      \
+    else W4_DSREAD(FB[(Q) & 7], BB, ((Q) & 7) * 1024);                              \
   } while (0)
 // every destination of the last 16 reads is pinned after the wait (no copy before the data lands)
 #define W4_PIN(FA, FB)                                                                              \
@@ -288,40 +286,25 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
                  "+v"(FB[6]), "+v"(FB[7]));                                                         \
   } while (0)
 
-  // k-step 2kt (ks 0): 16 groups of 4 MFMAs on FA/FB; the 16 reads of (kt, ks 1) go out two per group
-  // in the first half, so they have landed when the step ends (its lgkmcnt(0) costs nothing)
-  auto step_a = [&](const bf16x8_t (&FA)[8], const bf16x8_t (&FB)[8], bf16x8_t (&NA)[8], bf16x8_t (&NB)[8],
-                    uint32_t ba, uint32_t bb, bool first) {
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-#if PTK_W4_ABLATE != 2
-      if (q < 8) {
-        W4_READ(NA, NB, ba, bb, 2 * q);
-        W4_READ(NA, NB, ba, bb, 2 * q + 1);
-      }
-#endif
-      if (first) W4_GROUP(FA, FB, q, true); else W4_GROUP(FA, FB, q, false);
-    }
-  };
-  // k-step 2kt+1 (ks 1): the 16 LDS-DMA pieces of K-tile g+2 go out one per group, the 16 reads of
-  // the next K-tile's ks 0 one per group in groups 0..7 and two per group in groups 8..11
-  auto step_b = [&](const bf16x8_t (&FA)[8], const bf16x8_t (&FB)[8], bf16x8_t (&NA)[8], bf16x8_t (&NB)[8],
-                    uint32_t ba, uint32_t bb, int buf) {
-    const uint32_t da = lds0 + buf * W4_BUF, db = da + W4_OPB;
+  // one k-step: 16 groups of 4 MFMAs on FA/FB; the 16 fragment reads of the next k-step (slot rs,
+  // published by the last barrier) one per group in groups 0..7 and two per group in groups 8..11;
+  // the 8 LDS-DMA pieces of k-step +4 (slot ws) one every other group, i.e. one per 8 MFMAs: a
+  // piece's issue cost (tens of cycles) is paid in MFMA time by a lone wave per SIMD and grows with
+  // the density of memory instructions around it
+  // (FIRST: the tile's first k-step, accumulators initialised by the MFMA; a compile-time constant
+  // so that no branch sits between the MFMA groups)
+  auto kstep = [&](auto first_c, const bf16x8_t (&FA)[8], const bf16x8_t (&FB)[8], bf16x8_t (&NA)[8],
+                   bf16x8_t (&NB)[8], uint32_t rs, uint32_t ws) {
+    constexpr bool first = decltype(first_c)::value;
+    const uint32_t ba = frag_a + rs, bb = frag_b + rs;
+    const uint32_t da = lds_dma + ws, db = da + W4_SOPB;
 #if PTK_W4_ABLATE == 3
-    const uint32_t sa = dsa, sb = dsb;   // always K-tile 0 of the tile: L2-resident (timing only)
+    const uint32_t sa = dsa, sb = dsb;   // always k-step 0 of the tile: L2-resident (timing only)
 #else
-    const uint32_t sa = dsa + dkt * (W4_KT * 2), sb = dsb + dkt * (W4_KT * 2);
+    const uint32_t sa = dsa + dks * (W4_KS * 2), sb = dsb + dks * (W4_KS * 2);
 #endif
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-#if PTK_W4_ABLATE != 1
-      // one LDS-DMA piece per group of 4 MFMAs: a piece's issue cost (tens of cycles) fits in the MFMA
-      // gaps; two per group in the first half (the former schedule) left the SIMD stalled on issue
-      // (+6-7 % at 8192^3 and the step's K = 1152 shapes)
-      if (q & 1) W4_DMA(rsb, offb[q >> 1], sb, db + (q >> 1) * 1024);
-      else W4_DMA(rsa, offa[q >> 1], sa, da + (q >> 1) * 1024);
-#endif
 #if PTK_W4_ABLATE != 2
       if (q < 8) {
         W4_READ(NA, NB, ba, bb, q);
@@ -330,50 +313,65 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
         W4_READ(NA, NB, ba, bb, 9 + 2 * (q - 8));
       }
 #endif
-      W4_GROUP(FA, FB, q, false);
+#if PTK_W4_ABLATE != 1
+      if (q & 1) {
+        const int pc = q >> 1;   // pieces A0 B0 A1 B1 ...
+        if (pc & 1) W4_DMA(rsb, offb[pc >> 1], sb, db + (pc >> 1) * 1024);
+        else W4_DMA(rsa, offa[pc >> 1], sa, da + (pc >> 1) * 1024);
+      }
+#endif
+      W4_GROUP(FA, FB, q, first);
     }
   };
 
-  // ---- prologue: K-tiles 0 and 1, fragments of k-step 0
+  // ---- prologue: k-steps 0..3 into slots 0..3; 0..2 landed and published, fragments of k-step 0
+  // read, then a second barrier: k-step 1 overwrites slot 0 (ring invariant below)
   dma_tile(dt);
 #pragma unroll
-  for (int b = 0; b < 2; ++b) {
-    const uint32_t da = lds0 + b * W4_BUF, db = da + W4_OPB;
-    const uint32_t sa = dsa + dkt * (W4_KT * 2), sb = dsb + dkt * (W4_KT * 2);
+  for (int b = 0; b < 4; ++b) {
+    const uint32_t da = lds_dma + b * W4_SLOT, db = da + W4_SOPB;
+    const uint32_t sa = dsa + dks * (W4_KS * 2), sb = dsb + dks * (W4_KS * 2);
 #pragma unroll
-    for (int j = 0; j < 8; ++j) {
+    for (int j = 0; j < 4; ++j) {
       W4_DMA(rsa, offa[j], sa, da + j * 1024);
       W4_DMA(rsb, offb[j], sb, db + j * 1024);
     }
     dma_advance();
   }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
   __builtin_amdgcn_s_barrier();
 #pragma unroll
   for (int q = 0; q < 16; ++q) W4_READ(fa0, fb0, frag_a, frag_b, q);
   W4_PIN(fa0, fb0);
+  __builtin_amdgcn_s_barrier();
 
-  constexpr int NST = w4_nstore<ACT, OUT>();
+  // ring invariant at k-step i (i counts over the workgroup's whole stream): fragments of i are in
+  // registers; k-steps i+1 and (if i is even) i+2 have landed and are published; k-step i+3 is in
+  // flight; k-step i+4 goes to slot (i+4) % 5, whose last reader (the fragment reads of k-step i-1,
+  // done during k-step i-2) precedes the barrier that ends the last odd k-step <= i-1.  One wait +
+  // barrier per pair of k-steps (after the odd one) publishes k-steps i+2 and i+3: vmcnt(8) leaves
+  // only k-step i+4's 8 pieces in flight.  The epilogue's stores follow the barrier; the next wait
+  // (two k-steps later) drains them too.
+  uint32_t rs = W4_SLOT, ws = 4 * W4_SLOT;
   int t = loc, kt = 0;
-  for (int g = 0; g < total_kt; ++g) {
-    const int buf = g & 1;
-    step_a(fa0, fb0, fa1, fb1, (frag_a + buf * W4_BUF) ^ 64, (frag_b + buf * W4_BUF) ^ 64, kt == 0);
+  for (int g = 0; g < total_ks; g += 2) {
+    if (kt == 0) kstep(std::true_type{}, fa0, fb0, fa1, fb1, rs, ws);
+    else kstep(std::false_type{}, fa0, fb0, fa1, fb1, rs, ws);
     W4_PIN(fa1, fb1);
-    // K-tile g+1 must have landed (own DMA, then everyone's via the barrier); after the barrier
-    // every read of buffer g&1 is done, so K-tile g+2 may overwrite it
+    dma_advance();
+    rs = slot_next(rs);
+    ws = slot_next(ws);
+    kstep(std::false_type{}, fa1, fb1, fa0, fb0, rs, ws);
+    W4_PIN(fa0, fb0);
+    dma_advance();
+    rs = slot_next(rs);
+    ws = slot_next(ws);
 #if PTK_W4_ABLATE != 5
-    if (kt == 0) {
-      asm volatile("s_waitcnt vmcnt(%0)" :: "n"(NST) : "memory");   // previous tile's stores may fly
-    } else {
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 #endif
 #if PTK_W4_ABLATE != 4
     __builtin_amdgcn_s_barrier();
 #endif
-    step_b(fa1, fb1, fa0, fb0, frag_a + (buf ^ 1) * W4_BUF, frag_b + (buf ^ 1) * W4_BUF, buf);
-    W4_PIN(fa0, fb0);
-    dma_advance();
     if (kt == nt - 1) {
       asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");   // MFMA D -> accumulator read wait states
       int bm, bn;
