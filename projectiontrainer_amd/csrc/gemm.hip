@@ -819,15 +819,16 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // epilogue with the other's MFMA and quantise better (tools/gemm_bench.py --all, r01).
   // long K: the barrier-staggered 256x256 variant (+6-7 % at K >= 4096, tools/gemm_bench.py --all)
   const bool big_shape = a.M >= 1024 && a.N >= 512 && (a.K >= 6144 || (a.N >= 6144 && a.K >= 1152));
-  // persistent 4-wave 256x256 kernel (gemm_w4.hip) where it measured ahead of the 8-wave kernels
-  // (tools/gemm_bench.py --all, same box): the GEGLU gate|up projection (+4 %), plain bf16 projections
-  // with N > 2048 at K <= 2048 (SigLIP qkv +3.5 %, Gemma dh +1.6 %) and N <= 2048 at K 4096..8192
-  // (Gemma down +2.4 %); not the vocab-wide lm_head, the N = 1152 fp32 K = 13824 d(gate|up) or the
-  // 128x128-quantised shapes
-  const bool w4_auto = g_force_tiles == 0 && a.M >= 8192 && a.N <= 16384 &&
+  // persistent 4-wave 256x256 kernel (gemm_w4.hip) where it measured ahead of the 8-wave and
+  // 128x128 kernels (tools/gemm_bench.py --all, same box, r01): the GEGLU gate|up projection, and
+  // plain projections (bf16 or fp32 out, K <= 8192) whose 256x256 tiles fill >= 80 % of the
+  // persistent grid's rounds (SigLIP qkv +4 %, Gemma o +6 %, dh +17 %, down +3 %, dqkv +2 %).  Not the
+  // N = 1024 / 1536 shapes (352 / 528 tiles: 69 % round fill, the 128x128 kernel wins), the
+  // vocab-wide lm_head, the K = 11520 / 13824 projections or the GELU epilogues
+  const bool w4_auto = g_force_tiles == 0 && a.M >= 4096 && a.N <= 16384 &&
                        (act == ACT_GEGLU ||
-                        (act == ACT_NONE && out == OUT_BF16 &&
-                         ((a.N > 2048 && a.K <= 2048) || (a.N <= 2048 && a.K >= 4096 && a.K <= 8192))));
+                        (act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32) && a.K <= 8192 &&
+                         w4_round_fill(a.M, a.N) >= 0.8));
   if (batch == 1 && (g_force_tiles == 8 || w4_auto) && w4_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }

@@ -28,6 +28,12 @@
 #include <algorithm>
 #include <type_traits>
 
+#ifndef PTK_W4_RDS
+#define PTK_W4_RDS 0      // diagnostic builds: fragment-read placement in the k-step (1 = two per group, groups 0..7)
+#endif
+#ifndef PTK_W4_DMS
+#define PTK_W4_DMS 0      // diagnostic builds: DMA placement (1 = groups 8..15, 2 = groups 0..7, 3 = odd groups)
+#endif
 #ifndef PTK_W4_ABLATE
 #define PTK_W4_ABLATE 0   // diagnostic builds only: 1 = no DMA in the K loop, 2 = no fragment reads,
                           // 3 = the DMA re-reads one L2-resident K-tile, 4 = no K-loop barrier,
@@ -288,7 +294,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 
   // one k-step: 16 groups of 4 MFMAs on FA/FB; the 16 fragment reads of the next k-step (slot rs,
   // published by the last barrier) one per group in groups 0..7 and two per group in groups 8..11;
-  // the 8 LDS-DMA pieces of k-step +4 (slot ws) one every other group, i.e. one per 8 MFMAs: a
+  // the 8 LDS-DMA pieces of k-step +4 (slot ws) in the even groups, i.e. one per 8 MFMAs: a
   // piece's issue cost (tens of cycles) is paid in MFMA time by a lone wave per SIMD and grows with
   // the density of memory instructions around it
   // (FIRST: the tile's first k-step, accumulators initialised by the MFMA; a compile-time constant
@@ -306,6 +312,12 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
 #if PTK_W4_ABLATE != 2
+#if PTK_W4_RDS == 1
+      if (q < 8) {
+        W4_READ(NA, NB, ba, bb, 2 * q);
+        W4_READ(NA, NB, ba, bb, 2 * q + 1);
+      }
+#else
       if (q < 8) {
         W4_READ(NA, NB, ba, bb, q);
       } else if (q < 12) {
@@ -313,9 +325,21 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
         W4_READ(NA, NB, ba, bb, 9 + 2 * (q - 8));
       }
 #endif
+#endif
 #if PTK_W4_ABLATE != 1
+#if PTK_W4_DMS == 1
+      if (q >= 8) {
+        const int pc = q - 8;
+#elif PTK_W4_DMS == 2
+      if (q < 8) {
+        const int pc = q;
+#elif PTK_W4_DMS == 3
       if (q & 1) {
-        const int pc = q >> 1;   // pieces A0 B0 A1 B1 ...
+        const int pc = q >> 1;
+#else
+      if (!(q & 1)) {
+        const int pc = q >> 1;   // pieces A0 B0 A1 B1 ... in groups 0, 2, .., 14
+#endif
         if (pc & 1) W4_DMA(rsb, offb[pc >> 1], sb, db + (pc >> 1) * 1024);
         else W4_DMA(rsa, offa[pc >> 1], sa, da + (pc >> 1) * 1024);
       }
@@ -411,13 +435,24 @@ bool w4_supported(const GemmArgs& a, int act, int out) {
 
 static int g_num_cu = 0;
 
-int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid) {
+static int num_cu() {
   if (!g_num_cu) {
-    int dev = 0;
+    int dev = 0, n = 0;
     if (hipGetDevice(&dev) != hipSuccess ||
-        hipDeviceGetAttribute(&g_num_cu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || g_num_cu <= 0)
-      g_num_cu = 256;
+        hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || n <= 0)
+      n = 256;
+    g_num_cu = n;
   }
+  return g_num_cu;
+}
+
+double w4_round_fill(long M, long N) {
+  const long ntile = ((M + W4 - 1) / W4) * ((N + W4 - 1) / W4), cu = num_cu();
+  return (double)ntile / (double)(((ntile + cu - 1) / cu) * cu);
+}
+
+int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid) {
+  num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   long grid = std::min<long>(ntile, max_grid > 0 ? max_grid : g_num_cu);
   const long arows = a.M + a.amap.off;

@@ -55,6 +55,8 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
 // persistent 256x256 4-wave GEMM (gemm_w4.hip): batch 1 only; w4_supported says whether a shape qualifies
 bool w4_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid);
+// fraction of the persistent grid's tile rounds that hold work: ntile / (ceil(ntile / CUs) * CUs)
+double w4_round_fill(long M, long N);
 // live GEMM timing per activation class (events recorded around each launch when enabled)
 void timer_enable(int on);
 void force_small_tiles(int mode);
