@@ -91,16 +91,21 @@ PTK_DEV float block_max(float v, float* red) {
 
 // GELU variants (TF/activations.py: gelu_pytorch_tanh; torch nn.GELU default = erf)
 // 0.5 * (1 + tanh(u)) == sigmoid(2u): one exp + one reciprocal instead of tanhf
+// x * sigmoid(2u) = 0.5 x (1 + tanh(u)) with one v_exp_f32 and one v_rcp_f32 (hipcc lowers
+// __fdividef to the IEEE division sequence, 8 instructions: the GEGLU epilogue's largest cost)
+PTK_DEV float fast_sigmoid2(float u) {   // 1 / (1 + e^(-2u)); e^(-2u) -> inf gives 0, -> 0 gives 1
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u * -2.8853900817779268f));
+}
 PTK_DEV float gelu_tanh(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float u = k0 * (x + k1 * x * x * x);
-  return __fdividef(x, 1.f + __expf(-2.f * u));
+  return x * fast_sigmoid2(u);
 }
 PTK_DEV float gelu_tanh_grad(float x) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float x2 = x * x;
   const float u = k0 * (x + k1 * x2 * x);
-  const float s = __fdividef(1.f, 1.f + __expf(-2.f * u));
+  const float s = fast_sigmoid2(u);
   return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x2);
 }
 PTK_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
