@@ -826,7 +826,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // N = 1024 / 1536 shapes (352 / 528 tiles: 69 % round fill, the 128x128 kernel wins), the
   // vocab-wide lm_head, the K = 11520 / 13824 projections or the GELU epilogues
   const bool w4_auto = g_force_tiles == 0 && a.M >= 4096 && a.N <= 16384 &&
-                       (act == ACT_GEGLU ||
+                       (act == ACT_GEGLU || act == ACT_GEGLU_BWD ||
                         (act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32) && a.K <= 8192 &&
                          w4_round_fill(a.M, a.N) >= 0.8));
   if (batch == 1 && (g_force_tiles == 8 || w4_auto) && w4_supported(a, act, out)) {

@@ -153,9 +153,76 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, i
   }
 }
 
+// GEGLU backward (GEMM output = dh [M, I]; writes dg, du into the interleaved [M, 2I] layout, as
+// geglu_bwd_kernel does): the saved g and u of row block I, 8 columns per lane and column pair pp,
+// loaded one row block ahead of their use so their latency runs under the previous block's math
+template <int I>
+PTK_DEV void w4_gbwd_load(const GemmArgs& p, long row0, long col0, int lane, u16x8_t (&G)[4], u16x8_t (&U)[4]) {
+  const int q = lane >> 4;
+  const int cb = 16 * (q & 1) + 8 * (q >> 1);
+  const long r = row0 + 16 * I + (lane & 15);
+  const long rl = r < p.M ? r : 0;
+#pragma unroll
+  for (int pp = 0; pp < 4; ++pp) {
+    const long c = col0 + 32 * pp + cb;
+    const long cl = c < p.N ? c : 0;
+    G[pp] = *reinterpret_cast<const u16x8_t*>(p.aux_in + rl * p.ld_aux_in + cl);
+    U[pp] = *reinterpret_cast<const u16x8_t*>(p.aux_in2 + rl * p.ld_aux_in + cl);
+  }
+}
+template <int I>
+PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, int lane, char* sink,
+                          const u16x8_t (&G)[4], const u16x8_t (&U)[4]) {
+#pragma unroll
+  for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
+  const int q = lane >> 4;
+  const int cb = 16 * (q & 1) + 8 * (q >> 1);
+  const long r = row0 + 16 * I + (lane & 15);
+#pragma unroll
+  for (int pp = 0; pp < 4; ++pp) {
+    f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
+    swap16(x, y);
+    const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+    float dg[8], du[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float d = bfround(v[e]), g = bf2f(G[pp][e]), u = bf2f(U[pp][e]);
+      dg[e] = bfround(d * u) * gelu_tanh_grad(g);
+      du[e] = d * bfround(gelu_tanh(g));
+    }
+    const long c = col0 + 32 * pp + cb;
+    const bool rv = r < p.M && c < p.N;
+    const long cr = rv ? map_row32(p.cmap, (int)r) : -1;
+    bf16_t* o = cr >= 0 ? reinterpret_cast<bf16_t*>(p.C) + cr * p.ldc + (c >> 4) * 32 + (c & 15)
+                        : reinterpret_cast<bf16_t*>(sink);
+    stbf8(o, dg);
+    stbf8(o + 16, du);
+  }
+}
+
 template <int ACT, int OUT>
 PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][8], long row0, long col0, int lane) {
   char* sink = g_w4_sink + lane * 64;
+  if constexpr (ACT == ACT_GEGLU_BWD) {
+    u16x8_t G0[4], U0[4], G1[4], U1[4];
+    w4_gbwd_load<0>(p, row0, col0, lane, G0, U0);
+    w4_gbwd_load<1>(p, row0, col0, lane, G1, U1);
+    w4_gbwd_rows<0>(p, acc[0], row0, col0, lane, sink, G0, U0);
+    w4_gbwd_load<2>(p, row0, col0, lane, G0, U0);
+    w4_gbwd_rows<1>(p, acc[1], row0, col0, lane, sink, G1, U1);
+    w4_gbwd_load<3>(p, row0, col0, lane, G1, U1);
+    w4_gbwd_rows<2>(p, acc[2], row0, col0, lane, sink, G0, U0);
+    w4_gbwd_load<4>(p, row0, col0, lane, G0, U0);
+    w4_gbwd_rows<3>(p, acc[3], row0, col0, lane, sink, G1, U1);
+    w4_gbwd_load<5>(p, row0, col0, lane, G1, U1);
+    w4_gbwd_rows<4>(p, acc[4], row0, col0, lane, sink, G0, U0);
+    w4_gbwd_load<6>(p, row0, col0, lane, G0, U0);
+    w4_gbwd_rows<5>(p, acc[5], row0, col0, lane, sink, G1, U1);
+    w4_gbwd_load<7>(p, row0, col0, lane, G1, U1);
+    w4_gbwd_rows<6>(p, acc[6], row0, col0, lane, sink, G0, U0);
+    w4_gbwd_rows<7>(p, acc[7], row0, col0, lane, sink, G1, U1);
+    return;
+  }
   w4_rows<ACT, OUT, 0>(p, acc[0], row0, col0, lane, sink);
   w4_rows<ACT, OUT, 1>(p, acc[1], row0, col0, lane, sink);
   w4_rows<ACT, OUT, 2>(p, acc[2], row0, col0, lane, sink);
@@ -425,7 +492,7 @@ bool w4_supported(const GemmArgs& a, int act, int out) {
        (uintptr_t)a.aux2 | (uintptr_t)a.aux_in | (uintptr_t)a.aux_in2) & 15)
     return false;
   if (act == ACT_GEGLU && (a.N % 32)) return false;
-  if (act == ACT_GEGLU_BWD) return false;   // the streaming geglu_bwd pass after a plain GEMM is faster
+  if (act == ACT_GEGLU_BWD && (!a.aux_in || !a.aux_in2 || (a.N % 16) || (a.ldc % 8))) return false;
   if (act == ACT_GELU_ERF_BWD && !a.aux_in) return false;
   if (out != OUT_BF16 && (act != ACT_NONE)) return false;
   if (a.amap.g != 0) return false;   // gathered A rows: not an affine row panel
@@ -470,6 +537,7 @@ int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_
   PTK_W4_CASE(ACT_GELU_ERF, OUT_BF16)
   PTK_W4_CASE(ACT_GEGLU, OUT_BF16)
   PTK_W4_CASE(ACT_GELU_ERF_BWD, OUT_BF16)
+  PTK_W4_CASE(ACT_GEGLU_BWD, OUT_BF16)
 #undef PTK_W4_CASE
   return set_error("gemm_w4: unsupported (act=%d, out=%d)", act, out);
 }

@@ -12,6 +12,7 @@
 //   Q [B,Hkv,S,G,D] (rows (s,j) contiguous), K/V [B,Hkv,S,D], scores/P
 //   [B*Hkv, S*G, S].  QK^T and P.V run on the MFMA GEMM; masks/softmax are
 //   row kernels.
+#include <cstdlib>
 #include <algorithm>
 #include <math.h>
 #include <string.h>
@@ -53,6 +54,11 @@ constexpr int LM_SPLITK = 8;   // split-K for the vocab-long lm_head dX GEMM (R 
   do {        \
     if ((x)) return -1; \
   } while (0)
+
+static bool geglu_split() {
+  static const int v = [] { const char* e = getenv("PTK_GEGLU_SPLIT"); return e && e[0] == '1' ? 1 : 0; }();
+  return v != 0;
+}
 
 GemmArgs gemm(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K) {
   GemmArgs g;
@@ -357,11 +363,20 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
     // post-ff norm backward: for layers below the last it ran fused into the previous iteration's
     // input-norm backward (one pass over dR instead of two)
     if (l == nl - 1) CK(launch_post_norm_bwd(dR, sv.dn, L.ln_post_ff, sv.rstd_dn, w.dao, M, H, st));
-    // dh = dd . Wd (plain GEMM at full MFMA rate), then the GEGLU backward as one streaming pass (measured:
-    // the same step time as the GEGLU backward fused into this GEMM's epilogue, which reads g, u per tile)
+    // d(gate|up) = GEGLU backward of dh = dd . Wd, fused into the persistent 4-wave GEMM's register
+    // epilogue (g, u loaded one row block ahead; dh never reaches HBM).  PTK_GEGLU_SPLIT=1: the plain
+    // GEMM + one streaming geglu_bwd pass instead (A/B)
     if (l + 1 < nl) {
-      CK(launch_gemm(gemm(w.dao, H, L.wd_t, H, w.h, I, M, I, H), ACT_NONE, OUT_BF16, 1, st));
-      CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, M, I, st));
+      if (geglu_split()) {
+        CK(launch_gemm(gemm(w.dao, H, L.wd_t, H, w.h, I, M, I, H), ACT_NONE, OUT_BF16, 1, st));
+        CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, M, I, st));
+      } else {
+        GemmArgs g = gemm(w.dao, H, L.wd_t, H, w.dgu, 2 * I, M, I, H);
+        g.aux_in = sv.g;
+        g.aux_in2 = sv.u;
+        g.ld_aux_in = I;
+        CK(launch_gemm(g, ACT_GEGLU_BWD, OUT_BF16, 1, st));
+      }
       CK(launch_gemm(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), ACT_NONE, OUT_F32, 1, st));
     } else {   // last layer: MLP gradient is non-zero on the loss rows only (compact h, g, u, dgu)
       GemmArgs g = gemm(w.dao, H, L.wd_t, H, w.h, I, R, I, H);
