@@ -96,17 +96,33 @@ PTK_DEV float block_max(float v, float* red) {
 PTK_DEV float fast_sigmoid2(float u) {   // 1 / (1 + e^(-2u)); e^(-2u) -> inf gives 0, -> 0 gives 1
   return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(u * -2.8853900817779268f));
 }
-PTK_DEV float gelu_tanh(float x) {
-  const float k0 = 0.7978845608028654f, k1 = 0.044715f;
-  const float u = k0 * (x + k1 * x * x * x);
-  return x * fast_sigmoid2(u);
+PTK_DEV float gelu_tanh_arg(float x, float x2) {   // u = k0 (x + k1 x^3), one evaluation order everywhere
+  return 0.7978845608028654f * (x + 0.044715f * x2 * x);
 }
-PTK_DEV float gelu_tanh_grad(float x) {
+PTK_DEV float gelu_tanh(float x) { return x * fast_sigmoid2(gelu_tanh_arg(x, x * x)); }
+// two lanes of gelu_tanh with packed f32 math (v_pk_mul / v_pk_fma: half the VALU issue of the scalar
+// form; for epilogues, where no MFMA of the wave runs beside them)
+typedef __attribute__((ext_vector_type(2))) float f32x2_t;
+PTK_DEV f32x2_t gelu_tanh2(f32x2_t x) {
+  const f32x2_t u = 0.7978845608028654f * (x + 0.044715f * (x * x) * x);
+  const f32x2_t a = u * -2.8853900817779268f;
+  f32x2_t s;
+  s.x = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(a.x));
+  s.y = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(a.y));
+  return x * s;
+}
+// gelu_tanh and its derivative from one exp / rcp pair (the GEGLU backward needs both)
+PTK_DEV void gelu_tanh_fg(float x, float& f, float& df) {
   const float k0 = 0.7978845608028654f, k1 = 0.044715f;
   const float x2 = x * x;
-  const float u = k0 * (x + k1 * x2 * x);
-  const float s = fast_sigmoid2(u);
-  return s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x2);
+  const float s = fast_sigmoid2(gelu_tanh_arg(x, x2));
+  f = x * s;
+  df = s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x2);
+}
+PTK_DEV float gelu_tanh_grad(float x) {
+  float f, df;
+  gelu_tanh_fg(x, f, df);
+  return df;
 }
 PTK_DEV float gelu_erf(float x) { return 0.5f * x * (1.f + erff(x * 0.7071067811865476f)); }
 PTK_DEV float gelu_erf_grad(float x) {

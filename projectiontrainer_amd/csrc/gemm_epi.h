@@ -199,8 +199,10 @@ PTK_DEV void geglu_bwd_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
     const float d = bfround(el(dh, e));
-    el(dg, e) = bfround(d * el(u, e)) * gelu_tanh_grad(el(g, e));
-    el(du, e) = d * bfround(gelu_tanh(el(g, e)));
+    float f, df;
+    gelu_tanh_fg(el(g, e), f, df);
+    el(dg, e) = bfround(d * el(u, e)) * df;
+    el(du, e) = d * bfround(f);
   }
   const long cr = map_row(p.cmap, r);
   if (cr < 0) return;
@@ -218,8 +220,10 @@ PTK_DEV void geglu_bwd_vec8(const GemmArgs& p, char* Cz, long r, long c, const f
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     const float d = bfround(dh[e]);
-    dg[e] = bfround(d * u[e]) * gelu_tanh_grad(g[e]);
-    du[e] = d * bfround(gelu_tanh(g[e]));
+    float f, df;
+    gelu_tanh_fg(g[e], f, df);
+    dg[e] = bfround(d * u[e]) * df;
+    du[e] = d * bfround(f);
   }
   const long cr = map_row(p.cmap, r);
   if (cr < 0) return;

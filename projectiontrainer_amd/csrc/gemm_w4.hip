@@ -129,10 +129,15 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, i
       float u[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
       float h[8];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) {
+      for (int e = 0; e < 8; e += 2) {
         g[e] = bfround(g[e]);
+        g[e + 1] = bfround(g[e + 1]);
         u[e] = bfround(u[e]);
-        h[e] = bfround(gelu_tanh(g[e])) * u[e];
+        u[e + 1] = bfround(u[e + 1]);
+        const f32x2_t gl = gelu_tanh2(f32x2_t{g[e], g[e + 1]});
+        const f32x2_t hh = f32x2_t{bfround(gl.x), bfround(gl.y)} * f32x2_t{u[e], u[e + 1]};
+        h[e] = hh.x;
+        h[e + 1] = hh.y;
       }
       const long hc = col0 / 2 + 32 * pp + cb;
       const bool rv = r < p.M && 2 * hc < p.N;
@@ -187,8 +192,10 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long co
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const float d = bfround(v[e]), g = bf2f(G[pp][e]), u = bf2f(U[pp][e]);
-      dg[e] = bfround(d * u) * gelu_tanh_grad(g);
-      du[e] = d * bfround(gelu_tanh(g));
+      float f, df;
+      gelu_tanh_fg(g, f, df);
+      dg[e] = bfround(d * u) * df;
+      du[e] = d * bfround(f);
     }
     const long c = col0 + 32 * pp + cb;
     const bool rv = r < p.M && c < p.N;

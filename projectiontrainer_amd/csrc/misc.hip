@@ -407,8 +407,10 @@ __global__ void __launch_bounds__(256) geglu_bwd_kernel(const bf16_t* __restrict
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     const float d = bf2f(vd[k]), gg = bf2f(vg[k]), uu = bf2f(vu[k]);
-    og[k] = f2bf(bfround(d * uu) * gelu_tanh_grad(gg));
-    ou[k] = f2bf(d * bfround(gelu_tanh(gg)));
+    float f, df;
+    gelu_tanh_fg(gg, f, df);
+    og[k] = f2bf(bfround(d * uu) * df);
+    ou[k] = f2bf(d * bfround(f));
   }
   bf16_t* o = dgu + r * 2L * I + (c >> 4) * 32 + (c & 15);
   *reinterpret_cast<u16x8_t*>(o) = og;
