@@ -68,39 +68,67 @@ PTK_DEV void add8(float* v, const float* s) {
   v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
 }
 
-// 8 consecutive columns [c, c+8) of row r (c % 8 == 0, c < N); rows r >= M and unmapped rows
-// store into the sink so the store count per wave is fixed
+// per-lane row state of one row block, computed once for its four 8-column groups: the row's
+// validity, its clamped index and the element offsets of its rows in C (after the row map), the
+// residual and the side inputs / outputs (the 64-bit products and the row-map division stay out of
+// the per-store path)
+struct W4Row {
+  bool rv;          // r < M
+  bool cv;          // r < M and mapped (C row exists)
+  long ro_aux;      // rl * ld_aux
+  long ro_auxin;    // rl * ld_aux_in
+  long ro_rowadd;   // (rl % rowadd_period) * ld_rowadd
+  long ro_c;        // cr * ldc
+  long ro_resid;    // cr * ld_resid
+};
+PTK_DEV W4Row w4_row(const GemmArgs& p, long r) {
+  W4Row w;
+  w.rv = r < p.M;
+  const long rl = w.rv ? r : 0;
+  const long cr = w.rv ? map_row32(p.cmap, (int)r) : -1;
+  w.cv = cr >= 0;
+  const long crl = w.cv ? cr : 0;
+  w.ro_aux = rl * p.ld_aux;
+  w.ro_auxin = rl * p.ld_aux_in;
+  w.ro_rowadd = p.rowadd ? (long)((unsigned)rl % (unsigned)p.rowadd_period) * p.ld_rowadd : 0;
+  w.ro_c = crl * p.ldc;
+  w.ro_resid = crl * p.ld_resid;
+  return w;
+}
+
+// 8 consecutive columns [c, c+8) of one row (c % 8 == 0); rows r >= M, unmapped rows and columns
+// c >= N store into the sink
 template <int ACT, int OUT>
-PTK_DEV void w4_epi8(const GemmArgs& p, long r, long c_, float* v, char* sink) {
-  const bool rv = r < p.M && c_ < p.N;     // N % 8 == 0: c < N covers all 8 columns
-  const long rl = rv ? r : 0, c = rv ? c_ : 0;
+PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char* sink) {
+  const bool cin = c_ < p.N;                // N % 8 == 0: c < N covers all 8 columns
+  const bool rv = w.rv && cin, sv = w.cv && cin;
+  const long c = cin ? c_ : 0;
   if (p.bias) add8(v, p.bias + c);
-  if (p.rowadd) add8(v, p.rowadd + (long)((unsigned)rl % (unsigned)p.rowadd_period) * p.ld_rowadd + c);
+  if (p.rowadd) add8(v, p.rowadd + w.ro_rowadd + c);
   if constexpr (ACT == ACT_GELU_TANH) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(bfround(v[e]));
   } else if constexpr (ACT == ACT_GELU_ERF) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]);
-    if (p.aux) stbf8(rv ? p.aux + r * p.ld_aux + c : reinterpret_cast<bf16_t*>(sink), v);
+    if (p.aux) stbf8(rv ? p.aux + w.ro_aux + c : reinterpret_cast<bf16_t*>(sink), v);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = gelu_erf(v[e]);
   } else if constexpr (ACT == ACT_GELU_ERF_BWD) {
     float a[8];
-    ldbf8(p.aux_in + rl * p.ld_aux_in + c, a);
+    ldbf8(p.aux_in + w.ro_auxin + c, a);
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]) * gelu_erf_grad(a[e]);
   }
-  const long cr = rv ? map_row32(p.cmap, (int)r) : -1;
-  if (p.resid) add8(v, p.resid + (cr >= 0 ? cr : 0) * p.ld_resid + c);
+  if (p.resid) add8(v, p.resid + w.ro_resid + c);
   if constexpr (OUT == OUT_BF16) {
-    stbf8(cr >= 0 ? reinterpret_cast<bf16_t*>(p.C) + cr * p.ldc + c : reinterpret_cast<bf16_t*>(sink), v);
+    stbf8(sv ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + c : reinterpret_cast<bf16_t*>(sink), v);
   } else {
     if constexpr (OUT == OUT_F32_BFR) {
 #pragma unroll
       for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]);
     }
-    float* d = cr >= 0 ? reinterpret_cast<float*>(p.C) + cr * p.ldc + c : reinterpret_cast<float*>(sink);
+    float* d = sv ? reinterpret_cast<float*>(p.C) + w.ro_c + c : reinterpret_cast<float*>(sink);
     *reinterpret_cast<float4*>(d) = make_float4(v[0], v[1], v[2], v[3]);
     *reinterpret_cast<float4*>(d + 4) = make_float4(v[4], v[5], v[6], v[7]);
   }
@@ -117,6 +145,7 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, i
   const int cb = 16 * (q & 1) + 8 * (q >> 1);
   const long r = row0 + 16 * I + (lane & 15);
   if constexpr (ACT == ACT_GEGLU) {
+    const W4Row w = w4_row(p, r);
     // GEMM columns: 16-wide gate / up groups alternate (interleaved weights); tiles 4pp, 4pp+2 are
     // gate and 4pp+1, 4pp+3 up for h columns [col0/2 + 32pp, +32)
 #pragma unroll
@@ -140,20 +169,21 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, i
         h[e + 1] = hh.y;
       }
       const long hc = col0 / 2 + 32 * pp + cb;
-      const bool rv = r < p.M && 2 * hc < p.N;
+      const bool cin = 2 * hc < p.N;
+      const bool rv = w.rv && cin, sv = w.cv && cin;
       bf16_t* sk = reinterpret_cast<bf16_t*>(sink);
-      if (p.aux) stbf8(rv ? p.aux + r * p.ld_aux + hc : sk, g);
-      if (p.aux2) stbf8(rv ? p.aux2 + r * p.ld_aux + hc : sk, u);
-      const long cr = rv ? map_row32(p.cmap, (int)r) : -1;
-      stbf8(cr >= 0 ? reinterpret_cast<bf16_t*>(p.C) + cr * p.ldc + hc : sk, h);
+      if (p.aux) stbf8(rv ? p.aux + w.ro_aux + hc : sk, g);
+      if (p.aux2) stbf8(rv ? p.aux2 + w.ro_aux + hc : sk, u);
+      stbf8(sv ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + hc : sk, h);
     }
   } else {
+    const W4Row w = w4_row(p, r);
 #pragma unroll
     for (int pp = 0; pp < 4; ++pp) {
       f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
       swap16(x, y);
       float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-      w4_epi8<ACT, OUT>(p, r, col0 + 32 * pp + cb, v, sink);
+      w4_epi8<ACT, OUT>(p, w, col0 + 32 * pp + cb, v, sink);
     }
   }
 }
@@ -183,6 +213,7 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long co
   const int q = lane >> 4;
   const int cb = 16 * (q & 1) + 8 * (q >> 1);
   const long r = row0 + 16 * I + (lane & 15);
+  const W4Row w = w4_row(p, r);
 #pragma unroll
   for (int pp = 0; pp < 4; ++pp) {
     f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
@@ -198,10 +229,8 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long co
       du[e] = d * bfround(f);
     }
     const long c = col0 + 32 * pp + cb;
-    const bool rv = r < p.M && c < p.N;
-    const long cr = rv ? map_row32(p.cmap, (int)r) : -1;
-    bf16_t* o = cr >= 0 ? reinterpret_cast<bf16_t*>(p.C) + cr * p.ldc + (c >> 4) * 32 + (c & 15)
-                        : reinterpret_cast<bf16_t*>(sink);
+    bf16_t* o = w.cv && c < p.N ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + (c >> 4) * 32 + (c & 15)
+                                : reinterpret_cast<bf16_t*>(sink);
     stbf8(o, dg);
     stbf8(o + 16, du);
   }
