@@ -92,7 +92,7 @@ __global__ void __launch_bounds__(256) qknorm_rope_bwd_kernel(
     const bf16_t* __restrict__ qkv, const float* __restrict__ qw, const float* __restrict__ kw,
     const float* __restrict__ cos_t, const float* __restrict__ sin_t, AttnShape sh, const float* __restrict__ rstd_q,
     const float* __restrict__ rstd_k, const bf16_t* __restrict__ dQ, const bf16_t* __restrict__ dK,
-    const bf16_t* __restrict__ dV, bf16_t* __restrict__ dqkv) {
+    const bf16_t* __restrict__ dV, bf16_t* __restrict__ dqkv, FlashBwdArgs fb) {
   constexpr int D = EPL * 64;
   const int lane = threadIdx.x & 63;
   const int nh = sh.Hq + 2 * sh.Hkv;
@@ -100,6 +100,19 @@ __global__ void __launch_bounds__(256) qknorm_rope_bwd_kernel(
   if (m >= (long)sh.B * sh.S) return;
   const int b = (int)(m / sh.S), s = (int)(m - (long)b * sh.S);
   const int G = sh.Hq / sh.Hkv;
+  // deferred dK/dV reduce (D = 256 split slabs): this token's key row still lives as fp32 partials;
+  // sum them in piece order and round exactly like attn_dkv_reduce_kernel (bit-identical)
+  const float* dkv_src = nullptr;
+  int dkv_np = 0;
+  if (D == 256 && fb.dkv_deferred) {
+    const int slab = s / DKV_KEYS;
+    const int P = dkv_pieces(fb, slab);
+    if (P > 1) {
+      dkv_np = P;
+      dkv_src = fb.dkv_part + (long)dkv_part_base(fb, slab) * fb.nz * (2L * DKV_KEYS * D) +
+                (long)(s - slab * DKV_KEYS) * D + lane * EPL;
+    }
+  }
   const int fi = (lane & 31) * EPL;
   float cs[EPL], sn[EPL], wq[EPL], wk[EPL];
 #pragma unroll
@@ -133,8 +146,26 @@ __global__ void __launch_bounds__(256) qknorm_rope_bwd_kernel(
         dy = dV + (((long)b * sh.Hkv + (h - sh.Hq - sh.Hkv)) * sh.S + s) * D + lane * EPL;
         rsv[i] = 0.f;
       }
+      if (dkv_np > 0 && h >= sh.Hq) {
+        const int which = h < sh.Hq + sh.Hkv ? 0 : 1;   // 0 = dK, 1 = dV
+        const int kvh = which == 0 ? h - sh.Hq : h - sh.Hq - sh.Hkv;
+        const long z = (long)b * sh.Hkv + kvh;
+        const float* src = dkv_src + z * (2L * DKV_KEYS * D) + (long)which * DKV_KEYS * D;
+        const long pstride = (long)fb.nz * (2L * DKV_KEYS * D);
+        float acc[EPL];
 #pragma unroll
-      for (int e = 0; e < EPL; ++e) gy[i][e] = dy[e];
+        for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
+        for (int pc = 0; pc < dkv_np; ++pc) {
+#pragma unroll
+          for (int e = 0; e < EPL; ++e) acc[e] += src[pc * pstride + e];
+        }
+        const float mul = which == 0 ? fb.scale : 1.f;
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) gy[i][e] = f2bf(acc[e] * mul);
+      } else {
+#pragma unroll
+        for (int e = 0; e < EPL; ++e) gy[i][e] = dy[e];
+      }
       if (h < sh.Hq + sh.Hkv)
 #pragma unroll
         for (int e = 0; e < EPL; ++e) xr[i][e] = xrow[(long)h * D + e];
@@ -284,11 +315,19 @@ int launch_qknorm_rope_fwd(const bf16_t* qkv, const float* qw, const float* kw, 
 }
 int launch_qknorm_rope_bwd(const bf16_t* qkv, const float* qw, const float* kw, const float* cos_t,
                            const float* sin_t, AttnShape s, const float* rstd_q, const float* rstd_k,
-                           const bf16_t* dQ, const bf16_t* dK, const bf16_t* dV, bf16_t* dqkv, hipStream_t st) {
+                           const bf16_t* dQ, const bf16_t* dK, const bf16_t* dV, bf16_t* dqkv, hipStream_t st,
+                           const FlashBwdArgs* dkv) {
   if (s.Hq % s.Hkv) return set_error("qknorm_rope: Hq %% Hkv != 0");
+  FlashBwdArgs fb;
+  fb.dkv_deferred = 0;
+  if (dkv && dkv->dkv_deferred) {
+    if (s.D != 256 || dkv->D != 256 || dkv->nkeys != s.S || dkv->nz != s.B * s.Hkv || !dkv->dkv_part)
+      return set_error("qknorm_rope_bwd: deferred dK/dV plan does not match the shape");
+    fb = *dkv;
+  }
   const long waves = (long)s.B * s.S;   // one wave per token
   dim3 grid((unsigned)((waves + 3) / 4));
-  QKR_DISPATCH(qknorm_rope_bwd_kernel, qkv, qw, kw, cos_t, sin_t, s, rstd_q, rstd_k, dQ, dK, dV, dqkv)
+  QKR_DISPATCH(qknorm_rope_bwd_kernel, qkv, qw, kw, cos_t, sin_t, s, rstd_q, rstd_k, dQ, dK, dV, dqkv, fb)
   return hipGetLastError() == hipSuccess ? 0 : set_error("qknorm_rope_bwd launch failed");
 }
 int launch_softmax_fwd(const float* S, bf16_t* P, int nz, int rows, int cols, long ld, MaskSpec m, hipStream_t st) {

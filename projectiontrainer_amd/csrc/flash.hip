@@ -669,23 +669,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
 // into query pieces (~equal chunks); pieces of a split slab write fp32 partials that
 // attn_dkv_reduce_kernel sums in piece order (deterministic).  Blocks are ordered slab-major,
 // heaviest slabs first.
-constexpr int DKV_KEYS = 128, DKV_CH = 32;
-
-__host__ __device__ inline void dkv_slab_chunks(const FlashBwdArgs& a, int s, int& c_lo, int& c_hi) {
-  int r_lo = 0, r_hi = a.rows;
-  if (a.causal) {
-    r_lo = min(a.rows, s * DKV_KEYS * a.qdiv);
-    if (a.window > 0) r_hi = min(a.rows, (s * DKV_KEYS + DKV_KEYS + a.window - 1) * a.qdiv);
-  }
-  c_lo = r_lo / DKV_CH;
-  c_hi = max(c_lo, (r_hi + DKV_CH - 1) / DKV_CH);
-}
-__host__ __device__ inline int dkv_pieces(const FlashBwdArgs& a, int s) {
-  int lo, hi;
-  dkv_slab_chunks(a, s, lo, hi);
-  const int n = hi - lo;
-  return (a.dkv_target <= 0 || n <= a.dkv_target) ? 1 : (n + a.dkv_target - 1) / a.dkv_target;
-}
+// (DKV_KEYS, DKV_CH, dkv_slab_chunks, dkv_pieces, dkv_part_base: ptk_internal.h — qknorm_rope_bwd
+// sums the partials itself when the reduce is deferred)
 
 template <int KPW>   // keys per wave: 32 (4 waves, one per SIMD) or 16 (8 waves, two per SIMD)
 __global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel(FlashBwdArgs a) {
@@ -1061,7 +1046,11 @@ size_t attn_bwd_workspace_bytes(const FlashBwdArgs& a0, int nz) {
   return (size_t)ns * nz * 2 * DKV_KEYS * 256 * sizeof(float);
 }
 
-int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st) {
+int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs* defer) {
+  if (defer) {
+    *defer = a;
+    defer->dkv_deferred = 0;
+  }
   if (a.rows <= 0 || nz <= 0) return 0;
   if (a.rows % 64 || a.nkeys % 64) return set_error("attn_bwd: rows (%d) and keys (%d) must be multiples of 64",
                                                    a.rows, a.nkeys);
@@ -1091,7 +1080,10 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st) {
       // 32 keys per wave (one wave per SIMD) measured 209 us vs 252 us for 16 keys per wave (two per
       // SIMD, which spills the precomputed transposed-read addresses) at cfg2
       hipLaunchKernelGGL(attn_bwd_dkv256_kernel<32>, dim3((unsigned)(np * nz)), dim3(256), 0, st, b);
-      if (ns > 0)
+      if (ns > 0 && defer) {
+        *defer = b;
+        defer->dkv_deferred = 1;
+      } else if (ns > 0)
         hipLaunchKernelGGL(attn_dkv_reduce_kernel, dim3((unsigned)((nz * 2L * DKV_KEYS * 64 + 255) / 256), (unsigned)nslab),
                            dim3(256), 0, st, b);
       hipLaunchKernelGGL(attn_bwd_dq_kernel<256>, gq, dim3(512), 0, st, b);

@@ -59,6 +59,12 @@ static bool geglu_split() {
   static const int v = [] { const char* e = getenv("PTK_GEGLU_SPLIT"); return e && e[0] == '1' ? 1 : 0; }();
   return v != 0;
 }
+// PTK_DKV_REDUCE_SPLIT=1: separate attn_dkv_reduce_kernel pass (A/B) instead of summing the split-slab
+// dK/dV partials inside qknorm_rope_bwd
+static bool dkv_reduce_split() {
+  static const int v = [] { const char* e = getenv("PTK_DKV_REDUCE_SPLIT"); return e && e[0] == '1' ? 1 : 0; }();
+  return v != 0;
+}
 
 GemmArgs gemm(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K) {
   GemmArgs g;
@@ -396,6 +402,8 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
       g.cmap = RowMap{Sp, 0, (long)Hkv * Sp, 0};
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, Hkv, st));
     }
+    FlashBwdArgs dkv_plan;   // split-slab dK/dV partials finished by qknorm_rope_bwd
+    dkv_plan.dkv_deferred = 0;
     {  // flash attention backward: delta = rowsum(dO*O), dK/dV per key block, dQ per query block
       FlashBwdArgs fb;
       fb.Q = sv.Q; fb.K = sv.K; fb.V = sv.V; fb.O = sv.O; fb.dO = w.dO; fb.lse = sv.lse; fb.delta = w.delta;
@@ -408,10 +416,10 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
       fb.key_valid = w.key_valid;
       fb.scale = scale;
       fb.dkv_part = w.dkv_part; fb.dkv_part_bytes = w.dkv_part_bytes;
-      CK(launch_attn_bwd(fb, Z, st));
+      CK(launch_attn_bwd(fb, Z, st, dkv_reduce_split() ? nullptr : &dkv_plan));
     }
     CK(launch_qknorm_rope_bwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, sv.rstd_q, sv.rstd_k, w.dQ, w.dK, w.dV, w.dqkv,
-                              st));
+                              st, &dkv_plan));
     CK(launch_gemm(gemm(w.dqkv, Dqkv, L.wqkv_t, Dqkv, w.dtmp, H, M, H, Dqkv), ACT_NONE, OUT_F32, 1, st));
     if (l > 0) {
       // dR += rms_bwd(x_l, ln_in, dtmp), then layer l-1's post-ff norm backward on the new dR -> dao

@@ -100,7 +100,7 @@ int launch_qknorm_rope_fwd(const bf16_t* qkv, const float* qw, const float* kw, 
 int launch_qknorm_rope_bwd(const bf16_t* qkv, const float* qw, const float* kw, const float* cos_t,
                            const float* sin_t, AttnShape s, const float* rstd_q, const float* rstd_k,
                            const bf16_t* dQ, const bf16_t* dK, const bf16_t* dV, bf16_t* dqkv,
-                           hipStream_t st);
+                           hipStream_t st, const struct FlashBwdArgs* dkv = nullptr);
 // masked softmax over score rows: P = softmax(S) (bf16), masked entries 0.
 struct MaskSpec {
   int rows_per_batch;   // score rows per z
@@ -163,8 +163,42 @@ struct FlashBwdArgs {
   // b / nz for z = b % nz
   int dkv_items = 0;
   unsigned char dkv_item_slab[128], dkv_item_piece[128];
+  // set in the plan launch_attn_bwd hands back through `defer`: 1 = split slabs still hold fp32
+  // partials in dkv_part and the consumer (qknorm_rope_bwd) sums them instead of attn_dkv_reduce_kernel
+  int dkv_deferred = 0;
 };
-int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st);
+
+// dK/dV key slabs (flash.hip): slab s covers keys [s*DKV_KEYS, s*DKV_KEYS + DKV_KEYS), its query rows
+// are walked in DKV_CH-row chunks; a slab of more than dkv_target chunks is cut into pieces
+constexpr int DKV_KEYS = 128, DKV_CH = 32;
+__host__ __device__ inline void dkv_slab_chunks(const FlashBwdArgs& a, int s, int& c_lo, int& c_hi) {
+  int r_lo = 0, r_hi = a.rows;
+  if (a.causal) {
+    r_lo = min(a.rows, s * DKV_KEYS * a.qdiv);
+    if (a.window > 0) r_hi = min(a.rows, (s * DKV_KEYS + DKV_KEYS + a.window - 1) * a.qdiv);
+  }
+  c_lo = r_lo / DKV_CH;
+  c_hi = max(c_lo, (r_hi + DKV_CH - 1) / DKV_CH);
+}
+__host__ __device__ inline int dkv_pieces(const FlashBwdArgs& a, int s) {
+  int lo, hi;
+  dkv_slab_chunks(a, s, lo, hi);
+  const int n = hi - lo;
+  return (a.dkv_target <= 0 || n <= a.dkv_target) ? 1 : (n + a.dkv_target - 1) / a.dkv_target;
+}
+// first partial slot of slab s (slots are numbered slab-major over the split slabs)
+__host__ __device__ inline int dkv_part_base(const FlashBwdArgs& a, int s) {
+  int base = 0;
+  for (int t = 0; t < s; ++t) {
+    const int pt = dkv_pieces(a, t);
+    if (pt > 1) base += pt;
+  }
+  return base;
+}
+
+// defer != null: the D = 256 split-slab reduce is not launched; *defer receives the plan (with
+// dkv_deferred set when partials are pending) for launch_qknorm_rope_bwd to finish dK/dV
+int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs* defer = nullptr);
 // bytes of dkv_part for which launch_attn_bwd splits every heavy key slab (0 when it never splits)
 size_t attn_bwd_workspace_bytes(const FlashBwdArgs& a, int nz);
 
