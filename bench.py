@@ -2,8 +2,11 @@
 
     python bench.py [--gpus N] [--steps K] [--warmup W] [--config cfg2] [--no-cpu-baseline]
 
-N>1 runs as one process per GPU under torch.distributed.run (RCCL); batches are
-sharded (bs 32 per GPU, weak scaling) and the projector grads are all-reduced.
+N>1 runs as one process per GPU (RCCL): under `torch.distributed.run` the
+launcher's WORLD_SIZE must equal N; without a launcher bench.py starts
+`torch.distributed.run --nproc-per-node N` itself as a child process (before
+anything touches the GPU) and exits with its status.  Batches are sharded
+(bs 32 per GPU, weak scaling) and the projector grads are all-reduced.
 A step = SigLIP-L/16-384 fwd + projector fwd/bwd + Gemma3-1B fwd/loss/bwd +
 grad all-reduce + clip + AdamW, on synthetic device-resident inputs and
 random-init weights of the named architectures (no checkpoints offline).
@@ -14,30 +17,125 @@ from __future__ import annotations
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
-
-import numpy as np
-import torch
-import torch.distributed as dist
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
-from projectiontrainer_amd import _lib as L  # noqa: E402
-from projectiontrainer_amd import weights as W  # noqa: E402
-from projectiontrainer_amd.config import PRESETS  # noqa: E402
-from projectiontrainer_amd.flops import flops_per_image, geglu_step_flops  # noqa: E402
-from projectiontrainer_amd.stage1 import Stage1Engine  # noqa: E402
-
 MFMA_BF16_PEAK_TFLOPS = 2500.0   # MI355X dense bf16 (MI355X_MICROARCH.md, chip table)
 
 
-def cpu_baseline(cfg_name: str, seconds_budget: float = 30.0):
-    """The oracle (pure-torch fp32 CPU restatement, pinned to the reference's
-    fixtures) timed on this host: one step at the workload's shapes, bs 2."""
+def _args(argv=None):
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=None,
+                    help="GPUs (one process each); default: the launcher's WORLD_SIZE, else 1")
+    ap.add_argument("--steps", type=int, default=10)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--config", default="cfg2")
+    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
+    ap.add_argument("--text-len", type=int, default=None, help="text tokens T (default: the config's)")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-baseline-only", action="store_true",
+                    help="time only the CPU baseline (no GPU) and print it")
+    ap.add_argument("--prefetch", action="store_true",
+                    help="overlap the next step's SigLIP forward with this step's Gemma3 on a side stream")
+    ap.add_argument("--launch-check", action="store_true",
+                    help="launcher plumbing only: every rank joins a gloo group, rank 0 prints the world; no GPU")
+    return ap.parse_args(argv)
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _launch_or_check(args, argv):
+    """N ranks for --gpus N.  Runs before torch is imported, so no GPU has been touched: a child
+    `torch.distributed.run` is started (never exec'd over this process) and its status returned.
+    Returns None when this process is itself the (only or launched) rank."""
+    env_world = os.environ.get("WORLD_SIZE")
+    if env_world is not None:
+        if args.gpus is not None and int(env_world) != args.gpus:
+            print(f"bench.py: --gpus {args.gpus} but the launcher started WORLD_SIZE={env_world} ranks",
+                  file=sys.stderr, flush=True)
+            return 2
+        return None
+    n = 1 if args.gpus is None else args.gpus
+    if n < 1:
+        print("bench.py: --gpus must be >= 1", file=sys.stderr, flush=True)
+        return 2
+    if n == 1:
+        return None
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr=127.0.0.1", f"--master-port={_free_port()}", os.path.abspath(__file__)] + list(argv)
+    if "--gpus" not in " ".join(argv):
+        cmd += ["--gpus", str(n)]
+    return subprocess.call(cmd)
+
+
+def _launch_check():
+    import torch
+    import torch.distributed as dist
+    dist.init_process_group("gloo")
+    t = torch.ones(1)
+    dist.all_reduce(t)
+    if dist.get_rank() == 0:
+        print(json.dumps({"launch_check": True, "world": dist.get_world_size(), "ranks_seen": int(t.item()),
+                          "local_world": int(os.environ.get("LOCAL_WORLD_SIZE", "1"))}), flush=True)
+    dist.destroy_process_group()
+
+
+def _cpu_info():
+    """CPU model, the CPUs this process may run on, and physical cores among them (from /proc/cpuinfo)."""
+    model, cores, phys = None, set(), {}
+    try:
+        cpu = None
+        for line in open("/proc/cpuinfo"):
+            k, _, v = line.partition(":")
+            k, v = k.strip(), v.strip()
+            if k == "processor":
+                cpu = int(v)
+            elif k == "model name" and model is None:
+                model = v
+            elif k == "physical id":
+                phys.setdefault(cpu, [None, None])[0] = v
+            elif k == "core id":
+                phys.setdefault(cpu, [None, None])[1] = v
+    except OSError:
+        pass
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else list(range(os.cpu_count() or 1))
+    for c in aff:
+        cores.add(tuple(phys.get(c, (None, c))))
+    host_phys = len({tuple(v) for v in phys.values()}) or None
+    return {"cpu_model": model, "affinity_cpus": len(aff), "affinity_physical_cores": len(cores),
+            "host_physical_cores": host_phys, "host_logical_cpus": os.cpu_count()}
+
+
+def cpu_baseline(cfg_name: str, seconds_budget: float = 45.0, min_steps: int = 3, batch_size: int = 2):
+    """The oracle (pure-torch fp32 CPU restatement, pinned to the reference's fixtures) timed on this
+    host: one untimed warm-up step, then >= `min_steps` timed steps (median) at the workload's shapes,
+    bs 2.  Threads: the physical cores this process may use, capped by OMP_NUM_THREADS (the CPU share
+    a GPU job gets on the box)."""
+    import numpy as np
+    import torch
+
     from oracle import stage1_ref as R
-    cfg = PRESETS[cfg_name].replace(batch_size=2)
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    info = _cpu_info()
+    threads = info["affinity_physical_cores"]
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
+        threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
+    threads = max(1, threads)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(threads)
+    cfg = PRESETS[cfg_name].replace(batch_size=batch_size)
     g = torch.Generator().manual_seed(0)
     rn = lambda *s, std=0.02: torch.randn(*s, generator=g) * std
     v, t = cfg.vision, cfg.text
@@ -75,30 +173,44 @@ def cpu_baseline(cfg_name: str, seconds_budget: float = 30.0):
     sc = R.StepConfig(gradient_accumulation_steps=1)
     times = []
     t_start = time.perf_counter()
-    while True:
+    R.stage1_step(vp, v, lp, t, st, (px, ids, labels), sc)       # warm-up (allocator, MKL init)
+    while len(times) < min_steps or time.perf_counter() - t_start < seconds_budget * 0.25:
         t0 = time.perf_counter()
         R.stage1_step(vp, v, lp, t, st, (px, ids, labels), sc)
         times.append(time.perf_counter() - t0)
-        if len(times) >= 2 or time.perf_counter() - t_start > seconds_budget:
+        if len(times) >= min_steps and time.perf_counter() - t_start > seconds_budget:
             break
-    dt = times[-1] if len(times) > 1 else times[0]
-    return {"value": round(cfg.batch_size / dt, 4), "unit": "images/sec", "cores": torch.get_num_threads(),
-            "kind": "port",
-            "sample": f"oracle/stage1_ref.py fp32 CPU restatement, {cfg_name} shapes at bs 2 "
-                      f"(T={cfg.text_len}), {len(times)} step(s), last timed: {dt:.2f} s/step"}
+    torch.set_num_threads(prev)
+    med = float(np.median(times))
+    return {"value": round(cfg.batch_size / med, 4), "unit": "images/sec", "cores": threads, "kind": "port",
+            "sample": f"oracle/stage1_ref.py fp32 CPU restatement, {cfg_name} shapes at bs {cfg.batch_size} "
+                      f"(T={cfg.text_len}): 1 warm-up + {len(times)} timed steps, median {med:.2f} s/step "
+                      f"({', '.join(f'{x:.2f}' for x in times)}), {threads} threads",
+            **info}
 
 
-def main():
-    ap = argparse.ArgumentParser()
-    ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=10)
-    ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="cfg2")
-    ap.add_argument("--batch", type=int, default=None, help="per-GPU batch (default: the config's)")
-    ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--prefetch", action="store_true",
-                    help="overlap the next step's SigLIP forward with this step's Gemma3 on a side stream")
-    args = ap.parse_args()
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    args = _args(argv)
+    rc = _launch_or_check(args, argv)
+    if rc is not None:
+        sys.exit(rc)
+    if args.launch_check:
+        _launch_check()
+        return
+    if args.cpu_baseline_only:
+        print(json.dumps({"cpu_baseline": {c: cpu_baseline(c) for c in ("cfg1", args.config)}}), flush=True)
+        return
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from projectiontrainer_amd import _lib as L
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.flops import flops_per_image, geglu_step_flops
+    from projectiontrainer_amd.stage1 import Stage1Engine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -110,6 +222,8 @@ def main():
     cfg = PRESETS[args.config]
     if args.batch:
         cfg = cfg.replace(batch_size=args.batch)
+    if args.text_len:
+        cfg = cfg.replace(text_len=args.text_len)
 
     eng = Stage1Engine.synthetic(cfg, dev, seed=0, world_size=world, total_steps=10 ** 6,
                                  gradient_accumulation_steps=1)
@@ -120,8 +234,9 @@ def main():
 
     # --prefetch: every step runs the next step's (frozen) SigLIP forward on a side stream; the timed
     # window then holds exactly K vision forwards (each timed step issues the next one, the last is joined
-    # before e1) and K Gemma3/projector steps.  Off by default: +0.5 % img/s measured, and the overlapped
-    # SigLIP kernels share the CUs with the gate|up GEMMs the roofline times (their events read ~35 % longer)
+    # before the final event) and K Gemma3/projector steps.  Off by default: +0.5 % img/s measured, and the
+    # overlapped SigLIP kernels share the CUs with the gate|up GEMMs the roofline times (their events read
+    # ~35 % longer)
     nxt = px if args.prefetch else None
     for _ in range(args.warmup):
         eng.step(px, ids, labels, next_pixel_values=nxt)
@@ -129,36 +244,42 @@ def main():
     if world > 1:
         dist.barrier()
     L.lib().ptk_gemm_timer_enable((1 << 8) | (1 << L.ACT_GEGLU))   # events around the gate|up launches only
-    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    e0.record()
-    for _ in range(args.steps):
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    t_wall = time.perf_counter()
+    ev[0].record()
+    for k in range(args.steps):
         loss = eng.step(px, ids, labels, next_pixel_values=nxt)
-    eng.join_prefetch()
-    e1.record()
+        if k + 1 == args.steps:
+            eng.join_prefetch()
+        ev[k + 1].record()
     torch.cuda.synchronize()
     if world > 1:
         dist.barrier()
-    elapsed = e0.elapsed_time(e1) / 1e3
+    t_wall = time.perf_counter() - t_wall
+    elapsed = ev[0].elapsed_time(ev[-1]) / 1e3
+    step_ms = [ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)]
+    med_ms = float(np.median(step_ms))
     L.lib().ptk_gemm_timer_enable(0)
     import ctypes
     tot, cnt = ctypes.c_double(), ctypes.c_int()
     L.check(L.lib().ptk_gemm_timer_read(L.ACT_GEGLU, ctypes.byref(tot), ctypes.byref(cnt)), "timer")
-    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    t = torch.tensor([elapsed, med_ms], dtype=torch.float64, device=dev)
     if world > 1:
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    elapsed = float(t)
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)        # slowest rank bounds the job
+    elapsed, med_ms = float(t[0]), float(t[1])
     imgs = world * cfg.batch_size * args.steps
     value = imgs / elapsed
     fpi = flops_per_image(cfg)["total"]
     geglu_ms = tot.value / max(cnt.value, 1)
     traffic = None
     pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic_geglu.json")
-    if os.path.exists(pmc) and args.config == "cfg2" and cfg.batch_size == 32:
+    if os.path.exists(pmc) and args.config == "cfg2" and cfg.batch_size == 32 and cfg.text_len == 128:
         traffic = json.load(open(pmc))["traffic_bytes_per_launch"]   # rocprofv3 --pmc passes (tools/pmc_traffic.py)
     # algorithmic FLOPs of every timed gate|up launch / their summed HIP-event time
     achieved = geglu_step_flops(cfg) * args.steps / (tot.value / 1e3) / 1e12
     lm_name = {2560: "Gemma3-4B", 1152: "Gemma3-1B"}.get(cfg.text.hidden_size, f"Gemma3(h{cfg.text.hidden_size})")
-    metric = ("Stage-1 images/sec/node (SigLIP-L-384 + Gemma3-1B, 576+128 tok)" if args.config == "cfg2" else
+    headline = args.config == "cfg2" and cfg.text_len == 128
+    metric = ("Stage-1 images/sec/node (SigLIP-L-384 + Gemma3-1B, 576+128 tok)" if headline else
               f"Stage-1 images/sec/node ({args.config}: SigLIP + {lm_name}, {cfg.vision.num_patches}+{cfg.text_len} tok)")
     line = {
         "metric": metric,
@@ -175,11 +296,15 @@ def main():
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",
                      "launches": cnt.value, "avg_ms": round(geglu_ms, 4)},
+        "median_ms_per_step": round(med_ms, 3),
+        "value_at_median_step": round(world * cfg.batch_size / (med_ms / 1e3), 3),
         "step_mfma_frac": round(value * fpi / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
-        "flop_per_image": fpi, "loss": round(float(loss), 5),
+        "flop_per_image": fpi, "loss": round(float(loss), 5), "host_wall_s_timed": round(t_wall, 3),
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.config)
+        cb1 = cpu_baseline("cfg1", seconds_budget=20.0)
+        line["cpu_baseline_cfg1"] = {k: cb1[k] for k in ("value", "unit", "cores", "kind", "sample")}
     if rank == 0:
         print(json.dumps(line), flush=True)
     if world > 1:

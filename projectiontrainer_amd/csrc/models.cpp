@@ -54,6 +54,12 @@ constexpr int LM_SPLITK = 8;   // split-K for the vocab-long lm_head dX GEMM (R 
   do {        \
     if ((x)) return -1; \
   } while (0)
+// HIP runtime call: a failure records its own message (ptk_last_error) instead of leaving a stale one
+#define CKH(x)                                                                       \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) return set_error("%s: %s", #x, hipGetErrorString(e_));    \
+  } while (0)
 
 static bool geglu_split() {
   static const int v = [] { const char* e = getenv("PTK_GEGLU_SPLIT"); return e && e[0] == '1' ? 1 : 0; }();
@@ -323,7 +329,7 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
       g.amap = lossmap;
       g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
       CK(launch_gemm(g, ACT_GEGLU, OUT_BF16, 1, st));
-      CK(hipMemsetAsync(sv.dn, 0, (size_t)M * H * sizeof(bf16_t), st) != hipSuccess);
+      CKH(hipMemsetAsync(sv.dn, 0, (size_t)M * H * sizeof(bf16_t), st));
       GemmArgs g2 = gemm(w.h, I, L.wd, I, sv.dn, H, R, H, I);
       g2.cmap = lossmap;
       CK(launch_gemm(g2, ACT_NONE, OUT_BF16, 1, st));
@@ -355,7 +361,7 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
     CK(launch_sum_partials(w.dxf_part, LM_SPLITK + (rem ? 1 : 0), (long)R * H, w.dxf, st));
   }
   float* dR = bt->dx;
-  CK(hipMemsetAsync(dR, 0, (size_t)M * H * 4, st) != hipSuccess);
+  CKH(hipMemsetAsync(dR, 0, (size_t)M * H * 4, st));
   CK(launch_rmsnorm_bwd_scatter(w.x[nl], lossmap, wt->final_norm, w.rstd_f, w.dxf, dR, R, H, st));
 
   // ---------------- backward (dX only: weights are frozen)
@@ -389,7 +395,7 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
       g.amap = lossmap;
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
       CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, R, I, st));
-      CK(hipMemsetAsync(w.dtmp, 0, (size_t)M * H * sizeof(float), st) != hipSuccess);
+      CKH(hipMemsetAsync(w.dtmp, 0, (size_t)M * H * sizeof(float), st));
       GemmArgs g2 = gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, R, H, 2 * I);
       g2.cmap = lossmap;
       CK(launch_gemm(g2, ACT_NONE, OUT_F32, 1, st));

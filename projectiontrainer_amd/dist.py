@@ -8,6 +8,7 @@ gradient_accumulation_steps, sync_gradients, gather`.
 """
 from __future__ import annotations
 
+import math
 import os
 
 import torch
@@ -50,6 +51,10 @@ class DistState:
         t = t.reshape(-1)
         if self.num_processes == 1:
             return t
+        if dist.get_backend() == "gloo":        # CPU tests: gloo has no all_gather_into_tensor
+            parts = [torch.empty_like(t) for _ in range(self.num_processes)]
+            dist.all_gather(parts, t.contiguous())
+            return torch.cat(parts)
         out = torch.empty(self.num_processes * t.numel(), dtype=t.dtype, device=t.device)
         dist.all_gather_into_tensor(out, t.contiguous())
         return out
@@ -74,13 +79,53 @@ def from_accelerator(acc) -> DistState:
 
 def shard_batches(n_items: int, batch_size: int, rank: int, world: int, epoch: int, seed: int = 0,
                   shuffle: bool = True):
-    """Index batches for this rank: a seeded permutation cut into batches of
-    `batch_size`, batch i going to rank i % world (accelerate's prepared
-    DataLoader dispatch; the last incomplete batch is kept as in DataLoader)."""
+    """Index batches for this rank, as the reference's prepared DataLoader
+    yields them (`Stage1/projector_trainer.py:100-102` -> accelerate
+    `BatchSamplerShard` with its defaults `even_batches=True`, `drop_last=False`,
+    `split_batches=False`; ACC/data_loader.py:213-271).
+
+    One seeded permutation (the same on every rank, as accelerate's synchronised
+    sampler generator) is cut into batches of `batch_size`; batch i goes to rank
+    i % world.  With world > 1 every rank gets the SAME number of FULL batches:
+    the short last batch is completed, and missing batches are created, from the
+    start of the permutation (indices of the first `world` batches, repeated as
+    needed).  With world == 1 accelerate does not shard, so the short last batch
+    is kept as the plain DataLoader yields it."""
     g = torch.Generator().manual_seed(seed + epoch)
-    order = torch.randperm(n_items, generator=g) if shuffle else torch.arange(n_items)
+    order = (torch.randperm(n_items, generator=g) if shuffle else torch.arange(n_items)).tolist()
     batches = [order[i:i + batch_size] for i in range(0, n_items, batch_size)]
-    return [b for i, b in enumerate(batches) if i % world == rank]
+    if world == 1:
+        return [torch.tensor(b, dtype=torch.int64) for b in batches]
+    out, to_yield = [], None
+    initial = [i for b in batches[:world] for i in b]   # ACC :218-223 (first `world` batches)
+    for idx, b in enumerate(batches):
+        if idx % world == rank:
+            to_yield = b
+        if idx % world == world - 1 and len(b) == batch_size:
+            out.append(to_yield)
+            to_yield = None
+    if batches:
+        if to_yield is not None and len(to_yield) == batch_size:
+            out.append(to_yield)
+        while len(initial) < world * batch_size:         # degenerate: dataset smaller than one round
+            initial = initial + initial
+        idx, last = len(batches) - 1, list(batches[-1])
+        if len(last) == batch_size:
+            last, idx = [], idx + 1
+        cyc = 0
+        while idx % world != 0 or len(last) > 0:          # ACC :256-271: fill up to a multiple of world
+            end = cyc + batch_size - len(last)
+            last = last + initial[cyc:end]
+            if idx % world == rank:
+                out.append(last)
+            cyc, last, idx = end, [], idx + 1
+    return [torch.tensor(b, dtype=torch.int64) for b in out]
+
+
+def batches_per_rank(n_items: int, batch_size: int, world: int) -> int:
+    """len() of the prepared DataLoader on each rank (ACC/data_loader.py:170-186, even_batches)."""
+    n = math.ceil(n_items / batch_size)
+    return n if world == 1 else math.ceil(n / world)
 
 
 def allreduce_grads_(flat_grad, world: int, group=None):

@@ -84,21 +84,53 @@ class Gemma3CausalLM:
         (self.cos_l, self.sin_l), (self.cos_g, self.sin_g) = [(c.to(self.device), s.to(self.device))
                                                               for c, s in tabs]
 
+    @staticmethod
+    def config_from_hf(c) -> Gemma3TextConfig:
+        """Gemma3TextConfig from an HF config of either shape:
+        * transformers 4.51 (the reference's pin, requirements.txt:6): `sliding_window_pattern`,
+          `rope_theta`, `rope_local_base_freq`, `rope_scaling` ({"rope_type": "linear", "factor": f} or None);
+        * transformers >= 5: `layer_types` and per-layer-type `rope_parameters`."""
+        lt = getattr(c, "layer_types", None)
+        rp = getattr(c, "rope_parameters", None)
+        if lt is not None and isinstance(rp, dict) and "full_attention" in rp:
+            lt = list(lt)
+            pattern = lt.index("full_attention") + 1 if "full_attention" in lt else len(lt) + 1
+            want = ["sliding_attention" if (i + 1) % pattern else "full_attention" for i in range(len(lt))]
+            if lt != want:
+                raise ValueError(f"Gemma3 layer_types {lt} are not a periodic sliding/full pattern")
+            theta, local = rp["full_attention"]["rope_theta"], rp["sliding_attention"]["rope_theta"]
+            factor = float(rp["full_attention"].get("factor", 1.0))
+        else:
+            pattern = int(c.sliding_window_pattern)
+            theta, local = float(c.rope_theta), float(c.rope_local_base_freq)
+            rs = getattr(c, "rope_scaling", None) or {}
+            kind = rs.get("rope_type", rs.get("type", "default"))
+            if kind not in ("default", "linear"):
+                raise ValueError(f"Gemma3 rope_scaling type {kind!r} is not supported (default / linear only)")
+            factor = float(rs.get("factor", 1.0)) if kind == "linear" else 1.0
+        return Gemma3TextConfig(vocab_size=c.vocab_size, hidden_size=c.hidden_size,
+                                intermediate_size=c.intermediate_size, num_hidden_layers=c.num_hidden_layers,
+                                num_attention_heads=c.num_attention_heads, num_key_value_heads=c.num_key_value_heads,
+                                head_dim=c.head_dim, sliding_window=c.sliding_window, sliding_window_pattern=pattern,
+                                rope_theta=theta, rope_local_base_freq=local, rope_linear_factor=factor,
+                                query_pre_attn_scalar=c.query_pre_attn_scalar, rms_norm_eps=c.rms_norm_eps,
+                                pad_token_id=c.pad_token_id if c.pad_token_id is not None else 0)
+
+    @staticmethod
+    def check_not_quantized(model):
+        """The reference's --enable_qlora path loads the LM in 4 bit with LoRA adapters
+        (Stage1/train_projection_stage1.py:192-210); the HIP path runs bf16 GEMMs on dense weights."""
+        qc = getattr(getattr(model, "config", None), "quantization_config", None)
+        if (getattr(model, "is_loaded_in_4bit", False) or getattr(model, "is_loaded_in_8bit", False)
+                or getattr(model, "is_quantized", False) or qc is not None or hasattr(model, "peft_config")):
+            raise ValueError("Gemma3CausalLM.from_hf: quantised / QLoRA (peft) language models are not supported "
+                             "by the HIP Stage-1 path; pass the dense bf16 or fp32 Gemma3ForCausalLM "
+                             "(run without --enable_qlora)")
+
     @classmethod
     def from_hf(cls, model, device="cuda", max_pos=2048):
-        c = model.config
-        lt = list(c.layer_types)
-        pattern = lt.index("full_attention") + 1 if "full_attention" in lt else len(lt) + 1
-        rp = c.rope_parameters
-        cfg = Gemma3TextConfig(vocab_size=c.vocab_size, hidden_size=c.hidden_size,
-                               intermediate_size=c.intermediate_size, num_hidden_layers=c.num_hidden_layers,
-                               num_attention_heads=c.num_attention_heads, num_key_value_heads=c.num_key_value_heads,
-                               head_dim=c.head_dim, sliding_window=c.sliding_window, sliding_window_pattern=pattern,
-                               rope_theta=rp["full_attention"]["rope_theta"],
-                               rope_local_base_freq=rp["sliding_attention"]["rope_theta"],
-                               rope_linear_factor=float(rp["full_attention"].get("factor", 1.0)),
-                               query_pre_attn_scalar=c.query_pre_attn_scalar, rms_norm_eps=c.rms_norm_eps,
-                               pad_token_id=c.pad_token_id if c.pad_token_id is not None else 0)
+        cls.check_not_quantized(model)
+        cfg = cls.config_from_hf(model.config)
         sd = {k: v.detach().float() for k, v in model.state_dict().items()}
         return cls(cfg, sd, device, max_pos)
 
@@ -152,16 +184,22 @@ class Gemma3CausalLM:
             self._ws = torch.empty(n, dtype=torch.uint8, device=self.device)
         return self._ws
 
-    def loss_and_input_grad(self, x, dx, token_ids, labels, num_vision, loss_scale, loss):
+    def loss_and_input_grad(self, x, dx, token_ids, labels, num_vision, loss_scale, loss, pad_token_id=None):
         """x: f32 [B*Spad, H] LLM input rows (vision rows filled by the caller),
         token_ids/labels int64 [B, T].  Writes loss [1] (mean CE) and dx (grad of
-        loss*loss_scale w.r.t. x)."""
+        loss*loss_scale w.r.t. x).  pad_token_id: id whose text positions are
+        masked as keys (the trainer passes the tokenizer's, projector_trainer.py:207;
+        -1 masks none); None = the model config's."""
         B, T = token_ids.shape
         Sp = x.shape[0] // B
         ws = self.workspace(B, T, Sp)
         bt = L.Gemma3BatchC(B, T, num_vision, Sp, token_ids.data_ptr(), labels.data_ptr(), x.data_ptr(),
                             dx.data_ptr(), loss_scale, loss.data_ptr())
-        L.check(L.lib().ptk_gemma3_loss_fwd_bwd(self.c_cfg, self.c_w, bt, ws.data_ptr(), ws.numel(),
+        cfg = self.c_cfg
+        if pad_token_id is not None and pad_token_id != cfg.pad_token_id:
+            cfg = L.Gemma3ConfigC.from_buffer_copy(cfg)
+            cfg.pad_token_id = int(pad_token_id)
+        L.check(L.lib().ptk_gemma3_loss_fwd_bwd(cfg, self.c_w, bt, ws.data_ptr(), ws.numel(),
                                                 L.stream_ptr(self.device)), "ptk_gemma3_loss_fwd_bwd")
 
     def get_input_embeddings(self):

@@ -145,13 +145,18 @@ def cross_entropy_(logits, targets, gscale):
     return row_loss
 
 
-def transpose(x, rows_pad=None):
-    """[Z, rows, cols] or [rows, cols] bf16 -> [.., cols, rows_pad] (zero-padded)."""
+def transpose(x, rows_pad=None, out=None):
+    """[Z, rows, cols] or [rows, cols] bf16 -> [.., cols, rows_pad] (zero-padded); out: preallocated result."""
     squeeze = x.dim() == 2
     x3 = x.unsqueeze(0) if squeeze else x
     Z, rows, cols = x3.shape
     rp = rows if rows_pad is None else rows_pad
-    out = torch.empty((Z, cols, rp), dtype=x.dtype, device=x.device)
+    if out is None:
+        out = torch.empty((Z, cols, rp), dtype=x.dtype, device=x.device)
+    else:
+        if tuple(out.shape[-2:]) != (cols, rp) or out.numel() != Z * cols * rp or not out.is_contiguous():
+            raise L.PtkError(f"transpose: out {tuple(out.shape)} does not hold [{Z}, {cols}, {rp}]")
+        out = out.view(Z, cols, rp)
     check(L.lib().ptk_transpose_bf16(ptr(x3), x3.stride(1), ptr(out), rp, Z, x3.stride(0), cols * rp, rows, cols, rp,
                                      L.stream_ptr(x.device)), "transpose")
     return out[0] if squeeze else out

@@ -7,7 +7,8 @@ What changes underneath:
     `Gemma3CausalLM`); HF `SiglipModel` / `Gemma3ForCausalLM` instances passed
     in are converted once (weights re-laid out for the kernels);
   * one process per GPU with torch.distributed/RCCL instead of accelerate+DDP:
-    batches are dealt round-robin per rank, the projector's flat fp32 grads
+    batches are dealt to ranks as accelerate's prepared DataLoader deals them
+    (even_batches: equal counts of full batches per rank), the projector's flat fp32 grads
     are all-reduced once per step, clip + AdamW is one fused kernel;
   * the arithmetic quirks of the reference are kept on purpose:
     loss / gas twice before backward, an optimizer step on every micro-batch,
@@ -75,8 +76,10 @@ class ProjectionTrainerStage1:
             p.load_state_dict({k: v.detach().float().cpu() for k, v in sd.items()})
             projection_layer = p
         self.projection_layer = projection_layer.to(self.device)
-        pad = getattr(tokenizer, "pad_token_id", None)
-        self.pad_token_id = 0 if pad is None else pad
+        # text key mask `token_ids != tokenizer.pad_token_id`, all ones when the tokenizer has no pad
+        # token (projector_trainer.py:207-209); -1 never matches a token id
+        pad = getattr(tokenizer, "pad_token_id", None) if tokenizer is not None else None
+        self.pad_token_id = -1 if pad is None else int(pad)
 
         # schedule horizon from the UNSHARDED loader (projector_trainer.py:82-95, F7)
         n_batches = math.ceil(len(train_dataset) / batch_size)
@@ -87,6 +90,7 @@ class ProjectionTrainerStage1:
                                    gradient_accumulation_steps=acc.gradient_accumulation_steps,
                                    warmup_steps=self.num_warmup_steps, total_steps=self.max_train_steps,
                                    world_size=acc.num_processes)
+        self.engine.pad_token_id = self.pad_token_id
         self.global_step = 0
 
     # ------------------------------------------------------------------ data
@@ -119,7 +123,14 @@ class ProjectionTrainerStage1:
 
     # ------------------------------------------------------------------ train
     def train_step(self, batch):
-        """One reference iteration (projector_trainer.py:152-271); returns the gathered mean loss."""
+        """One reference iteration (projector_trainer.py:152-271); returns the gathered mean loss, or None
+        when the vision tower raised: the reference logs the error and skips the batch (`continue`,
+        :174-176) before the projector, the LLM or the optimizer run."""
+        try:
+            self.engine.encode_vision(batch["pixel_values"], batch["token_ids"])
+        except Exception as e:   # noqa: BLE001 -- the reference catches every exception here
+            logger.error("Error getting vision embeddings: %s", e, exc_info=True)
+            return None
         loss = self.engine.step(batch["pixel_values"], batch["token_ids"], batch["labels"])
         self.global_step += 1
         return self.accelerator.gather(loss).mean()
@@ -132,12 +143,16 @@ class ProjectionTrainerStage1:
         for epoch in range(self.num_epochs):
             epoch_loss, n = 0.0, 0
             for batch in self._batches(self.train_dataset, epoch):
-                avg = float(self.train_step(batch))          # host sync, as the reference's .item()
+                avg = self.train_step(batch)
+                if avg is None:
+                    continue
+                avg = float(avg)                              # host sync, as the reference's .item()
                 epoch_loss += avg
                 n += 1
                 self._log({"train/batch_loss": avg, "train/learning_rate": self.engine.last_lr,
                            "step": self.global_step}, self.global_step)
-            n_opt = math.ceil(math.ceil(len(self.train_dataset) / self.batch_size) /
+            # len(self.train_loader) AFTER prepare: the per-rank batch count (projector_trainer.py:275)
+            n_opt = math.ceil(D.batches_per_rank(len(self.train_dataset), self.batch_size, acc.num_processes) /
                               max(1, acc.gradient_accumulation_steps))
             self._log({"train/epoch_loss": epoch_loss / max(1, n_opt), "epoch": epoch + 1}, self.global_step)
             if acc.is_main_process and self.save_every_n_epochs > 0 and (epoch + 1) % self.save_every_n_epochs == 0:

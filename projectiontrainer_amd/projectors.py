@@ -46,6 +46,7 @@ class MLPProjector(nn.Module):
             self._views.append((o, k, tuple(p.shape)))
             o += k
         self.flat, self.flat_grad = flat, grad
+        self._w1b = None          # bf16 shadows are (re)allocated on the new device by refresh_shadows
         self._shadow_dirty = True
 
     def _apply(self, fn, *args, **kw):      # keep the flat layout across .to()/.cuda()
@@ -85,9 +86,10 @@ class MLPProjector(nn.Module):
         if getattr(self, "_w1b", None) is None:
             self._w1b = torch.empty(self.w1.shape, dtype=torch.bfloat16, device=self.flat.device)
             self._w2b = torch.empty(self.w2.shape, dtype=torch.bfloat16, device=self.flat.device)
+            self._w2t = torch.empty((self.inter_dim, self.llm_dim), dtype=torch.bfloat16, device=self.flat.device)
         K.cast_bf16(self.w1.detach(), self._w1b)
         K.cast_bf16(self.w2.detach(), self._w2b)
-        self._w2t = K.transpose(self._w2b)
+        K.transpose(self._w2b, out=self._w2t)     # in place: no allocation per optimizer step
         self.c = L.ProjectorC(self.vision_dim, self.inter_dim, self.llm_dim, self._w1b.data_ptr(),
                               self.b1.data_ptr(), self._w2b.data_ptr(), self.b2.data_ptr(), self._w2t.data_ptr())
         self._shadow_dirty = False

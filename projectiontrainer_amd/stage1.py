@@ -57,6 +57,10 @@ class Stage1Engine:
         self.lr0, self.wd, self.gas, self.max_norm = learning_rate, weight_decay, gradient_accumulation_steps, max_grad_norm
         self.warmup, self.total, self.betas, self.eps = warmup_steps, total_steps, betas, eps
         self.pg, self.world = process_group, world_size
+        # text key mask `token_ids != tokenizer.pad_token_id` (projector_trainer.py:207-209): the trainer
+        # sets the tokenizer's id (-1 = tokenizer without a pad token: every text key attends); None = the
+        # LM config's pad_token_id
+        self.pad_token_id = None
         self.opt_step = 0        # optimizer steps (AdamW bias correction)
         self.sched_step = 0      # LambdaLR steps (advanced num_processes times per step, F7)
         n = projector.flat.numel()
@@ -68,8 +72,12 @@ class Stage1Engine:
         self.last_lr = learning_rate * cosine_lambda(0, warmup_steps, total_steps)
         self.vstream = None        # side stream of the vision prefetch
         self._prefetched = None    # event: the current buffer's features were computed ahead
+        self._vision_ready = False  # encode_vision ran this step's tower on the main stream
 
     def _buffers(self, B, T):
+        """Step buffers are allocated for the largest batch seen at this text length; a smaller batch
+        (the short last batch of an epoch) runs on leading views of them, so nothing is reallocated and
+        then reallocated back (the kernels take the row counts explicitly)."""
         if self._shape == (B, T):
             return
         vc, tc = self.vision.cfg, self.llm.cfg
@@ -77,29 +85,45 @@ class Stage1Engine:
         S = (N - 1) + T
         Sp = Gemma3CausalLM.seq_pad(S)
         dev, bf = self.device, torch.bfloat16
+        if self._prefetched is not None:
+            raise RuntimeError("Stage1Engine: the batch shape changed while a vision prefetch was pending")
+        if getattr(self, "_cap", None) is None or self._cap[1] != T or self._cap[0] < B:
+            C = B
+            self._full = dict(
+                px=[torch.empty((C, vc.num_channels, vc.image_size, vc.image_size), dtype=bf, device=dev)
+                    for _ in range(2)],
+                vis=[torch.empty((C * N, Dv), dtype=bf, device=dev) for _ in range(2)],
+                a=torch.empty((C * N, I), dtype=bf, device=dev),
+                h=torch.empty((C * N, I), dtype=bf, device=dev),
+                x=torch.empty((C * Sp, Dl), dtype=torch.float32, device=dev),
+                dx=torch.empty((C * Sp, Dl), dtype=torch.float32, device=dev),
+                dy=torch.empty((C * N, Dl), dtype=bf, device=dev))
+            self.proj_ws = torch.empty(self.proj.workspace_bytes(C * N), dtype=torch.uint8, device=dev)
+            self.vision.workspace(C)
+            self.llm.workspace(C, T, Sp)
+            self._cap = (C, T)
+            self._cur = 0
+            self._released = [None, None]   # event per buffer: the projector backward reading it has run
+        f = self._full
         self.N, self.Sp = N, Sp
-        self.px_bufs = [torch.empty((B, vc.num_channels, vc.image_size, vc.image_size), dtype=bf, device=dev)
-                        for _ in range(2)]
-        self.vis_bufs = [torch.empty((B * N, Dv), dtype=bf, device=dev) for _ in range(2)]
-        self._cur = 0
-        self._released = [None, None]   # event per buffer: the projector backward reading it has run
-        self._prefetched = None
-        self.px, self.vis = self.px_bufs[0], self.vis_bufs[0]
-        self.a = torch.empty((B * N, I), dtype=bf, device=dev)
-        self.h = torch.empty((B * N, I), dtype=bf, device=dev)
-        self.x = torch.empty((B * Sp, Dl), dtype=torch.float32, device=dev)
-        self.dx = torch.empty((B * Sp, Dl), dtype=torch.float32, device=dev)
-        self.dy = torch.empty((B * N, Dl), dtype=bf, device=dev)
-        self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
-        self.proj_ws = torch.empty(self.proj.workspace_bytes(B * N), dtype=torch.uint8, device=dev)
-        self.vision.workspace(B)
-        self.llm.workspace(B, T, Sp)
+        self.px_bufs = [t[:B] for t in f["px"]]
+        self.vis_bufs = [t[:B * N] for t in f["vis"]]
+        self.px, self.vis = self.px_bufs[self._cur], self.vis_bufs[self._cur]
+        self.a, self.h, self.dy = f["a"][:B * N], f["h"][:B * N], f["dy"][:B * N]
+        self.x, self.dx = f["x"][:B * Sp], f["dx"][:B * Sp]
+        if getattr(self, "loss", None) is None:
+            self.loss = torch.zeros(1, dtype=torch.float32, device=dev)
         self._shape = (B, T)
 
     # ---------------------------------------------------------------- pieces
     def _vision(self, pixel_values, i):
         """pixels -> bf16 px_bufs[i] -> SigLIP features vis_bufs[i], on the current stream."""
         px = self.px_bufs[i]
+        if tuple(pixel_values.shape) != tuple(px.shape):
+            raise ValueError(f"pixel_values {tuple(pixel_values.shape)} do not match the vision tower's "
+                             f"input {tuple(px.shape)}")
+        if pixel_values.device != px.device:
+            raise ValueError(f"pixel_values on {pixel_values.device}, the vision tower runs on {px.device}")
         if pixel_values.dtype == torch.bfloat16:
             px.copy_(pixel_values)
         else:
@@ -117,6 +141,8 @@ class Stage1Engine:
         if self._prefetched is not None:
             main.wait_event(self._prefetched)
             self._prefetched = None
+        elif self._vision_ready:
+            self._vision_ready = False       # encode_vision already ran this batch's tower
         else:
             self._vision(pixel_values, i)
         self.px, self.vis = self.px_bufs[i], self.vis_bufs[i]
@@ -139,7 +165,7 @@ class Stage1Engine:
             self._prefetched = ready
             self._cur = j
         self.llm.loss_and_input_grad(self.x, self.dx, token_ids, labels, self.N - 1,
-                                     1.0 / float(self.gas * self.gas), self.loss)
+                                     1.0 / float(self.gas * self.gas), self.loss, pad_token_id=self.pad_token_id)
         L.check(L.lib().ptk_gather_vision_grad(self.dx.data_ptr(), B, self.N, self.Sp, self.llm.cfg.hidden_size,
                                                self.dy.data_ptr(), L.stream_ptr(self.device)), "gather_vision_grad")
         self.proj.bwd_into(self.vis, self.a, self.h, self.dy, self.proj_ws)
@@ -147,6 +173,17 @@ class Stage1Engine:
         rel.record(main)
         self._released[i] = rel
         return self.loss
+
+    def encode_vision(self, pixel_values, token_ids):
+        """This step's SigLIP forward on its own, ahead of forward_backward (which then skips it): the
+        trainer's skip-batch boundary (projector_trainer.py:158-176 logs a vision-tower exception and
+        `continue`s before the projector runs).  An exception here leaves no projector state touched."""
+        B, T = token_ids.shape
+        self._buffers(B, T)
+        if self._prefetched is not None:
+            raise RuntimeError("Stage1Engine.encode_vision: a vision prefetch is pending")
+        self._vision(pixel_values, self._cur)
+        self._vision_ready = True
 
     def join_prefetch(self):
         """Make the current stream wait for an outstanding vision prefetch (end of a timed region)."""

@@ -1,4 +1,5 @@
-"""One Stage-1 forward/backward at architecture-true Gemma3-1B dims (bs 2, S 703, 2 layers), results
+"""One Stage-1 forward/backward at architecture-true Gemma3-1B dims (bs 2, S 703, 2 layers: one sliding-window and
+one full-attention layer, so both dK/dV split plans run), results
 saved to argv[1]. Run by tests/test_dkv_fused_gpu.py under PTK_DKV_REDUCE_SPLIT=0/1 (the switch is read
 once per process, so each setting needs its own process)."""
 import os
@@ -21,7 +22,8 @@ def main(out_path):
     gpu = torch.device("cuda:0")
     cfg = PRESETS["cfg2"]
     cfg = cfg.replace(vision=cfg.vision.__class__(**{**cfg.vision.__dict__, "num_hidden_layers": 1}),
-                      text=cfg.text.__class__(**{**cfg.text.__dict__, "num_hidden_layers": 2}),
+                      text=cfg.text.__class__(**{**cfg.text.__dict__, "num_hidden_layers": 2,
+                                                          "sliding_window_pattern": 2}),
                       batch_size=2, text_len=128)
     vp = W.siglip_vision_params(cfg.vision, seed=3)
     lp = W.gemma3_params(cfg.text, seed=4)

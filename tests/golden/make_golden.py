@@ -14,12 +14,30 @@ the batch (after the DataLoader's shuffle), SigLIP patch embeddings,
 projector output and its gradient, loss, LR, raw / clipped projector grads
 and the projector params after each AdamW step.
 
+Fixtures:
+  tiny, tiny_gqa      tiny dims, fp32 (no mixed precision)
+  tiny_bf16           tiny dims under `accelerate launch --mixed_precision bf16`
+                      (run_projection_train_stage1.sh:6): both towers loaded in bf16
+                      (train_projection_stage1.py:169-183,204-210), the projector fp32
+                      under autocast -- the precision flow of SURVEY F8
+  cfg1, cfg1_bf16     BASELINE cfg1 shapes: SigLIP-B/16-224 + Gemma3-1B (26 layers,
+                      vocab 262144), bs 2, T 64, fp32 / bf16 as above
+
+Large tensors are stored as a strided sub-sample `<key>@sub<sr>x<sc>` (every
+sr-th row, every sc-th column of the [rows, last-dim] view) plus the exact
+`@norm` and `@sum` of the whole tensor; the pixel batch of the real-size
+fixtures is stored as the sample order the shuffled loader produced
+(`s<i>_order`), the pixels themselves being regenerated from the seed.
+Each fixture runs in its own process (accelerate's state is a singleton).
+
 Only data (inputs and expected outputs) is written; no reference source.
 """
 from __future__ import annotations
 
 import argparse
+import math
 import os
+import subprocess
 import sys
 import tempfile
 import types
@@ -36,7 +54,23 @@ from projectiontrainer_amd import weights as W  # noqa: E402
 REF_STAGE1 = "/root/reference/Stage1"
 
 
-def run(name: str, gas: int, seed_batch: int, num_epochs: int = 2, lr: float = 1e-4):
+SUB_BUDGET = 8192   # elements kept per large tensor
+
+
+def sub_strides(shape):
+    """(row stride, column stride) of the stored sub-sample of a tensor viewed as [rows, last-dim]."""
+    C = shape[-1] if len(shape) else 1
+    R = int(np.prod(shape[:-1])) if len(shape) > 1 else 1
+    sc = 1 if C <= 1024 else math.ceil(C / 512)
+    kept_c = math.ceil(C / sc)
+    sr = max(1, math.ceil(R / max(1, SUB_BUDGET // kept_c)))
+    return sr, sc
+
+
+def run(name: str, gas: int, seed_batch: int, num_epochs: int = 2, lr: float = 1e-4, precision: str = "no"):
+    """precision "bf16": ACCELERATE_MIXED_PRECISION=bf16 (what `accelerate launch --mixed_precision bf16`
+    exports) and both towers cast to bf16 as train_projection_stage1.py:169-183,204-210 loads them."""
+    os.environ["ACCELERATE_MIXED_PRECISION"] = precision
     sys.path.insert(0, REF_STAGE1)
     import transformers
     import accelerate
@@ -46,7 +80,7 @@ def run(name: str, gas: int, seed_batch: int, num_epochs: int = 2, lr: float = 1
     from accelerator_setup import setup_accelerator_and_logging  # reference
 
     torch.manual_seed(0)
-    cfg = PRESETS[name]
+    cfg = PRESETS[name.replace("_bf16", "")]
     vis_kw, txt_kw = to_hf_dicts(cfg)
     sig = SiglipModel(SiglipConfig(
         text_config=dict(vocab_size=64, hidden_size=64, intermediate_size=128, num_hidden_layers=1,
@@ -61,6 +95,9 @@ def run(name: str, gas: int, seed_batch: int, num_epochs: int = 2, lr: float = 1
     res = llm.load_state_dict({k: torch.from_numpy(v) for k, v in lp.items()}, strict=False)
     assert set(res.missing_keys) <= {"lm_head.weight"}, res
     assert llm.lm_head.weight.data_ptr() == llm.model.embed_tokens.weight.data_ptr()
+    if precision == "bf16":
+        sig, llm = sig.to(torch.bfloat16), llm.to(torch.bfloat16)
+        assert llm.lm_head.weight.data_ptr() == llm.model.embed_tokens.weight.data_ptr()
     proj = MLPProjector(cfg.vision.hidden_size, cfg.text.hidden_size)
     pp = W.projector_params(cfg.vision.hidden_size, cfg.text.hidden_size, cfg.expansion_factor)
     proj.load_state_dict({k: torch.from_numpy(v) for k, v in pp.items()})
@@ -72,6 +109,7 @@ def run(name: str, gas: int, seed_batch: int, num_epochs: int = 2, lr: float = 1
     args = types.SimpleNamespace(gradient_accumulation_steps=gas, disable_wandb=True,
                                  batch_size=cfg.batch_size, wandb_project="x", wandb_run_name=None)
     acc = setup_accelerator_and_logging(args)
+    assert acc.mixed_precision == precision, (acc.mixed_precision, precision)
     tok = types.SimpleNamespace(pad_token_id=cfg.text.pad_token_id, eos_token_id=cfg.text.eos_token_id)
     out = tempfile.mkdtemp()
     trainer = ProjectionTrainerStage1(acc, sig, llm, proj, None, tok, data, None, output_dir=out,
@@ -82,12 +120,24 @@ def run(name: str, gas: int, seed_batch: int, num_epochs: int = 2, lr: float = 1
     rec = {}
     step = {"i": 0}
 
+    big = cfg.batch_size * cfg.vision.num_channels * cfg.vision.image_size ** 2 > 65536
+
     def put(k, v):
-        a = v.detach().cpu().numpy().copy() if torch.is_tensor(v) else np.asarray(v)
+        a = v.detach().cpu().float().numpy().copy() if torch.is_tensor(v) and v.is_floating_point() else \
+            (v.detach().cpu().numpy().copy() if torch.is_tensor(v) else np.asarray(v))
         key = f"s{step['i']}_{k}"
-        if a.ndim == 2 and a.size > 16384:
-            # large projector matrices: every 16th row + exact norm/sum (keeps fixtures small)
-            rec[key + "@rows16"] = a[::16]
+        if k == "pixel_values" and big:
+            # which dataset samples (in which order) the shuffled loader put in this batch
+            rec[f"s{step['i']}_order"] = np.array([int(np.argmin([np.abs(a[j] - px[i]).max() for i in range(len(px))]))
+                                                    for j in range(a.shape[0])])
+            return
+        if a.ndim >= 2 and a.size > 16384:
+            if name in ("tiny", "tiny_gqa") and a.ndim == 2:
+                # round-1 layout of the tiny fixtures: every 16th row
+                rec[key + "@rows16"] = a[::16]
+            else:
+                sr, sc = sub_strides(a.shape)
+                rec[key + f"@sub{sr}x{sc}"] = a.reshape(-1, a.shape[-1])[::sr, ::sc]
             rec[key + "@norm"] = np.array(np.linalg.norm(a.astype(np.float64)))
             rec[key + "@sum"] = np.array(a.astype(np.float64).sum())
         else:
@@ -127,7 +177,7 @@ def run(name: str, gas: int, seed_batch: int, num_epochs: int = 2, lr: float = 1
     opt.register_step_post_hook(post)
 
     trainer.train()
-    meta = dict(name=name, gas=gas, seed_batch=seed_batch, lr=lr, num_epochs=num_epochs,
+    meta = dict(name=name, gas=gas, seed_batch=seed_batch, lr=lr, num_epochs=num_epochs, precision=precision,
                 steps=step["i"], max_train_steps=trainer.max_train_steps,
                 torch=torch.__version__, transformers=transformers.__version__,
                 accelerate=accelerate.__version__)
@@ -138,15 +188,30 @@ def run(name: str, gas: int, seed_batch: int, num_epochs: int = 2, lr: float = 1
     return rec
 
 
+FIXTURES = {   # name: (gas, batch seed, precision)
+    "tiny": (2, 11, "no"),
+    "tiny_gqa": (1, 12, "no"),
+    "tiny_bf16": (2, 13, "bf16"),
+    "cfg1": (2, 14, "no"),
+    "cfg1_bf16": (2, 15, "bf16"),
+}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--out", default=os.path.dirname(os.path.abspath(__file__)))
+    ap.add_argument("--only", default=None, help="one fixture (run in this process)")
     a = ap.parse_args()
-    for name, gas, seed in (("tiny", 2, 11), ("tiny_gqa", 1, 12)):
-        rec = run(name, gas, seed)
-        path = os.path.join(a.out, f"{name}.npz")
-        np.savez_compressed(path, **rec)
-        print(path, os.path.getsize(path), "bytes", rec["meta"])
+    if a.only is None:
+        for name in FIXTURES:
+            subprocess.check_call([sys.executable, os.path.abspath(__file__), "--out", a.out, "--only", name])
+        return
+    gas, seed, precision = FIXTURES[a.only]
+    torch.set_num_threads(min(8, os.cpu_count() or 8))
+    rec = run(a.only, gas, seed, precision=precision)
+    path = os.path.join(a.out, f"{a.only}.npz")
+    np.savez_compressed(path, **rec)
+    print(path, os.path.getsize(path), "bytes", rec["meta"])
 
 
 if __name__ == "__main__":

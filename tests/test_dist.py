@@ -21,17 +21,67 @@ def _port():
     return p
 
 
-def test_shard_batches_partition():
-    from projectiontrainer_amd.dist import shard_batches
-    for n, bs, world in ((10, 3, 2), (64, 8, 4), (7, 2, 3)):
+def test_shard_batches_even_batches():
+    """accelerate's even_batches: every rank gets the same number of full batches (world > 1), every sample
+    is covered, the filler indices come from the start of the permutation; world 1 keeps the short batch."""
+    from projectiontrainer_amd.dist import batches_per_rank, shard_batches
+    for n, bs, world in ((10, 3, 2), (64, 8, 4), (7, 2, 3), (5, 4, 3), (1, 2, 2), (16, 4, 4)):
         parts = [shard_batches(n, bs, r, world, epoch=1) for r in range(world)]
-        allidx = torch.cat([torch.cat(p) for p in parts if p]).tolist()
-        assert sorted(allidx) == list(range(n))
         counts = [len(p) for p in parts]
-        assert max(counts) - min(counts) <= 1
+        assert len(set(counts)) == 1 and counts[0] == batches_per_rank(n, bs, world), (n, bs, world, counts)
+        assert all(len(b) == bs for p in parts for b in p)
+        allidx = torch.cat([torch.cat(p) for p in parts]).tolist()
+        assert set(allidx) == set(range(n))
+    one = shard_batches(7, 2, 0, 1, epoch=0)
+    assert [len(b) for b in one] == [2, 2, 2, 1]
     # deterministic per epoch, different across epochs
     assert torch.equal(torch.cat(shard_batches(20, 4, 0, 1, 0)), torch.cat(shard_batches(20, 4, 0, 1, 0)))
     assert not torch.equal(torch.cat(shard_batches(20, 4, 0, 1, 0)), torch.cat(shard_batches(20, 4, 0, 1, 1)))
+
+
+def test_shard_batches_matches_accelerate():
+    """Index for index the batches accelerate's BatchSamplerShard (the reference's prepared DataLoader,
+    Stage1/projector_trainer.py:100-102) yields for the same permutation."""
+    from torch.utils.data import BatchSampler
+    from accelerate.data_loader import BatchSamplerShard
+    from projectiontrainer_amd.dist import shard_batches
+    for n in range(0, 30):
+        for bs in (1, 2, 3, 5):
+            for world in (1, 2, 3, 4):
+                order = torch.randperm(n, generator=torch.Generator().manual_seed(11)).tolist()
+                for r in range(world):
+                    ours = [b.tolist() for b in shard_batches(n, bs, r, world, epoch=0, seed=11)]
+                    ref = ([list(b) for b in BatchSampler(order, bs, False)] if world == 1 else
+                           [list(b) for b in BatchSamplerShard(BatchSampler(order, bs, False), world, r)])
+                    assert ours == ref, (n, bs, world, r)
+
+
+def test_uneven_dataset_world3_gloo_cpu():
+    """7 samples, bs 2, world 3, 2 epochs: every rank runs the same number of steps (no rank left waiting
+    in a collective), all batches are full, and the replicas stay identical."""
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(dist_worker.oracle_even_loop, args=(3, _port(), td), nprocs=3, join=True)
+        ps = [np.load(f"{td}/param{r}.npy") for r in range(3)]
+        sz = [np.load(f"{td}/sizes{r}.npy") for r in range(3)]
+        ls = [np.load(f"{td}/losses{r}.npy") for r in range(3)]
+    for r in (1, 2):
+        np.testing.assert_array_equal(ps[0], ps[r])
+        np.testing.assert_array_equal(ls[0], ls[r])
+    assert all(list(s) == [2, 2, 2, 2] for s in sz), sz
+
+
+def test_from_accelerator_cpu():
+    """An accelerate.Accelerator handed to the trainer (as train_projection_stage1.py:338 does) is wrapped
+    with the fields the trainer reads."""
+    from accelerate import Accelerator
+    from projectiontrainer_amd.dist import from_accelerator
+    acc = Accelerator(cpu=True, gradient_accumulation_steps=2)
+    st = from_accelerator(acc)
+    assert (st.num_processes, st.process_index, st.gradient_accumulation_steps) == (1, 0, 2)
+    assert st.is_main_process and st.sync_gradients and st.device == torch.device("cpu")
+    t = torch.tensor([1.5])
+    assert torch.equal(st.gather(t), t)
+    assert torch.equal(st.all_reduce_sum_(t.clone()), t)
 
 
 def test_ddp_grad_average_gloo_cpu():
@@ -94,3 +144,28 @@ def test_engine_ddp_two_ranks_one_gpu(gpu):
         g = eng.proj.flat_grad.clone()
         tot = g if tot is None else tot + g
     np.testing.assert_allclose(g0, tot.cpu().numpy(), rtol=1e-6, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_trainer_uneven_dataset_world3(gpu):
+    """The real ProjectionTrainerStage1 at world 3 (gloo, one device) on 7 samples at bs 2: it finishes,
+    every rank ran 2 steps per epoch, the replicas are identical, and the epoch loss is divided by the
+    per-rank batch count (len(train_loader) after prepare)."""
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(dist_worker.trainer_even, args=(3, _port(), td), nprocs=3, join=True)
+        ps = [np.load(f"{td}/param{r}.npy") for r in range(3)]
+        st = [np.load(f"{td}/steps{r}.npy") for r in range(3)]
+        ep = np.load(f"{td}/eploss0.npy")
+    for r in (1, 2):
+        np.testing.assert_array_equal(ps[0], ps[r])
+    assert all(int(s[0]) == 4 and int(s[1]) == 12 for s in st), st
+    assert len(ep) == 2 and all(5.0 < e < 7.5 for e in ep), ep   # mean of per-step losses (~ln 512)
+
+
+@pytest.mark.gpu
+def test_nccl_backend_world1(gpu):
+    """RCCL ("nccl" backend) initialised at world 1 on the GPU; the grad all-reduce and loss gather run on it."""
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(dist_worker.nccl_world1, args=(1, _port(), td), nprocs=1, join=True)
+        r = np.load(f"{td}/nccl.npy")
+    assert r[0] == 1 and r[1] == 3.0 and r[2] == 0.0 and r[3] == 1 and r[4] == 1, r
