@@ -1001,15 +1001,23 @@ static void dkv_plan(FlashBwdArgs& a, int nz, int& nslab, long& npieces, long& n
     total += hi - lo;
   }
   const int ncu = num_cus();
-  const int base = (int)std::max(4L, (total * nz + ncu - 1) / ncu);
+  // the work-item table holds 128 (slab, piece) entries: a target is admissible only if its pieces fit
+  auto items_for = [&](int t) {
+    long items = 0;
+    a.dkv_target = t;
+    for (int s = 0; s < nslab; ++s) items += dkv_pieces(a, s);
+    return items;
+  };
+  int base = (int)std::max(4L, (total * nz + ncu - 1) / ncu);
+  // few z (small batch, long sequence): the one-piece-per-CU target would cut slabs into more pieces than
+  // the table holds; raise it until they fit (one piece per slab always does: nslab <= 128 is checked by
+  // the caller)
+  while (items_for(base) > 128 && base <= total) base += std::max(1, base / 8);
   int best = base;
   double best_span = dkv_makespan(a, nz, nslab, base, ncu);
   for (int k = 9; k >= 3; --k) {   // targets base * k / 12 (3/4 .. 1/4)
     const int t = std::max(4, base * k / 12);
-    long items = 0;
-    a.dkv_target = t;
-    for (int s = 0; s < nslab; ++s) items += dkv_pieces(a, s);
-    if (items > 128) break;
+    if (items_for(t) > 128) break;
     const double sp = dkv_makespan(a, nz, nslab, t, ncu);
     if (sp < best_span - 1e-9) { best_span = sp; best = t; }
   }
@@ -1075,7 +1083,7 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs*
         b.dkv_items = nslab;
         for (int s = 0; s < nslab && s < 128; ++s) { b.dkv_item_slab[s] = (unsigned char)s; b.dkv_item_piece[s] = 0; }
       }
-      if (b.dkv_items > 128 || nslab > 255) return set_error("attn_bwd: %d dK/dV work items (max 128)", b.dkv_items);
+      if (b.dkv_items > 128 || nslab > 128) return set_error("attn_bwd: %d dK/dV work items over %d key slabs (max 128)", b.dkv_items, nslab);
       hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
       // 32 keys per wave (one wave per SIMD) measured 209 us vs 252 us for 16 keys per wave (two per
       // SIMD, which spills the precomputed transposed-read addresses) at cfg2

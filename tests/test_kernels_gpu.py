@@ -359,15 +359,17 @@ def test_flash_fwd_gemma_layout(gpu, Hkv, G, window):
     torch.testing.assert_close(lg, lref, rtol=1e-3, atol=1e-3)
 
 
-@pytest.mark.parametrize("D,Hkv,G,window,S,split", [(256, 1, 4, 0, 320, True), (256, 1, 4, 0, 320, False),
-                                                     (256, 1, 4, 100, 320, True), (256, 2, 2, 64, 320, True),
-                                                     (256, 1, 4, 0, 704, True), (64, 1, 2, 8, 320, True)])
-def test_flash_bwd_vs_autograd(gpu, D, Hkv, G, window, S, split):
+@pytest.mark.parametrize("D,Hkv,G,window,S,split,B", [(256, 1, 4, 0, 320, True, 2), (256, 1, 4, 0, 320, False, 2),
+                                                       (256, 1, 4, 100, 320, True, 2), (256, 2, 2, 64, 320, True, 2),
+                                                       (256, 1, 4, 0, 704, True, 2), (64, 1, 2, 8, 320, True, 2),
+                                                       (256, 1, 4, 512, 1088, True, 1), (256, 1, 4, 0, 1088, True, 1)])
+def test_flash_bwd_vs_autograd(gpu, D, Hkv, G, window, S, split, B):
     """dQ/dK/dV of softmax(scale QK^T + causal/window/key-pad mask) V vs torch autograd (fp32 math on the
     same bf16 inputs).  Uses the forward kernel's O and LSE as the backward does.  split: heavy key slabs
-    cut into query pieces (fp32 partials + ordered reduce) vs one piece per slab; S 704 = the cfg2 length."""
+    cut into query pieces (fp32 partials + ordered reduce) vs one piece per slab; S 704 = the cfg2 length;
+    S 1088 at batch 1 = the reference's default T 512 (few z: the split plan must stay within its
+    128-entry work table)."""
     Kn, L = _k()
-    B = 2
     Hq = Hkv * G
     Q = rnd(B * Hkv, S * G, D, dev=gpu, seed=51)
     Kt = rnd(B * Hkv, S, D, dev=gpu, seed=52)
@@ -375,7 +377,7 @@ def test_flash_bwd_vs_autograd(gpu, D, Hkv, G, window, S, split):
     dO = rnd(B * Hkv, S * G, D, dev=gpu, seed=54)
     kv = torch.ones(B, S, dtype=torch.int32, device=gpu)
     kv[0, 200:215] = 0
-    kv[1, S - 30:] = 0
+    kv[B - 1, S - 30:] = 0
     scale = D ** -0.5
     O = torch.zeros(B * Hkv, S * G, D, dtype=torch.bfloat16, device=gpu)
     lse = torch.zeros(B * Hkv, S * G, dtype=torch.float32, device=gpu)

@@ -2,7 +2,8 @@
 
 Fixtures come from running Stage1/projector_trainer.py (reference) on CPU in
 fp32 (tests/golden/make_golden.py).  fp32 restatement vs fp32 reference:
-tolerance rtol 1e-4 / atol 1e-6 (different op order in matmul/softmax)."""
+tolerance rtol 1e-4 / atol 1e-6 (different op order in matmul/softmax); post-AdamW
+params atol 0.05 lr (a grad near zero makes Adam's m / sqrt(v) sensitive to that order)."""
 import numpy as np
 import pytest
 import torch
@@ -10,21 +11,26 @@ import torch
 from oracle import stage1_ref as R
 from tests import golden_util as G
 
-CASES = ["tiny", "tiny_gqa"]
+CASES = ["tiny", "tiny_gqa", "cfg1"]          # fp32 reference runs (cfg1: SigLIP-B/16-224 + Gemma3-1B)
+ALL = CASES + ["tiny_bf16", "cfg1_bf16"]      # + the --mixed_precision bf16 runs
 
 
-@pytest.mark.parametrize("name", CASES)
+def rms(t):
+    return float(t.double().pow(2).mean().sqrt())
+
+
+@pytest.mark.parametrize("name", ALL)
 def test_weight_generator_stable(name):
     d, _ = G.load(name)
-    cfg, vp, lp, pp = G.params_for(name)
+    cfg, vp, lp, pp = G.params_for(name.replace("_bf16", ""))    # fingerprint of the fp32 generator output
     np.testing.assert_array_equal(G.fingerprint(vp, lp, pp), d["weight_fingerprint"])
 
 
-@pytest.mark.parametrize("name", CASES)
+@pytest.mark.parametrize("name", ALL)
 def test_batch_contract(name):
     """labels = ids with pad -> -100; vision labels -100; mask = 1 for vision, ids != pad."""
     d, _ = G.load(name)
-    cfg = G.PRESETS[name]
+    cfg = G.PRESETS[name.replace("_bf16", "")]
     for s in (0, 1):
         ids = d[f"s{s}_token_ids"]
         nv = cfg.num_vision_tokens
@@ -37,7 +43,7 @@ def test_batch_contract(name):
 
 @pytest.mark.parametrize("name", CASES)
 def test_oracle_matches_reference_two_steps(name):
-    torch.set_num_threads(4)
+    torch.set_num_threads(8)
     d, meta = G.load(name)
     cfg, vp, lp, pp = G.params_for(name)
     state = R.init_state(pp)
@@ -46,11 +52,13 @@ def test_oracle_matches_reference_two_steps(name):
     for s in range(meta["steps"]):
         out = R.stage1_step(vp, cfg.vision, lp, cfg.text, state, G.batch(d, s), sc)
         G.check_tensor(d, f"s{s}_patch", out["patch"], 1e-4, 1e-5)
-        G.check_tensor(d, f"s{s}_proj", out["proj"], 1e-4, 1e-5)
+        G.check_tensor(d, f"s{s}_proj", out["proj"], 1e-4, 5e-5)
         np.testing.assert_allclose(float(out["loss"]), float(d[f"s{s}_loss"]), rtol=1e-5)
         np.testing.assert_allclose(out["lr"], float(d[f"s{s}_lr"]), rtol=1e-12)
-        G.check_tensor(d, f"s{s}_d_proj", out["d_proj"], 1e-3, 1e-7)
+        # grads: rtol 1e-3 plus an absolute floor of 2e-4 x the tensor's rms (elements near zero carry
+        # the fp32 summation-order noise of the 26-layer backward at cfg1 dims)
+        G.check_tensor(d, f"s{s}_d_proj", out["d_proj"], 1e-3, max(1e-7, 2e-4 * rms(out["d_proj"])))
         for k in pp:
-            G.check_tensor(d, f"s{s}_grad.{k}", out["grads"][k], 1e-3, 1e-7)
-            G.check_tensor(d, f"s{s}_clipped.{k}", out["clipped"][k], 1e-3, 1e-7)
-            G.check_tensor(d, f"s{s}_param.{k}", state.params[k], 1e-5, 2e-6)
+            G.check_tensor(d, f"s{s}_grad.{k}", out["grads"][k], 1e-3, max(1e-7, 2e-4 * rms(out["grads"][k])))
+            G.check_tensor(d, f"s{s}_clipped.{k}", out["clipped"][k], 1e-3, max(1e-7, 2e-4 * rms(out["clipped"][k])))
+            G.check_tensor(d, f"s{s}_param.{k}", state.params[k], 1e-5, 0.05 * meta["lr"])   # Adam: ~lr per step

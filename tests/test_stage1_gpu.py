@@ -1,18 +1,34 @@
 """Whole-step parity of the HIP Stage-1 path.
 
 1. Against the reference's own golden fixtures (tests/golden/*.npz, produced by
-   running Stage1/projector_trainer.py on CPU in fp32): two full optimizer
-   steps (SigLIP fwd, projector, Gemma3 fwd/loss/bwd, clip, AdamW, schedule).
+   running Stage1/projector_trainer.py on CPU): two full optimizer steps (SigLIP
+   fwd, projector, Gemma3 fwd/loss/bwd, clip, AdamW, schedule) at
+   * tiny dims, fp32 (tiny, tiny_gqa) and under `--mixed_precision bf16` (tiny_bf16);
+   * BASELINE cfg1 dims (SigLIP-B/16-224 + the full 26-layer Gemma3-1B, vocab
+     262144, bs 2, T 64), fp32 (cfg1) and bf16 (cfg1_bf16).
 2. Against the CPU oracle at architecture-true sizes (SigLIP-L/16-384 and
-   Gemma3-1B dims, fewer layers, S = 703 > sliding window 512).
+   Gemma3-1B dims at full depth, S = 703 > sliding window 512, and T = 512).
 
-Tolerances (bf16 GEMM operands vs the fp32 reference, stated by north_star's
-"stated fp tolerance"): loss |d| <= 2e-2 abs; projector output / patch
-embeddings rel-L2 <= 2e-2; projector grads cosine >= 0.999 and rel-L2 <= 3e-2;
-post-AdamW params: max |d| <= 2.5 * sum(lr so far) (Adam's early steps move each
-weight by ~lr, so a sign flip of a near-zero bf16-vs-fp32 grad moves it by at most
-~2 lr per step) and median |d| <= 0.05 * lr.
+Tolerances.  Every fixture has a twin made from the same weights and batch at the
+other precision (tiny / tiny_bf16, tiny_gqa / tiny_gqa_bf16, cfg1 / cfg1_bf16), so
+the reference's OWN mixed-precision noise is known per tensor:
+noise = rel-L2 / cosine of the reference's bf16 run against its fp32 run.  The HIP
+path (bf16 GEMM operands, fp32 accumulation, SURVEY F8 flow) must agree with either
+reference run at least as closely as the two reference runs agree with each other
+(x1.5), and within SURVEY.md:297's bar wherever that noise is below it:
+  loss |d| <= 2e-2 abs;
+  patch embeddings / projector output / d(projector output) / projector grads:
+    rel-L2 <= max(2e-2, 1.5 * noise_rel_l2), cosine >= min(0.999, 1 - 1.5 * (1 - noise_cos));
+  post-AdamW params: max |d| <= 2.5 * sum(lr so far) (Adam's early steps move each weight by
+    ~lr, so a sign flip of a near-zero grad moves it by at most ~2 lr per step) and
+    median |d| <= 0.05 * lr.
+(Measured, cfg1: the reference's bf16 run vs its fp32 run is at rel-L2 0.04 / cos 0.9992 on
+d(projector output) after one step and 0.11 / 0.994 after two.)  Every measured value is
+appended to gpurun_out/parity_metrics.jsonl (when that directory exists).
 """
+import json
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -20,6 +36,16 @@ import torch
 from tests import golden_util as G
 
 pytestmark = pytest.mark.gpu
+
+LOSS_TOL, RL2, COS = 2e-2, 2e-2, 0.999
+_LOG = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "gpurun_out",
+                    "parity_metrics.jsonl")
+
+
+def record(test, key, **vals):
+    if os.path.isdir(os.path.dirname(_LOG)):
+        with open(_LOG, "a") as f:
+            f.write(json.dumps({"test": test, "key": key, **{k: float(v) for k, v in vals.items()}}) + "\n")
 
 
 def rel_l2(a, b):
@@ -32,24 +58,51 @@ def cosine(a, b):
     return float(a @ b / max(np.linalg.norm(a) * np.linalg.norm(b), 1e-30))
 
 
-def compare(d, key, got, rl2, cos=None, atol=None, med=None):
+def _stored(d, key):
+    if key in d.files:
+        return d[key]
+    k, _, _ = G.sub_key(d, key)
+    return d[k]
+
+
+def twin_noise(name, key):
+    """(rel-L2, cosine) of the reference's bf16 run against its fp32 run for one fixture tensor."""
+    base = name.replace("_bf16", "")
+    a, _ = G.load(base)
+    b, _ = G.load(base + "_bf16")
+    x, y = _stored(a, key), _stored(b, key)
+    return rel_l2(y, x), cosine(y, x)
+
+
+def compare(d, key, got, rl2, cos=None, atol=None, med=None, test="", name=None):
     got = got.detach().double().cpu().numpy() if torch.is_tensor(got) else np.asarray(got)
+    if name is not None and atol is None:
+        n_rl2, n_cos = twin_noise(name, key)
+        rl2 = max(rl2, 1.5 * n_rl2)
+        if cos is not None:
+            cos = min(cos, 1.0 - 1.5 * (1.0 - n_cos))
     if key in d.files:
         ref = d[key]
         g = got
     else:
-        ref = d[key + "@rows16"]
-        g = got[::16]
-        np.testing.assert_allclose(np.linalg.norm(got), float(d[key + "@norm"]), rtol=max(rl2 or 0.0, 1e-3), err_msg=key)
+        k, sr, sc = G.sub_key(d, key)
+        ref, g = d[k], G.sub_sample(got, sr, sc)
+        nrel = abs(np.linalg.norm(got) / float(d[key + "@norm"]) - 1.0)
+        record(test, key + "@norm", rel=nrel)
+        assert nrel <= max(rl2 or 0.0, 1e-3), (key, "norm", nrel)
     if atol is not None:
-        assert np.max(np.abs(g - ref)) <= atol, (key, np.max(np.abs(g - ref)))
+        mx, md = np.max(np.abs(g - ref)), np.median(np.abs(g - ref))
+        record(test, key, max_abs=mx, median_abs=md, atol=atol)
+        assert mx <= atol, (key, mx)
         if med is not None:
-            assert np.median(np.abs(g - ref)) <= med, (key, np.median(np.abs(g - ref)))
+            assert md <= med, (key, md)
     else:
         r = rel_l2(g, ref)
-        assert r <= rl2, (key, r)
+        c = cosine(g, ref) if cos is not None else 1.0
+        record(test, key, rel_l2=r, cos=c, tol_rel_l2=rl2, tol_cos=cos if cos is not None else 0.0)
+        assert r <= rl2, (key, r, rl2)
         if cos is not None:
-            assert cosine(g, ref) >= cos, (key, cosine(g, ref))
+            assert c >= cos, (key, c, cos)
 
 
 def build_engine(name, gpu, gas, lr, total):
@@ -67,48 +120,59 @@ def build_engine(name, gpu, gas, lr, total):
     return cfg, eng
 
 
-@pytest.mark.parametrize("name", ["tiny", "tiny_gqa"])
+@pytest.mark.parametrize("name", ["tiny", "tiny_gqa", "tiny_bf16", "tiny_gqa_bf16", "cfg1", "cfg1_bf16"])
 def test_two_steps_vs_reference_golden(gpu, name):
     d, meta = G.load(name)
     cfg, eng = build_engine(name, gpu, meta["gas"], meta["lr"], meta["max_train_steps"])
     N, Nv = cfg.vision.num_patches, cfg.num_vision_tokens
     lr_sum = 0.0
+    t = f"golden[{name}]"
     for s in range(meta["steps"]):
         px, ids, labels = G.batch(d, s)
         loss = eng.forward_backward(torch.from_numpy(px).to(gpu), torch.from_numpy(ids).to(gpu),
                                     torch.from_numpy(labels).to(gpu))
         torch.cuda.synchronize()
-        assert abs(float(loss) - float(d[f"s{s}_loss"])) <= 2e-2, (float(loss), float(d[f"s{s}_loss"]))
+        dl = abs(float(loss) - float(d[f"s{s}_loss"]))
+        record(t, f"s{s}_loss", abs=dl)
+        assert dl <= LOSS_TOL, (float(loss), float(d[f"s{s}_loss"]))
         vis = eng.vis.view(cfg.batch_size, N, -1)[:, 1:].float()
-        compare(d, f"s{s}_patch", vis, 2e-2)
+        compare(d, f"s{s}_patch", vis, RL2, cos=COS, test=t, name=name)
         xv = eng.x.view(cfg.batch_size, eng.Sp, -1)[:, :Nv]
-        compare(d, f"s{s}_proj", xv, 2e-2)
+        compare(d, f"s{s}_proj", xv, RL2, cos=COS, test=t, name=name)
         dxv = eng.dx.view(cfg.batch_size, eng.Sp, -1)[:, :Nv]
-        compare(d, f"s{s}_d_proj", dxv, 5e-2, cos=0.998)
+        compare(d, f"s{s}_d_proj", dxv, RL2, cos=COS, test=t, name=name)
         for k, g in zip(["model.0.weight", "model.0.bias", "model.2.weight", "model.2.bias"], eng.proj.grads()):
-            compare(d, f"s{s}_grad.{k}", g, 5e-2, cos=0.998)
+            compare(d, f"s{s}_grad.{k}", g, RL2, cos=COS, test=t, name=name)
         eng.optimizer_step()
         torch.cuda.synchronize()
         assert abs(eng.last_lr - float(d[f"s{s}_lr"])) <= 1e-12
         lr_sum += eng.last_lr
         for k, p in zip(["model.0.weight", "model.0.bias", "model.2.weight", "model.2.bias"],
                         [eng.proj.w1, eng.proj.b1, eng.proj.w2, eng.proj.b2]):
-            compare(d, f"s{s}_param.{k}", p, None, atol=2.5 * lr_sum + 1e-6, med=0.05 * meta["lr"])
+            compare(d, f"s{s}_param.{k}", p, None, atol=2.5 * lr_sum + 1e-6, med=0.05 * meta["lr"], test=t)
 
 
 @pytest.mark.slow
-@pytest.mark.parametrize("preset,bs,T", [("cfg2", 2, 128), ("cfg5", 1, 256)])
-def test_architecture_scale_vs_oracle(gpu, preset, bs, T):
-    """SigLIP-L/16-384 (2 layers) + Gemma3 dims (6 layers: sliding x5 + full) vs the fp32 CPU oracle.
-    cfg2: Gemma3-1B, bs 2, T 128 (S = 703 > window 512, left-padded captions).
-    cfg5: Gemma3-4B (hidden 2560, GQA 8:4, window 1024, linear RoPE x8 on the full layer, vocab
-    262 208 = 4 097 x 64, which leaves a remainder slice in the split-K lm_head backward), bs 1, T 256."""
+@pytest.mark.parametrize("preset,bs,T,vl,tl", [("cfg2", 2, 128, None, None), ("cfg2", 1, 512, None, None),
+                                               ("cfg5", 1, 256, 2, 6)])
+def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
+    """Full architecture vs the fp32 CPU oracle (the oracle is pinned to the reference by the fixtures).
+    cfg2: SigLIP-L/16-384 (24 layers) + Gemma3-1B (26 layers) at bs 2, T 128 (S = 703 > window 512,
+    left-padded captions), and at the reference's default caption length T = 512
+    (train_projection_stage1.py:27; S = 1087, bs 1).
+    cfg5: Gemma3-4B dims (hidden 2560, GQA 8:4, window 1024, linear RoPE x8 on the full layer, vocab
+    262 208 = 4 097 x 64, which leaves a remainder slice in the split-K lm_head backward) at 2 SigLIP and
+    6 Gemma layers, bs 1, T 256.
+    The HIP path runs the reference's bf16 flow (pure-bf16 SigLIP, bf16 GEMM operands) and the
+    oracle fp32, so these tolerances bound the bf16-vs-fp32 difference of the whole step."""
     from oracle import stage1_ref as R
     from projectiontrainer_amd import weights as W
     from projectiontrainer_amd.config import PRESETS
     cfg = PRESETS[preset]
-    cfg = cfg.replace(vision=cfg.vision.__class__(**{**cfg.vision.__dict__, "num_hidden_layers": 2}),
-                      text=cfg.text.__class__(**{**cfg.text.__dict__, "num_hidden_layers": 6}),
+    v_kw = {} if vl is None else {"num_hidden_layers": vl}
+    t_kw = {} if tl is None else {"num_hidden_layers": tl}
+    cfg = cfg.replace(vision=cfg.vision.__class__(**{**cfg.vision.__dict__, **v_kw}),
+                      text=cfg.text.__class__(**{**cfg.text.__dict__, **t_kw}),
                       batch_size=bs, text_len=T)
     vp = W.siglip_vision_params(cfg.vision, seed=3)
     lp = W.gemma3_params(cfg.text, seed=4)
@@ -127,21 +191,30 @@ def test_architecture_scale_vs_oracle(gpu, preset, bs, T):
     loss = eng.forward_backward(torch.from_numpy(px).to(gpu), torch.from_numpy(ids).to(gpu),
                                 torch.from_numpy(labels).to(gpu))
     torch.cuda.synchronize()
+    N, Nv = cfg.vision.num_patches, cfg.num_vision_tokens
+    vis = eng.vis.view(bs, N, -1)[:, 1:].float().cpu()
+    xv = eng.x.view(bs, eng.Sp, -1)[:, :Nv].cpu()
+    dxv = eng.dx.view(bs, eng.Sp, -1)[:, :Nv].cpu()
+    grads = [g.cpu() for g in eng.proj.grads()]
+    loss = float(loss)
+    del eng, lm, vt
+    torch.cuda.empty_cache()
     torch.set_num_threads(min(16, torch.get_num_threads()))
     st = R.init_state(pp)
     out = R.stage1_step(vp, cfg.vision, lp, cfg.text, st, (px, ids, labels), R.StepConfig(gradient_accumulation_steps=1),
                         embed_dtype=torch.bfloat16)
-    assert abs(float(loss) - float(out["loss"])) <= 2e-2, (float(loss), float(out["loss"]))
-    N, Nv = cfg.vision.num_patches, cfg.num_vision_tokens
-    vis = eng.vis.view(bs, N, -1)[:, 1:].float().cpu()
-    assert rel_l2(vis, out["patch"]) <= 3e-2
-    xv = eng.x.view(bs, eng.Sp, -1)[:, :Nv].cpu()
-    assert rel_l2(xv, out["proj"]) <= 3e-2
-    dxv = eng.dx.view(bs, eng.Sp, -1)[:, :Nv].cpu()
-    assert cosine(dxv, out["d_proj"]) >= 0.995, cosine(dxv, out["d_proj"])
-    for k, g in zip(["model.0.weight", "model.0.bias", "model.2.weight", "model.2.bias"], eng.proj.grads()):
-        gc, rc = g.cpu(), out["grads"][k]
-        assert cosine(gc, rc) >= 0.995 and rel_l2(gc, rc) <= 6e-2, (k, cosine(gc, rc), rel_l2(gc, rc))
+    t = f"arch[{preset}-bs{bs}-T{T}]"
+    # no reference twin at these sizes: the bar is SURVEY.md:297's, with rel-L2 on the backward quantities
+    # widened to the reference's own bf16-vs-fp32 noise measured at cfg1 (0.04 on d(projector output))
+    record(t, "loss", abs=abs(loss - float(out["loss"])))
+    assert abs(loss - float(out["loss"])) <= LOSS_TOL, (loss, float(out["loss"]))
+    for key, got, ref, rtol in (("patch", vis, out["patch"], RL2), ("proj", xv, out["proj"], RL2),
+                                ("d_proj", dxv, out["d_proj"], 4e-2)) + tuple(
+            ("grad." + k, gc, out["grads"][k], 4e-2)
+            for k, gc in zip(["model.0.weight", "model.0.bias", "model.2.weight", "model.2.bias"], grads)):
+        r, c = rel_l2(got, ref), cosine(got, ref)
+        record(t, key, rel_l2=r, cos=c, tol_rel_l2=rtol, tol_cos=COS)
+        assert r <= rtol and c >= COS, (key, r, c)
 
 
 @pytest.mark.slow
