@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTK_ABI_VERSION 1
+#define PTK_ABI_VERSION 2
 
 int ptk_abi_version(void);
 const char* ptk_last_error(void);
@@ -259,16 +259,58 @@ typedef struct {
 typedef struct {
   int batch, text_len, num_vision, seq_pad;   /* S = num_vision + text_len <= seq_pad, seq_pad % 64 == 0 */
   const int64_t* token_ids;                   /* [B, T] */
-  const int64_t* labels;                      /* [B, T] (pad -> -100) */
+  const int64_t* labels;                      /* [B, T - label_offset] (pad -> -100): targets of text positions
+                                                 label_offset .. T-1 */
   float* x;        /* f32 [B*seq_pad, H]: vision rows pre-filled; text/pad rows written here */
   float* dx;       /* f32 [B*seq_pad, H]: out, d(loss*loss_scale)/dx */
   float loss_scale;
   float* loss;     /* device f32 [1]: mean CE over valid targets */
+  /* text positions before label_offset carry no target (Stage 1: 0; Stage 2: the question length, whose
+   * labels are -100 at Stage2/trainer.py:390-396): their logits are never computed */
+  int label_offset;
 } ptk_gemma3_batch;
 
 size_t ptk_gemma3_workspace_bytes(const ptk_gemma3_config* c, int batch, int text_len, int seq_pad);
 int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_batch* b,
                             void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * Gemma3 forward + loss + FULL backward (unfrozen LLM, Stage 2, cfg4)       *
+ * replaces language_model(inputs_embeds, attention_mask) + the manual CE   *
+ * + accelerator.backward(loss) of VQATrainerStage2.train                  *
+ * (Stage2/trainer.py:339-423): d(inputs_embeds) as the frozen path, plus   *
+ * every parameter's gradient ACCUMULATED into caller-owned bf16 .grad      *
+ * buffers (bf16(grad + bf16(g)), autograd's accumulation into bf16 params, *
+ * train_vqa_stage2.py:180-187 loads the LLM in bf16).  The tied embedding  *
+ * receives the lm_head term and the question/answer-embedding term         *
+ * (trainer.py:351-360).  Grads must be zeroed by the caller (zero_grad).   *
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  void* wqkv; void* wo; void* wgu; void* wd;    /* bf16, the layouts of ptk_gemma3_layer (wgu interleaved) */
+  void* ln_in; void* ln_post_attn; void* ln_pre_ff; void* ln_post_ff;   /* bf16 [H] */
+  void* q_norm; void* k_norm;                                           /* bf16 [hd] */
+} ptk_gemma3_layer_grads;
+
+typedef struct {
+  void* embed;        /* bf16 [V, H] (tied lm_head + input embedding) */
+  void* final_norm;   /* bf16 [H] */
+  const ptk_gemma3_layer_grads* layers;   /* HOST array [layers] */
+} ptk_gemma3_grads;
+
+size_t ptk_gemma3_train_workspace_bytes(const ptk_gemma3_config* c, int batch, int text_len, int seq_pad);
+int ptk_gemma3_train_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_batch* b,
+                             const ptk_gemma3_grads* g, void* ws, size_t ws_bytes, void* stream);
+
+/* clip_grad_norm_ + AdamW over bf16 parameters (Stage2/trainer.py:426-443, optimizer :145-149).
+ * ptk_bf16_grad_scale_sumsq: g = bf16(g * scale) in place (scale 1: untouched), *out = sum g^2 (fp32,
+ * deterministic; partial: >= ptk_bf16_sumsq_partial_floats() floats).  Sum the *out of every shard / rank
+ * first (all-reduce), then ptk_adamw_bf16 clips by max_norm (<= 0: no clip) with that total and applies
+ * AdamW with every tensor op rounded to bf16, as torch's single-tensor AdamW on bf16 parameters. */
+int ptk_bf16_sumsq_partial_floats(void);
+int ptk_bf16_grad_scale_sumsq(void* g, int64_t n, float scale, float* partial, float* out, void* stream);
+int ptk_adamw_bf16(void* params, void* grads, void* exp_avg, void* exp_avg_sq, int64_t n, const float* sumsq_total,
+                   float max_norm, double lr, double beta1, double beta2, double eps, double weight_decay, int step,
+                   float* norm_out, void* stream);
 
 /* ------------------------------------------------------------------------ *
  * clip_grad_norm_(max_norm) + AdamW over a flat f32 parameter buffer        *

@@ -102,7 +102,16 @@ class Gemma3WeightsC(C.Structure):
 class Gemma3BatchC(C.Structure):
     _fields_ = [("batch", c_int), ("text_len", c_int), ("num_vision", c_int), ("seq_pad", c_int),
                 ("token_ids", c_void_p), ("labels", c_void_p), ("x", c_void_p), ("dx", c_void_p),
-                ("loss_scale", c_float), ("loss", c_void_p)]
+                ("loss_scale", c_float), ("loss", c_void_p), ("label_offset", c_int)]
+
+
+class Gemma3LayerGradsC(C.Structure):
+    _fields_ = [(n, c_void_p) for n in ("wqkv", "wo", "wgu", "wd", "ln_in", "ln_post_attn", "ln_pre_ff",
+                                        "ln_post_ff", "q_norm", "k_norm")]
+
+
+class Gemma3GradsC(C.Structure):
+    _fields_ = [("embed", c_void_p), ("final_norm", c_void_p), ("layers", C.POINTER(Gemma3LayerGradsC))]
 
 
 class ImageDesc(C.Structure):
@@ -110,6 +119,8 @@ class ImageDesc(C.Structure):
                 ("kh", C.c_int32), ("kv", C.c_int32), ("pad_", C.c_int32),
                 ("coef_off", c_int64), ("tmp_off", c_int64)]
 
+
+ABI_VERSION = 2      # include/ptk.h PTK_ABI_VERSION
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -147,6 +158,14 @@ SIGNATURES = {
     "ptk_gemma3_workspace_bytes": (c_size_t, [C.POINTER(Gemma3ConfigC), c_int, c_int, c_int]),
     "ptk_gemma3_loss_fwd_bwd": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC),
                                         C.POINTER(Gemma3BatchC), c_void_p, c_size_t, c_void_p]),
+    "ptk_gemma3_train_workspace_bytes": (c_size_t, [C.POINTER(Gemma3ConfigC), c_int, c_int, c_int]),
+    "ptk_gemma3_train_fwd_bwd": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC),
+                                         C.POINTER(Gemma3BatchC), C.POINTER(Gemma3GradsC), c_void_p, c_size_t,
+                                         c_void_p]),
+    "ptk_bf16_sumsq_partial_floats": (c_int, []),
+    "ptk_bf16_grad_scale_sumsq": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p]),
+    "ptk_adamw_bf16": (c_int, [c_void_p] * 4 + [c_int64, c_void_p, c_float] + [C.c_double] * 5 +
+                       [c_int, c_void_p, c_void_p]),
     "ptk_resize_ksize": (c_int, [c_int, c_int]),
     "ptk_resize_coeffs": (c_int, [c_int, c_int, c_void_p, c_void_p]),
     "ptk_image_preprocess": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
@@ -174,7 +193,7 @@ def lib():
                 continue   # an older diagnostic build may predate an entry point
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
-        if L.ptk_abi_version() != 1:
+        if L.ptk_abi_version() != ABI_VERSION:
             raise PtkError("libptk ABI version mismatch")
         _lib = L
     return _lib

@@ -103,6 +103,9 @@ struct GemmaLayerSave {
   float *x2, *rstd_in, *rstd_ao, *rstd_pre, *rstd_dn, *rstd_q, *rstd_k;
   bf16_t *qkv, *Q, *K, *V, *O, *ao, *g, *u, *dn;
   float* lse;
+  // unfrozen LLM only: the GEMM inputs the weight grads contract with (input-norm / pre-ff-norm outputs,
+  // GEGLU output); the frozen path keeps them in one scratch buffer
+  bf16_t *xn_in = nullptr, *xn_ff = nullptr, *h = nullptr;
 };
 struct GemmaWs {
   std::vector<float*> x;          // L+1 residual-stream snapshots
@@ -112,9 +115,12 @@ struct GemmaWs {
   float* dkv_part;          // split-query dK/dV partials of the attention backward
   size_t dkv_part_bytes;
   int32_t* key_valid;
+  // unfrozen LLM only: feature-major GEMM operands of dW = dY^T X (K = tokens) and norm-grad partials
+  bf16_t *TA = nullptr, *TB = nullptr, *TL = nullptr, *TX = nullptr;
+  float* wpart = nullptr;
 };
 
-GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp) {
+GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp, bool train = false) {
   const long H = c->hidden, I = c->inter, D = c->head_dim, Hq = c->heads, Hkv = c->kv_heads, G = Hq / Hkv;
   const long M = (long)B * Sp, Dq = Hq * D, Dqkv = (Hq + 2 * Hkv) * D, R = (long)B * T, V = c->vocab;
   const long Z = (long)B * Hkv, SG = (long)Sp * G;
@@ -141,6 +147,11 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp)
     s.g = bp.take<bf16_t>(M * I);
     s.u = bp.take<bf16_t>(M * I);
     s.dn = bp.take<bf16_t>(M * H);
+    if (train) {
+      s.xn_in = bp.take<bf16_t>(M * H);
+      s.xn_ff = bp.take<bf16_t>(M * H);
+      s.h = bp.take<bf16_t>(M * I);
+    }
     w.L.push_back(s);
   }
   w.P = nullptr;
@@ -181,7 +192,31 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp)
   w.dxf_part = bp.take<float>((long)(LM_SPLITK + 1) * R * H);   // + one slot for a vocab remainder
   w.count = bp.take<float>(4);
   w.gscale = bp.take<float>(4);
+  if (train) {
+    const long Rp = (R + 63) / 64 * 64;
+    w.TA = bp.take<bf16_t>(std::max(std::max(2 * I, Dqkv), H) * M);
+    w.TB = bp.take<bf16_t>(std::max(std::max(H, Dq), I) * M);
+    w.TL = bp.take<bf16_t>(V * Rp);
+    w.TX = bp.take<bf16_t>(H * Rp);
+    w.wpart = bp.take<float>(std::max((long)rms_wgrad_partial_floats((int)M, (int)H), 2 * ((M + 63) / 64) * D));
+  }
   return w;
+}
+
+// dW (+)= dY^T X over K token rows: both operands are token-major, so each is first transposed to a
+// K-contiguous feature-major copy (rows gathered through a map, zero-padded to a multiple of 64), then one
+// MFMA GEMM accumulates into the bf16 .grad (bf16(grad + bf16(acc)), autograd's accumulation).
+int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* x, long ldx, RowMap xmap, int Nx,
+                int rows, bf16_t* TA, bf16_t* TB, void* grad, hipStream_t st) {
+  if (!grad) return 0;
+  const int Kp = (rows + 63) / 64 * 64;
+  CK(launch_transpose_rows(dy, lddy, ymap, rows, Ny, TA, Kp, Kp, st));
+  CK(launch_transpose_rows(x, ldx, xmap, rows, Nx, TB, Kp, Kp, st));
+  GemmArgs g = gemm(TA, Kp, TB, Kp, grad, Nx, Ny, Nx, Kp);
+  g.bf16_linear = 1;
+  g.resid16 = (const bf16_t*)grad;
+  g.ld_resid16 = Nx;
+  return launch_gemm(g, ACT_NONE, OUT_BF16, 1, st);
 }
 
 }  // namespace
@@ -261,33 +296,53 @@ size_t ptk_gemma3_workspace_bytes(const ptk_gemma3_config* c, int batch, int tex
   return bp.off + 256;
 }
 
-int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,
-                            void* ws, size_t ws_bytes, void* stream) {
-  hipStream_t st = (hipStream_t)stream;
+size_t ptk_gemma3_train_workspace_bytes(const ptk_gemma3_config* c, int batch, int text_len, int seq_pad) {
+  Bump bp(nullptr);
+  gemma_layout(bp, c, batch, text_len, seq_pad, true);
+  return bp.off + 256;
+}
+
+}  // extern "C"
+
+namespace {
+
+// Gemma3 forward + causal-LM loss + backward.  gr == nullptr: the frozen LLM of Stage 1 (dX only);
+// otherwise every parameter's grad is accumulated into *gr as well (unfrozen LLM, Stage 2).
+int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,
+              const ptk_gemma3_grads* gr, void* ws, size_t ws_bytes, hipStream_t st) {
+  const bool train = gr != nullptr;
   const int B = bt->batch, T = bt->text_len, Nv = bt->num_vision, Sp = bt->seq_pad, S = Nv + T;
+  const int lo = bt->label_offset;
   if (Sp % 64 || S > Sp) return set_error("gemma3: seq_pad %d must be a multiple of 64 and >= %d", Sp, S);
   if (Sp > wt->rope_max_pos) return set_error("gemma3: seq_pad %d exceeds rope table (%d)", Sp, wt->rope_max_pos);
   if (c->heads % c->kv_heads) return set_error("gemma3: heads %% kv_heads");
   if (Nv < 1) return set_error("gemma3: num_vision must be >= 1");
-  if (ws_bytes < ptk_gemma3_workspace_bytes(c, B, T, Sp)) return set_error("gemma3: workspace too small");
+  if (lo < 0 || lo >= T) return set_error("gemma3: label_offset %d outside [0, text_len %d)", lo, T);
+  const size_t need = train ? ptk_gemma3_train_workspace_bytes(c, B, T, Sp) : ptk_gemma3_workspace_bytes(c, B, T, Sp);
+  if (ws_bytes < need) return set_error("gemma3: workspace too small");
   if (c->vocab % 64 || c->vocab < 64 * LM_SPLITK) return set_error("gemma3: vocab must be a multiple of 64 and >= %d", 64 * LM_SPLITK);
+  if (train && (!gr->layers || !gr->embed || !gr->final_norm)) return set_error("gemma3 train: grads missing");
   const int H = c->hidden, I = c->inter, D = c->head_dim, Hq = c->heads, Hkv = c->kv_heads, G = Hq / Hkv;
-  const int M = B * Sp, Dq = Hq * D, Dqkv = (Hq + 2 * Hkv) * D, R = B * T, V = c->vocab;
+  const int M = B * Sp, Dq = Hq * D, Dqkv = (Hq + 2 * Hkv) * D, Tl = T - lo, R = B * Tl, V = c->vocab;
   const int Z = B * Hkv, SG = Sp * G, nl = c->layers;
   const float eps = c->eps, scale = 1.0f / sqrtf(c->query_pre_attn_scalar);
   Bump bp(ws);
-  GemmaWs w = gemma_layout(bp, c, B, T, Sp);
+  GemmaWs w = gemma_layout(bp, c, B, T, Sp, train);
   AttnShape ash{B, Sp, Hq, Hkv, D};
+  const RowMap ident{0, 0, 0, 0};
+  const int Rp = (R + 63) / 64 * 64;
 
   // K11/K12: text embeddings (x bf16(sqrt H)), padded rows, key-valid mask; vision rows already in x
   const float escale = bfround_host(sqrtf((float)H));
   CK(launch_build_llm_inputs((const bf16_t*)wt->embed, bt->token_ids, B, T, Nv, S, Sp, H, escale, c->pad_token_id,
                              bt->x, w.key_valid, st));
   w.x[0] = bt->x;
-  CK(launch_rmsnorm_fwd(w.x[0], H, RowMap{0, 0, 0, 0}, wt->layers[0].ln_in, w.xn, w.L[0].rstd_in, M, H, eps, st));
+  CK(launch_rmsnorm_fwd(w.x[0], H, ident, wt->layers[0].ln_in, train ? w.L[0].xn_in : w.xn, w.L[0].rstd_in, M, H,
+                        eps, st));
 
-  // position Nv-1+t predicts token t: the only rows the loss reads from the last layer
-  const RowMap lossmap{T, 0, Sp, Nv - 1};
+  // position Nv-1+t predicts text token t: the only rows the loss reads from the last layer are those of
+  // the targets t >= label_offset
+  const RowMap lossmap{Tl, 0, Sp, Nv - 1 + lo};
 
   // ---------------- forward
   for (int l = 0; l < nl; ++l) {
@@ -296,7 +351,10 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
     const bool sliding = (l + 1) % c->sliding_pattern != 0;
     const float* cs = sliding ? wt->rope_cos_local : wt->rope_cos_global;
     const float* sn = sliding ? wt->rope_sin_local : wt->rope_sin_global;
-    CK(launch_gemm(gemm(w.xn, H, L.wqkv, H, sv.qkv, Dqkv, M, Dqkv, H), ACT_NONE, OUT_BF16, 1, st));
+    bf16_t* xin = train ? sv.xn_in : w.xn;
+    bf16_t* xff = train ? sv.xn_ff : w.xn;
+    bf16_t* hh = train ? sv.h : w.h;
+    CK(launch_gemm(gemm(xin, H, L.wqkv, H, sv.qkv, Dqkv, M, Dqkv, H), ACT_NONE, OUT_BF16, 1, st));
     CK(launch_qknorm_rope_fwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, eps, sv.Q, sv.K, sv.V, sv.rstd_q, sv.rstd_k,
                               st));
     {  // causal / sliding-window GQA attention, flash; O token-major, LSE kept for the backward
@@ -315,28 +373,29 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
       CK(launch_attn_fwd(fa, Z, st));
     }
     CK(launch_gemm(gemm(sv.O, Dq, L.wo, Dq, sv.ao, H, M, H, Dq), ACT_NONE, OUT_BF16, 1, st));
-    CK(launch_residual_norm_fwd(sv.ao, w.x[l], L.ln_post_attn, L.ln_pre_ff, sv.x2, w.xn, sv.rstd_ao, sv.rstd_pre, M,
+    CK(launch_residual_norm_fwd(sv.ao, w.x[l], L.ln_post_attn, L.ln_pre_ff, sv.x2, xff, sv.rstd_ao, sv.rstd_pre, M,
                                 H, eps, st));
     if (l + 1 < nl) {
-      GemmArgs g = gemm(w.xn, H, L.wgu, H, w.h, I, M, 2 * I, H);
+      GemmArgs g = gemm(xff, H, L.wgu, H, hh, I, M, 2 * I, H);
       g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
       CK(launch_gemm(g, ACT_GEGLU, OUT_BF16, 1, st));
-      CK(launch_gemm(gemm(w.h, I, L.wd, I, sv.dn, H, M, H, I), ACT_NONE, OUT_BF16, 1, st));
+      CK(launch_gemm(gemm(hh, I, L.wd, I, sv.dn, H, M, H, I), ACT_NONE, OUT_BF16, 1, st));
     } else {
       // last layer: only the loss rows reach the loss, so its MLP runs on those R rows (h, g, u compact);
       // the other rows of dn are zero (their residual output is never read, their gradient is zero)
-      GemmArgs g = gemm(w.xn, H, L.wgu, H, w.h, I, R, 2 * I, H);
+      GemmArgs g = gemm(xff, H, L.wgu, H, hh, I, R, 2 * I, H);
       g.amap = lossmap;
       g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
       CK(launch_gemm(g, ACT_GEGLU, OUT_BF16, 1, st));
       CKH(hipMemsetAsync(sv.dn, 0, (size_t)M * H * sizeof(bf16_t), st));
-      GemmArgs g2 = gemm(w.h, I, L.wd, I, sv.dn, H, R, H, I);
+      GemmArgs g2 = gemm(hh, I, L.wd, I, sv.dn, H, R, H, I);
       g2.cmap = lossmap;
       CK(launch_gemm(g2, ACT_NONE, OUT_BF16, 1, st));
     }
     const float* wnext = (l + 1 < nl) ? wt->layers[l + 1].ln_in : nullptr;
     float* rnext = (l + 1 < nl) ? w.L[l + 1].rstd_in : nullptr;
-    CK(launch_residual_norm_fwd(sv.dn, sv.x2, L.ln_post_ff, wnext, w.x[l + 1], w.xn, sv.rstd_dn, rnext, M, H, eps,
+    bf16_t* xnext = (train && l + 1 < nl) ? w.L[l + 1].xn_in : w.xn;
+    CK(launch_residual_norm_fwd(sv.dn, sv.x2, L.ln_post_ff, wnext, w.x[l + 1], xnext, sv.rstd_dn, rnext, M, H, eps,
                                 st));
   }
 
@@ -346,6 +405,8 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
   CK(launch_count_valid(bt->labels, R, bt->loss_scale, w.gscale, w.count, st));
   CK(launch_ce_fwd_bwd(w.logits, V, R, V, bt->labels, w.row_loss, w.gscale, st));
   CK(launch_loss_reduce(w.row_loss, R, w.count, bt->loss, st));
+  // tied lm_head weight grad: dE += dlogits^T . xf (the logits rows outside the loss rows have zero grad)
+  if (train) CK(weight_grad(w.logits, V, ident, V, w.xf, H, ident, H, R, w.TL, w.TX, gr->embed, st));
   {  // d(xf) = dlogits . E, K = vocab: split-K over LM_SPLITK equal slices (fp32 partials, ordered sum);
      // a vocab that is not a multiple of 64 * LM_SPLITK (Gemma3-4B: 262 208 = 4 097 x 64) leaves a
      // remainder slice, computed into one more partial
@@ -363,22 +424,34 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
   float* dR = bt->dx;
   CKH(hipMemsetAsync(dR, 0, (size_t)M * H * 4, st));
   CK(launch_rmsnorm_bwd_scatter(w.x[nl], lossmap, wt->final_norm, w.rstd_f, w.dxf, dR, R, H, st));
+  if (train)
+    CK(launch_rms_wgrad(w.x[nl], H, lossmap, w.rstd_f, w.dxf, H, 1, R, H, (bf16_t*)gr->final_norm, w.wpart, st));
 
-  // ---------------- backward (dX only: weights are frozen)
+  // ---------------- backward (dX; with gr, also every weight grad)
   for (int l = nl - 1; l >= 0; --l) {
     const ptk_gemma3_layer& L = wt->layers[l];
+    const ptk_gemma3_layer_grads* GL = train ? &gr->layers[l] : nullptr;
     GemmaLayerSave& sv = w.L[l];
     const bool sliding = (l + 1) % c->sliding_pattern != 0;
     const float* cs = sliding ? wt->rope_cos_local : wt->rope_cos_global;
     const float* sn = sliding ? wt->rope_sin_local : wt->rope_sin_global;
+    const bool last = l == nl - 1;
     // MLP half
     // post-ff norm backward: for layers below the last it ran fused into the previous iteration's
     // input-norm backward (one pass over dR instead of two)
-    if (l == nl - 1) CK(launch_post_norm_bwd(dR, sv.dn, L.ln_post_ff, sv.rstd_dn, w.dao, M, H, st));
+    if (last) {
+      CK(launch_post_norm_bwd(dR, sv.dn, L.ln_post_ff, sv.rstd_dn, w.dao, M, H, st));
+      if (train)
+        CK(launch_rms_wgrad_bx(sv.dn, H, ident, sv.rstd_dn, dR, H, 1, M, H, (bf16_t*)GL->ln_post_ff, w.wpart, st));
+    }
+    // down projection weight grad: d(dn)^T . h (last layer: the loss rows and the compact h)
+    if (train)
+      CK(last ? weight_grad(w.dao, H, lossmap, H, sv.h, I, ident, I, R, w.TA, w.TB, GL->wd, st)
+              : weight_grad(w.dao, H, ident, H, sv.h, I, ident, I, M, w.TA, w.TB, GL->wd, st));
     // d(gate|up) = GEGLU backward of dh = dd . Wd, fused into the persistent 4-wave GEMM's register
     // epilogue (g, u loaded one row block ahead; dh never reaches HBM).  PTK_GEGLU_SPLIT=1: the plain
     // GEMM + one streaming geglu_bwd pass instead (A/B)
-    if (l + 1 < nl) {
+    if (!last) {
       if (geglu_split()) {
         CK(launch_gemm(gemm(w.dao, H, L.wd_t, H, w.h, I, M, I, H), ACT_NONE, OUT_BF16, 1, st));
         CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, M, I, st));
@@ -389,19 +462,26 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
         g.ld_aux_in = I;
         CK(launch_gemm(g, ACT_GEGLU_BWD, OUT_BF16, 1, st));
       }
+      if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, ident, H, M, w.TA, w.TB, GL->wgu, st));
       CK(launch_gemm(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), ACT_NONE, OUT_F32, 1, st));
     } else {   // last layer: MLP gradient is non-zero on the loss rows only (compact h, g, u, dgu)
       GemmArgs g = gemm(w.dao, H, L.wd_t, H, w.h, I, R, I, H);
       g.amap = lossmap;
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
       CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, R, I, st));
+      if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, lossmap, H, R, w.TA, w.TB, GL->wgu, st));
       CKH(hipMemsetAsync(w.dtmp, 0, (size_t)M * H * sizeof(float), st));
       GemmArgs g2 = gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, R, H, 2 * I);
       g2.cmap = lossmap;
       CK(launch_gemm(g2, ACT_NONE, OUT_F32, 1, st));
     }
+    if (train) CK(launch_rms_wgrad(sv.x2, H, ident, sv.rstd_pre, w.dtmp, H, 1, M, H, (bf16_t*)GL->ln_pre_ff, w.wpart, st));
     CK(launch_residual_norm_bwd(sv.x2, L.ln_pre_ff, sv.rstd_pre, w.dtmp, dR, sv.ao, L.ln_post_attn, sv.rstd_ao, w.dao,
                                 M, H, st));
+    if (train) {
+      CK(launch_rms_wgrad_bx(sv.ao, H, ident, sv.rstd_ao, dR, H, 1, M, H, (bf16_t*)GL->ln_post_attn, w.wpart, st));
+      CK(weight_grad(w.dao, H, ident, H, sv.O, Dq, ident, Dq, M, w.TA, w.TB, GL->wo, st));
+    }
     {  // dO (Q layout) = dao . Wo, one GEMM per kv head group of output columns
       GemmArgs g = gemm(w.dao, H, L.wo_t, H, w.dO, (long)G * D, M, G * D, H);
       g.sB0 = (long)G * D * H; g.sC0 = (long)Sp * G * D;
@@ -422,22 +502,62 @@ int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights
       fb.key_valid = w.key_valid;
       fb.scale = scale;
       fb.dkv_part = w.dkv_part; fb.dkv_part_bytes = w.dkv_part_bytes;
-      CK(launch_attn_bwd(fb, Z, st, dkv_reduce_split() ? nullptr : &dkv_plan));
+      // the k_norm weight grad reads the complete dK: the unfrozen path reduces split slabs in attn_bwd
+      CK(launch_attn_bwd(fb, Z, st, (dkv_reduce_split() || train) ? nullptr : &dkv_plan));
     }
     CK(launch_qknorm_rope_bwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, sv.rstd_q, sv.rstd_k, w.dQ, w.dK, w.dV, w.dqkv,
                               st, &dkv_plan));
+    if (train) {
+      CK(launch_qknorm_wgrad(sv.qkv, cs, sn, ash, sv.rstd_q, sv.rstd_k, w.dQ, w.dK, (bf16_t*)GL->q_norm,
+                             (bf16_t*)GL->k_norm, w.wpart, st));
+      CK(weight_grad(w.dqkv, Dqkv, ident, Dqkv, sv.xn_in, H, ident, H, M, w.TA, w.TB, GL->wqkv, st));
+    }
     CK(launch_gemm(gemm(w.dqkv, Dqkv, L.wqkv_t, Dqkv, w.dtmp, H, M, H, Dqkv), ACT_NONE, OUT_F32, 1, st));
+    if (train) CK(launch_rms_wgrad(w.x[l], H, ident, sv.rstd_in, w.dtmp, H, 1, M, H, (bf16_t*)GL->ln_in, w.wpart, st));
     if (l > 0) {
       // dR += rms_bwd(x_l, ln_in, dtmp), then layer l-1's post-ff norm backward on the new dR -> dao
       const ptk_gemma3_layer& Lp = wt->layers[l - 1];
       const GemmaLayerSave& sp = w.L[l - 1];
       CK(launch_residual_norm_bwd(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, sp.dn, Lp.ln_post_ff, sp.rstd_dn, w.dao,
                                   M, H, st));
+      if (train)
+        CK(launch_rms_wgrad_bx(sp.dn, H, ident, sp.rstd_dn, dR, H, 1, M, H, (bf16_t*)gr->layers[l - 1].ln_post_ff,
+                               w.wpart, st));
     } else {
       CK(launch_rmsnorm_bwd_f32(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, dR, M, H, st));
     }
   }
+  // input-embedding grads of every text token (tied with the lm_head grad above)
+  if (train) CK(launch_embed_grad(bt->token_ids, B, T, Nv, Sp, H, escale, dR, (bf16_t*)gr->embed, st));
   return 0;
+}
+
+}  // namespace
+
+extern "C" {
+
+int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,
+                            void* ws, size_t ws_bytes, void* stream) {
+  return gemma_run(c, wt, bt, nullptr, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int ptk_gemma3_train_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,
+                             const ptk_gemma3_grads* g, void* ws, size_t ws_bytes, void* stream) {
+  if (!g) return set_error("gemma3 train: grads is NULL");
+  return gemma_run(c, wt, bt, g, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int ptk_bf16_sumsq_partial_floats(void) { return scale_sumsq_partial_floats(); }
+
+int ptk_bf16_grad_scale_sumsq(void* g, int64_t n, float scale, float* partial, float* out, void* stream) {
+  return launch_scale_sumsq_bf16((bf16_t*)g, n, scale, partial, out, (hipStream_t)stream);
+}
+
+int ptk_adamw_bf16(void* params, void* grads, void* exp_avg, void* exp_avg_sq, int64_t n, const float* sumsq_total,
+                   float max_norm, double lr, double beta1, double beta2, double eps, double weight_decay, int step,
+                   float* norm_out, void* stream) {
+  return launch_adamw_bf16((bf16_t*)params, (bf16_t*)grads, (bf16_t*)exp_avg, (bf16_t*)exp_avg_sq, n, sumsq_total,
+                           max_norm, lr, beta1, beta2, eps, weight_decay, step, norm_out, (hipStream_t)stream);
 }
 
 }  // extern "C"

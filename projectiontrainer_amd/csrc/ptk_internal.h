@@ -227,4 +227,27 @@ int launch_sum_partials(const float* part, int nsplit, long n, float* out, hipSt
 int launch_geglu_bwd(const bf16_t* dh, const bf16_t* g, const bf16_t* u, bf16_t* dgu, long M, int I, hipStream_t st);
 int launch_fill_normal_bf16(bf16_t* out, long n, uint64_t seed, float std, float mean, hipStream_t st);
 
+// ---- unfrozen-LLM step (train.hip) ----
+// out [cols][rows_pad] bf16 = in[map(r)][c] (r < rows), zero for rows <= r < rows_pad
+int launch_transpose_rows(const bf16_t* in, long ld_in, RowMap map, int rows, int cols, bf16_t* out, long ld_out,
+                          int rows_pad, hipStream_t st);
+// RMSNorm weight grad: grad[c] = bf16(grad[c] + bf16(sum_r dy'[r,c] * x[map(r),c] * rstd[r])), dy' = dy or bf16(dy);
+// partial >= rms_wgrad_partial_floats(rows, cols) floats
+int rms_wgrad_partial_floats(int rows, int cols);
+int launch_rms_wgrad(const float* x, long ldx, RowMap xmap, const float* rstd, const float* dy, long lddy,
+                     int dy_round, int rows, int cols, bf16_t* grad, float* partial, hipStream_t st);
+int launch_rms_wgrad_bx(const bf16_t* x, long ldx, RowMap xmap, const float* rstd, const float* dy, long lddy,
+                        int dy_round, int rows, int cols, bf16_t* grad, float* partial, hipStream_t st);
+// q_norm / k_norm weight grads from the attention-layout dQ / dK (partial >= 2 * ceil(B*S/64) * D floats)
+int launch_qknorm_wgrad(const bf16_t* qkv, const float* cos_t, const float* sin_t, AttnShape s, const float* rstd_q,
+                        const float* rstd_k, const bf16_t* dQ, const bf16_t* dK, bf16_t* gq, bf16_t* gk,
+                        float* partial, hipStream_t st);
+int launch_embed_grad(const int64_t* ids, int B, int T, int Nv, int Spad, int H, float escale, const float* dx,
+                      bf16_t* dE, hipStream_t st);
+int scale_sumsq_partial_floats();
+int launch_scale_sumsq_bf16(bf16_t* g, long n, float scale, float* partial, float* out, hipStream_t st);
+int launch_adamw_bf16(bf16_t* p, bf16_t* g, bf16_t* m, bf16_t* v, long n, const float* sumsq, float max_norm,
+                      double lr, double b1, double b2, double eps, double wd, int step, float* norm_out,
+                      hipStream_t st);
+
 }  // namespace ptk

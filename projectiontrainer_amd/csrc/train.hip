@@ -1,0 +1,383 @@
+// Kernels of the unfrozen-LLM step (Stage 2, BASELINE cfg4): the weight-gradient plumbing around the
+// MFMA GEMMs and the bf16 optimizer.  All HBM-bound.
+//
+//   transpose_rows     token-major activations / output grads -> feature-major operands of dW = dY^T X
+//                      (the GEMM contracts K-contiguous rows; K is the token axis here)
+//   rms_wgrad          Gemma3RMSNorm weight grads: dw[c] = sum_r dy[r,c] * x[r,c] * rstd[r]
+//                      (modeling_gemma3.py:136-150, output (x * rstd) * (1 + w))
+//   qknorm_wgrad       q_norm / k_norm weight grads through the rotate-half RoPE (:356-360, :208-258)
+//   embed_grad         input-embedding grads of the question / answer tokens
+//                      (Stage2/trainer.py:351-360: weight[ids] * embed_scale), summed per token id
+//   scale_sumsq / adamw_bf16
+//                      clip_grad_norm_(1.0) + torch.optim.AdamW over bf16 parameters, every tensor op
+//                      rounded to bf16 as torch's single-tensor AdamW does on bf16 params
+//                      (Stage2/trainer.py:145-149, :426-443; the LLM is loaded in bf16 under
+//                      --mixed_precision bf16, train_vqa_stage2.py:141-147,180-187)
+#include <math.h>
+
+#include "common.h"
+#include "ptk_internal.h"
+
+namespace ptk {
+
+#define RET_OK(name) return hipGetLastError() == hipSuccess ? 0 : set_error(name " launch failed")
+
+// ---------------------------------------------------------------- transpose with a row gather
+// out [cols][rows_pad] = in[map(r)][c] for r < rows, 0 for rows <= r < rows_pad.  64x64 LDS tiles.
+__global__ void __launch_bounds__(256) transpose_rows_kernel(const bf16_t* __restrict__ in, long ld_in, RowMap map,
+                                                             int rows, int cols, bf16_t* __restrict__ out,
+                                                             long ld_out, int rows_pad) {
+  __shared__ bf16_t tile[64][66];
+  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
+  const int tx = threadIdx.x & 15, ty = threadIdx.x >> 4;
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int r = r0 + ty + 16 * k;
+    const int c = c0 + tx * 4;
+    u16x4_t v = {0, 0, 0, 0};
+    if (r < rows) {
+      const long sr = map_row(map, r);
+      const bf16_t* src = in + sr * ld_in;
+      if (c + 3 < cols && ((ld_in & 3) == 0)) {
+        v = *reinterpret_cast<const u16x4_t*>(src + c);
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) v[e] = (c + e < cols) ? src[c + e] : 0;
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < 4; ++e) tile[ty + 16 * k][tx * 4 + e] = v[e];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const int oc = c0 + ty + 16 * k;
+    const int orr = r0 + tx * 4;
+    if (oc >= cols || orr >= rows_pad) continue;
+    u16x4_t v;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = tile[tx * 4 + e][ty + 16 * k];
+    if (orr + 3 < rows_pad && ((ld_out & 3) == 0)) {
+      *reinterpret_cast<u16x4_t*>(out + (long)oc * ld_out + orr) = v;
+    } else {
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        if (orr + e < rows_pad) out[(long)oc * ld_out + orr + e] = v[e];
+    }
+  }
+}
+
+int launch_transpose_rows(const bf16_t* in, long ld_in, RowMap map, int rows, int cols, bf16_t* out, long ld_out,
+                          int rows_pad, hipStream_t st) {
+  if (cols <= 0 || rows_pad <= 0) return 0;
+  if (rows_pad < rows) return set_error("transpose_rows: rows_pad < rows");
+  dim3 grid((unsigned)((cols + 63) / 64), (unsigned)((rows_pad + 63) / 64));
+  hipLaunchKernelGGL(transpose_rows_kernel, grid, dim3(256), 0, st, in, ld_in, map, rows, cols, out, ld_out, rows_pad);
+  RET_OK("transpose_rows");
+}
+
+// ---------------------------------------------------------------- RMSNorm weight grads
+// partial[blk][c] = sum over the block's rows of dy[r,c] * x[xmap(r),c] * rstd[r]; dy optionally rounded to
+// bf16 first (the post-norms' output grads arrive as bf16 in the reference's autocast graph).
+// 256 threads own float4 column groups c = 4 t + 1024 j; WG_ROWS rows per block.
+constexpr int WG_ROWS = 64;
+PTK_DEV float4 ldv4(const float* p) { return *reinterpret_cast<const float4*>(p); }
+PTK_DEV float4 ldv4(const bf16_t* p) {
+  u16x4_t u = *reinterpret_cast<const u16x4_t*>(p);
+  return make_float4(bf2f(u[0]), bf2f(u[1]), bf2f(u[2]), bf2f(u[3]));
+}
+
+template <typename TX, typename TD, int NJ>
+__global__ void __launch_bounds__(256) rms_wgrad_partial_kernel(const TX* __restrict__ x, long ldx, RowMap xmap,
+                                                                const float* __restrict__ rstd,
+                                                                const TD* __restrict__ dy, long lddy, int dy_round,
+                                                                int rows, int cols, float* __restrict__ partial) {
+  float4 acc[NJ];
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
+  const int r0 = blockIdx.x * WG_ROWS, r1 = min(rows, r0 + WG_ROWS);
+  for (int r = r0; r < r1; ++r) {
+    const float rs = rstd[r];
+    const TX* xr = x + map_row(xmap, r) * ldx;
+    const TD* dr = dy + (long)r * lddy;
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = threadIdx.x * 4 + 1024 * j;
+      if (c < cols) {
+        float4 xv = ldv4(xr + c), dv = ldv4(dr + c);
+        if (dy_round) dv = make_float4(bfround(dv.x), bfround(dv.y), bfround(dv.z), bfround(dv.w));
+        acc[j].x += dv.x * xv.x * rs;
+        acc[j].y += dv.y * xv.y * rs;
+        acc[j].z += dv.z * xv.z * rs;
+        acc[j].w += dv.w * xv.w * rs;
+      }
+    }
+  }
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) {
+    const int c = threadIdx.x * 4 + 1024 * j;
+    if (c < cols) *reinterpret_cast<float4*>(partial + (long)blockIdx.x * cols + c) = acc[j];
+  }
+}
+
+// grad[c] = bf16(grad[c] + bf16(sum_b partial[b][c]))   (autograd accumulation into a bf16 .grad)
+__global__ void __launch_bounds__(256) wgrad_finish_kernel(const float* __restrict__ partial, int nblk, int cols,
+                                                           bf16_t* __restrict__ grad) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += partial[(long)b * cols + c];
+  grad[c] = f2bf(bf2f(grad[c]) + bfround(s));
+}
+
+template <typename TX, typename TD>
+static int rms_wgrad_t(const TX* x, long ldx, RowMap xmap, const float* rstd, const TD* dy, long lddy, int dy_round,
+                       int rows, int cols, bf16_t* grad, float* partial, hipStream_t st) {
+  if (rows <= 0) return 0;
+  if (cols % 4 || cols > 4096) return set_error("rms_wgrad: cols %d (multiple of 4, <= 4096)", cols);
+  const int nblk = (rows + WG_ROWS - 1) / WG_ROWS;
+  const int nj = (cols + 1023) / 1024;
+  const dim3 g((unsigned)nblk);
+  switch (nj) {
+    case 1: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 1>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
+    case 2: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 2>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
+    case 3: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 3>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
+    default: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 4>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
+  }
+  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, st, partial, nblk, cols,
+                     grad);
+  RET_OK("rms_wgrad");
+}
+
+int rms_wgrad_partial_floats(int rows, int cols) { return ((rows + WG_ROWS - 1) / WG_ROWS) * cols; }
+
+int launch_rms_wgrad(const float* x, long ldx, RowMap xmap, const float* rstd, const float* dy, long lddy,
+                     int dy_round, int rows, int cols, bf16_t* grad, float* partial, hipStream_t st) {
+  return rms_wgrad_t<float, float>(x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, grad, partial, st);
+}
+int launch_rms_wgrad_bx(const bf16_t* x, long ldx, RowMap xmap, const float* rstd, const float* dy, long lddy,
+                        int dy_round, int rows, int cols, bf16_t* grad, float* partial, hipStream_t st) {
+  return rms_wgrad_t<bf16_t, float>(x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, grad, partial, st);
+}
+
+// ---------------------------------------------------------------- q_norm / k_norm weight grads
+// One block per WG_ROWS token rows, one thread per head-dim element d (D <= 256, D even).  For every (row,
+// head): dn[d] = RoPE^T(dq)[d] (dq = grad of the rotated, normed head), x_hat[d] = q[d] * rstd[row, head];
+// dw[d] += dn[d] * x_hat[d].  RoPE (rotate-half, cos/sin tables of D/2): rot[d] = n[d] c[d] - n[d+h] s[d]
+// (d < h), rot[d] = n[d] c[d-h] + n[d-h] s[d-h] (d >= h), so dn[d] = dr[d] c[d] + dr[d+h] s[d] (d < h),
+// dn[d] = dr[d] c[d-h] - dr[d-h] s[d-h] (d >= h).
+// dQ is in the attention layout [B, Hkv, S, G, D], dK in [B, Hkv, S, D]; qkv rows are token-major.
+__global__ void __launch_bounds__(256) qknorm_wgrad_partial_kernel(const bf16_t* __restrict__ qkv,
+                                                                   const float* __restrict__ cos_t,
+                                                                   const float* __restrict__ sin_t,
+                                                                   const float* __restrict__ rstd_q,
+                                                                   const float* __restrict__ rstd_k,
+                                                                   const bf16_t* __restrict__ dQ,
+                                                                   const bf16_t* __restrict__ dK, AttnShape s,
+                                                                   float* __restrict__ part_q,
+                                                                   float* __restrict__ part_k) {
+  const int D = s.D, h = D / 2, d = threadIdx.x;
+  const int G = s.Hq / s.Hkv, Dqkv = (s.Hq + 2 * s.Hkv) * D;
+  const long M = (long)s.B * s.S;
+  const long r0 = (long)blockIdx.x * WG_ROWS, r1 = min(M, r0 + WG_ROWS);
+  float aq = 0.f, ak = 0.f;
+  if (d < D) {
+    const int dp = d < h ? d + h : d - h, dc = d < h ? d : d - h;
+    for (long r = r0; r < r1; ++r) {
+      const int b = (int)(r / s.S), pos = (int)(r - (long)b * s.S);
+      const float c = cos_t[(long)pos * h + dc], sn = sin_t[(long)pos * h + dc];
+      const bf16_t* qrow = qkv + r * Dqkv;
+      for (int hq = 0; hq < s.Hq; ++hq) {
+        const int kvh = hq / G, j = hq - kvh * G;
+        const bf16_t* g = dQ + ((((long)b * s.Hkv + kvh) * s.S + pos) * G + j) * D;
+        const float dn = d < h ? bf2f(g[d]) * c + bf2f(g[dp]) * sn : bf2f(g[d]) * c - bf2f(g[dp]) * sn;
+        aq += dn * bf2f(qrow[hq * D + d]) * rstd_q[r * s.Hq + hq];
+      }
+      for (int kvh = 0; kvh < s.Hkv; ++kvh) {
+        const bf16_t* g = dK + (((long)b * s.Hkv + kvh) * s.S + pos) * D;
+        const float dn = d < h ? bf2f(g[d]) * c + bf2f(g[dp]) * sn : bf2f(g[d]) * c - bf2f(g[dp]) * sn;
+        ak += dn * bf2f(qrow[(s.Hq + kvh) * D + d]) * rstd_k[r * s.Hkv + kvh];
+      }
+    }
+    part_q[(long)blockIdx.x * D + d] = aq;
+    part_k[(long)blockIdx.x * D + d] = ak;
+  }
+}
+
+int launch_qknorm_wgrad(const bf16_t* qkv, const float* cos_t, const float* sin_t, AttnShape s, const float* rstd_q,
+                        const float* rstd_k, const bf16_t* dQ, const bf16_t* dK, bf16_t* gq, bf16_t* gk,
+                        float* partial, hipStream_t st) {
+  if (s.D > 256 || s.D % 2) return set_error("qknorm_wgrad: head_dim %d", s.D);
+  const long M = (long)s.B * s.S;
+  const int nblk = (int)((M + WG_ROWS - 1) / WG_ROWS);
+  float* pq = partial;
+  float* pk = partial + (long)nblk * s.D;
+  hipLaunchKernelGGL(qknorm_wgrad_partial_kernel, dim3((unsigned)nblk), dim3(256), 0, st, qkv, cos_t, sin_t, rstd_q,
+                     rstd_k, dQ, dK, s, pq, pk);
+  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((s.D + 255) / 256)), dim3(256), 0, st, pq, nblk, s.D, gq);
+  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((s.D + 255) / 256)), dim3(256), 0, st, pk, nblk, s.D, gk);
+  RET_OK("qknorm_wgrad");
+}
+
+// ---------------------------------------------------------------- input-embedding grads
+// Text position t of sample b sits at LLM row b*Spad + Nv + t and embeds token ids[b*T + t] as
+// bf16(E[id] * escale).  Its grad into E[id] is bf16(bf16(dx_row) * escale) (the bf16 mul's backward on the
+// fp32 grad cast to bf16); rows sharing an id are summed in position order by the block of the FIRST
+// occurrence (deterministic, no atomics), then added to the tied weight's bf16 grad.
+constexpr int EG_MAX = 16384;   // text tokens per batch (the LDS match list)
+__global__ void __launch_bounds__(256) embed_grad_kernel(const int64_t* __restrict__ ids, int B, int T, int Nv,
+                                                         int Spad, int H, float escale, const float* __restrict__ dx,
+                                                         bf16_t* __restrict__ dE) {
+  __shared__ int list[EG_MAX];
+  __shared__ int wcount[4];
+  __shared__ int total_s;
+  const int n = B * T, i = blockIdx.x;
+  const int64_t id = ids[i];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (threadIdx.x == 0) total_s = 0;
+  __syncthreads();
+  // stream compaction of the positions holding this id, in position order (ballot + prefix counts)
+  for (int j0 = 0; j0 < n; j0 += 256) {
+    const int j = j0 + threadIdx.x;
+    const bool m = j < n && ids[j] == id;
+    const unsigned long long mask = __ballot(m);
+    if (lane == 0) wcount[wv] = __popcll(mask);
+    __syncthreads();
+    int base = total_s;
+    for (int k = 0; k < wv; ++k) base += wcount[k];
+    if (m) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = j;
+    __syncthreads();
+    if (threadIdx.x == 0) total_s += wcount[0] + wcount[1] + wcount[2] + wcount[3];
+    __syncthreads();
+  }
+  const int cnt = total_s;
+  if (list[0] != i) return;   // the block of the first occurrence owns this id
+  for (int c = threadIdx.x; c < H; c += 256) {
+    float acc = 0.f;
+    for (int k = 0; k < cnt; ++k) {
+      const int j = list[k], b = j / T, t = j - b * T;
+      acc += bfround(bfround(dx[((long)b * Spad + Nv + t) * H + c]) * escale);
+    }
+    bf16_t* g = dE + id * (long)H + c;
+    *g = f2bf(bf2f(*g) + bfround(acc));
+  }
+}
+
+int launch_embed_grad(const int64_t* ids, int B, int T, int Nv, int Spad, int H, float escale, const float* dx,
+                      bf16_t* dE, hipStream_t st) {
+  if (B * T <= 0) return 0;
+  if (B * T > EG_MAX) return set_error("embed_grad: %d text tokens per batch (max %d)", B * T, EG_MAX);
+  hipLaunchKernelGGL(embed_grad_kernel, dim3((unsigned)(B * T)), dim3(256), 0, st, ids, B, T, Nv, Spad, H, escale, dx,
+                     dE);
+  RET_OK("embed_grad");
+}
+
+// ---------------------------------------------------------------- bf16 grad scale + sum of squares
+// g = bf16(g * scale) in place when scale != 1 (DDP's 1/world average of a summed gradient), and
+// out[0] = sum g^2 in fp32: SS_BLOCKS fixed block partials summed in block order by one block (the same
+// grid for a given n, so the result is bit-reproducible).
+constexpr int SS_BLOCKS = 1024;
+__global__ void __launch_bounds__(256) scale_sumsq_kernel(bf16_t* __restrict__ g, long n, float scale,
+                                                          float* __restrict__ partial) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (long i = ((long)blockIdx.x * 256 + threadIdx.x) * 8; i < n; i += (long)gridDim.x * 2048) {
+    if (i + 7 < n) {
+      u16x8_t u = *reinterpret_cast<const u16x8_t*>(g + i);
+      if (scale != 1.f) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) u[e] = f2bf(bf2f(u[e]) * scale);
+        *reinterpret_cast<u16x8_t*>(g + i) = u;
+      }
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const float v = bf2f(u[e]);
+        s += v * v;
+      }
+    } else {
+      for (long j = i; j < n; ++j) {
+        float v = bf2f(g[j]);
+        if (scale != 1.f) {
+          v = bfround(v * scale);
+          g[j] = f2bf(v);
+        }
+        s += v * v;
+      }
+    }
+  }
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) partial[blockIdx.x] = s;
+}
+__global__ void __launch_bounds__(256) sum_blocks_kernel(const float* __restrict__ partial, int nb,
+                                                         float* __restrict__ out) {
+  __shared__ float red[4];
+  float s = 0.f;
+  for (int i = threadIdx.x; i < nb; i += 256) s += partial[i];
+  s = block_sum<256>(s, red);
+  if (threadIdx.x == 0) out[0] = s;
+}
+
+int scale_sumsq_partial_floats() { return SS_BLOCKS; }
+
+int launch_scale_sumsq_bf16(bf16_t* g, long n, float scale, float* partial, float* out, hipStream_t st) {
+  if (n <= 0) {
+    hipLaunchKernelGGL(sum_blocks_kernel, dim3(1), dim3(256), 0, st, partial, 0, out);
+    RET_OK("scale_sumsq");
+  }
+  hipLaunchKernelGGL(scale_sumsq_kernel, dim3(SS_BLOCKS), dim3(256), 0, st, g, n, scale, partial);
+  hipLaunchKernelGGL(sum_blocks_kernel, dim3(1), dim3(256), 0, st, partial, SS_BLOCKS, out);
+  RET_OK("scale_sumsq");
+}
+
+// ---------------------------------------------------------------- clip + AdamW on bf16 parameters
+// clip_grad_norm_(max_norm) on bf16 grads: total = ||g|| (fp32 sum of squares, rounded to bf16 as the
+// reference's bf16 norm tensor), coef = bf16(max_norm / bf16(total + 1e-6)) clamped to 1, g = bf16(g coef).
+// Then torch's _single_tensor_adamw on bf16 tensors, each in-place op rounded to bf16:
+//   p = bf16(p (1 - lr wd)); m = bf16(m + (1-b1)(g - m)); v = bf16(v b2); v = bf16(v + (1-b2) g g);
+//   den = bf16(sqrt(v)); den = bf16(den / bc2s); den = bf16(den + eps); p = bf16(p - step_size m / den).
+__global__ void __launch_bounds__(256) adamw_bf16_kernel(bf16_t* __restrict__ p, bf16_t* __restrict__ g,
+                                                         bf16_t* __restrict__ m, bf16_t* __restrict__ v, long n,
+                                                         const float* __restrict__ sumsq, float max_norm,
+                                                         float decay, float b1c, float b2, float b2c, float step_size,
+                                                         float bc2s, float eps, float* norm_out) {
+  float coef = 1.f;
+  if (max_norm > 0.f) {
+    const float total = bfround(sqrtf(sumsq[0]));
+    coef = fminf(bfround(max_norm / bfround(total + 1e-6f)), 1.f);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && norm_out) norm_out[0] = total;
+  }
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long)gridDim.x * 256) {
+    float gi = bf2f(g[i]);
+    if (coef != 1.f) {
+      gi = bfround(gi * coef);
+      g[i] = f2bf(gi);
+    }
+    float pi = bfround(bf2f(p[i]) * decay);
+    const float mo = bf2f(m[i]);
+    const float mi = bfround(mo + b1c * (gi - mo));
+    float vi = bfround(bf2f(v[i]) * b2);
+    vi = bfround(vi + b2c * gi * gi);
+    float den = bfround(sqrtf(vi));
+    den = bfround(den / bc2s);
+    den = bfround(den + eps);
+    pi = bfround(pi - step_size * mi / den);
+    p[i] = f2bf(pi);
+    m[i] = f2bf(mi);
+    v[i] = f2bf(vi);
+  }
+}
+
+int launch_adamw_bf16(bf16_t* p, bf16_t* g, bf16_t* m, bf16_t* v, long n, const float* sumsq, float max_norm,
+                      double lr, double b1, double b2, double eps, double wd, int step, float* norm_out,
+                      hipStream_t st) {
+  if (n <= 0) return 0;
+  if (step < 1) return set_error("adamw_bf16: step must be >= 1");
+  const double bc1 = 1.0 - pow(b1, step), bc2 = 1.0 - pow(b2, step);
+  const long blocks = std::min<long>(4096, (n + 255) / 256);
+  hipLaunchKernelGGL(adamw_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, p, g, m, v, n, sumsq, max_norm,
+                     (float)(1.0 - lr * wd), (float)(1.0 - b1), (float)b2, (float)(1.0 - b2), (float)(lr / bc1),
+                     (float)sqrt(bc2), (float)eps, norm_out);
+  RET_OK("adamw_bf16");
+}
+
+}  // namespace ptk

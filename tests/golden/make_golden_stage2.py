@@ -1,0 +1,229 @@
+"""Generate Stage-2 golden fixtures by running the REFERENCE VQA trainer on CPU.
+
+Run in the build container only (needs /root/reference and HF transformers):
+
+    python tests/golden/make_golden_stage2.py            # writes tests/golden/s2_<name>.npz
+
+It imports `Stage2/trainer.py` (VQATrainerStage2, vqa_collate_fn) and
+`Stage1/accelerator_setup.py` from /root/reference, builds random-init HF
+`SiglipModel` / `Gemma3ForCausalLM` from tiny configs with the repo's
+deterministic weights, a frozen `Stage1/projectors.py` MLPProjector, and runs
+`trainer.train()` with the LLM unfrozen (BASELINE cfg4's setting:
+`--unfreeze_llm`, projector and vision encoder frozen, no QLoRA) for 2 epochs of
+3 micro-batches at gradient_accumulation_steps 2 (syncs at micro-batch 2 and at
+the end of each epoch: 4 optimizer steps, the first under warmup).  The
+per-epoch validation (`generate` with sampling) and `save_model` are replaced
+by no-ops on the instance: outside the training step.
+
+Twins (same weights and data): `s2_tiny` without mixed precision, `s2_tiny_bf16`
+under `--mixed_precision bf16` (models and projector cast to bf16 as
+train_vqa_stage2.py:141-187,274 does).
+
+Recorded per micro-batch: the collated batch (question / answer ids, pixel
+order), the manual-CE loss.  Per optimizer step: LR, the accumulated LLM grads
+before clipping, the grad norm, and every LLM parameter after AdamW.  Matrices
+larger than 1024 elements are sub-sampled (`@sub<sr>x<sc>`, see
+make_golden.py) with their exact `@norm` / `@sum`.
+Only data (inputs and expected outputs) is written; no reference source.
+"""
+from __future__ import annotations
+
+import argparse
+import math
+import os
+import subprocess
+import sys
+import tempfile
+import types
+
+import numpy as np
+import torch
+
+REPO = os.path.dirname(os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+sys.path.insert(0, REPO)
+
+from projectiontrainer_amd.config import PRESETS, to_hf_dicts  # noqa: E402
+from projectiontrainer_amd import weights as W  # noqa: E402
+
+REF = "/root/reference"
+SUB_BUDGET = 512
+
+
+def sub_strides(shape):
+    C = shape[-1] if len(shape) else 1
+    R = int(np.prod(shape[:-1])) if len(shape) > 1 else 1
+    sc = 1 if C <= 256 else math.ceil(C / 128)
+    kept_c = math.ceil(C / sc)
+    sr = max(1, math.ceil(R / max(1, SUB_BUDGET // kept_c)))
+    return sr, sc
+
+
+def stage2_items(cfg, n, seed):
+    """Synthetic VQA samples in the reference dataset's item format (Stage2/dataset.py:115-119): pixel
+    values, question ids without special tokens, answer ids starting with BOS (add_special_tokens)."""
+    rng = np.random.default_rng(seed)
+    v, t = cfg.vision, cfg.text
+    px = rng.uniform(-1.0, 1.0, (n, v.num_channels, v.image_size, v.image_size)).astype(np.float32)
+    items = []
+    for i in range(n):
+        q = rng.integers(3, t.vocab_size, int(rng.integers(3, 9)), dtype=np.int64)
+        a = np.concatenate([[t.bos_token_id], rng.integers(3, t.vocab_size, int(rng.integers(4, 13)), dtype=np.int64)])
+        items.append({"pixel_values": torch.from_numpy(px[i]), "question_input_ids": torch.from_numpy(q),
+                      "answer_input_ids": torch.from_numpy(a.astype(np.int64))})
+    return items
+
+
+class _Tok:
+    """The tokenizer surface VQATrainerStage2.train / vqa_collate_fn touch."""
+    def __init__(self, pad, eos, side):
+        self.pad_token_id, self.eos_token_id, self.padding_side = pad, eos, side
+        self.pad_token = "<pad>"
+
+
+def run(name: str, precision: str, gas: int = 2, lr: float = 1e-3, num_epochs: int = 2, n_items: int = 6,
+        batch_size: int = 2, seed: int = 21, side: str = "left"):
+    os.environ["ACCELERATE_MIXED_PRECISION"] = precision
+    sys.path.insert(0, REF)
+    import transformers
+    import accelerate
+    from transformers import SiglipConfig, SiglipModel, Gemma3TextConfig, Gemma3ForCausalLM
+    from Stage1.projectors import MLPProjector                  # reference
+    from Stage1.accelerator_setup import setup_accelerator_and_logging  # reference
+    from Stage2.trainer import VQATrainerStage2                 # reference
+
+    torch.manual_seed(0)
+    cfg = PRESETS["tiny"]
+    vis_kw, txt_kw = to_hf_dicts(cfg)
+    sig = SiglipModel(SiglipConfig(
+        text_config=dict(vocab_size=64, hidden_size=64, intermediate_size=128, num_hidden_layers=1,
+                         num_attention_heads=1, max_position_embeddings=16, bos_token_id=None,
+                         eos_token_id=None, pad_token_id=None),
+        vision_config=vis_kw)).float()
+    vp = W.siglip_vision_params(cfg.vision)
+    sig.load_state_dict({k: torch.from_numpy(v) for k, v in vp.items()}, strict=False)
+    llm = Gemma3ForCausalLM(Gemma3TextConfig(**txt_kw)).float()
+    lp = W.gemma3_params(cfg.text)
+    res = llm.load_state_dict({k: torch.from_numpy(v) for k, v in lp.items()}, strict=False)
+    assert set(res.missing_keys) <= {"lm_head.weight"}, res
+    proj = MLPProjector(cfg.vision.hidden_size, cfg.text.hidden_size)
+    pp = W.projector_params(cfg.vision.hidden_size, cfg.text.hidden_size, cfg.expansion_factor)
+    proj.load_state_dict({k: torch.from_numpy(v) for k, v in pp.items()})
+    if precision == "bf16":
+        sig, llm, proj = sig.to(torch.bfloat16), llm.to(torch.bfloat16), proj.to(dtype=torch.bfloat16)
+
+    data = stage2_items(cfg, n_items, seed)
+    args = types.SimpleNamespace(gradient_accumulation_steps=gas, disable_wandb=True, batch_size=batch_size,
+                                 wandb_project="x", wandb_run_name=None)
+    acc = setup_accelerator_and_logging(args)
+    assert acc.mixed_precision == precision, (acc.mixed_precision, precision)
+    tok = _Tok(cfg.text.pad_token_id, cfg.text.eos_token_id, side)
+    out = tempfile.mkdtemp()
+    trainer = VQATrainerStage2(acc, sig, llm, proj, tok, data, data[:2], out, batch_size, lr, 0.01, num_epochs, gas,
+                               0.05, freeze_vision_encoder=True, freeze_projection_layer=True, freeze_llm=False,
+                               enable_qlora=False, train_ve_first_epoch=False, wandb_project="x")
+    trainer.evaluate = lambda *a, **k: None          # validation generate(): outside the training step
+    trainer.save_model = lambda *a, **k: None        # accelerate.save_state: outside the training step
+
+    rec = {}
+    st = {"micro": 0, "opt": 0}
+    llm_u = acc.unwrap_model(trainer.language_model)
+    names = [n for n, _ in llm_u.named_parameters()]
+    params = dict(llm_u.named_parameters())
+
+    def put(key, v):
+        a = v.detach().cpu().float().numpy().copy() if torch.is_tensor(v) and v.is_floating_point() else \
+            (v.detach().cpu().numpy().copy() if torch.is_tensor(v) else np.asarray(v))
+        if a.ndim >= 2 and a.size > 1024:
+            sr, sc = sub_strides(a.shape)
+            rec[key + f"@sub{sr}x{sc}"] = a.reshape(-1, a.shape[-1])[::sr, ::sc]
+            rec[key + "@norm"] = np.array(np.linalg.norm(a.astype(np.float64)))
+            rec[key + "@sum"] = np.array(a.astype(np.float64).sum())
+        else:
+            rec[key] = a
+
+    class Loader:
+        """Records each collated batch the prepared loader yields (same object iterated underneath)."""
+        def __init__(self, inner):
+            self.inner = inner
+
+        def __len__(self):
+            return len(self.inner)
+
+        def __iter__(self):
+            for b in self.inner:
+                m = st["micro"]
+                put(f"m{m}_question_input_ids", b["question_input_ids"])
+                put(f"m{m}_answer_input_ids", b["answer_input_ids"])
+                px = b["pixel_values"].float().numpy()
+                ref = np.stack([it["pixel_values"].numpy() for it in data])
+                rec[f"m{m}_order"] = np.array([int(np.argmin(np.abs(ref - px[j]).reshape(len(data), -1).max(1)))
+                                               for j in range(px.shape[0])])
+                yield b
+
+    trainer.train_loader = Loader(trainer.train_loader)
+
+    def ce_hook(mod, a, o):
+        if isinstance(mod, torch.nn.CrossEntropyLoss):
+            put(f"m{st['micro']}_loss", o)
+            st["micro"] += 1
+    hk = torch.nn.modules.module.register_module_forward_hook(ce_hook)
+
+    orig_clip = acc.clip_grad_norm_
+
+    def clip(parameters, max_norm, *a, **k):
+        parameters = list(parameters)
+        if any(p is params[names[0]] for p in parameters):
+            for n in names:
+                put(f"o{st['opt']}_grad.{n}", params[n].grad)
+        total = orig_clip(parameters, max_norm, *a, **k)
+        rec[f"o{st['opt']}_grad_norm"] = np.array(float(total))
+        return total
+    acc.clip_grad_norm_ = clip
+
+    opt = trainer.optimizer.optimizer
+
+    def pre(o, a, kw):
+        rec[f"o{st['opt']}_lr"] = np.array(o.param_groups[0]["lr"])
+        rec[f"o{st['opt']}_micro"] = np.array(st["micro"])
+
+    def post(o, a, kw):
+        for n in names:
+            put(f"o{st['opt']}_param.{n}", params[n])
+        st["opt"] += 1
+    opt.register_step_pre_hook(pre)
+    opt.register_step_post_hook(post)
+
+    trainer.train()
+    hk.remove()
+    meta = dict(name=name, precision=precision, gas=gas, lr=lr, num_epochs=num_epochs, n_items=n_items,
+                batch_size=batch_size, seed=seed, padding_side=side, warmup_ratio=0.05, weight_decay=0.01,
+                max_grad_norm=1.0, micro_batches=st["micro"], opt_steps=st["opt"],
+                max_train_steps=trainer.max_train_steps, param_names=names,
+                torch=torch.__version__, transformers=transformers.__version__, accelerate=accelerate.__version__)
+    rec["meta"] = np.array(repr(meta))
+    fp = np.array([float(np.sum(v.astype(np.float64))) for d in (vp, lp, pp) for v in d.values()])
+    rec["weight_fingerprint"] = fp
+    return rec
+
+
+FIXTURES = {"s2_tiny": "no", "s2_tiny_bf16": "bf16"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--out", default=os.path.dirname(os.path.abspath(__file__)))
+    ap.add_argument("--only", default=None)
+    a = ap.parse_args()
+    if a.only is None:
+        for name in FIXTURES:
+            subprocess.check_call([sys.executable, os.path.abspath(__file__), "--out", a.out, "--only", name])
+        return
+    torch.set_num_threads(min(8, os.cpu_count() or 8))
+    rec = run(a.only, FIXTURES[a.only])
+    path = os.path.join(a.out, f"{a.only}.npz")
+    np.savez_compressed(path, **rec)
+    print(path, os.path.getsize(path), "bytes", rec["meta"])
+
+
+if __name__ == "__main__":
+    main()

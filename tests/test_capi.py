@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
         assert n in L.SIGNATURES, f"{n} missing from the ctypes binding"
-    assert lib.ptk_abi_version() == 1
+    assert lib.ptk_abi_version() == L.ABI_VERSION == 2
 
 
 def test_error_reporting_without_gpu():
@@ -53,6 +53,8 @@ STRUCTS = {
     "ptk_gemma3_layer": ("Gemma3LayerC", None),
     "ptk_gemma3_weights": ("Gemma3WeightsC", None),
     "ptk_gemma3_batch": ("Gemma3BatchC", None),
+    "ptk_gemma3_layer_grads": ("Gemma3LayerGradsC", None),
+    "ptk_gemma3_grads": ("Gemma3GradsC", None),
     "ptk_image_desc": ("ImageDesc", None),
 }
 

@@ -14,16 +14,20 @@ other precision (tiny / tiny_bf16, tiny_gqa / tiny_gqa_bf16, cfg1 / cfg1_bf16), 
 the reference's OWN mixed-precision noise is known per tensor:
 noise = rel-L2 / cosine of the reference's bf16 run against its fp32 run.  The HIP
 path (bf16 GEMM operands, fp32 accumulation, SURVEY F8 flow) must agree with either
-reference run at least as closely as the two reference runs agree with each other
-(x1.5), and within SURVEY.md:297's bar wherever that noise is below it:
+reference run within twice the distance between the two reference runs (two bf16
+implementations of one function each sit ~noise away from fp32), and within
+SURVEY.md:297's bar wherever that noise is below it:
   loss |d| <= 2e-2 abs;
   patch embeddings / projector output / d(projector output) / projector grads:
-    rel-L2 <= max(2e-2, 1.5 * noise_rel_l2), cosine >= min(0.999, 1 - 1.5 * (1 - noise_cos));
+    rel-L2 <= max(2e-2, 2 * noise_rel_l2), cosine >= min(0.999, 1 - 2 * (1 - noise_cos));
   post-AdamW params: max |d| <= 2.5 * sum(lr so far) (Adam's early steps move each weight by
     ~lr, so a sign flip of a near-zero grad moves it by at most ~2 lr per step) and
     median |d| <= 0.05 * lr.
 (Measured, cfg1: the reference's bf16 run vs its fp32 run is at rel-L2 0.04 / cos 0.9992 on
-d(projector output) after one step and 0.11 / 0.994 after two.)  Every measured value is
+d(projector output) after one step and 0.11 / 0.994 after two; the HIP path vs the fp32 run
+0.036 / 0.9994 and 0.10 / 0.995, vs the bf16 run 0.037 / 0.9994 and 0.089 / 0.996.  The
+second step's spread comes from the first AdamW update: Adam moves every weight by ~lr in
+the direction of its gradient's sign, so near-zero gradients flip weights chaotically.)  Every measured value is
 appended to gpurun_out/parity_metrics.jsonl (when that directory exists).
 """
 import json
@@ -78,9 +82,9 @@ def compare(d, key, got, rl2, cos=None, atol=None, med=None, test="", name=None)
     got = got.detach().double().cpu().numpy() if torch.is_tensor(got) else np.asarray(got)
     if name is not None and atol is None:
         n_rl2, n_cos = twin_noise(name, key)
-        rl2 = max(rl2, 1.5 * n_rl2)
+        rl2 = max(rl2, 2.0 * n_rl2)
         if cos is not None:
-            cos = min(cos, 1.0 - 1.5 * (1.0 - n_cos))
+            cos = min(cos, 1.0 - 2.0 * (1.0 - n_cos))
     if key in d.files:
         ref = d[key]
         g = got
