@@ -42,6 +42,8 @@ def _args(argv=None):
                     help="time only the CPU baseline (no GPU) and print it")
     ap.add_argument("--prefetch", action="store_true",
                     help="overlap the next step's SigLIP forward with this step's Gemma3 on a side stream")
+    ap.add_argument("--gas", type=int, default=1,
+                    help="Stage 2 (cfg4): micro-batches per optimizer step (one bench step = gas micro-batches)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher plumbing only: every rank joins a gloo group, rank 0 prints the world; no GPU")
     return ap.parse_args(argv)
@@ -225,6 +227,14 @@ def main(argv=None):
     if args.text_len:
         cfg = cfg.replace(text_len=args.text_len)
 
+    if cfg.question_len > 0:
+        line = bench_stage2(args, cfg, world, rank, dev)
+        if rank == 0:
+            print(json.dumps(line), flush=True)
+        if world > 1:
+            dist.destroy_process_group()
+        return
+
     eng = Stage1Engine.synthetic(cfg, dev, seed=0, world_size=world, total_steps=10 ** 6,
                                  gradient_accumulation_steps=1)
     px, ids, labels = W.synthetic_batch(cfg, seed=1234 + rank)
@@ -309,6 +319,84 @@ def main(argv=None):
         print(json.dumps(line), flush=True)
     if world > 1:
         dist.destroy_process_group()
+
+
+def bench_stage2(args, cfg, world, rank, dev):
+    """BASELINE cfg4: Stage-2 VQA fine-tune, Gemma3-1B unfrozen (Stage2/trainer.py:299-444).  One step =
+    `--gas` micro-batches (frozen SigLIP + projector forward, Gemma3 forward, manual CE, full backward with
+    every weight grad) + the optimizer step (ZeRO-1 reduce-scatter over RCCL for world > 1, clip, bf16
+    AdamW, all-gather)."""
+    import ctypes
+
+    import numpy as np
+    import torch
+    import torch.distributed as dist
+
+    from projectiontrainer_amd import _lib as L
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.flops import stage2_flops_per_image
+    from projectiontrainer_amd.stage2 import synthetic_engine
+
+    eng = synthetic_engine(cfg, dev, seed=0, world_size=world, rank=rank, total_steps=10 ** 6,
+                           gradient_accumulation_steps=args.gas, learning_rate=1e-5)
+    px, q, a = W.synthetic_vqa_batch(cfg, seed=1234 + rank)
+    px, q, a = (torch.from_numpy(t).to(dev) for t in (px, q, a))
+
+    def step():
+        for _ in range(args.gas):
+            loss = eng.forward_backward(px, q, a)
+        eng.optimizer_step()
+        return loss
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    L.lib().ptk_gemm_timer_enable((1 << 8) | (1 << L.ACT_GEGLU))
+    ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
+    ev[0].record()
+    for k in range(args.steps):
+        loss = step()
+        ev[k + 1].record()
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = ev[0].elapsed_time(ev[-1]) / 1e3
+    med_ms = float(np.median([ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)]))
+    L.lib().ptk_gemm_timer_enable(0)
+    tot, cnt = ctypes.c_double(), ctypes.c_int()
+    L.check(L.lib().ptk_gemm_timer_read(L.ACT_GEGLU, ctypes.byref(tot), ctypes.byref(cnt)), "timer")
+    t = torch.tensor([elapsed, med_ms], dtype=torch.float64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    elapsed, med_ms = float(t[0]), float(t[1])
+    imgs = world * cfg.batch_size * args.gas * args.steps
+    value = imgs / elapsed
+    fpi = stage2_flops_per_image(cfg)["total"]
+    # gate|up launches per micro-batch: layers 0..L-2 on all B*S rows, the last on the B*Ta answer rows
+    tc = cfg.text
+    ta = cfg.text_len - cfg.question_len
+    gu = 2.0 * 2 * tc.intermediate_size * tc.hidden_size * cfg.batch_size * (cfg.seq_len * (tc.num_hidden_layers - 1) + ta)
+    achieved = gu * args.gas * args.steps / (tot.value / 1e3) / 1e12
+    return {
+        "metric": "Stage-2 VQA fine-tune images/sec/node (SigLIP-L-384 + Gemma3-1B unfrozen, 576+64+256 tok)",
+        "value": round(value, 3), "unit": "images/sec", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": round(elapsed / args.steps * 1e3, 3), "higher_is_better": True,
+        "scaling": "weak", "vs_baseline": None, "dtype": "bf16", "data": "synthetic",
+        "config": {"workload": f"{args.config}: Stage 2 VQA, SigLIP-ViT-L/16-384 + projector frozen fwd, Gemma3-1B "
+                               f"fwd + full bwd (all weight grads) + ZeRO-1 bf16 AdamW, {cfg.num_vision_tokens} vis + "
+                               f"{cfg.question_len} Q + {ta} A tokens, gas {args.gas}",
+                   "global_batch": world * cfg.batch_size * args.gas, "per_gpu_batch": cfg.batch_size,
+                   "seq_len": cfg.seq_len, "parallelism": f"dp{world}-zero1"},
+        "roofline": {"bound": "mfma", "kernel": "gemm_w4_kernel<ACT_GEGLU> (Gemma3 gate|up projection)",
+                     "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": None,
+                     "launches": cnt.value, "avg_ms": round(tot.value / max(cnt.value, 1), 4)},
+        "median_ms_per_step": round(med_ms, 3),
+        "step_mfma_frac": round(value * fpi / (world * MFMA_BF16_PEAK_TFLOPS * 1e12), 4),
+        "flop_per_image": fpi, "loss": round(float(loss), 5),
+    }
 
 
 if __name__ == "__main__":

@@ -81,6 +81,9 @@ class Stage1Config:
     expansion_factor: int = 10               # Stage1/projectors.py:13
     batch_size: int = 32
     text_len: int = 128
+    # Stage 2 (VQA): the first question_len text tokens are the question (no targets), the rest the answer
+    # (Stage2/trainer.py:370-396); Stage 1: 0 (every text token is a target)
+    question_len: int = 0
 
     @property
     def num_vision_tokens(self) -> int:
@@ -127,6 +130,8 @@ PRESETS = {
     "cfg1": Stage1Config(vision=SIGLIP_B16_224, text=GEMMA3_1B, batch_size=2, text_len=64),
     # BASELINE.json configs[4]
     "cfg5": Stage1Config(vision=SIGLIP_L16_384, text=GEMMA3_4B, batch_size=16, text_len=256),
+    # BASELINE.json configs[3]: Stage 2 VQA fine-tune, Gemma3-1B unfrozen, 576 vis + 64 Q + 256 A tokens
+    "cfg4": Stage1Config(vision=SIGLIP_L16_384, text=GEMMA3_1B, batch_size=16, text_len=64 + 256, question_len=64),
     "tiny": Stage1Config(vision=SIGLIP_TINY, text=GEMMA3_TINY, batch_size=3, text_len=16),
     "tiny_gqa": Stage1Config(vision=SIGLIP_TINY, text=GEMMA3_TINY_GQA, batch_size=3, text_len=16),
 }

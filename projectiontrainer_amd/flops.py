@@ -51,3 +51,21 @@ def geglu_step_flops(cfg: Stage1Config) -> float:
     t = cfg.text
     per_row = 2.0 * 2 * t.intermediate_size * t.hidden_size
     return per_row * cfg.batch_size * (cfg.seq_len * (t.num_hidden_layers - 1) + cfg.text_len)
+
+
+def stage2_flops_per_image(cfg: Stage1Config) -> dict:
+    """Algorithmic FLOPs of one Stage-2 (unfrozen LLM) micro-batch per image: frozen SigLIP and projector
+    forward; Gemma3 forward with the lm_head on the answer rows (the question rows carry no target,
+    Stage2/trainer.py:390-396); backward = dX (as Stage 1) + every weight's dW = dY^T X (dense GEMMs on all
+    S rows, the tied lm_head on the answer rows).  The optimizer is HBM-bound and not counted."""
+    f = flops_per_image(cfg)
+    t = cfg.text
+    S, H = cfg.seq_len, t.hidden_size
+    Ta = cfg.text_len - cfg.question_len
+    dense = 2 * S * H * (t.q_dim + 2 * t.kv_dim) + 2 * S * t.q_dim * H + 2 * S * H * 2 * t.intermediate_size \
+        + 2 * S * t.intermediate_size * H
+    head_all, head = 2 * cfg.text_len * H * t.vocab_size, 2 * Ta * H * t.vocab_size
+    g_f = f["llm_fwd"] - head_all + head
+    g_b = f["llm_bwd"] - head_all + head + t.num_hidden_layers * dense + head
+    total = f["vit_fwd"] + f["proj_fwd"] + g_f + g_b
+    return dict(vit_fwd=f["vit_fwd"], proj_fwd=f["proj_fwd"], llm_fwd=g_f, llm_bwd=g_b, total=total)

@@ -1,0 +1,187 @@
+"""VQATrainerStage2 — the reference's Stage-2 trainer API (`Stage2/trainer.py:63-769`)
+running its step on libptk (`stage2.Stage2Engine`).
+
+Same constructor signature, `.train()`, `.evaluate(epoch, global_step)`,
+`.save_model(path)` and the module-level `vqa_collate_fn(batch, tokenizer)`.
+Supported configuration: BASELINE cfg4 — the LLM unfrozen (`freeze_llm=False`,
+no QLoRA), projector and vision encoder frozen; anything else raises
+NotImplementedError (QLoRA/peft needs 4-bit kernels; a trainable vision
+encoder or projector needs their backward passes).
+
+Kept reference semantics (Stage2/trainer.py:248-488):
+  * batches dealt as accelerate's prepared DataLoader deals them (even_batches),
+    padded per batch by `vqa_collate_fn` on the tokenizer's padding side;
+  * `accelerator.accumulate`: an optimizer step when (micro+1) % gas == 0 or at
+    the end of the rank's loader; loss / gas before `backward`, which divides by
+    gas again, grads summed over micro-batches;
+  * clip_grad_norm_(llm, 1.0), AdamW(lr, wd) over the LLM parameters, cosine
+    schedule with warmup (horizon from the unsharded loader), stepped
+    num_processes times per optimizer step;
+  * logging keys `train/batch_loss` (every micro-batch), `train/step_loss` (sync
+    micro-batches), `train/loss` = sum of sync losses / len(train_loader) per
+    epoch, `val/loss`.
+Validation by sampled `generate` (:595-647) is out of scope: `evaluate` computes
+the validation loss only.  `save_model` writes the fine-tuned LLM as HF-named
+bf16 tensors (`language_model/model.safetensors`, accelerate's save_model
+layout) plus the optimizer state of this rank (`optimizer_rank{r}.pt`).
+"""
+from __future__ import annotations
+
+import logging
+import math
+import os
+
+import torch
+
+from . import dist as D
+from .gemma3 import Gemma3CausalLM
+from .projectors import MLPProjector
+from .siglip import SiglipVisionTower
+from .stage2 import Stage2Engine
+
+logger = logging.getLogger(__name__)
+
+
+def vqa_collate_fn(batch, tokenizer):
+    """Stage2/trainer.py:18-61: stack pixel values; pad question and answer ids to the longest of the
+    batch with tokenizer.pad_token_id on tokenizer.padding_side."""
+    pad_id, side = tokenizer.pad_token_id, getattr(tokenizer, "padding_side", "right")
+
+    def pad(seqs):
+        n = max(s.shape[0] for s in seqs)
+        out = []
+        for s in seqs:
+            p = torch.full((n - s.shape[0],), pad_id, dtype=s.dtype)
+            out.append(torch.cat([p, s]) if side == "left" else torch.cat([s, p]))
+        return torch.stack(out)
+    return {"pixel_values": torch.stack([it["pixel_values"] for it in batch]),
+            "question_input_ids": pad([it["question_input_ids"] for it in batch]),
+            "answer_input_ids": pad([it["answer_input_ids"] for it in batch])}
+
+
+class VQATrainerStage2:
+    def __init__(self, accelerator, vision_encoder, language_model, projection_layer, tokenizer, train_dataset,
+                 val_dataset, output_dir: str, batch_size: int, learning_rate: float, weight_decay: float,
+                 num_epochs: int, gradient_accumulation_steps: int, warmup_ratio: float, freeze_vision_encoder: bool,
+                 freeze_projection_layer: bool, freeze_llm: bool, enable_qlora: bool, train_ve_first_epoch: bool,
+                 wandb_project: str, log_fn=None, seed: int = 0):
+        if enable_qlora:
+            raise NotImplementedError("VQATrainerStage2 (HIP): QLoRA / 4-bit LLMs are not supported; run with the "
+                                      "dense bf16 LLM and --unfreeze_llm")
+        if freeze_llm or not freeze_projection_layer or not freeze_vision_encoder or train_ve_first_epoch:
+            raise NotImplementedError("VQATrainerStage2 (HIP) supports the BASELINE cfg4 setting: LLM unfrozen, "
+                                      "projector and vision encoder frozen")
+        if accelerator is None:
+            accelerator = D.DistState(gradient_accumulation_steps)
+        elif not isinstance(accelerator, D.DistState):
+            accelerator = D.from_accelerator(accelerator)
+        self.accelerator = acc = accelerator
+        self.device = acc.device
+        self.tokenizer = tokenizer
+        self.output_dir, self.num_epochs, self.batch_size = output_dir, num_epochs, batch_size
+        self.train_dataset, self.val_dataset = train_dataset, val_dataset
+        self.wandb_project, self.log_fn, self.seed = wandb_project, log_fn, seed
+        self.gas = gradient_accumulation_steps
+        self.validation_dir = os.path.join(output_dir, "validation_examples")
+        if acc.is_main_process:
+            os.makedirs(self.validation_dir, exist_ok=True)
+
+        self.vision_encoder = vision_encoder if isinstance(vision_encoder, SiglipVisionTower) \
+            else SiglipVisionTower.from_hf(vision_encoder, self.device)
+        self.language_model = language_model if isinstance(language_model, Gemma3CausalLM) \
+            else Gemma3CausalLM.from_hf(language_model, self.device, max_pos=4096)
+        if not isinstance(projection_layer, MLPProjector):
+            sd = projection_layer.state_dict()
+            p = MLPProjector(sd["model.0.weight"].shape[1], sd["model.2.weight"].shape[0])
+            p.load_state_dict({k: v.detach().float().cpu() for k, v in sd.items()})
+            projection_layer = p
+        self.projection_layer = projection_layer.to(self.device)
+
+        # schedule horizon from the UNSHARDED loader (Stage2/trainer.py:151-165)
+        n_batches = math.ceil(len(train_dataset) / batch_size)
+        self.max_train_steps = num_epochs * math.ceil(n_batches / gradient_accumulation_steps)
+        self.num_warmup_steps = math.ceil(warmup_ratio * self.max_train_steps)
+        pad = getattr(tokenizer, "pad_token_id", None)
+        self.engine = Stage2Engine(self.vision_encoder, self.language_model, self.projection_layer,
+                                   learning_rate=learning_rate, weight_decay=weight_decay,
+                                   gradient_accumulation_steps=gradient_accumulation_steps,
+                                   warmup_steps=self.num_warmup_steps, total_steps=self.max_train_steps,
+                                   world_size=acc.num_processes, rank=acc.process_index,
+                                   pad_token_id=-1 if pad is None else int(pad))
+        self.global_step = 0
+
+    # ------------------------------------------------------------------ data
+    def _batches(self, dataset, epoch, shuffle=True):
+        acc = self.accelerator
+        for idx in D.shard_batches(len(dataset), self.batch_size, acc.process_index, acc.num_processes, epoch,
+                                   self.seed, shuffle):
+            b = vqa_collate_fn([dataset[int(i)] for i in idx], self.tokenizer)
+            yield {k: v.to(self.device, non_blocking=True) for k, v in b.items()}
+
+    def _log(self, d, step):
+        if self.accelerator.is_main_process:
+            if self.log_fn is not None:
+                self.log_fn(d, step)
+            else:
+                logger.info("step %d %s", step, d)
+
+    # ------------------------------------------------------------------ train
+    def train(self):
+        acc = self.accelerator
+        logger.info("Process %d: Starting Stage 2 training for %d epochs on device %s", acc.process_index,
+                    self.num_epochs, self.device)
+        n_local = D.batches_per_rank(len(self.train_dataset), self.batch_size, acc.num_processes)
+        for epoch in range(self.num_epochs):
+            epoch_train_loss = 0.0
+            for i, batch in enumerate(self._batches(self.train_dataset, epoch)):
+                loss = self.engine.forward_backward(batch["pixel_values"], batch["question_input_ids"],
+                                                    batch["answer_input_ids"])
+                sync = (i + 1) % self.gas == 0 or i + 1 == n_local
+                log = {}
+                if sync:
+                    self.engine.optimizer_step()
+                    self.global_step += 1
+                    avg_loss_step = float(acc.gather(loss).mean())
+                    epoch_train_loss += avg_loss_step
+                    log["train/step_loss"] = avg_loss_step
+                log.update({"train/batch_loss": float(acc.gather(loss).mean()),
+                            "train/learning_rate": self.engine.last_lr, "step": self.global_step})
+                self._log(log, self.global_step)
+            avg = epoch_train_loss / max(1, n_local)      # len(self.train_loader) (Stage2/trainer.py:468)
+            self._log({"train/loss": avg, "train/learning_rate": self.engine.last_lr, "epoch": epoch + 1},
+                      self.global_step)
+            if self.val_dataset is not None:
+                self.evaluate(epoch, self.global_step)
+            if acc.is_main_process:
+                self.save_model(os.path.join(self.output_dir, f"checkpoint-epoch_{epoch + 1}"))
+        logger.info("Process %d: Stage 2 training complete!", acc.process_index)
+
+    def evaluate(self, epoch, global_step):
+        """Validation loss (Stage2/trainer.py:490-593; the sampled generate() is out of scope).  The grads the
+        loss pass accumulates are discarded."""
+        tot, n = 0.0, 0
+        for batch in self._batches(self.val_dataset, 0, shuffle=False):
+            loss = self.engine.forward_backward(batch["pixel_values"], batch["question_input_ids"],
+                                                batch["answer_input_ids"])
+            tot += float(self.accelerator.gather(loss).mean())
+            n += 1
+        self.engine.state.zero_grad()
+        avg = tot / max(1, n)
+        self._log({"val/loss": avg, "epoch": epoch + 1}, global_step)
+        return avg
+
+    def save_model(self, path):
+        """language_model/model.safetensors (HF names, bf16) + this rank's optimizer state."""
+        if not self.accelerator.is_main_process:
+            return
+        from safetensors.torch import save_file
+        llm_dir = os.path.join(path, "language_model")
+        os.makedirs(llm_dir, exist_ok=True)
+        torch.cuda.synchronize(self.device)
+        sd = {k: v.detach().contiguous().cpu() for k, v in self.engine.state.state_dict_hf().items()}
+        save_file(sd, os.path.join(llm_dir, "model.safetensors"))
+        eng = self.engine
+        torch.save({"exp_avg": eng.exp_avg.cpu(), "exp_avg_sq": eng.exp_avg_sq.cpu(), "step": eng.opt_step,
+                    "sched_step": eng.sched_step, "shard": (eng.shard_lo, eng.shard_n)},
+                   os.path.join(path, f"optimizer_rank{self.accelerator.process_index}.pt"))
+        logger.info("Full language model saved to %s", llm_dir)

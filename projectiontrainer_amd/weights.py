@@ -105,3 +105,44 @@ def synthetic_batch(cfg: Stage1Config, seed: int = 1234, max_pad: int | None = N
     labels = ids.copy()
     labels[ids == t.pad_token_id] = -100
     return px, ids, labels
+
+
+def synthetic_vqa_items(cfg: Stage1Config, n: int, seed: int = 21, q_len=(3, 8), a_len=(4, 12)):
+    """n VQA samples in the reference's Stage-2 item format (Stage2/dataset.py:115-119): pixel_values
+    f32 [3,H,W] in [-1,1), question ids (tokenised without special tokens, :98-103) of length in q_len,
+    answer ids (with special tokens: BOS first, :106-110) of 1 + length in a_len."""
+    import torch
+    rng = np.random.default_rng(seed)
+    v, t = cfg.vision, cfg.text
+    px = rng.uniform(-1.0, 1.0, (n, v.num_channels, v.image_size, v.image_size)).astype(np.float32)
+    items = []
+    for i in range(n):
+        q = rng.integers(3, t.vocab_size, int(rng.integers(q_len[0], q_len[1] + 1)), dtype=np.int64)
+        a = np.concatenate([[t.bos_token_id],
+                            rng.integers(3, t.vocab_size, int(rng.integers(a_len[0], a_len[1] + 1)), dtype=np.int64)])
+        items.append({"pixel_values": torch.from_numpy(px[i]), "question_input_ids": torch.from_numpy(q),
+                      "answer_input_ids": torch.from_numpy(a.astype(np.int64))})
+    return items
+
+
+def synthetic_vqa_batch(cfg: Stage1Config, seed: int = 1234, padding_side: str = "left"):
+    """One collated Stage-2 batch (vqa_collate_fn output, Stage2/trainer.py:18-61) at cfg's shapes:
+    pixel_values f32 [B,3,H,W], question ids [B, question_len], answer ids [B, text_len - question_len]
+    (BOS first), each sample's tokens covering 3/4..all of the padded length (pad id elsewhere)."""
+    v, t = cfg.vision, cfg.text
+    B, Tq = cfg.batch_size, cfg.question_len
+    Ta = cfg.text_len - Tq
+    rng = np.random.default_rng(seed)
+    px = rng.uniform(-1.0, 1.0, (B, v.num_channels, v.image_size, v.image_size)).astype(np.float32)
+    q = np.full((B, Tq), t.pad_token_id, dtype=np.int64)
+    a = np.full((B, Ta), t.pad_token_id, dtype=np.int64)
+    for b in range(B):
+        nq = int(rng.integers(max(1, 3 * Tq // 4), Tq + 1))
+        na = int(rng.integers(max(2, 3 * Ta // 4), Ta + 1))
+        qq = rng.integers(3, t.vocab_size, nq, dtype=np.int64)
+        aa = np.concatenate([[t.bos_token_id], rng.integers(3, t.vocab_size, na - 1, dtype=np.int64)])
+        if padding_side == "left":
+            q[b, Tq - nq:], a[b, Ta - na:] = qq, aa
+        else:
+            q[b, :nq], a[b, :na] = qq, aa
+    return px, q, a

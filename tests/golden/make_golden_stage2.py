@@ -58,21 +58,6 @@ def sub_strides(shape):
     return sr, sc
 
 
-def stage2_items(cfg, n, seed):
-    """Synthetic VQA samples in the reference dataset's item format (Stage2/dataset.py:115-119): pixel
-    values, question ids without special tokens, answer ids starting with BOS (add_special_tokens)."""
-    rng = np.random.default_rng(seed)
-    v, t = cfg.vision, cfg.text
-    px = rng.uniform(-1.0, 1.0, (n, v.num_channels, v.image_size, v.image_size)).astype(np.float32)
-    items = []
-    for i in range(n):
-        q = rng.integers(3, t.vocab_size, int(rng.integers(3, 9)), dtype=np.int64)
-        a = np.concatenate([[t.bos_token_id], rng.integers(3, t.vocab_size, int(rng.integers(4, 13)), dtype=np.int64)])
-        items.append({"pixel_values": torch.from_numpy(px[i]), "question_input_ids": torch.from_numpy(q),
-                      "answer_input_ids": torch.from_numpy(a.astype(np.int64))})
-    return items
-
-
 class _Tok:
     """The tokenizer surface VQATrainerStage2.train / vqa_collate_fn touch."""
     def __init__(self, pad, eos, side):
@@ -111,7 +96,7 @@ def run(name: str, precision: str, gas: int = 2, lr: float = 1e-3, num_epochs: i
     if precision == "bf16":
         sig, llm, proj = sig.to(torch.bfloat16), llm.to(torch.bfloat16), proj.to(dtype=torch.bfloat16)
 
-    data = stage2_items(cfg, n_items, seed)
+    data = W.synthetic_vqa_items(cfg, n_items, seed)
     args = types.SimpleNamespace(gradient_accumulation_steps=gas, disable_wandb=True, batch_size=batch_size,
                                  wandb_project="x", wandb_run_name=None)
     acc = setup_accelerator_and_logging(args)

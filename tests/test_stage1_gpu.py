@@ -19,7 +19,8 @@ implementations of one function each sit ~noise away from fp32), and within
 SURVEY.md:297's bar wherever that noise is below it:
   loss |d| <= 2e-2 abs;
   patch embeddings / projector output / d(projector output) / projector grads:
-    rel-L2 <= max(2e-2, 2 * noise_rel_l2), cosine >= min(0.999, 1 - 2 * (1 - noise_cos));
+    rel-L2 <= max(2e-2, 2 * noise_rel_l2), cosine >= min(0.999, 1 - 4 * (1 - noise_cos)) (1 - cos
+    ~ rel-L2^2 / 2, so both are a factor 2 on the distance);
   post-AdamW params: max |d| <= 2.5 * sum(lr so far) (Adam's early steps move each weight by
     ~lr, so a sign flip of a near-zero grad moves it by at most ~2 lr per step) and
     median |d| <= 0.05 * lr.
@@ -84,7 +85,7 @@ def compare(d, key, got, rl2, cos=None, atol=None, med=None, test="", name=None)
         n_rl2, n_cos = twin_noise(name, key)
         rl2 = max(rl2, 2.0 * n_rl2)
         if cos is not None:
-            cos = min(cos, 1.0 - 2.0 * (1.0 - n_cos))
+            cos = min(cos, 1.0 - 4.0 * (1.0 - n_cos))   # 1 - cos ~ rel-L2^2 / 2: factor 2 on the distance
     if key in d.files:
         ref = d[key]
         g = got
