@@ -266,7 +266,7 @@ def reduce_scatter_(out_shard, flat, world, rank, group=None):
     """Sum of `flat` over ranks, this rank's contiguous shard into out_shard (RCCL reduce-scatter; gloo
     has none: all-reduce and slice)."""
     if dist.get_backend(group) == "gloo":
-        t = flat.clone()
+        t = flat.float()            # gloo has no bf16 sum: fp32 sum of the bf16 values, one rounding
         dist.all_reduce(t, op=dist.ReduceOp.SUM, group=group)
         n = out_shard.numel()
         out_shard.copy_(t[rank * n:(rank + 1) * n])
@@ -277,8 +277,8 @@ def reduce_scatter_(out_shard, flat, world, rank, group=None):
 
 def all_gather_(flat, shard, world, group=None):
     if dist.get_backend(group) == "gloo":
-        parts = [torch.empty_like(shard) for _ in range(world)]
-        dist.all_gather(parts, shard, group=group)
+        parts = [torch.empty(shard.shape, dtype=torch.float32, device=shard.device) for _ in range(world)]
+        dist.all_gather(parts, shard.float(), group=group)     # bf16 -> fp32 -> bf16 is exact
         flat.copy_(torch.cat(parts))
     else:
         dist.all_gather_into_tensor(flat, shard, group=group)

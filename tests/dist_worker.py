@@ -179,3 +179,25 @@ def nccl_world1(rank, world, port, out_dir):
             np.array([dist.get_backend() == "nccl", float(t[0]), float((eng.proj.flat_grad - g).abs().max()),
                       loss.numel(), acc.num_processes]))
     dist.destroy_process_group()
+
+
+def stage2_zero(rank, world, port, out_dir):
+    """GPU (one device shared) / gloo, world 2: Stage2Engine with ZeRO-1 sharding; each rank runs one half of a
+    batch, then the sharded optimizer step.  Saves the replica's flat parameters."""
+    _init(rank, world, port, "gloo")
+    import math
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.stage2 import synthetic_engine
+    dev = torch.device("cuda:0")
+    cfg = PRESETS["tiny"].replace(batch_size=4, text_len=8 + 12, question_len=8)
+    torch.manual_seed(0)
+    eng = synthetic_engine(cfg, dev, seed=3, world_size=world, rank=rank, learning_rate=1e-3, total_steps=10)
+    px, q, a = (torch.from_numpy(t).to(dev) for t in W.synthetic_vqa_batch(cfg, seed=9))
+    sl = slice(2 * rank, 2 * rank + 2)
+    eng.forward_backward(px[sl], q[sl], a[sl])
+    eng.optimizer_step()
+    torch.cuda.synchronize()
+    np.save(os.path.join(out_dir, f"s2param{rank}.npy"), eng.state.flat.float().cpu().numpy())
+    np.save(os.path.join(out_dir, f"s2norm{rank}.npy"), eng.grad_norm.cpu().numpy())
+    dist.destroy_process_group()

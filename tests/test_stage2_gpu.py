@@ -153,3 +153,124 @@ def test_stage2_state_roundtrip(gpu):
     assert torch.equal(lay["wgu_t"], lay["wgu"].t().contiguous())
     assert torch.equal(lay["ln_pre_ff"], st.view("1.ln_pre_ff").float())
     assert torch.equal(llm.embed_t, llm.embed.t().contiguous())
+
+
+def test_stage2_zero1_two_ranks_match_single_process(gpu):
+    """ZeRO-1 (reduce-scatter of the bf16 grads, sharded bf16 AdamW, all-gather) at world 2 (gloo on one
+    device) gives bit-identical replicas equal to one process that accumulates both halves of the batch and
+    halves the grad (DDP's average; exact in bf16), then steps the whole buffer."""
+    import tempfile
+    import torch.multiprocessing as mp
+    from tests import dist_worker
+    from tests.test_dist import _port
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.stage2 import synthetic_engine
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(dist_worker.stage2_zero, args=(2, _port(), td), nprocs=2, join=True)
+        p0, p1 = np.load(f"{td}/s2param0.npy"), np.load(f"{td}/s2param1.npy")
+        n0 = np.load(f"{td}/s2norm0.npy")
+    np.testing.assert_array_equal(p0, p1)
+    cfg = PRESETS["tiny"].replace(batch_size=4, text_len=8 + 12, question_len=8)
+    torch.manual_seed(0)
+    eng = synthetic_engine(cfg, gpu, seed=3, learning_rate=1e-3, total_steps=10)
+    px, q, a = (torch.from_numpy(t).to(gpu) for t in W.synthetic_vqa_batch(cfg, seed=9))
+    for r in range(2):
+        sl = slice(2 * r, 2 * r + 2)
+        eng.forward_backward(px[sl], q[sl], a[sl])
+    eng.state.grad.mul_(0.5)
+    eng.optimizer_step()
+    torch.cuda.synchronize()
+    flat = eng.state.flat.float().cpu().numpy()
+    n = min(flat.size, p0.size)        # the stores differ only in their zero tail (shards padded per world)
+    assert not flat[n:].any() and not p0[n:].any()
+    # every matrix and norm weight is bit-identical.  The tied embedding is not: each micro-batch adds two
+    # terms to its bf16 grad (lm_head GEMM, then the input-embedding scatter), so accumulating both halves
+    # in one process rounds ((G0 + L1) + E1) where the reduce-scatter rounds G0 + (L1 + E1) -- the same
+    # bf16 order dependence the reference has between DDP and accumulation.  There: within 2 lr (one Adam
+    # step moves a weight by ~lr).
+    e0, e1 = eng.state.offsets["embed"][0], eng.state.offsets["embed"][0] + cfg.text.vocab_size * cfg.text.hidden_size
+    mask = np.ones(n, dtype=bool)
+    mask[e0:e1] = False
+    np.testing.assert_array_equal(flat[:n][mask], p0[:n][mask])
+    assert np.abs(flat[e0:e1] - p0[e0:e1]).max() <= 2e-3
+    np.testing.assert_allclose(float(eng.grad_norm), float(n0[0]), rtol=1e-6)
+
+
+def test_vqa_trainer_api_with_hf_models(gpu, tmp_path):
+    """VQATrainerStage2 driven as train_vqa_stage2.py:313-340 drives the reference's: HF SiglipModel /
+    Gemma3ForCausalLM loaded in bf16, a frozen projector, cfg4 flags.  Two epochs of 3 micro-batches at
+    gas 2: 4 optimizer steps (syncs at micro-batch 2 and at each epoch end), the reference's log keys, a
+    checkpoint HF Gemma3ForCausalLM loads; and the trainer's parameters are bit-identical to a Stage2Engine
+    replay of the same batches (the trainer adds plumbing only)."""
+    import types
+    from safetensors.torch import load_file
+    from transformers import Gemma3ForCausalLM, Gemma3TextConfig, SiglipConfig, SiglipModel
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd import dist as D
+    from projectiontrainer_amd.config import PRESETS, to_hf_dicts
+    from projectiontrainer_amd.projectors import MLPProjector
+    from projectiontrainer_amd.vqa_trainer import VQATrainerStage2, vqa_collate_fn
+    cfg = PRESETS["tiny"]
+    vis_kw, txt_kw = to_hf_dicts(cfg)
+    vp, lp = W.siglip_vision_params(cfg.vision), W.gemma3_params(cfg.text)
+    pp = {k: G.bf16_round(v) for k, v in W.projector_params(cfg.vision.hidden_size, cfg.text.hidden_size).items()}
+
+    def models():
+        sig = SiglipModel(SiglipConfig(text_config=dict(vocab_size=64, hidden_size=64, intermediate_size=128,
+                                                        num_hidden_layers=1, num_attention_heads=1,
+                                                        max_position_embeddings=16, bos_token_id=None,
+                                                        eos_token_id=None, pad_token_id=None),
+                                       vision_config=vis_kw))
+        sig.load_state_dict({k: torch.from_numpy(v) for k, v in vp.items()}, strict=False)
+        llm = Gemma3ForCausalLM(Gemma3TextConfig(**txt_kw))
+        llm.load_state_dict({k: torch.from_numpy(v) for k, v in lp.items()}, strict=False)
+        proj = MLPProjector(cfg.vision.hidden_size, cfg.text.hidden_size)
+        proj.load_state_dict({k: torch.from_numpy(v) for k, v in pp.items()})
+        return sig.to(torch.bfloat16), llm.to(torch.bfloat16), proj
+
+    data = W.synthetic_vqa_items(cfg, 6, seed=21)
+    tok = types.SimpleNamespace(pad_token_id=0, eos_token_id=1, padding_side="left")
+    logs = []
+    sig, llm, proj = models()
+    tr = VQATrainerStage2(D.DistState(2), sig, llm, proj, tok, data, data[:2], str(tmp_path), 2, 1e-3, 0.01, 2, 2,
+                          0.05, freeze_vision_encoder=True, freeze_projection_layer=True, freeze_llm=False,
+                          enable_qlora=False, train_ve_first_epoch=False, wandb_project="x",
+                          log_fn=lambda d, s: logs.append(d))
+    assert tr.max_train_steps == 4 and tr.num_warmup_steps == 1
+    tr.train()
+    torch.cuda.synchronize()
+    assert tr.global_step == 4
+    assert len([x for x in logs if "train/batch_loss" in x]) == 6
+    assert len([x for x in logs if "train/step_loss" in x]) == 4
+    assert len([x for x in logs if "val/loss" in x]) == 2 and len([x for x in logs if "train/loss" in x]) == 2
+    sd = load_file(str(tmp_path / "checkpoint-epoch_2" / "language_model" / "model.safetensors"))
+    hf = Gemma3ForCausalLM(Gemma3TextConfig(**txt_kw)).to(torch.bfloat16)
+    res = hf.load_state_dict(sd, strict=False)
+    assert set(res.missing_keys) <= {"lm_head.weight"} and not res.unexpected_keys
+    for k, v in tr.engine.state.state_dict_hf().items():
+        assert torch.equal(sd[k], v.cpu()), k
+    # replay through the engine alone
+    from projectiontrainer_amd.stage2 import Stage2Engine
+    from projectiontrainer_amd.gemma3 import Gemma3CausalLM
+    from projectiontrainer_amd.siglip import SiglipVisionTower
+    sig, llm, proj = models()
+    eng = Stage2Engine(SiglipVisionTower.from_hf(sig, gpu), Gemma3CausalLM.from_hf(llm, gpu, max_pos=4096),
+                       proj.to(gpu), learning_rate=1e-3, weight_decay=0.01, gradient_accumulation_steps=2,
+                       warmup_steps=1, total_steps=4, pad_token_id=0)
+    for epoch in range(2):
+        idx = D.shard_batches(6, 2, 0, 1, epoch, 0, True)
+        for i, b in enumerate(idx):
+            bt = vqa_collate_fn([data[int(j)] for j in b], tok)
+            eng.forward_backward(bt["pixel_values"].to(gpu), bt["question_input_ids"].to(gpu),
+                                 bt["answer_input_ids"].to(gpu))
+            if (i + 1) % 2 == 0 or i + 1 == len(idx):
+                eng.optimizer_step()
+        # evaluate() runs a loss pass over the validation set and discards its grads
+        for b in D.shard_batches(2, 2, 0, 1, 0, 0, False):
+            bt = vqa_collate_fn([data[int(j)] for j in b], tok)
+            eng.forward_backward(bt["pixel_values"].to(gpu), bt["question_input_ids"].to(gpu),
+                                 bt["answer_input_ids"].to(gpu))
+        eng.state.zero_grad()
+    torch.cuda.synchronize()
+    assert torch.equal(eng.state.flat, tr.engine.state.flat)
