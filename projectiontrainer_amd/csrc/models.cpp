@@ -118,6 +118,8 @@ struct GemmaWs {
   // unfrozen LLM only: feature-major GEMM operands of dW = dY^T X (K = tokens) and norm-grad partials
   bf16_t *TA = nullptr, *TB = nullptr, *TL = nullptr, *TX = nullptr;
   float* wpart = nullptr;
+  float* skpart = nullptr;     // split-K partials (gemm_split)
+  long sk_floats = 0;
 };
 
 GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp, bool train = false) {
@@ -198,16 +200,53 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
     w.TB = bp.take<bf16_t>(std::max(std::max(H, Dq), I) * M);
     w.TL = bp.take<bf16_t>(V * Rp);
     w.TX = bp.take<bf16_t>(H * Rp);
-    w.wpart = bp.take<float>(std::max((long)rms_wgrad_partial_floats((int)M, (int)H), 2 * ((M + 63) / 64) * D));
+    w.wpart = bp.take<float>(std::max((long)rms_wgrad_partial_floats((int)M, (int)H),
+                                      (long)qknorm_wgrad_partial_floats(M, (int)D)));
   }
+  // split-K partials (gemm_split): 2 slices of the largest [M, H] / [2I, H] output, 4 of the small dW ones
+  w.sk_floats = std::max(std::max(2 * M * H, 2 * 2 * I * H), 4 * std::max(Dqkv, H) * H);
+  w.skpart = bp.take<float>(w.sk_floats);
   return w;
+}
+
+// Split-K for long-K GEMMs whose 256x256 tile grid fills few of the CUs' rounds (measured, tools/splitk_probe.py
+// r02: the cfg4 shapes dW_qkv 313 -> 73 us and dW_o 313 -> 68 us at 4 slices; dW_down, dW_gate|up, the
+// d(gate|up) dX and the down projection at 280 tiles -8..-16 % at 2 slices; the cfg2 d(gate|up) dX at 440
+// tiles is slower split, the vocab-wide lm_head dW too).  ACT_NONE only; OUT_F32, or OUT_BF16 with the
+// optional bf16 accumulate (bf16_linear + resid16, the weight-grad epilogue).  The slices go to the batched
+// 128x128 kernel as fp32 partials [S][M][N]; one pass sums them in slice order (deterministic).
+int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStream_t st) {
+  const long nbig = (long)((a.M + 255) / 256) * ((a.N + 255) / 256);
+  int S = 1;
+  if (a.K >= 4096 && nbig <= 64) S = 4;
+  else if (a.K >= 4096 && nbig <= 300) S = 2;
+  while (S > 1 && ((long)S * a.M * a.N > part_floats || a.K / S < 1024 || a.N % 4 || a.ldc % 4)) S /= 2;
+  const bool plain = !a.rowadd && !a.resid && !a.aux && !a.aux_in && a.amap.g == 0 && a.amap.off == 0 &&
+                     a.cmap.g == 0 && a.cmap.off == 0 && a.bias == nullptr && a.alpha == 1.f;
+  if (S == 1 || !plain || !part) return launch_gemm(a, ACT_NONE, out, 1, st);
+  const int kc = (a.K / S + 63) / 64 * 64;
+  const int nfull = a.K / kc, rem = a.K - nfull * kc;
+  GemmArgs b = a;
+  b.C = part; b.ldc = a.N; b.K = kc;
+  b.sA0 = kc; b.sB0 = kc; b.sC0 = (long)a.M * a.N;
+  b.bf16_linear = 0; b.resid16 = nullptr; b.ld_resid16 = 0;
+  CK(launch_gemm(b, ACT_NONE, OUT_F32, nfull, st));
+  if (rem) {
+    GemmArgs r = b;
+    r.A = a.A + (long)nfull * kc; r.B = a.B + (long)nfull * kc; r.K = rem;
+    r.C = part + (long)nfull * a.M * a.N;
+    CK(launch_gemm(r, ACT_NONE, OUT_F32, 1, st));
+  }
+  const bool bf = out == OUT_BF16;
+  return launch_splitk_reduce(part, nfull + (rem ? 1 : 0), a.M, a.N, a.C, a.ldc, bf ? 1 : 0,
+                              bf ? a.resid16 : nullptr, a.ld_resid16, st);
 }
 
 // dW (+)= dY^T X over K token rows: both operands are token-major, so each is first transposed to a
 // K-contiguous feature-major copy (rows gathered through a map, zero-padded to a multiple of 64), then one
 // MFMA GEMM accumulates into the bf16 .grad (bf16(grad + bf16(acc)), autograd's accumulation).
 int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* x, long ldx, RowMap xmap, int Nx,
-                int rows, bf16_t* TA, bf16_t* TB, void* grad, hipStream_t st) {
+                int rows, bf16_t* TA, bf16_t* TB, void* grad, float* skpart, long sk_floats, hipStream_t st) {
   if (!grad) return 0;
   const int Kp = (rows + 63) / 64 * 64;
   CK(launch_transpose_rows(dy, lddy, ymap, rows, Ny, TA, Kp, Kp, st));
@@ -216,7 +255,7 @@ int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* 
   g.bf16_linear = 1;
   g.resid16 = (const bf16_t*)grad;
   g.ld_resid16 = Nx;
-  return launch_gemm(g, ACT_NONE, OUT_BF16, 1, st);
+  return gemm_split(g, OUT_BF16, skpart, sk_floats, st);
 }
 
 }  // namespace
@@ -379,7 +418,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
       GemmArgs g = gemm(xff, H, L.wgu, H, hh, I, M, 2 * I, H);
       g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
       CK(launch_gemm(g, ACT_GEGLU, OUT_BF16, 1, st));
-      CK(launch_gemm(gemm(hh, I, L.wd, I, sv.dn, H, M, H, I), ACT_NONE, OUT_BF16, 1, st));
+      CK(gemm_split(gemm(hh, I, L.wd, I, sv.dn, H, M, H, I), OUT_BF16, w.skpart, w.sk_floats, st));
     } else {
       // last layer: only the loss rows reach the loss, so its MLP runs on those R rows (h, g, u compact);
       // the other rows of dn are zero (their residual output is never read, their gradient is zero)
@@ -406,7 +445,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
   CK(launch_ce_fwd_bwd(w.logits, V, R, V, bt->labels, w.row_loss, w.gscale, st));
   CK(launch_loss_reduce(w.row_loss, R, w.count, bt->loss, st));
   // tied lm_head weight grad: dE += dlogits^T . xf (the logits rows outside the loss rows have zero grad)
-  if (train) CK(weight_grad(w.logits, V, ident, V, w.xf, H, ident, H, R, w.TL, w.TX, gr->embed, st));
+  if (train) CK(weight_grad(w.logits, V, ident, V, w.xf, H, ident, H, R, w.TL, w.TX, gr->embed, w.skpart, w.sk_floats, st));
   {  // d(xf) = dlogits . E, K = vocab: split-K over LM_SPLITK equal slices (fp32 partials, ordered sum);
      // a vocab that is not a multiple of 64 * LM_SPLITK (Gemma3-4B: 262 208 = 4 097 x 64) leaves a
      // remainder slice, computed into one more partial
@@ -446,8 +485,8 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
     }
     // down projection weight grad: d(dn)^T . h (last layer: the loss rows and the compact h)
     if (train)
-      CK(last ? weight_grad(w.dao, H, lossmap, H, sv.h, I, ident, I, R, w.TA, w.TB, GL->wd, st)
-              : weight_grad(w.dao, H, ident, H, sv.h, I, ident, I, M, w.TA, w.TB, GL->wd, st));
+      CK(last ? weight_grad(w.dao, H, lossmap, H, sv.h, I, ident, I, R, w.TA, w.TB, GL->wd, w.skpart, w.sk_floats, st)
+              : weight_grad(w.dao, H, ident, H, sv.h, I, ident, I, M, w.TA, w.TB, GL->wd, w.skpart, w.sk_floats, st));
     // d(gate|up) = GEGLU backward of dh = dd . Wd, fused into the persistent 4-wave GEMM's register
     // epilogue (g, u loaded one row block ahead; dh never reaches HBM).  PTK_GEGLU_SPLIT=1: the plain
     // GEMM + one streaming geglu_bwd pass instead (A/B)
@@ -462,14 +501,14 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
         g.ld_aux_in = I;
         CK(launch_gemm(g, ACT_GEGLU_BWD, OUT_BF16, 1, st));
       }
-      if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, ident, H, M, w.TA, w.TB, GL->wgu, st));
-      CK(launch_gemm(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), ACT_NONE, OUT_F32, 1, st));
+      if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, ident, H, M, w.TA, w.TB, GL->wgu, w.skpart, w.sk_floats, st));
+      CK(gemm_split(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), OUT_F32, w.skpart, w.sk_floats, st));
     } else {   // last layer: MLP gradient is non-zero on the loss rows only (compact h, g, u, dgu)
       GemmArgs g = gemm(w.dao, H, L.wd_t, H, w.h, I, R, I, H);
       g.amap = lossmap;
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
       CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, R, I, st));
-      if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, lossmap, H, R, w.TA, w.TB, GL->wgu, st));
+      if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, lossmap, H, R, w.TA, w.TB, GL->wgu, w.skpart, w.sk_floats, st));
       CKH(hipMemsetAsync(w.dtmp, 0, (size_t)M * H * sizeof(float), st));
       GemmArgs g2 = gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, R, H, 2 * I);
       g2.cmap = lossmap;
@@ -480,7 +519,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
                                 M, H, st));
     if (train) {
       CK(launch_rms_wgrad_bx(sv.ao, H, ident, sv.rstd_ao, dR, H, 1, M, H, (bf16_t*)GL->ln_post_attn, w.wpart, st));
-      CK(weight_grad(w.dao, H, ident, H, sv.O, Dq, ident, Dq, M, w.TA, w.TB, GL->wo, st));
+      CK(weight_grad(w.dao, H, ident, H, sv.O, Dq, ident, Dq, M, w.TA, w.TB, GL->wo, w.skpart, w.sk_floats, st));
     }
     {  // dO (Q layout) = dao . Wo, one GEMM per kv head group of output columns
       GemmArgs g = gemm(w.dao, H, L.wo_t, H, w.dO, (long)G * D, M, G * D, H);
@@ -510,7 +549,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
     if (train) {
       CK(launch_qknorm_wgrad(sv.qkv, cs, sn, ash, sv.rstd_q, sv.rstd_k, w.dQ, w.dK, (bf16_t*)GL->q_norm,
                              (bf16_t*)GL->k_norm, w.wpart, st));
-      CK(weight_grad(w.dqkv, Dqkv, ident, Dqkv, sv.xn_in, H, ident, H, M, w.TA, w.TB, GL->wqkv, st));
+      CK(weight_grad(w.dqkv, Dqkv, ident, Dqkv, sv.xn_in, H, ident, H, M, w.TA, w.TB, GL->wqkv, w.skpart, w.sk_floats, st));
     }
     CK(launch_gemm(gemm(w.dqkv, Dqkv, L.wqkv_t, Dqkv, w.dtmp, H, M, H, Dqkv), ACT_NONE, OUT_F32, 1, st));
     if (train) CK(launch_rms_wgrad(w.x[l], H, ident, sv.rstd_in, w.dtmp, H, 1, M, H, (bf16_t*)GL->ln_in, w.wpart, st));

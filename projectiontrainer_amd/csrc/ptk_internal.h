@@ -242,6 +242,10 @@ int launch_rms_wgrad_bx(const bf16_t* x, long ldx, RowMap xmap, const float* rst
 int launch_qknorm_wgrad(const bf16_t* qkv, const float* cos_t, const float* sin_t, AttnShape s, const float* rstd_q,
                         const float* rstd_k, const bf16_t* dQ, const bf16_t* dK, bf16_t* gq, bf16_t* gk,
                         float* partial, hipStream_t st);
+int qknorm_wgrad_partial_floats(long M, int D);
+// split-K partial reduce: C = sum_s part[s] (fp32) or bf16(resid + bf16(sum)) (bf16; resid may be null / alias C)
+int launch_splitk_reduce(const float* part, int S, int M, int N, void* C, long ldc, int out_bf16, const bf16_t* resid,
+                         long ldr, hipStream_t st);
 int launch_embed_grad(const int64_t* ids, int B, int T, int Nv, int Spad, int H, float escale, const float* dx,
                       bf16_t* dE, hipStream_t st);
 int scale_sumsq_partial_floats();

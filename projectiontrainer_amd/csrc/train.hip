@@ -80,7 +80,7 @@ int launch_transpose_rows(const bf16_t* in, long ld_in, RowMap map, int rows, in
 // partial[blk][c] = sum over the block's rows of dy[r,c] * x[xmap(r),c] * rstd[r]; dy optionally rounded to
 // bf16 first (the post-norms' output grads arrive as bf16 in the reference's autocast graph).
 // 256 threads own float4 column groups c = 4 t + 1024 j; WG_ROWS rows per block.
-constexpr int WG_ROWS = 64;
+constexpr int WG_ROWS = 32;
 PTK_DEV float4 ldv4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 PTK_DEV float4 ldv4(const bf16_t* p) {
   u16x4_t u = *reinterpret_cast<const u16x4_t*>(p);
@@ -120,14 +120,22 @@ __global__ void __launch_bounds__(256) rms_wgrad_partial_kernel(const TX* __rest
   }
 }
 
-// grad[c] = bf16(grad[c] + bf16(sum_b partial[b][c]))   (autograd accumulation into a bf16 .grad)
+// grad[c] = bf16(grad[c] + bf16(sum_b partial[b][c]))   (autograd accumulation into a bf16 .grad).
+// Block: 64 columns x 4 row groups (coalesced 256-B partial rows), fixed summation order.
 __global__ void __launch_bounds__(256) wgrad_finish_kernel(const float* __restrict__ partial, int nblk, int cols,
                                                            bf16_t* __restrict__ grad) {
-  const int c = blockIdx.x * 256 + threadIdx.x;
-  if (c >= cols) return;
+  __shared__ float red[4][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
   float s = 0.f;
-  for (int b = 0; b < nblk; ++b) s += partial[(long)b * cols + c];
-  grad[c] = f2bf(bf2f(grad[c]) + bfround(s));
+  if (c < cols)
+    for (int b = grp; b < nblk; b += 4) s += partial[(long)b * cols + c];
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp == 0 && c < cols) {
+    const float t = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+    grad[c] = f2bf(bf2f(grad[c]) + bfround(t));
+  }
 }
 
 template <typename TX, typename TD>
@@ -144,7 +152,7 @@ static int rms_wgrad_t(const TX* x, long ldx, RowMap xmap, const float* rstd, co
     case 3: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 3>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
     default: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 4>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
   }
-  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, st, partial, nblk, cols,
+  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((cols + 63) / 64)), dim3(256), 0, st, partial, nblk, cols,
                      grad);
   RET_OK("rms_wgrad");
 }
@@ -161,12 +169,18 @@ int launch_rms_wgrad_bx(const bf16_t* x, long ldx, RowMap xmap, const float* rst
 }
 
 // ---------------------------------------------------------------- q_norm / k_norm weight grads
-// One block per WG_ROWS token rows, one thread per head-dim element d (D <= 256, D even).  For every (row,
-// head): dn[d] = RoPE^T(dq)[d] (dq = grad of the rotated, normed head), x_hat[d] = q[d] * rstd[row, head];
+// For every (token row, head): dn = RoPE^T(dr) (dr = grad of the rotated, normed head), x_hat = x * rstd;
 // dw[d] += dn[d] * x_hat[d].  RoPE (rotate-half, cos/sin tables of D/2): rot[d] = n[d] c[d] - n[d+h] s[d]
 // (d < h), rot[d] = n[d] c[d-h] + n[d-h] s[d-h] (d >= h), so dn[d] = dr[d] c[d] + dr[d+h] s[d] (d < h),
 // dn[d] = dr[d] c[d-h] - dr[d-h] s[d-h] (d >= h).
 // dQ is in the attention layout [B, Hkv, S, G, D], dK in [B, Hkv, S, D]; qkv rows are token-major.
+// D = 256: one wave per token (4 lanes-elements each: lane l owns d = 4l..4l+3, its RoPE partner d +- 128 is
+// lane l +- 32, loaded directly), QK_ROWS tokens per block; per-block partials [blk][D], fixed-order finish.
+constexpr int QK_ROWS = 32;
+PTK_DEV float4 ldb4(const bf16_t* p) {
+  u16x4_t u = *reinterpret_cast<const u16x4_t*>(p);
+  return make_float4(bf2f(u[0]), bf2f(u[1]), bf2f(u[2]), bf2f(u[3]));
+}
 __global__ void __launch_bounds__(256) qknorm_wgrad_partial_kernel(const bf16_t* __restrict__ qkv,
                                                                    const float* __restrict__ cos_t,
                                                                    const float* __restrict__ sin_t,
@@ -176,47 +190,145 @@ __global__ void __launch_bounds__(256) qknorm_wgrad_partial_kernel(const bf16_t*
                                                                    const bf16_t* __restrict__ dK, AttnShape s,
                                                                    float* __restrict__ part_q,
                                                                    float* __restrict__ part_k) {
+  __shared__ float4 red_q[4][64], red_k[4][64];
+  const int D = 256, h = 128;
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const int d = 4 * lane, dp = d < h ? d + h : d - h, dc = d < h ? d : d - h;
+  const float sg = d < h ? 1.f : -1.f;
+  const int G = s.Hq / s.Hkv, Dqkv = (s.Hq + 2 * s.Hkv) * D;
+  const long M = (long)s.B * s.S;
+  float4 aq = make_float4(0.f, 0.f, 0.f, 0.f), ak = aq;
+  for (long r = (long)blockIdx.x * QK_ROWS + wv; r < min(M, (long)(blockIdx.x + 1) * QK_ROWS); r += 4) {
+    const int b = (int)(r / s.S), pos = (int)(r - (long)b * s.S);
+    const float4 c = *reinterpret_cast<const float4*>(cos_t + (long)pos * h + dc);
+    const float4 sn = *reinterpret_cast<const float4*>(sin_t + (long)pos * h + dc);
+    const bf16_t* qrow = qkv + r * Dqkv;
+    for (int hq = 0; hq < s.Hq; ++hq) {
+      const int kvh = hq / G, j = hq - kvh * G;
+      const bf16_t* g = dQ + ((((long)b * s.Hkv + kvh) * s.S + pos) * G + j) * D;
+      const float4 g0 = ldb4(g + d), g1 = ldb4(g + dp), x = ldb4(qrow + hq * D + d);
+      const float rs = rstd_q[r * s.Hq + hq];
+      aq.x += (g0.x * c.x + sg * g1.x * sn.x) * x.x * rs;
+      aq.y += (g0.y * c.y + sg * g1.y * sn.y) * x.y * rs;
+      aq.z += (g0.z * c.z + sg * g1.z * sn.z) * x.z * rs;
+      aq.w += (g0.w * c.w + sg * g1.w * sn.w) * x.w * rs;
+    }
+    for (int kvh = 0; kvh < s.Hkv; ++kvh) {
+      const bf16_t* g = dK + (((long)b * s.Hkv + kvh) * s.S + pos) * D;
+      const float4 g0 = ldb4(g + d), g1 = ldb4(g + dp), x = ldb4(qrow + (s.Hq + kvh) * D + d);
+      const float rs = rstd_k[r * s.Hkv + kvh];
+      ak.x += (g0.x * c.x + sg * g1.x * sn.x) * x.x * rs;
+      ak.y += (g0.y * c.y + sg * g1.y * sn.y) * x.y * rs;
+      ak.z += (g0.z * c.z + sg * g1.z * sn.z) * x.z * rs;
+      ak.w += (g0.w * c.w + sg * g1.w * sn.w) * x.w * rs;
+    }
+  }
+  red_q[wv][lane] = aq;
+  red_k[wv][lane] = ak;
+  __syncthreads();
+  if (wv == 0) {
+    float4 tq = red_q[0][lane], tk = red_k[0][lane];
+    for (int w = 1; w < 4; ++w) {
+      const float4 a = red_q[w][lane], bk = red_k[w][lane];
+      tq.x += a.x; tq.y += a.y; tq.z += a.z; tq.w += a.w;
+      tk.x += bk.x; tk.y += bk.y; tk.z += bk.z; tk.w += bk.w;
+    }
+    *reinterpret_cast<float4*>(part_q + (long)blockIdx.x * D + d) = tq;
+    *reinterpret_cast<float4*>(part_k + (long)blockIdx.x * D + d) = tk;
+  }
+}
+
+// generic head_dim (tests, tiny models): one thread per element d, QK_ROWS tokens per block
+__global__ void __launch_bounds__(256) qknorm_wgrad_partial_any_kernel(const bf16_t* __restrict__ qkv,
+                                                                       const float* __restrict__ cos_t,
+                                                                       const float* __restrict__ sin_t,
+                                                                       const float* __restrict__ rstd_q,
+                                                                       const float* __restrict__ rstd_k,
+                                                                       const bf16_t* __restrict__ dQ,
+                                                                       const bf16_t* __restrict__ dK, AttnShape s,
+                                                                       float* __restrict__ part_q,
+                                                                       float* __restrict__ part_k) {
   const int D = s.D, h = D / 2, d = threadIdx.x;
   const int G = s.Hq / s.Hkv, Dqkv = (s.Hq + 2 * s.Hkv) * D;
   const long M = (long)s.B * s.S;
-  const long r0 = (long)blockIdx.x * WG_ROWS, r1 = min(M, r0 + WG_ROWS);
+  const long r0 = (long)blockIdx.x * QK_ROWS, r1 = min(M, r0 + QK_ROWS);
+  if (d >= D) return;
   float aq = 0.f, ak = 0.f;
-  if (d < D) {
-    const int dp = d < h ? d + h : d - h, dc = d < h ? d : d - h;
-    for (long r = r0; r < r1; ++r) {
-      const int b = (int)(r / s.S), pos = (int)(r - (long)b * s.S);
-      const float c = cos_t[(long)pos * h + dc], sn = sin_t[(long)pos * h + dc];
-      const bf16_t* qrow = qkv + r * Dqkv;
-      for (int hq = 0; hq < s.Hq; ++hq) {
-        const int kvh = hq / G, j = hq - kvh * G;
-        const bf16_t* g = dQ + ((((long)b * s.Hkv + kvh) * s.S + pos) * G + j) * D;
-        const float dn = d < h ? bf2f(g[d]) * c + bf2f(g[dp]) * sn : bf2f(g[d]) * c - bf2f(g[dp]) * sn;
-        aq += dn * bf2f(qrow[hq * D + d]) * rstd_q[r * s.Hq + hq];
-      }
-      for (int kvh = 0; kvh < s.Hkv; ++kvh) {
-        const bf16_t* g = dK + (((long)b * s.Hkv + kvh) * s.S + pos) * D;
-        const float dn = d < h ? bf2f(g[d]) * c + bf2f(g[dp]) * sn : bf2f(g[d]) * c - bf2f(g[dp]) * sn;
-        ak += dn * bf2f(qrow[(s.Hq + kvh) * D + d]) * rstd_k[r * s.Hkv + kvh];
-      }
+  const int dp = d < h ? d + h : d - h, dc = d < h ? d : d - h;
+  const float sg = d < h ? 1.f : -1.f;
+  for (long r = r0; r < r1; ++r) {
+    const int b = (int)(r / s.S), pos = (int)(r - (long)b * s.S);
+    const float c = cos_t[(long)pos * h + dc], sn = sin_t[(long)pos * h + dc];
+    const bf16_t* qrow = qkv + r * Dqkv;
+    for (int hq = 0; hq < s.Hq; ++hq) {
+      const int kvh = hq / G, j = hq - kvh * G;
+      const bf16_t* g = dQ + ((((long)b * s.Hkv + kvh) * s.S + pos) * G + j) * D;
+      aq += (bf2f(g[d]) * c + sg * bf2f(g[dp]) * sn) * bf2f(qrow[hq * D + d]) * rstd_q[r * s.Hq + hq];
     }
-    part_q[(long)blockIdx.x * D + d] = aq;
-    part_k[(long)blockIdx.x * D + d] = ak;
+    for (int kvh = 0; kvh < s.Hkv; ++kvh) {
+      const bf16_t* g = dK + (((long)b * s.Hkv + kvh) * s.S + pos) * D;
+      ak += (bf2f(g[d]) * c + sg * bf2f(g[dp]) * sn) * bf2f(qrow[(s.Hq + kvh) * D + d]) * rstd_k[r * s.Hkv + kvh];
+    }
   }
+  part_q[(long)blockIdx.x * D + d] = aq;
+  part_k[(long)blockIdx.x * D + d] = ak;
 }
 
 int launch_qknorm_wgrad(const bf16_t* qkv, const float* cos_t, const float* sin_t, AttnShape s, const float* rstd_q,
                         const float* rstd_k, const bf16_t* dQ, const bf16_t* dK, bf16_t* gq, bf16_t* gk,
                         float* partial, hipStream_t st) {
-  if (s.D > 256 || s.D % 2) return set_error("qknorm_wgrad: head_dim %d", s.D);
+  if (s.D > 256 || s.D % 8) return set_error("qknorm_wgrad: head_dim %d", s.D);
   const long M = (long)s.B * s.S;
-  const int nblk = (int)((M + WG_ROWS - 1) / WG_ROWS);
+  const int nblk = (int)((M + QK_ROWS - 1) / QK_ROWS);
   float* pq = partial;
   float* pk = partial + (long)nblk * s.D;
-  hipLaunchKernelGGL(qknorm_wgrad_partial_kernel, dim3((unsigned)nblk), dim3(256), 0, st, qkv, cos_t, sin_t, rstd_q,
-                     rstd_k, dQ, dK, s, pq, pk);
-  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((s.D + 255) / 256)), dim3(256), 0, st, pq, nblk, s.D, gq);
-  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((s.D + 255) / 256)), dim3(256), 0, st, pk, nblk, s.D, gk);
+  if (s.D == 256)
+    hipLaunchKernelGGL(qknorm_wgrad_partial_kernel, dim3((unsigned)nblk), dim3(256), 0, st, qkv, cos_t, sin_t, rstd_q,
+                       rstd_k, dQ, dK, s, pq, pk);
+  else
+    hipLaunchKernelGGL(qknorm_wgrad_partial_any_kernel, dim3((unsigned)nblk), dim3(256), 0, st, qkv, cos_t, sin_t,
+                       rstd_q, rstd_k, dQ, dK, s, pq, pk);
+  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((s.D + 63) / 64)), dim3(256), 0, st, pq, nblk, s.D, gq);
+  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((s.D + 63) / 64)), dim3(256), 0, st, pk, nblk, s.D, gk);
   RET_OK("qknorm_wgrad");
+}
+
+int qknorm_wgrad_partial_floats(long M, int D) { return (int)(2 * ((M + QK_ROWS - 1) / QK_ROWS) * D); }
+
+// ---------------------------------------------------------------- split-K reduce
+// C = sum_s part[s] (fp32 out) or C = bf16(resid + bf16(sum_s part[s])) (bf16 out, resid may alias C or be
+// null); part [S][M][N] packed, C [M][ldc].  Fixed summation order.
+__global__ void __launch_bounds__(256) splitk_reduce_kernel(const float* __restrict__ part, int S, int M, int N,
+                                                            void* C, long ldc, int out_bf16,
+                                                            const bf16_t* resid, long ldr) {
+  const long i = ((long)blockIdx.x * 256 + threadIdx.x) * 4;
+  const long MN = (long)M * N;
+  if (i >= MN) return;
+  const int m = (int)(i / N), n = (int)(i - (long)m * N);
+  float4 acc = *reinterpret_cast<const float4*>(part + i);
+  for (int z = 1; z < S; ++z) {
+    const float4 v = *reinterpret_cast<const float4*>(part + (long)z * MN + i);
+    acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+  }
+  if (!out_bf16) {
+    *reinterpret_cast<float4*>((float*)C + (long)m * ldc + n) = acc;
+    return;
+  }
+  float4 r = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (resid) r = ldb4(resid + (long)m * ldr + n);
+  u16x4_t o;
+  o[0] = f2bf(r.x + bfround(acc.x)); o[1] = f2bf(r.y + bfround(acc.y));
+  o[2] = f2bf(r.z + bfround(acc.z)); o[3] = f2bf(r.w + bfround(acc.w));
+  *reinterpret_cast<u16x4_t*>((bf16_t*)C + (long)m * ldc + n) = o;
+}
+
+int launch_splitk_reduce(const float* part, int S, int M, int N, void* C, long ldc, int out_bf16, const bf16_t* resid,
+                         long ldr, hipStream_t st) {
+  if (N % 4 || ldc % 4 || (resid && ldr % 4)) return set_error("splitk_reduce: N / ld must be multiples of 4");
+  const long n4 = (long)M * N / 4;
+  hipLaunchKernelGGL(splitk_reduce_kernel, dim3((unsigned)((n4 + 255) / 256)), dim3(256), 0, st, part, S, M, N, C, ldc,
+                     out_bf16, resid, ldr);
+  RET_OK("splitk_reduce");
 }
 
 // ---------------------------------------------------------------- input-embedding grads

@@ -60,14 +60,22 @@ class Gemma3TrainState:
     def __init__(self, llm: Gemma3CausalLM, world_size: int = 1):
         self.llm, self.world = llm, world_size
         cfg, dev = llm.cfg, llm.device
-        segs = [("embed", tuple(llm.embed.shape)), ("final_norm", (cfg.hidden_size,))]
+        # matrices first, then every norm weight in one contiguous region (its fp32 mirror, which the norm
+        # kernels read, is refreshed with one copy)
+        segs = [("embed", tuple(llm.embed.shape))]
         for i, lay in enumerate(llm.layers):
-            segs += [(f"{i}.{k}", tuple(lay[k].shape)) for k in LAYER_KEYS]
+            segs += [(f"{i}.{k}", tuple(lay[k].shape)) for k in ("wqkv", "wo", "wgu", "wd")]
+        norm_segs = [("final_norm", (cfg.hidden_size,))]
+        for i, lay in enumerate(llm.layers):
+            norm_segs += [(f"{i}.{k}", tuple(lay[k].shape)) for k in NORM_KEYS]
         off, self.offsets = 0, {}
-        for name, shape in segs:
+        for j, (name, shape) in enumerate(segs + norm_segs):
+            if j == len(segs):
+                self.norm_lo = off
             self.offsets[name] = (off, shape)
             n = math.prod(shape)
             off += (n + self.ALIGN - 1) // self.ALIGN * self.ALIGN
+        self.norm_hi = off
         unit = self.ALIGN * world_size
         self.numel = (off + unit - 1) // unit * unit          # equal ZeRO shards
         self.flat = torch.zeros(self.numel, dtype=torch.bfloat16, device=dev)
@@ -80,9 +88,14 @@ class Gemma3TrainState:
             for k in LAYER_KEYS:
                 self.view(f"{i}.{k}").copy_(lay[k])
         llm.embed = self.view("embed")
+        self.norm32 = torch.zeros(self.norm_hi - self.norm_lo, dtype=torch.float32, device=dev)
+        n32 = lambda name: self.norm32[self.offsets[name][0] - self.norm_lo:][:math.prod(self.offsets[name][1])]
+        llm.final_norm = n32("final_norm")
         for i, lay in enumerate(llm.layers):
             for k in ("wqkv", "wo", "wgu", "wd"):
                 lay[k] = self.view(f"{i}.{k}")
+            for k in NORM_KEYS:
+                lay[k] = n32(f"{i}.{k}").view(self.offsets[f"{i}.{k}"][1])
         self.refresh()
         llm._build_c()
         self._build_grads_c()
@@ -105,10 +118,8 @@ class Gemma3TrainState:
     def refresh(self):
         """Derived copies the kernels read: transposed matrices (dX GEMMs) and fp32 norm weights."""
         llm = self.llm
-        llm.final_norm.copy_(self.view("final_norm"))
-        for i, lay in enumerate(llm.layers):
-            for k in NORM_KEYS:
-                lay[k].copy_(self.view(f"{i}.{k}"))
+        self.norm32.copy_(self.flat[self.norm_lo:self.norm_hi])
+        for lay in llm.layers:
             for k in ("wqkv", "wo", "wgu", "wd"):
                 K.transpose(lay[k], out=lay[k + "_t"])
         K.transpose(llm.embed, out=llm.embed_t)
