@@ -19,6 +19,8 @@
 // which makes every 16-lane ds_read_b128 group conflict-free.
 // Block ids are remapped so each XCD walks a contiguous range of tiles in
 // GROUP_M-row groups (L2 reuse of A row-panels and B column-panels).
+#include <stdlib.h>
+
 #include "common.h"
 #include "ptk_internal.h"
 #include "gemm_epi.h"
@@ -806,12 +808,44 @@ int timer_read(int cls, double* total_ms, int* count) {
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm launch failed");             \
   }
 
+// Plain GEMMs (no epilogue beyond the output cast) go to hipBLASLt (blaslt.cpp) where it measured ahead
+// of the MFMA kernels (tools/blaslt_probe.py, r02, same box): the q|k|v projection (+24 %), the down
+// projection (+14 %), dO (+19 %), the vocab-wide lm_head (+18 %) and every shape whose 256x256 grid
+// quantises badly (cfg4 M = 14336: down +74 %, d(gate|up) dX +53 %); not the K <= 1024 o projection
+// (-8 %), the d(gate|up) dX at 440 tiles and K = 13824 (-19 %: the staggered 256x256 kernel's K loop) or
+// K = 1536 (tie).  A fixed rule, so the choice (and the rounding) is the same in every process and rank.
+// PTK_BLASLT=0: every GEMM on the MFMA kernels; =1: every plain GEMM on hipBLASLt (A/B switches).
+static int blaslt_mode() {
+  static const int v = [] { const char* e = getenv("PTK_BLASLT"); return e ? (e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2) : 2; }();
+  return v;
+}
+bool blaslt_preferred(const GemmArgs& a, int act, int out) {
+  const int mode = blaslt_mode();
+  if (mode == 0 || !blaslt_supported(a, act, out)) return false;
+  if (mode == 1) return true;
+  if (a.M < 1024 || a.N < 512) return false;
+  if (a.N >= 16384) return true;
+  if (a.K <= 1024) return false;
+  if (a.K >= 12288 && w4_round_fill(a.M, a.N) >= 0.8) return false;
+  if (a.K == 1536 && a.N == 1152) return false;
+  return true;
+}
+
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
   if (a.K <= 0 || a.K % BK) return set_error("gemm: K=%d must be a positive multiple of 64", a.K);
   if ((a.lda % 8) || (a.ldb % 8)) return set_error("gemm: lda/ldb must be multiples of 8 (16-B rows)");
   if (((uintptr_t)a.A | (uintptr_t)a.B) & 15) return set_error("gemm: A/B must be 16-B aligned");
   if (a.zin <= 0) return set_error("gemm: zin must be >= 1");
+  if (batch == 1 && g_force_tiles == 0 && blaslt_preferred(a, act, out)) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
+    if (e0) (void)hipEventRecord(e0, st);
+    const int r = launch_gemm_blaslt(a, out, st);
+    if (e1) (void)hipEventRecord(e1, st);
+    if (r < 0) return -1;
+    if (r == 1) return 0;
+  }
   const long ntile = (long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (ntile > 0x7fffffffL) return set_error("gemm: too many tiles");
   // 256x256 (one block per CU) only where the K loop amortises its lock-step epilogue: long K or

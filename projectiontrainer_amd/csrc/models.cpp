@@ -223,6 +223,21 @@ int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStr
   while (S > 1 && ((long)S * a.M * a.N > part_floats || a.K / S < 1024 || a.N % 4 || a.ldc % 4)) S /= 2;
   const bool plain = !a.rowadd && !a.resid && !a.aux && !a.aux_in && a.amap.g == 0 && a.amap.off == 0 &&
                      a.cmap.g == 0 && a.cmap.off == 0 && a.bias == nullptr && a.alpha == 1.f;
+  // few-tile weight grads (dW_qkv, dW_o: <= 64 tiles) split 4 ways on the MFMA kernels beat hipBLASLt
+  // (818 / 560 vs 638 / 519 TFLOP/s, tools/blaslt_probe.py r02); the larger ones go to hipBLASLt
+  if (S < 4 && plain && part && a.bf16_linear && a.resid16 && (long)a.M * a.N <= part_floats && a.N % 4 == 0) {
+    // the weight-grad accumulate: a plain fp32 GEMM (hipBLASLt where the shape rule prefers it) into the
+    // partial buffer, then bf16(grad + bf16(sum)) as autograd accumulates
+    GemmArgs b = a;
+    b.C = part; b.ldc = a.N;
+    b.bf16_linear = 0; b.resid16 = nullptr; b.ld_resid16 = 0;
+    if (blaslt_preferred(b, ACT_NONE, OUT_F32)) {
+      CK(launch_gemm(b, ACT_NONE, OUT_F32, 1, st));
+      return launch_splitk_reduce(part, 1, a.M, a.N, a.C, a.ldc, 1, a.resid16, a.ld_resid16, st);
+    }
+  } else if (plain && blaslt_preferred(a, ACT_NONE, out)) {
+    return launch_gemm(a, ACT_NONE, out, 1, st);
+  }
   if (S == 1 || !plain || !part) return launch_gemm(a, ACT_NONE, out, 1, st);
   const int kc = (a.K / S + 63) / 64 * 64;
   const int nfull = a.K / kc, rem = a.K - nfull * kc;

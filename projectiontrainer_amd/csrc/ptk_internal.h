@@ -52,6 +52,10 @@ constexpr int SK_MAX_BLOCKS = 512;
 constexpr long SK_SLAB_FLOATS = 256L * 256;
 
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
+// plain GEMMs on hipBLASLt (blaslt.cpp): 1 launched, 0 not available for the shape, < 0 error
+bool blaslt_supported(const GemmArgs& a, int act, int out);
+bool blaslt_preferred(const GemmArgs& a, int act, int out);   // the shape rule of gemm.hip
+int launch_gemm_blaslt(const GemmArgs& a, int out, hipStream_t st);
 // persistent 256x256 4-wave GEMM (gemm_w4.hip): batch 1 only; w4_supported says whether a shape qualifies
 bool w4_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid);

@@ -121,21 +121,44 @@ __global__ void __launch_bounds__(256) rms_wgrad_partial_kernel(const TX* __rest
 }
 
 // grad[c] = bf16(grad[c] + bf16(sum_b partial[b][c]))   (autograd accumulation into a bf16 .grad).
-// Block: 64 columns x 4 row groups (coalesced 256-B partial rows), fixed summation order.
-__global__ void __launch_bounds__(256) wgrad_finish_kernel(const float* __restrict__ partial, int nblk, int cols,
-                                                           bf16_t* __restrict__ grad) {
+// Two stages, fixed order: colsum16 folds groups of 16 partial rows (64 columns x 4 row-groups per block,
+// coalesced), repeated until at most 16 rows remain; wgrad_finish sums those and accumulates.
+__global__ void __launch_bounds__(256) colsum16_kernel(const float* __restrict__ in, int rows, int cols,
+                                                       float* __restrict__ out) {
   __shared__ float red[4][64];
   const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
-  const int c = blockIdx.x * 64 + cl;
+  const int c = blockIdx.x * 64 + cl, r0 = blockIdx.y * 16;
   float s = 0.f;
   if (c < cols)
-    for (int b = grp; b < nblk; b += 4) s += partial[(long)b * cols + c];
+    for (int r = r0 + grp; r < min(rows, r0 + 16); r += 4) s += in[(long)r * cols + c];
   red[grp][cl] = s;
   __syncthreads();
-  if (grp == 0 && c < cols) {
-    const float t = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
-    grad[c] = f2bf(bf2f(grad[c]) + bfround(t));
+  if (grp == 0 && c < cols) out[(long)blockIdx.y * cols + c] = (red[0][cl] + red[1][cl]) + (red[2][cl] + red[3][cl]);
+}
+
+__global__ void __launch_bounds__(256) wgrad_finish_kernel(const float* __restrict__ partial, int nblk, int cols,
+                                                           bf16_t* __restrict__ grad) {
+  const int c = blockIdx.x * 256 + threadIdx.x;
+  if (c >= cols) return;
+  float s = 0.f;
+  for (int b = 0; b < nblk; ++b) s += partial[(long)b * cols + c];
+  grad[c] = f2bf(bf2f(grad[c]) + bfround(s));
+}
+
+// partial [nblk][cols] -> grad; `scratch` holds ceil(nblk/16) * cols floats (the folded rows ping-pong in
+// partial's own head and scratch)
+static void wgrad_finish(float* partial, int nblk, int cols, bf16_t* grad, float* scratch, hipStream_t st) {
+  float* src = partial;
+  float* dst = scratch;
+  while (nblk > 16) {
+    const int n2 = (nblk + 15) / 16;
+    hipLaunchKernelGGL(colsum16_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)n2), dim3(256), 0, st, src, nblk,
+                       cols, dst);
+    std::swap(src, dst);
+    nblk = n2;
   }
+  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((cols + 255) / 256)), dim3(256), 0, st, src, nblk, cols,
+                     grad);
 }
 
 template <typename TX, typename TD>
@@ -152,12 +175,14 @@ static int rms_wgrad_t(const TX* x, long ldx, RowMap xmap, const float* rstd, co
     case 3: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 3>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
     default: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 4>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
   }
-  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((cols + 63) / 64)), dim3(256), 0, st, partial, nblk, cols,
-                     grad);
+  wgrad_finish(partial, nblk, cols, grad, partial + (long)nblk * cols, st);
   RET_OK("rms_wgrad");
 }
 
-int rms_wgrad_partial_floats(int rows, int cols) { return ((rows + WG_ROWS - 1) / WG_ROWS) * cols; }
+int rms_wgrad_partial_floats(int rows, int cols) {
+  const int nblk = (rows + WG_ROWS - 1) / WG_ROWS;
+  return (nblk + (nblk + 15) / 16) * cols;   // partials + the first fold
+}
 
 int launch_rms_wgrad(const float* x, long ldx, RowMap xmap, const float* rstd, const float* dy, long lddy,
                      int dy_round, int rows, int cols, bf16_t* grad, float* partial, hipStream_t st) {
@@ -288,12 +313,16 @@ int launch_qknorm_wgrad(const bf16_t* qkv, const float* cos_t, const float* sin_
   else
     hipLaunchKernelGGL(qknorm_wgrad_partial_any_kernel, dim3((unsigned)nblk), dim3(256), 0, st, qkv, cos_t, sin_t,
                        rstd_q, rstd_k, dQ, dK, s, pq, pk);
-  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((s.D + 63) / 64)), dim3(256), 0, st, pq, nblk, s.D, gq);
-  hipLaunchKernelGGL(wgrad_finish_kernel, dim3((unsigned)((s.D + 63) / 64)), dim3(256), 0, st, pk, nblk, s.D, gk);
+  float* scratch = pk + (long)nblk * s.D;
+  wgrad_finish(pq, nblk, s.D, gq, scratch, st);
+  wgrad_finish(pk, nblk, s.D, gk, scratch, st);
   RET_OK("qknorm_wgrad");
 }
 
-int qknorm_wgrad_partial_floats(long M, int D) { return (int)(2 * ((M + QK_ROWS - 1) / QK_ROWS) * D); }
+int qknorm_wgrad_partial_floats(long M, int D) {
+  const long nblk = (M + QK_ROWS - 1) / QK_ROWS;
+  return (int)((2 * nblk + (nblk + 15) / 16) * D);
+}
 
 // ---------------------------------------------------------------- split-K reduce
 // C = sum_s part[s] (fp32 out) or C = bf16(resid + bf16(sum_s part[s])) (bf16 out, resid may alias C or be
