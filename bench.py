@@ -42,8 +42,10 @@ def _args(argv=None):
                     help="time only the CPU baseline (no GPU) and print it")
     ap.add_argument("--prefetch", action="store_true",
                     help="overlap the next step's SigLIP forward with this step's Gemma3 on a side stream")
-    ap.add_argument("--gas", type=int, default=1,
-                    help="Stage 2 (cfg4): micro-batches per optimizer step (one bench step = gas micro-batches)")
+    ap.add_argument("--gas", type=int, default=8,
+                    help="Stage 2 (cfg4): micro-batches per optimizer step (one bench step = gas micro-batches); "
+                         "default 8 = GRAD_ACCUM_STEPS of Stage2/run_vqa_train_stage2.sh and the CLI default "
+                         "(train_vqa_stage2.py:106)")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher plumbing only: every rank joins a gloo group, rank 0 prints the world; no GPU")
     return ap.parse_args(argv)

@@ -205,6 +205,7 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
   }
   // split-K partials (gemm_split): 2 slices of the largest [M, H] / [2I, H] output, 4 of the small dW ones
   w.sk_floats = std::max(std::max(2 * M * H, 2 * 2 * I * H), 4 * std::max(Dqkv, H) * H);
+  if (train) w.sk_floats = std::max(w.sk_floats, V * H);   // the tied embedding's fp32 dW before its accumulate
   w.skpart = bp.take<float>(w.sk_floats);
   return w;
 }
@@ -257,12 +258,28 @@ int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStr
                               bf ? a.resid16 : nullptr, a.ld_resid16, st);
 }
 
+// PTK_BLASLT_TN=0: the transpose + MFMA path for every weight grad (A/B)
+static bool blaslt_tn_enabled() {
+  static const int v = [] { const char* e = getenv("PTK_BLASLT_TN"); return e && e[0] == '0' ? 0 : 1; }();
+  return v != 0;
+}
+
 // dW (+)= dY^T X over K token rows: both operands are token-major, so each is first transposed to a
 // K-contiguous feature-major copy (rows gathered through a map, zero-padded to a multiple of 64), then one
 // MFMA GEMM accumulates into the bf16 .grad (bf16(grad + bf16(acc)), autograd's accumulation).
 int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* x, long ldx, RowMap xmap, int Nx,
                 int rows, bf16_t* TA, bf16_t* TB, void* grad, float* skpart, long sk_floats, hipStream_t st) {
   if (!grad) return 0;
+  // token-major operands straight into hipBLASLt's dY^T X (no transposes) for every contiguous-row weight
+  // grad that is not a few-tile one (those split-K on the MFMA kernels, see gemm_split); fp32 result,
+  // then the exact bf16 accumulate
+  const long nbig = (long)((Ny + 255) / 256) * ((Nx + 255) / 256);
+  const bool ident_rows = ymap.g == 0 && ymap.off == 0 && xmap.g == 0 && xmap.off == 0;
+  if (ident_rows && nbig > 64 && (long)Ny * Nx <= sk_floats && Nx % 4 == 0 && blaslt_tn_enabled()) {
+    const int r = launch_gemm_blaslt_tn((const bf16_t*)dy, lddy, Ny, (const bf16_t*)x, ldx, Nx, rows, skpart, Nx, st);
+    if (r < 0) return -1;
+    if (r == 1) return launch_splitk_reduce(skpart, 1, Ny, Nx, grad, Nx, 1, (const bf16_t*)grad, Nx, st);
+  }
   const int Kp = (rows + 63) / 64 * 64;
   CK(launch_transpose_rows(dy, lddy, ymap, rows, Ny, TA, Kp, Kp, st));
   CK(launch_transpose_rows(x, ldx, xmap, rows, Nx, TB, Kp, Kp, st));

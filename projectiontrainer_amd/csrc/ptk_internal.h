@@ -56,6 +56,9 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
 bool blaslt_supported(const GemmArgs& a, int act, int out);
 bool blaslt_preferred(const GemmArgs& a, int act, int out);   // the shape rule of gemm.hip
 int launch_gemm_blaslt(const GemmArgs& a, int out, hipStream_t st);
+// C[Ny, Nx] (fp32, ldc) = dY^T . X over K rows of the token-major dY [K, Ny] (lddy) and X [K, Nx] (ldx)
+int launch_gemm_blaslt_tn(const bf16_t* dy, long lddy, int Ny, const bf16_t* x, long ldx, int Nx, int K, float* C,
+                          long ldc, hipStream_t st);
 // persistent 256x256 4-wave GEMM (gemm_w4.hip): batch 1 only; w4_supported says whether a shape qualifies
 bool w4_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid);
