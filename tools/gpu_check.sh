@@ -31,7 +31,9 @@ for step in "$@"; do
     pmcdkv) run pmcdkv 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_INSTS_VALU --kernel-include-regex "dkv256" --output-format csv -d gpurun_out/pmc_dkv -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     stage2)  run stage2 600 python -m pytest tests/test_stage2_gpu.py -q -x -rs ;;
     prof2)   run prof2 900 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof2 -o run -- python3 bench.py --config cfg4 --steps 3 --warmup 1 ;;
-    sqpmc)   run sqpmc 600 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES --output-format csv -d gpurun_out/sqpmc -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    bench4)  run bench4 600 python bench.py --config cfg4 --steps 4 --warmup 1 --no-cpu-baseline ;;
+    sqpmc4)  run sqpmc4 600 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sqpmc4 -o run -- python3 bench.py --config cfg4 --gas 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
+    sqpmc)   run sqpmc 600 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sqpmc -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
   esac
 done
