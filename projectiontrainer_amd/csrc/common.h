@@ -103,13 +103,11 @@ PTK_DEV float gelu_tanh(float x) { return x * fast_sigmoid2(gelu_tanh_arg(x, x *
 // two lanes of gelu_tanh with packed f32 math (v_pk_mul / v_pk_fma: half the VALU issue of the scalar
 // form; for epilogues, where no MFMA of the wave runs beside them)
 typedef __attribute__((ext_vector_type(2))) float f32x2_t;
-PTK_DEV f32x2_t gelu_tanh2(f32x2_t x) {
-  const f32x2_t u = 0.7978845608028654f * (x + 0.044715f * (x * x) * x);
-  const f32x2_t a = u * -2.8853900817779268f;
-  f32x2_t s;
-  s.x = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(a.x));
-  s.y = __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(a.y));
-  return x * s;
+PTK_DEV f32x2_t gelu_tanh2(f32x2_t x) {   // e^(-2u) = exp2(x (c1 + c2 x^2)), factored as in gelu_tanh_fg2
+  constexpr float k0 = 0.7978845608028654f, k1 = 0.044715f, l2e2 = -2.8853900817779268f;
+  const f32x2_t a = x * ((x * x) * (k0 * k1 * l2e2) + k0 * l2e2);
+  const f32x2_t e = f32x2_t{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + 1.f;
+  return x * f32x2_t{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
 }
 // gelu_tanh and its derivative from one exp / rcp pair (the GEGLU backward needs both)
 PTK_DEV void gelu_tanh_fg(float x, float& f, float& df) {
@@ -119,6 +117,29 @@ PTK_DEV void gelu_tanh_fg(float x, float& f, float& df) {
   f = x * s;
   df = s + 2.f * x * s * (1.f - s) * k0 * (1.f + 3.f * k1 * x2);
 }
+// gelu_tanh_fg on two lanes with packed f32 math (v_pk_mul / v_pk_fma for everything but the exp / rcp),
+// the polynomial factored for the fewest packed operations:
+//   e^(-2u) = exp2(x (c1 + c2 x^2)),  f = x s,  f' = s + f (1 - s) (2 k0 + 6 k0 k1 x^2)
+// (the same function as gelu_tanh_fg up to fp32 rounding; epilogues only: beside MFMAs packed f32 is an
+// anti-lever, MI355X_MICROARCH.md)
+PTK_DEV void gelu_tanh_fg2(f32x2_t x, f32x2_t& f, f32x2_t& df) {
+  constexpr float k0 = 0.7978845608028654f, k1 = 0.044715f, l2e2 = -2.8853900817779268f;
+  const f32x2_t x2 = x * x;
+  const f32x2_t a = x * (x2 * (k0 * k1 * l2e2) + k0 * l2e2);
+  const f32x2_t e = f32x2_t{__builtin_amdgcn_exp2f(a.x), __builtin_amdgcn_exp2f(a.y)} + 1.f;
+  const f32x2_t s = f32x2_t{__builtin_amdgcn_rcpf(e.x), __builtin_amdgcn_rcpf(e.y)};
+  f = x * s;
+  const f32x2_t q = f - f * s;                              // f (1 - s)
+  df = q * (x2 * (6.f * k0 * k1) + 2.f * k0) + s;
+}
+// bf16 round trip of two lanes: one v_cvt_pk_bf16_f32 and two unpacks
+typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+PTK_DEV f32x2_t bfround2(f32x2_t v) {
+  const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
+  return f32x2_t{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+// two bf16 packed in a dword (element 0 in the low half) -> two f32
+PTK_DEV f32x2_t bf2x2(uint32_t w) { return f32x2_t{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)}; }
 PTK_DEV float gelu_tanh_grad(float x) {
   float f, df;
   gelu_tanh_fg(x, f, df);

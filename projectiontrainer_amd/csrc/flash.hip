@@ -32,8 +32,14 @@ typedef __attribute__((ext_vector_type(4))) short s16x4_t;
 typedef const __attribute__((address_space(1))) void* fa_gptr_t;
 typedef __attribute__((address_space(3))) void* fa_lptr_t;
 
+// LDS-DMA of 16 B per lane (lds: wave-uniform base; lane i lands at lds + 16 i).  Inline asm on purpose:
+// for the builtin, hipcc's wait-count pass assumes any later LDS read may alias an in-flight DMA and
+// inserts s_waitcnt vmcnt(0) before the first one of every tile, draining the whole K/V ring (tiles t+1..t+3)
+// each iteration.  The kernels publish landed tiles themselves (counted vm_wait + barrier), so the DMA is
+// kept out of the compiler's view.
 PTK_DEV void fa_glds16(const void* src, void* lds) {
-  __builtin_amdgcn_global_load_lds((fa_gptr_t)src, (fa_lptr_t)lds, 16, 0, 0);
+  const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(fa_lptr_t)lds);
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
 }
 
 // 16-B chunk swizzles (chunk index within a row of D/8 chunks)
@@ -63,6 +69,12 @@ PTK_DEV void vm_wait(int n) {
     default: asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); break;
   }
 }
+
+// wait for a register loaded from global memory before the K/V loop (an empty asm that reads and writes it):
+// otherwise hipcc's wait-count pass places the wait at the first use INSIDE the loop, every iteration,
+// where its s_waitcnt vmcnt also drains the LDS-DMA ring
+template <typename T>
+PTK_DEV void fa_pin(T& x) { asm volatile("" : "+v"(x)); }
 
 // K/V tiles of 32 keys in a 4-deep LDS ring (tile t+3 staged while tile t computes); every wave
 // issues the same number of LDS-DMA ops per tile (its share of K, V and, when present, 4 of the
@@ -134,6 +146,10 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
 #pragma unroll
     for (int ks = 0; ks < KS; ++ks) qf[qg][ks] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * ks);
   }
+#pragma unroll
+  for (int qg = 0; qg < QG; ++qg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) fa_pin(qf[qg][ks]);
   const int causal = a.causal != 0, nowin = a.window <= 0;
   const bool unmasked = !kvl && !causal && nowin;
   // query positions of this wave's rows (interior-tile test)
@@ -188,7 +204,9 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
   for (int t = t_lo; t < t_hi; ++t) {
     const int buf = (t - t_lo) & (FA_NBUF - 1);
     vm_wait(ops * min(FA_NBUF - 2, t_hi - 1 - t));
-    __syncthreads();
+    // raw barrier (the counted wait above publishes tile t; every LDS read of the buffer restaged below
+    // was consumed by an MFMA or a compare in the previous iteration)
+    __builtin_amdgcn_s_barrier();
     if (t + FA_NBUF - 1 < t_hi) stage(t + FA_NBUF - 1, (buf + FA_NBUF - 1) & (FA_NBUF - 1));
     if (idle) continue;
     const char* kb = smem + buf * 2 * R::TILE;
@@ -392,8 +410,15 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
     df[ks] = *reinterpret_cast<const bf16x8_t*>(a.dO + qoff + 32 * ks);
   }
   const float L2E = 1.4426950408889634f;
-  const float lse2 = a.lse[z * a.rows + qrow_c] * L2E;
-  const float dlt = a.delta[z * a.rows + qrow_c];
+  float lse2 = a.lse[z * a.rows + qrow_c] * L2E;
+  float dlt = a.delta[z * a.rows + qrow_c];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    fa_pin(qf[ks]);
+    fa_pin(df[ks]);
+  }
+  fa_pin(lse2);
+  fa_pin(dlt);
   const int qpos = qrow_c / a.qdiv;
   const float sl2 = a.scale * L2E;
   const int causal = a.causal != 0, nowin = a.window <= 0;
@@ -438,7 +463,9 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
   for (int t = t_lo; t < t_hi; ++t) {
     const int buf = (t - t_lo) & (FA_NBUF - 1);
     vm_wait(ops * min(FA_NBUF - 2, t_hi - 1 - t));
-    __syncthreads();
+    // raw barrier (the counted wait above publishes tile t; every LDS read of the buffer restaged below
+    // was consumed by an MFMA or a compare in the previous iteration)
+    __builtin_amdgcn_s_barrier();
     if (t + FA_NBUF - 1 < t_hi) stage(t + FA_NBUF - 1, (buf + FA_NBUF - 1) & (FA_NBUF - 1));
     const char* kb = smem + buf * 2 * R::TILE;
     const char* vb = kb + R::TILE;
@@ -721,6 +748,13 @@ __global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel
     }
     kok[kg] = key[kg] < a.nkeys && (!a.key_valid || a.key_valid[b * a.nkeys + kc] != 0);
   }
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      fa_pin(kf[kg][ks]);
+      fa_pin(vf[kg][ks]);
+    }
   const bf16_t* Qz = a.Q + z * (long)a.rows * D;
   const bf16_t* dOz = a.dO + z * (long)a.rows * D;
   const float L2E = 1.4426950408889634f;

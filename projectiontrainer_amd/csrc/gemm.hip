@@ -859,10 +859,12 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // persistent grid's rounds (SigLIP qkv +4 %, Gemma o +6 %, dh +17 %, down +3 %, dqkv +2 %).  Not the
   // N = 1024 / 1536 shapes (352 / 528 tiles: 69 % round fill, the 128x128 kernel wins), the
   // vocab-wide lm_head, the K = 11520 / 13824 projections or the GELU epilogues
+  // (r02: + the GELU-tanh epilogue with packed f32 math, SigLIP fc1 887 -> 936 TFLOP/s, tools/gemm_bench.py --all)
   const bool w4_auto = g_force_tiles == 0 && a.M >= 4096 && a.N <= 16384 &&
                        (act == ACT_GEGLU || act == ACT_GEGLU_BWD ||
-                        (act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32) && a.K <= 8192 &&
-                         w4_round_fill(a.M, a.N) >= 0.8));
+                        ((act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32)) ||
+                         (act == ACT_GELU_TANH && out == OUT_BF16)) &&
+                            a.K <= 8192 && w4_round_fill(a.M, a.N) >= 0.8);
   if (batch == 1 && (g_force_tiles == 8 || w4_auto) && w4_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }

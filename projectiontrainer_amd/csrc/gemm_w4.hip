@@ -107,7 +107,11 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
   if (p.rowadd) add8(v, p.rowadd + w.ro_rowadd + c);
   if constexpr (ACT == ACT_GELU_TANH) {
 #pragma unroll
-    for (int e = 0; e < 8; ++e) v[e] = gelu_tanh(bfround(v[e]));
+    for (int e = 0; e < 8; e += 2) {
+      const f32x2_t y = gelu_tanh2(bfround2(f32x2_t{v[e], v[e + 1]}));
+      v[e] = y.x;
+      v[e + 1] = y.y;
+    }
   } else if constexpr (ACT == ACT_GELU_ERF) {
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]);
@@ -154,27 +158,24 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, i
       f32x4_t u0 = a[4 * pp + 1] * p.alpha, u1 = a[4 * pp + 3] * p.alpha;
       swap16(g0, g1);
       swap16(u0, u1);
-      float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
-      float u[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-      float h[8];
+      const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+      const float u[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+      // g, u rounded to bf16 once: the packed dwords are stored as they are and unpacked for the math
+      uint32_t gp[4], up[4], hp[4];
 #pragma unroll
       for (int e = 0; e < 8; e += 2) {
-        g[e] = bfround(g[e]);
-        g[e + 1] = bfround(g[e + 1]);
-        u[e] = bfround(u[e]);
-        u[e + 1] = bfround(u[e + 1]);
-        const f32x2_t gl = gelu_tanh2(f32x2_t{g[e], g[e + 1]});
-        const f32x2_t hh = f32x2_t{bfround(gl.x), bfround(gl.y)} * f32x2_t{u[e], u[e + 1]};
-        h[e] = hh.x;
-        h[e + 1] = hh.y;
+        gp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{g[e], g[e + 1]}, bf16x2_t));
+        up[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{u[e], u[e + 1]}, bf16x2_t));
+        const f32x2_t hh = bfround2(gelu_tanh2(bf2x2(gp[e / 2]))) * bf2x2(up[e / 2]);
+        hp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(hh, bf16x2_t));
       }
       const long hc = col0 / 2 + 32 * pp + cb;
       const bool cin = 2 * hc < p.N;
       const bool rv = w.rv && cin, sv = w.cv && cin;
       bf16_t* sk = reinterpret_cast<bf16_t*>(sink);
-      if (p.aux) stbf8(rv ? p.aux + w.ro_aux + hc : sk, g);
-      if (p.aux2) stbf8(rv ? p.aux2 + w.ro_aux + hc : sk, u);
-      stbf8(sv ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + hc : sk, h);
+      if (p.aux) *reinterpret_cast<uint4*>(rv ? p.aux + w.ro_aux + hc : sk) = uint4{gp[0], gp[1], gp[2], gp[3]};
+      if (p.aux2) *reinterpret_cast<uint4*>(rv ? p.aux2 + w.ro_aux + hc : sk) = uint4{up[0], up[1], up[2], up[3]};
+      *reinterpret_cast<uint4*>(sv ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + hc : sk) = uint4{hp[0], hp[1], hp[2], hp[3]};
     }
   } else {
     const W4Row w = w4_row(p, r);
@@ -219,14 +220,19 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long co
     f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
     swap16(x, y);
     const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+    const uint4 gw = __builtin_bit_cast(uint4, G[pp]), uw = __builtin_bit_cast(uint4, U[pp]);
+    const uint32_t gv[4] = {gw.x, gw.y, gw.z, gw.w}, uv[4] = {uw.x, uw.y, uw.z, uw.w};
     float dg[8], du[8];
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float d = bfround(v[e]), g = bf2f(G[pp][e]), u = bf2f(U[pp][e]);
-      float f, df;
-      gelu_tanh_fg(g, f, df);
-      dg[e] = bfround(d * u) * df;
-      du[e] = d * bfround(f);
+    for (int e = 0; e < 8; e += 2) {   // packed pairs: the same per-element math as gelu_tanh_fg
+      const f32x2_t d = bfround2(f32x2_t{v[e], v[e + 1]}), g = bf2x2(gv[e / 2]), u = bf2x2(uv[e / 2]);
+      f32x2_t f, df;
+      gelu_tanh_fg2(g, f, df);
+      const f32x2_t a = bfround2(d * u) * df, b = d * bfround2(f);
+      dg[e] = a.x;
+      dg[e + 1] = a.y;
+      du[e] = b.x;
+      du[e + 1] = b.y;
     }
     const long c = col0 + 32 * pp + cb;
     bf16_t* o = w.cv && c < p.N ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + (c >> 4) * 32 + (c & 15)
@@ -305,7 +311,8 @@ PTK_DEV u32x4_t w4_rsrc(const void* base, uint32_t bytes) {
 PTK_DEV uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_ptr_t)p; }
 
 template <int ACT, int OUT>
-__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
+__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes,
+                                                          uint32_t stagger) {
   __shared__ __attribute__((aligned(16))) char smem[W4_NSLOT * W4_SLOT];   // 160 KiB: the k-step ring
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -319,6 +326,10 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
     loc = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
   }
   if (loc >= ntile) return;
+  // stagger > 0: every other CU of an XCD starts ~stagger/1024 x 1k cycles late, so half the CUs run
+  // their epilogue (stores) while the other half runs MFMAs
+  if (stagger && ((blockIdx.x >> 3) & 1))
+    for (uint32_t i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(16);
   const int nt = p.K / W4_KT;                              // 64-deep K-tiles per output tile
   const int nks = 2 * nt;                                  // 32-deep k-steps per output tile
   const int total_ks = ((ntile - loc + G - 1) / G) * nks;
@@ -556,6 +567,10 @@ double w4_round_fill(long M, long N) {
 
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid) {
   num_cu();
+  static const uint32_t stagger = [] {   // diagnostic: PTK_W4_STAGGER=<units of ~1k cycles> (default 0)
+    const char* e = getenv("PTK_W4_STAGGER");
+    return e ? (uint32_t)atoi(e) : 0u;
+  }();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   long grid = std::min<long>(ntile, max_grid > 0 ? max_grid : g_num_cu);
   const long arows = a.M + a.amap.off;
@@ -563,7 +578,7 @@ int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
 #define PTK_W4_CASE(ACT_, OUT_)                                                                   \
   if (act == ACT_ && out == OUT_) {                                                               \
-    hipLaunchKernelGGL((gemm_w4_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb); \
+    hipLaunchKernelGGL((gemm_w4_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb, stagger); \
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_w4 launch failed");              \
   }
   PTK_W4_CASE(ACT_NONE, OUT_BF16)

@@ -34,6 +34,8 @@ for step in "$@"; do
     bench4)  run bench4 600 python bench.py --config cfg4 --steps 4 --warmup 1 --no-cpu-baseline ;;
     sqpmc4)  run sqpmc4 600 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sqpmc4 -o run -- python3 bench.py --config cfg4 --gas 1 --steps 2 --warmup 1 --no-cpu-baseline ;;
     sqpmc)   run sqpmc 600 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d gpurun_out/sqpmc -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcattn1) run pmcattn1 600 rocprofv3 --kernel-trace --pmc SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_WAIT_INST_LDS SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_VALU_MFMA_BUSY_CYCLES --kernel-include-regex "attn_" --output-format csv -d gpurun_out/pmc_attn1 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
+    pmcattn2) run pmcattn2 600 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_VALU SQ_INSTS_LDS SQ_WAVES GRBM_GUI_ACTIVE --kernel-include-regex "attn_" --output-format csv -d gpurun_out/pmc_attn2 -o run -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline ;;
     *) echo "unknown step $step" ;;
   esac
 done
