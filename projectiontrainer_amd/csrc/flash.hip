@@ -20,8 +20,10 @@
 // for the backward.  Semantics: softmax(scale * Q K^T + mask) V, as
 // TF/models/siglip/modeling_siglip.py:289-300 and gemma3 :365-379 (sdpa).
 #include <algorithm>
+#include <cstdlib>
 #include <functional>
 #include <queue>
+#include <type_traits>
 #include <vector>
 #include "common.h"
 #include "ptk_internal.h"
@@ -330,6 +332,306 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
     if (a.lse && g == 0)
       a.lse[(long)z * a.rows + qrow[qg]] = (m_run[qg] * sl2 + log2f(l_run[qg])) * 0.6931471805599453f;
   }
+}
+
+// ---------------------------------------------------------------- forward, head_dim 256
+// The 8-wave, 16-rows-per-wave structure of attn_fwd_kernel, re-cut for instruction count (the loop was
+// issue-bound: ~190 non-MFMA VALU + ~115 SALU per 32 MFMAs):
+//   * K/V tiles by buffer_load ... lds: one descriptor per tensor, a per-lane 32-bit offset fixed for the
+//     whole kernel and the tile's byte offset in an SGPR, so a DMA piece costs no VALU;
+//   * separate K and V rings (4 x 16 KiB each) and the tile loop unrolled by the ring depth, so every LDS
+//     read address is a lane offset + an immediate (no per-tile address arithmetic);
+//   * the key-valid flags compressed once per block into one 32-bit mask per key tile (LDS), read as a
+//     scalar per tile: the interior test is a compare, the mask one bit test per score;
+//   * online softmax with a deferred running max: it moves only when a tile's max exceeds it by more than
+//     FA_DEFER (log2 units; P <= 2^FA_DEFER is exact enough in fp32 sums and bf16 operands), so the O
+//     rescale runs a few times per row block instead of on most tiles.
+constexpr float FA_DEFER = 8.f;
+constexpr int FA_MAXT = 128;   // key tiles (of 32) the mask table holds: nkeys <= 4096
+
+#define FA_DMA(VOFF, SOFF, RSRC, LDS)                                                                      \
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen lds"                   \
+               :: "v"(VOFF), "s"(LDS), "s"(RSRC), "s"(SOFF) : "memory")
+typedef __attribute__((ext_vector_type(4))) unsigned int fa_u32x4_t;
+PTK_DEV fa_u32x4_t fa_rsrc(const void* base, uint32_t bytes) {
+  const uint64_t p = (uint64_t)base;
+  fa_u32x4_t r;
+  r[0] = __builtin_amdgcn_readfirstlane((uint32_t)p);
+  r[1] = __builtin_amdgcn_readfirstlane((uint32_t)(p >> 32));   // stride 0: raw buffer
+  r[2] = __builtin_amdgcn_readfirstlane(bytes);                  // num_records: reads past it return 0
+  r[3] = 0x00020000u;
+  return r;
+}
+PTK_DEV uint32_t fa_lds_addr(const void* p) { return (uint32_t)(uintptr_t)(fa_lptr_t)p; }
+template <int N> using fa_ic = std::integral_constant<int, N>;
+
+__global__ void __launch_bounds__(512, 1) attn_fwd256_kernel(FlashArgs a) {
+  constexpr int D = 256, KT = 32, KS = 8, DS = 16, NB = 4;
+  constexpr int TILE = KT * D * 2;   // one K or V tile, 16 KiB
+  __shared__ __attribute__((aligned(16))) char smem[2 * NB * TILE + FA_MAXT * 4];   // K ring, V ring, key masks
+  char* const kring = smem;
+  char* const vring = smem + NB * TILE;
+  uint32_t* const kmask_s = reinterpret_cast<uint32_t*>(smem + 2 * NB * TILE);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
+  const int z = blockIdx.x % nz, z0 = z / a.zin, z1 = z - z0 * a.zin;
+  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;   // heaviest (latest) row blocks first
+  const bf16_t* Q = a.Q + z0 * a.sQ0 + z1 * a.sQ1;
+  const bf16_t* K = a.K + z0 * a.sK0 + z1 * a.sK1;
+  const bf16_t* V = a.V + z0 * a.sK0 + z1 * a.sK1;
+  const long b = z / a.zdiv;
+  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
+
+  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
+  int k_hi = a.nkeys, k_lo = 0;
+  if (a.causal) {
+    k_hi = min(k_hi, pos_hi + 1);
+    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
+  }
+  const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
+
+  // ---- per-tile key masks (valid and < nkeys), written before any DMA is in flight
+  for (int tt = wave; tt < t_hi; tt += 8) {
+    const int key = tt * KT + (lane & 31);
+    const bool ok = key < a.nkeys && (!kvl || kvl[min(key, a.nkeys - 1)] != 0);
+    const uint64_t m = __ballot(ok);
+    if (lane == 0) kmask_s[tt] = (uint32_t)m;
+  }
+
+  // ---- Q fragments: B operand of S^T = K Q^T, lane holds Q[row c16][8g + 32ks .. +7]
+  const int wrow0 = r0 + wave * 16;
+  const int qrow = wrow0 + c16;
+  const int qrow_c = min(qrow, a.rows - 1);
+  const int qpos = qrow_c / a.qdiv;
+  bf16x8_t qf[KS];
+  {
+    const bf16_t* qp = Q + map_row(a.qmap, qrow_c) * a.ldq + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * ks);
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) fa_pin(qf[ks]);
+  __syncthreads();   // key masks published (no LDS-DMA in flight yet)
+
+  const int causal = a.causal != 0, nowin = a.window <= 0;
+  const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
+  const int wpos_hi = min(wrow0 + 15, a.rows - 1) / a.qdiv;
+
+  // ---- DMA: wave w stages rows 4w..4w+3 of each tile (2 pieces of 2 rows x 512 B per tensor); lane i of
+  // a piece writes LDS row 2j + (i >> 5), chunk i & 31, and fetches logical chunk (i & 31) ^ swz(row)
+  const fa_u32x4_t rsk = fa_rsrc(K, (uint32_t)((long)a.nkeys * a.ldk * 2));
+  const fa_u32x4_t rsv = fa_rsrc(V, (uint32_t)((long)a.nkeys * a.ldk * 2));
+  uint32_t dk[2], dv[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (wave * 2 + j) * 2 + (lane >> 5);
+    dk[j] = (uint32_t)row * (uint32_t)a.ldk * 2u + 16u * ((lane & 31) ^ swz_k<D>(row));
+    dv[j] = (uint32_t)row * (uint32_t)a.ldk * 2u + 16u * ((lane & 31) ^ swz_v<D>(row));
+  }
+  const uint32_t lds_k = __builtin_amdgcn_readfirstlane(fa_lds_addr(kring) + wave * 2048);
+  const uint32_t lds_v = __builtin_amdgcn_readfirstlane(fa_lds_addr(vring) + wave * 2048);
+  const uint32_t tile_bytes = __builtin_amdgcn_readfirstlane((uint32_t)KT * (uint32_t)a.ldk * 2u);
+  auto stage = [&](int bb, int t) __attribute__((always_inline)) {
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)t * tile_bytes);
+    FA_DMA(dk[0], so, rsk, lds_k + bb * TILE);
+    FA_DMA(dk[1], so, rsk, lds_k + bb * TILE + 1024);
+    FA_DMA(dv[0], so, rsv, lds_v + bb * TILE);
+    FA_DMA(dv[1], so, rsv, lds_v + bb * TILE + 1024);
+  };
+
+  // ---- LDS read offsets.  K rows 16ms + c16, chunk (4ks + g) ^ (row & 15): ks bit 2 and ms untouched by
+  // the swizzle (immediates).  V^T rows 16hh + 4g + q4, chunk (2ds + (p4 >> 1)) ^ 2(row & 7): ds bit 3, hh
+  // untouched (immediates).
+  // (lane addresses include the ring base, so the per-read immediates stay below 64 KiB)
+  int koff[4];
+  const char* vaddr[8];
+  {
+    const int q4 = c16 >> 2, p4 = c16 & 3, vrow = 4 * g + q4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) koff[i] = c16 * (D * 2) + ((i * 4 + g) ^ swz_k<D>(c16)) * 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint32_t va = fa_lds_addr(vring) + vrow * (D * 2) + ((2 * i + (p4 >> 1)) ^ swz_v<D>(vrow)) * 16 + 8 * (p4 & 1);
+      vaddr[i] = (const char*)(fa_lptr_t)(uintptr_t)__builtin_amdgcn_readfirstlane(0) + va;
+    }
+  }
+
+  f32x4_t o[DS];
+#pragma unroll
+  for (int i = 0; i < DS; ++i) o[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl2 = a.scale * 1.4426950408889634f;   // scores in log2 units
+  const float defer = FA_DEFER / sl2;                 // the deferral in raw score units
+  const bool idle = wrow0 >= a.rows;                  // rows past the end: stage and keep the barriers only
+
+  // Tile t lives in ring slot (t - t_lo) % NB (compile-time in each unrolled copy); tile t + 2 is staged at
+  // iteration t into the slot of tile t - 2.  Waves 4-7 (the second wave of each SIMD) run one phase behind
+  // waves 0-3: between two barriers a SIMD's early wave runs S(t), softmax(t), P(t)V(t) while its late wave
+  // runs P(t-1)V(t-1), S(t), softmax(t), so one wave's softmax and LDS waits face the other's MFMAs instead
+  // of both waves contending for the same pipe in lockstep.  Same operations on O in the same order: results
+  // are identical for both orders.
+  auto sync = [&](int bb, int t) __attribute__((always_inline)) {
+    // tile t landed (this wave's 4 pieces; tile t+1 may stay in flight), then the barrier publishes every
+    // wave's share; the slot restaged below held tile t-2, whose last reader (a late wave's P.V of tile t-2)
+    // ran before this barrier
+    if (t + 1 < t_hi) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < t_hi) stage((bb + 2) % NB, t + 2);
+  };
+  // S^T = K Q^T for tile t: s[ms] holds keys 16ms + 4g + j, query column c16
+  auto qk = [&](auto BUF, f32x4_t (&s)[2]) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    const char* kb = kring + bb * TILE;
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms) {
+      s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + koff[ks & 3] + (ks >> 2) * 256 + ms * 16 * (D * 2));
+        s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
+      }
+    }
+  };
+  // mask + online softmax (running max deferred) -> P (bf16); rescales O when the max moved.  A tile whose
+  // every key is valid and visible to every row of the wave (below the causal diagonal, inside the window)
+  // skips the mask.
+  auto softmax = [&](int t, f32x4_t (&s)[2], bf16x8_t& pf) __attribute__((always_inline)) {
+    const uint32_t km = kmask_s[t];
+    const bool interior = km == 0xffffffffu && (!causal || t * KT + KT - 1 <= wpos_lo) &&
+                          (nowin || t * KT > wpos_hi - a.window);
+    float mt = -INFINITY;
+    if (interior) {
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mt = fmaxf(mt, s[ms][j]);
+    } else {
+      // the row's visible keys of this tile as a 32-bit mask: valid, kl <= qpos - t KT (causal),
+      // kl > qpos - W - t KT (window)
+      uint32_t vis = km;
+      if (causal) {
+        const int d = qpos - t * KT;
+        vis &= d >= 31 ? 0xffffffffu : (d < 0 ? 0u : (2u << d) - 1u);
+        if (!nowin) {
+          const int e = d - a.window;
+          vis &= e < 0 ? 0xffffffffu : (e >= 31 ? 0u : ~((2u << e) - 1u));
+        }
+      }
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kl = ms * 16 + 4 * g + j;
+          const float v = ((vis >> kl) & 1u) ? s[ms][j] : -INFINITY;
+          s[ms][j] = v;
+          mt = fmaxf(mt, v);
+        }
+    }
+    mt = xor32_max(xor16_max(mt));
+    const bool up = mt > m_run + defer;   // m_run = -inf: any finite tile max moves it
+    const float m_new = up ? mt : m_run;
+    const float alpha = (up && m_run != -INFINITY) ? __builtin_amdgcn_exp2f((m_run - m_new) * sl2) : 1.f;
+    const float mc = (m_new == -INFINITY) ? 0.f : m_new * sl2;
+    float rs = 0.f;
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[ms][j], sl2, -mc));   // exp2(-inf) = 0 for masked keys
+        rs += p;   // fp32 row sum (P itself enters P.V in bf16)
+        pf[ms * 4 + j] = (short)f2bf(p);
+      }
+    rs = xor32_sum(xor16_sum(rs));
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+    if (__any(alpha != 1.f)) {
+#pragma unroll
+      for (int i = 0; i < DS; ++i) o[i] *= alpha;
+    }
+  };
+  // O^T += V^T P^T : k order {4g+0..3, 16+4g+0..3} on both operands
+  auto pv = [&](auto BUF, const bf16x8_t& pf) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      bf16x8_t vf;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const char* addr = vaddr[ds & 7] + bb * TILE + (ds >> 3) * 256 + hh * 16 * (D * 2);
+        const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
+        vf[4 * hh + 0] = r[0]; vf[4 * hh + 1] = r[1]; vf[4 * hh + 2] = r[2]; vf[4 * hh + 3] = r[3];
+      }
+      o[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[ds], 0, 0, 0);
+    }
+  };
+  auto early = [&](auto BUF, int t) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    sync(bb, t);
+    if (idle) return;
+    f32x4_t s[2];
+    bf16x8_t pf;
+    qk(BUF, s);
+    softmax(t, s, pf);
+    pv(BUF, pf);
+  };
+  bf16x8_t pprev;   // late waves: P of the previous tile, applied after the next barrier
+  // (called for t = t_lo .. t_hi: the call at t_hi only applies the last tile's P.V, whose slot nothing
+  // restages after the last barrier)
+  auto late = [&](auto BUF, int t) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    if (t < t_hi) sync(bb, t);
+    if (idle) return;
+    if (t > t_lo) pv(fa_ic<(bb + NB - 1) % NB>{}, pprev);
+    if (t == t_hi) return;
+    f32x4_t s[2];
+    qk(BUF, s);
+    softmax(t, s, pprev);
+  };
+
+  if (t_lo < t_hi) stage(0, t_lo);
+  if (t_lo + 1 < t_hi) stage(1, t_lo + 1);
+  if (wave < 4 || a.variant == 1) {
+    for (int t = t_lo; t < t_hi;) {
+      early(fa_ic<0>{}, t);
+      if (++t >= t_hi) break;
+      early(fa_ic<1>{}, t);
+      if (++t >= t_hi) break;
+      early(fa_ic<2>{}, t);
+      if (++t >= t_hi) break;
+      early(fa_ic<3>{}, t);
+      ++t;
+    }
+  } else {
+    for (int t = t_lo; t <= t_hi;) {
+      late(fa_ic<0>{}, t);
+      if (++t > t_hi) break;
+      late(fa_ic<1>{}, t);
+      if (++t > t_hi) break;
+      late(fa_ic<2>{}, t);
+      if (++t > t_hi) break;
+      late(fa_ic<3>{}, t);
+      ++t;
+    }
+    // the last tile's P.V: its slot is still intact (nothing restages after the last barrier)
+  }
+
+  // ---- epilogue: O[q][d] = O^T[d][q] / l ; lane holds d = 16ds + 4g + j for query c16
+  if (qrow >= a.rows) return;
+  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+  bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow) * a.ldo + 4 * g;
+#pragma unroll
+  for (int ds = 0; ds < DS; ++ds) {
+    u16x4_t u;
+    u[0] = f2bf(o[ds][0] * inv); u[1] = f2bf(o[ds][1] * inv);
+    u[2] = f2bf(o[ds][2] * inv); u[3] = f2bf(o[ds][3] * inv);
+    *reinterpret_cast<u16x4_t*>(op + 16 * ds) = u;
+  }
+  if (a.lse && g == 0)
+    a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_run)) * 0.6931471805599453f;
 }
 
 // ============================================================================ backward
@@ -1148,7 +1450,21 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
     case 64: hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(512), 0, st, a); break;
     // QG = 2 (256-row blocks) measured slower on the Gemma3 step: 352 blocks of double work on 256 CUs
     // quantise worse than 704 (110 vs 78 us per layer), and it spills
-    case 256: hipLaunchKernelGGL((attn_fwd_kernel<256, 1>), grid, dim3(512), 0, st, a); break;
+    case 256: {
+      // PTK_ATTN_FWD8W=1: the 8-wave, 16-rows-per-wave form (A/B)
+      static const bool w8 = getenv("PTK_ATTN_FWD8W") && atoi(getenv("PTK_ATTN_FWD8W")) == 1;
+      if (w8) hipLaunchKernelGGL((attn_fwd_kernel<256, 1>), grid, dim3(512), 0, st, a);
+      else if ((a.nkeys + 31) / 32 > FA_MAXT || (long)a.nkeys * a.ldk * 2 > 0x7fffffffL)
+        hipLaunchKernelGGL((attn_fwd_kernel<256, 1>), grid, dim3(512), 0, st, a);
+      else {
+        // PTK_ATTN_NOSTAGGER=1: every wave in the early order (A/B)
+        static const bool nst = getenv("PTK_ATTN_NOSTAGGER") && atoi(getenv("PTK_ATTN_NOSTAGGER")) == 1;
+        FlashArgs b = a;
+        b.variant = nst ? 1 : 0;
+        hipLaunchKernelGGL(attn_fwd256_kernel, grid, dim3(512), 0, st, b);
+      }
+      break;
+    }
     default: return set_error("attn_fwd: head_dim %d unsupported (64, 256)", a.D);
   }
   return hipGetLastError() == hipSuccess ? 0 : set_error("attn_fwd launch failed");

@@ -139,6 +139,7 @@ struct FlashArgs {
   int qdiv = 1, causal = 0, window = 0;
   const int32_t* key_valid = nullptr;   // [B][nkeys]
   float scale = 1.f;
+  int variant = 0;   // set by launch_attn_fwd (A/B switches)
 };
 int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st);
 // backward; Q, dO, dQ: [nz][rows][D]; K, V, dK, dV: [nz][nkeys][D]; lse, delta: [nz][rows];
