@@ -27,6 +27,9 @@
 #include <vector>
 #include "common.h"
 #include "ptk_internal.h"
+#ifndef PTK_FA_ABL
+#define PTK_FA_ABL 0   // diagnostic ablation builds of attn_fwd256_kernel (make faabl): wrong results by construction
+#endif
 
 namespace ptk {
 
@@ -479,8 +482,12 @@ __global__ void __launch_bounds__(512, 1) attn_fwd256_kernel(FlashArgs a) {
     // ran before this barrier
     if (t + 1 < t_hi) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
     else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#if PTK_FA_ABL != 1
     __builtin_amdgcn_s_barrier();
+#endif
+#if PTK_FA_ABL != 2
     if (t + 2 < t_hi) stage((bb + 2) % NB, t + 2);
+#endif
   };
   // S^T = K Q^T for tile t: s[ms] holds keys 16ms + 4g + j, query column c16
   auto qk = [&](auto BUF, f32x4_t (&s)[2]) __attribute__((always_inline)) {
@@ -491,8 +498,16 @@ __global__ void __launch_bounds__(512, 1) attn_fwd256_kernel(FlashArgs a) {
       s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int ks = 0; ks < KS; ++ks) {
+#if PTK_FA_ABL == 6
+        const bf16x8_t kf = qf[(ks + 1) & 7];
+#else
         const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + koff[ks & 3] + (ks >> 2) * 256 + ms * 16 * (D * 2));
+#endif
+#if PTK_FA_ABL == 3
+        s[ms][ks & 3] += (float)kf[ks];
+#else
         s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
+#endif
       }
     }
   };
@@ -500,6 +515,14 @@ __global__ void __launch_bounds__(512, 1) attn_fwd256_kernel(FlashArgs a) {
   // every key is valid and visible to every row of the wave (below the causal diagonal, inside the window)
   // skips the mask.
   auto softmax = [&](int t, f32x4_t (&s)[2], bf16x8_t& pf) __attribute__((always_inline)) {
+#if PTK_FA_ABL == 5
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pf[ms * 4 + j] = (short)f2bf(s[ms][j]);
+    l_run += s[0][0];
+    return;
+#endif
     const uint32_t km = kmask_s[t];
     const bool interior = km == 0xffffffffu && (!causal || t * KT + KT - 1 <= wpos_lo) &&
                           (nowin || t * KT > wpos_hi - a.window);
@@ -562,10 +585,18 @@ __global__ void __launch_bounds__(512, 1) attn_fwd256_kernel(FlashArgs a) {
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const char* addr = vaddr[ds & 7] + bb * TILE + (ds >> 3) * 256 + hh * 16 * (D * 2);
+#if PTK_FA_ABL == 7
+        const s16x4_t r = {qf[ds & 7][hh], qf[ds & 7][hh + 2], qf[ds & 7][hh + 4], qf[ds & 7][hh + 6]};
+#else
         const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
+#endif
         vf[4 * hh + 0] = r[0]; vf[4 * hh + 1] = r[1]; vf[4 * hh + 2] = r[2]; vf[4 * hh + 3] = r[3];
       }
+#if PTK_FA_ABL == 4
+      o[ds][0] += (float)vf[ds & 7] * (float)pf[1];
+#else
       o[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[ds], 0, 0, 0);
+#endif
     }
   };
   auto early = [&](auto BUF, int t) __attribute__((always_inline)) {
@@ -832,6 +863,231 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
         kt[4 * hh + 0] = r[0]; kt[4 * hh + 1] = r[1]; kt[4 * hh + 2] = r[2]; kt[4 * hh + 3] = r[3];
       }
       acc[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, dsf, acc[ds], 0, 0, 0);
+    }
+  }
+  if (qrow >= a.rows) return;
+  bf16_t* op = a.dQ + (z * a.rows + qrow) * (long)D + 4 * g;
+#pragma unroll
+  for (int ds = 0; ds < DS; ++ds) {
+    u16x4_t u;
+    u[0] = f2bf(acc[ds][0] * a.scale); u[1] = f2bf(acc[ds][1] * a.scale);
+    u[2] = f2bf(acc[ds][2] * a.scale); u[3] = f2bf(acc[ds][3] * a.scale);
+    *reinterpret_cast<u16x4_t*>(op + 16 * ds) = u;
+  }
+}
+
+// ---------------------------------------------------------------- dQ, head_dim 256
+// The forward's structure (attn_fwd256_kernel) applied to the dQ pass: 8 waves x 16 query rows, K and V
+// tiles of 32 keys by buffer_load ... lds into separate 4-slot rings (K read by rows for S and transposed
+// for dQ, so its image uses the dual-use swizzle), the loop unrolled by the ring depth, per-tile key masks,
+// late waves one phase behind.  Per tile and wave: S^T = K Q^T, dP^T = V dO^T, P = exp(S scale - LSE),
+// dS = P (dP - delta), dQ^T += K^T dS^T.  Same arithmetic, in the same order, as attn_bwd_dq_kernel.
+__global__ void __launch_bounds__(512, 1) attn_bwd_dq256_kernel(FlashBwdArgs a) {
+  constexpr int D = 256, KT = 32, KS = 8, DS = 16, NB = 4;
+  constexpr int TILE = KT * D * 2;
+  __shared__ __attribute__((aligned(16))) char smem[2 * NB * TILE + FA_MAXT * 4];
+  char* const kring = smem;
+  char* const vring = smem + NB * TILE;
+  uint32_t* const kmask_s = reinterpret_cast<uint32_t*>(smem + 2 * NB * TILE);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
+  const long z = blockIdx.x % nz;
+  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;
+  const bf16_t* K = a.K + z * (long)a.nkeys * D;
+  const bf16_t* V = a.V + z * (long)a.nkeys * D;
+  const long b = z / a.zdiv;
+  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
+  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
+  int k_hi = a.nkeys, k_lo = 0;
+  if (a.causal) {
+    k_hi = min(k_hi, pos_hi + 1);
+    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
+  }
+  const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
+
+  for (int tt = wave; tt < t_hi; tt += 8) {
+    const int key = tt * KT + (lane & 31);
+    const bool ok = key < a.nkeys && (!kvl || kvl[min(key, a.nkeys - 1)] != 0);
+    const uint64_t m = __ballot(ok);
+    if (lane == 0) kmask_s[tt] = (uint32_t)m;
+  }
+
+  const int wrow0 = r0 + wave * 16;
+  const int qrow = wrow0 + c16;
+  const int qrow_c = min(qrow, a.rows - 1);
+  const long qoff = (z * a.rows + qrow_c) * (long)D + 8 * g;
+  bf16x8_t qf[KS], df[KS];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    qf[ks] = *reinterpret_cast<const bf16x8_t*>(a.Q + qoff + 32 * ks);
+    df[ks] = *reinterpret_cast<const bf16x8_t*>(a.dO + qoff + 32 * ks);
+  }
+  const float L2E = 1.4426950408889634f;
+  float lse2 = a.lse[z * a.rows + qrow_c] * L2E;
+  float dlt = a.delta[z * a.rows + qrow_c];
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) {
+    fa_pin(qf[ks]);
+    fa_pin(df[ks]);
+  }
+  fa_pin(lse2);
+  fa_pin(dlt);
+  __syncthreads();   // key masks published (no LDS-DMA in flight yet)
+  const int qpos = qrow_c / a.qdiv;
+  const float sl2 = a.scale * L2E;
+  const int causal = a.causal != 0, nowin = a.window <= 0;
+  const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
+  const int wpos_hi = min(wrow0 + 15, a.rows - 1) / a.qdiv;
+  const bool idle = wrow0 >= a.rows;
+
+  const fa_u32x4_t rsk = fa_rsrc(K, (uint32_t)((long)a.nkeys * D * 2));
+  const fa_u32x4_t rsv = fa_rsrc(V, (uint32_t)((long)a.nkeys * D * 2));
+  uint32_t dof[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int row = (wave * 2 + j) * 2 + (lane >> 5);
+    dof[j] = (uint32_t)row * (D * 2) + 16u * ((lane & 31) ^ swz_rt(row));
+  }
+  const uint32_t lds_k = __builtin_amdgcn_readfirstlane(fa_lds_addr(kring) + wave * 2048);
+  const uint32_t lds_v = __builtin_amdgcn_readfirstlane(fa_lds_addr(vring) + wave * 2048);
+  auto stage = [&](int bb, int t) __attribute__((always_inline)) {
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)t * (uint32_t)(KT * D * 2));
+    FA_DMA(dof[0], so, rsk, lds_k + bb * TILE);
+    FA_DMA(dof[1], so, rsk, lds_k + bb * TILE + 1024);
+    FA_DMA(dof[0], so, rsv, lds_v + bb * TILE);
+    FA_DMA(dof[1], so, rsv, lds_v + bb * TILE + 1024);
+  };
+  // row reads (K for S, V for dP): rows 16ms + c16, chunk (4ks + g) ^ 2(row & 7): ks bit 2, ms untouched;
+  // transposed K reads (dQ): rows 16hh + 4g + q4, chunk (2ds + (p4 >> 1)) ^ 2(row & 7): ds bit 3, hh untouched
+  int roff[4], toff[8];
+  const char* vrow_base;
+  {
+    const int q4 = c16 >> 2, p4 = c16 & 3, trow = 4 * g + q4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) roff[i] = c16 * (D * 2) + ((i * 4 + g) ^ swz_rt(c16)) * 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) toff[i] = trow * (D * 2) + ((2 * i + (p4 >> 1)) ^ swz_rt(trow)) * 16 + 8 * (p4 & 1);
+    vrow_base = (const char*)(fa_lptr_t)(uintptr_t)__builtin_amdgcn_readfirstlane(0) + fa_lds_addr(vring);
+  }
+
+  f32x4_t acc[DS];
+#pragma unroll
+  for (int i = 0; i < DS; ++i) acc[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+
+  auto sync = [&](int bb, int t) __attribute__((always_inline)) {
+    if (t + 1 < t_hi) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < t_hi) stage((bb + 2) % NB, t + 2);
+  };
+  // S^T, dP^T for tile t, then dS^T (bf16, k order 4g+j / 16+4g+j as the dQ product's B operand)
+  auto sdp = [&](auto BUF, int t, bf16x8_t& dsf) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    const char* kb = kring + bb * TILE;
+    const char* vb = vrow_base + bb * TILE;
+    f32x4_t s[2], dp[2];
+#pragma unroll
+    for (int ms = 0; ms < 2; ++ms) {
+      s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      dp[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int off = roff[ks & 3] + (ks >> 2) * 256 + ms * 16 * (D * 2);
+        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + off);
+        const bf16x8_t vf = *reinterpret_cast<const bf16x8_t*>(vb + off);
+        s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
+        dp[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[ks], dp[ms], 0, 0, 0);
+      }
+    }
+    const uint32_t km = kmask_s[t];
+    const bool interior = km == 0xffffffffu && (!causal || t * KT + KT - 1 <= wpos_lo) &&
+                          (nowin || t * KT > wpos_hi - a.window);
+    if (interior) {
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float p = __builtin_amdgcn_exp2f(fmaf(s[ms][j], sl2, -lse2));
+          dsf[ms * 4 + j] = (short)f2bf(bfround(p) * (dp[ms][j] - dlt));
+        }
+    } else {
+      uint32_t vis = km;
+      if (causal) {
+        const int d = qpos - t * KT;
+        vis &= d >= 31 ? 0xffffffffu : (d < 0 ? 0u : (2u << d) - 1u);
+        if (!nowin) {
+          const int e = d - a.window;
+          vis &= e < 0 ? 0xffffffffu : (e >= 31 ? 0u : ~((2u << e) - 1u));
+        }
+      }
+#pragma unroll
+      for (int ms = 0; ms < 2; ++ms)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int kl = ms * 16 + 4 * g + j;
+          const float p = __builtin_amdgcn_exp2f(((vis >> kl) & 1u) ? fmaf(s[ms][j], sl2, -lse2) : -INFINITY);
+          dsf[ms * 4 + j] = (short)f2bf(bfround(p) * (dp[ms][j] - dlt));
+        }
+    }
+  };
+  auto dq = [&](auto BUF, const bf16x8_t& dsf) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    const char* kb = kring + bb * TILE;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      bf16x8_t kt;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const char* addr = kb + toff[ds & 7] + (ds >> 3) * 256 + hh * 16 * (D * 2);
+        const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
+        kt[4 * hh + 0] = r[0]; kt[4 * hh + 1] = r[1]; kt[4 * hh + 2] = r[2]; kt[4 * hh + 3] = r[3];
+      }
+      acc[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, dsf, acc[ds], 0, 0, 0);
+    }
+  };
+  auto early = [&](auto BUF, int t) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    sync(bb, t);
+    if (idle) return;
+    bf16x8_t dsf;
+    sdp(BUF, t, dsf);
+    dq(BUF, dsf);
+  };
+  bf16x8_t dprev;
+  auto late = [&](auto BUF, int t) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    if (t < t_hi) sync(bb, t);
+    if (idle) return;
+    if (t > t_lo) dq(fa_ic<(bb + NB - 1) % NB>{}, dprev);
+    if (t == t_hi) return;
+    sdp(BUF, t, dprev);
+  };
+  if (t_lo < t_hi) stage(0, t_lo);
+  if (t_lo + 1 < t_hi) stage(1, t_lo + 1);
+  if (wave < 4) {
+    for (int t = t_lo; t < t_hi;) {
+      early(fa_ic<0>{}, t);
+      if (++t >= t_hi) break;
+      early(fa_ic<1>{}, t);
+      if (++t >= t_hi) break;
+      early(fa_ic<2>{}, t);
+      if (++t >= t_hi) break;
+      early(fa_ic<3>{}, t);
+      ++t;
+    }
+  } else {
+    for (int t = t_lo; t <= t_hi;) {
+      late(fa_ic<0>{}, t);
+      if (++t > t_hi) break;
+      late(fa_ic<1>{}, t);
+      if (++t > t_hi) break;
+      late(fa_ic<2>{}, t);
+      if (++t > t_hi) break;
+      late(fa_ic<3>{}, t);
+      ++t;
     }
   }
   if (qrow >= a.rows) return;
@@ -1248,6 +1504,264 @@ __global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel
   }
 }
 
+// dK/dV (head_dim 256), instruction-lean form of attn_bwd_dkv256_kernel<32> (same slab / piece plan, same
+// arithmetic in the same order, so the same results): Q, dO and the chunk's LSE | delta arrive by
+// buffer_load ... lds with per-lane offsets fixed for the kernel and the chunk's byte offset in an SGPR;
+// separate Q and dO rings with the chunk loop unrolled by the ring depth (every LDS read = lane offset +
+// immediate); the causal / window position test by shift (query heads per kv head a power of two); a wave
+// whose 32 keys are all invisible to a chunk's rows (the causal diagonal and the window edge of the slab)
+// skips that chunk's MFMAs.
+__global__ void __launch_bounds__(256, 1) attn_bwd_dkv256b_kernel(FlashBwdArgs a) {
+  constexpr int D = 256, KS = D / 32, DS = D / 16, KPW = 32, KG = 2, NB = 4;
+  constexpr int TILE = DKV_CH * D * 2;   // 16 KiB: 32 rows of Q or dO
+  __shared__ __attribute__((aligned(16))) char smem[2 * NB * TILE + NB * 256];   // Q ring, dO ring, (lse|delta) ring
+  char* const qring = smem;
+  char* const oring = smem + NB * TILE;
+  const float* const ldring = reinterpret_cast<const float*>(smem + 2 * NB * TILE);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nz = a.nz;
+  const int item = blockIdx.x / nz;
+  const long z = blockIdx.x - (long)item * nz;
+  const int s = a.dkv_item_slab[item], piece = a.dkv_item_piece[item];
+  const int P = dkv_pieces(a, s);
+  int base = 0;
+  for (int s2 = 0; s2 < s; ++s2) {
+    const int P2 = dkv_pieces(a, s2);
+    if (P2 > 1) base += P2;
+  }
+  int c0, c1;
+  {
+    int lo, hi;
+    dkv_slab_chunks(a, s, lo, hi);
+    const int n = hi - lo;
+    c0 = lo + (int)((long)piece * n / P);
+    c1 = lo + (int)((long)(piece + 1) * n / P);
+  }
+  const long b = z / a.zdiv;
+  const int kw = s * DKV_KEYS + wave * KPW;   // the wave's first key
+
+  bf16x8_t kf[KG][KS], vf[KG][KS];
+  int key[KG];
+  bool kok[KG];
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) {
+    key[kg] = kw + 16 * kg + c16;
+    const int kc = min(key[kg], a.nkeys - 1);
+    const long ko = (z * a.nkeys + kc) * (long)D + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      kf[kg][ks] = *reinterpret_cast<const bf16x8_t*>(a.K + ko + 32 * ks);
+      vf[kg][ks] = *reinterpret_cast<const bf16x8_t*>(a.V + ko + 32 * ks);
+    }
+    kok[kg] = key[kg] < a.nkeys && (!a.key_valid || a.key_valid[b * a.nkeys + kc] != 0);
+  }
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg)
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) {
+      fa_pin(kf[kg][ks]);
+      fa_pin(vf[kg][ks]);
+    }
+  const float L2E = 1.4426950408889634f;
+  const float sl2 = a.scale * L2E;
+  const int qshift = __builtin_ctz(a.qdiv);   // host guarantees a power of two
+  const int causal = a.causal != 0, nowin = a.window <= 0;
+  bool kall = true;
+#pragma unroll
+  for (int kg = 0; kg < KG; ++kg) kall = kall && kok[kg];
+  const bool wkall = __all(kall);   // every key of the wave valid
+
+  // ---- DMA: wave w stages rows 8w..8w+7 of a chunk's Q and dO (4 pieces of 2 rows each), and one piece of
+  // the chunk's LSE (waves 0, 1) or delta (waves 2, 3): 9 ops per wave per chunk
+  const fa_u32x4_t rsq = fa_rsrc(a.Q + z * (long)a.rows * D, (uint32_t)((long)a.rows * D * 2));
+  const fa_u32x4_t rso = fa_rsrc(a.dO + z * (long)a.rows * D, (uint32_t)((long)a.rows * D * 2));
+  const fa_u32x4_t rsl = fa_rsrc(wave < 2 ? (const void*)(a.lse + z * a.rows) : (const void*)(a.delta + z * a.rows),
+                                 (uint32_t)((long)a.rows * 4));
+  uint32_t dof[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = (wave * 4 + j) * 2 + (lane >> 5);
+    dof[j] = (uint32_t)row * (D * 2) + 16u * ((lane & 31) ^ swz_rt(row));
+  }
+  const uint32_t dol = (uint32_t)lane * 16u + (uint32_t)(wave & 1) * 64u;
+  const uint32_t lds_q = __builtin_amdgcn_readfirstlane(fa_lds_addr(qring) + wave * 4096);
+  const uint32_t lds_o = __builtin_amdgcn_readfirstlane(fa_lds_addr(oring) + wave * 4096);
+  // (lse | delta) slot: [32 LSE | 32 delta] floats; wave w's 4 lanes land 64 B at slot + 64 w
+  const uint32_t lds_l = __builtin_amdgcn_readfirstlane(fa_lds_addr(smem + 2 * NB * TILE) + wave * 64);
+  auto stage = [&](int bb, int c) __attribute__((always_inline)) {
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)c * (uint32_t)TILE);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) FA_DMA(dof[j], so, rsq, lds_q + bb * TILE + j * 1024);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) FA_DMA(dof[j], so, rso, lds_o + bb * TILE + j * 1024);
+    const uint32_t sl = __builtin_amdgcn_readfirstlane((uint32_t)c * (uint32_t)(DKV_CH * 4));
+    if (lane < 4) FA_DMA(dol, sl, rsl, lds_l + bb * 256);
+  };
+
+  // ---- LDS read offsets (lane part; slot, k-step and row-group parts are immediates)
+  int roff[4], toff[8];
+  {
+    const int q4 = c16 >> 2, p4 = c16 & 3, trow = 4 * g + q4;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) roff[i] = c16 * (D * 2) + ((i * 4 + g) ^ swz_rt(c16)) * 16;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) toff[i] = trow * (D * 2) + ((2 * i + (p4 >> 1)) ^ swz_rt(trow)) * 16 + 8 * (p4 & 1);
+  }
+  const char* const obase = (const char*)(fa_lptr_t)(uintptr_t)__builtin_amdgcn_readfirstlane(0) + fa_lds_addr(oring);
+
+  f32x4_t dv[DS][KG], dk[DS][KG];
+#pragma unroll
+  for (int i = 0; i < DS; ++i)
+#pragma unroll
+    for (int kg = 0; kg < KG; ++kg) {
+      dv[i][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      dk[i][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+    }
+
+  auto step = [&](auto BUF, int c) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    // chunk c landed; chunks c+1, c+2 may stay in flight (9 ops each)
+    const int ahead = c1 - 1 - c;
+    if (ahead >= 2) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+    else if (ahead == 1) asm volatile("s_waitcnt vmcnt(9)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (c + NB - 1 < c1) stage((bb + NB - 1) % NB, c + NB - 1);
+    // rows of this chunk: positions cpos_lo..cpos_hi; the wave's keys kw..kw+31
+    const int cpos_lo = (c * DKV_CH) >> qshift, cpos_hi = (c * DKV_CH + DKV_CH - 1) >> qshift;
+    if ((causal && kw > cpos_hi) || (!nowin && kw + KPW - 1 <= cpos_lo - a.window)) return;   // all invisible
+    const char* qb = qring + bb * TILE;
+    const char* ob = obase + bb * TILE;
+    const float* ld = ldring + bb * 64;
+
+    // ---- S = Q K^T, dP = dO V^T for 32 rows x 32 keys (key on the lane)
+    f32x4_t sc[2][KG], dp[2][KG];
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt)
+#pragma unroll
+      for (int kg = 0; kg < KG; ++kg) {
+        sc[qt][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+        dp[qt][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+      }
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const int off = roff[ks & 3] + (ks >> 2) * 256 + qt * 16 * (D * 2);
+        const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(qb + off);
+        const bf16x8_t oa = *reinterpret_cast<const bf16x8_t*>(ob + off);
+#pragma unroll
+        for (int kg = 0; kg < KG; ++kg) {
+          sc[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kg][ks], sc[qt][kg], 0, 0, 0);
+          dp[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[kg][ks], dp[qt][kg], 0, 0, 0);
+        }
+      }
+    }
+    // ---- P = exp(S*scale - LSE) (bf16), dS = P (dP - delta) (bf16); slot 4qt + j of lane group g <-> row 16qt + 4g + j
+    bf16x8_t pf[KG], dsf[KG];
+    const bool interior = wkall && (!causal || kw + KPW - 1 <= cpos_lo) && (nowin || kw > cpos_hi - a.window);
+#pragma unroll
+    for (int qt = 0; qt < 2; ++qt) {
+      const float4 l4 = *reinterpret_cast<const float4*>(ld + qt * 16 + 4 * g);
+      const float4 d4 = *reinterpret_cast<const float4*>(ld + 32 + qt * 16 + 4 * g);
+      const float lv[4] = {l4.x * L2E, l4.y * L2E, l4.z * L2E, l4.w * L2E}, dl[4] = {d4.x, d4.y, d4.z, d4.w};
+      if (interior) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg) {
+            const bf16_t pb = f2bf(__builtin_amdgcn_exp2f(fmaf(sc[qt][kg][j], sl2, -lv[j])));
+            pf[kg][4 * qt + j] = (short)pb;
+            dsf[kg][4 * qt + j] = (short)f2bf(bf2f(pb) * (dp[qt][kg][j] - dl[j]));
+          }
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int pos = (c * DKV_CH + qt * 16 + 4 * g + j) >> qshift;
+#pragma unroll
+          for (int kg = 0; kg < KG; ++kg) {
+            const int ok = (int)kok[kg] & ((int)(key[kg] <= pos) | !causal) & ((int)(key[kg] > pos - a.window) | nowin);
+            const float p = __builtin_amdgcn_exp2f(ok ? fmaf(sc[qt][kg][j], sl2, -lv[j]) : -INFINITY);
+            const bf16_t pb = f2bf(p);
+            pf[kg][4 * qt + j] = (short)pb;
+            dsf[kg][4 * qt + j] = (short)f2bf(bf2f(pb) * (dp[qt][kg][j] - dl[j]));
+          }
+        }
+      }
+    }
+    // ---- dV^T += dO^T P, dK^T += Q^T dS (A operands by transposed LDS reads)
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      bf16x8_t ot, qt_;
+#pragma unroll
+      for (int hh = 0; hh < 2; ++hh) {
+        const int off = toff[ds & 7] + (ds >> 3) * 256 + hh * 16 * (D * 2);
+        const s16x4_t ro = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(ob + off));
+        const s16x4_t rq = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(qb + off));
+        ot[4 * hh + 0] = ro[0]; ot[4 * hh + 1] = ro[1]; ot[4 * hh + 2] = ro[2]; ot[4 * hh + 3] = ro[3];
+        qt_[4 * hh + 0] = rq[0]; qt_[4 * hh + 1] = rq[1]; qt_[4 * hh + 2] = rq[2]; qt_[4 * hh + 3] = rq[3];
+      }
+#pragma unroll
+      for (int kg = 0; kg < KG; ++kg) {
+        dv[ds][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ot, pf[kg], dv[ds][kg], 0, 0, 0);
+        dk[ds][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt_, dsf[kg], dk[ds][kg], 0, 0, 0);
+      }
+    }
+  };
+
+  // chunk c lives in ring slot (c - c0) % NB (compile-time in each unrolled copy)
+  if (c0 < c1) stage(0, c0);
+  if (c0 + 1 < c1) stage(1, c0 + 1);
+  if (c0 + 2 < c1) stage(2, c0 + 2);
+  for (int c = c0; c < c1;) {
+    step(fa_ic<0>{}, c);
+    if (++c >= c1) break;
+    step(fa_ic<1>{}, c);
+    if (++c >= c1) break;
+    step(fa_ic<2>{}, c);
+    if (++c >= c1) break;
+    step(fa_ic<3>{}, c);
+    ++c;
+  }
+
+  // ---- outputs: lane holds dV^T[16ds + 4g + j][key]
+  if (P == 1) {
+#pragma unroll
+    for (int kg = 0; kg < KG; ++kg) {
+      if (key[kg] >= a.nkeys) continue;
+      bf16_t* dvp = a.dV + (z * a.nkeys + key[kg]) * (long)D + 4 * g;
+      bf16_t* dkp = a.dK + (z * a.nkeys + key[kg]) * (long)D + 4 * g;
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) {
+        u16x4_t uv, uk;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          uv[j] = f2bf(dv[ds][kg][j]);
+          uk[j] = f2bf(dk[ds][kg][j] * a.scale);
+        }
+        *reinterpret_cast<u16x4_t*>(dvp + 16 * ds) = uv;
+        *reinterpret_cast<u16x4_t*>(dkp + 16 * ds) = uk;
+      }
+    }
+  } else {
+    float* part = a.dkv_part + ((long)(base + piece) * nz + z) * (2L * DKV_KEYS * D);
+#pragma unroll
+    for (int kg = 0; kg < KG; ++kg) {
+      const int kl = wave * KPW + 16 * kg + c16;
+      float* pk = part + (long)kl * D + 4 * g;
+      float* pv = pk + (long)DKV_KEYS * D;
+#pragma unroll
+      for (int ds = 0; ds < DS; ++ds) {
+        *reinterpret_cast<float4*>(pk + 16 * ds) = make_float4(dk[ds][kg][0], dk[ds][kg][1], dk[ds][kg][2], dk[ds][kg][3]);
+        *reinterpret_cast<float4*>(pv + 16 * ds) = make_float4(dv[ds][kg][0], dv[ds][kg][1], dv[ds][kg][2], dv[ds][kg][3]);
+      }
+    }
+  }
+}
+
 // sums the partials of every split slab in piece order -> bf16 dK (x scale), dV
 __global__ void __launch_bounds__(256) attn_dkv_reduce_kernel(FlashBwdArgs a) {
   constexpr int D = 256;
@@ -1423,14 +1937,24 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs*
       hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
       // 32 keys per wave (one wave per SIMD) measured 209 us vs 252 us for 16 keys per wave (two per
       // SIMD, which spills the precomputed transposed-read addresses) at cfg2
-      hipLaunchKernelGGL(attn_bwd_dkv256_kernel<32>, dim3((unsigned)(np * nz)), dim3(256), 0, st, b);
+      // PTK_ATTN_DKV_OLD=1: the previous dK/dV kernel (A/B)
+      static const bool dkv_old = getenv("PTK_ATTN_DKV_OLD") && atoi(getenv("PTK_ATTN_DKV_OLD")) == 1;
+      if (dkv_old || (b.qdiv & (b.qdiv - 1)) || (long)b.rows * 256 * 2 > 0x7fffffffL)
+        hipLaunchKernelGGL(attn_bwd_dkv256_kernel<32>, dim3((unsigned)(np * nz)), dim3(256), 0, st, b);
+      else
+        hipLaunchKernelGGL(attn_bwd_dkv256b_kernel, dim3((unsigned)(np * nz)), dim3(256), 0, st, b);
       if (ns > 0 && defer) {
         *defer = b;
         defer->dkv_deferred = 1;
       } else if (ns > 0)
         hipLaunchKernelGGL(attn_dkv_reduce_kernel, dim3((unsigned)((nz * 2L * DKV_KEYS * 64 + 255) / 256), (unsigned)nslab),
                            dim3(256), 0, st, b);
-      hipLaunchKernelGGL(attn_bwd_dq_kernel<256>, gq, dim3(512), 0, st, b);
+      // PTK_ATTN_DQ_OLD=1: the previous dQ kernel (A/B)
+      static const bool dq_old = getenv("PTK_ATTN_DQ_OLD") && atoi(getenv("PTK_ATTN_DQ_OLD")) == 1;
+      if (dq_old || (a.nkeys + 31) / 32 > FA_MAXT)
+        hipLaunchKernelGGL(attn_bwd_dq_kernel<256>, gq, dim3(512), 0, st, b);
+      else
+        hipLaunchKernelGGL(attn_bwd_dq256_kernel, gq, dim3(512), 0, st, b);
       break;
     }
     default: return set_error("attn_bwd: head_dim %d unsupported (64, 256)", a.D);
