@@ -876,12 +876,263 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
   }
 }
 
+// ---------------------------------------------------------------- forward, head_dim 64 (SigLIP)
+// attn_fwd256_kernel's structure at head_dim 64: 64-key tiles (8 KiB per tensor: one LDS-DMA piece per
+// tensor per wave), K/V rings of 4 slots (64 KiB, so two blocks can share a CU), the loop unrolled by
+// the ring depth, per-tile key masks, deferred running max, late waves one phase behind.  Per tile and
+// wave: S^T = K Q^T (8 MFMAs), 16 scores per lane, O^T += V^T P^T (8 MFMAs).
+__global__ void __launch_bounds__(512, 2) attn_fwd64_kernel(FlashArgs a) {
+  constexpr int D = 64, KT = 64, KS = 2, DS = 4, MS = 4, ST = 2, NB = 4;
+  constexpr int TILE = KT * D * 2;   // 8 KiB
+  __shared__ __attribute__((aligned(16))) char smem[2 * NB * TILE + FA_MAXT * 4];
+  char* const kring = smem;
+  char* const vring = smem + NB * TILE;
+  uint32_t* const kmask_s = reinterpret_cast<uint32_t*>(smem + 2 * NB * TILE);   // 2 words per 64-key tile
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int g = lane >> 4, c16 = lane & 15;
+  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
+  const int z = blockIdx.x % nz, z0 = z / a.zin, z1 = z - z0 * a.zin;
+  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;
+  const bf16_t* Q = a.Q + z0 * a.sQ0 + z1 * a.sQ1;
+  const bf16_t* K = a.K + z0 * a.sK0 + z1 * a.sK1;
+  const bf16_t* V = a.V + z0 * a.sK0 + z1 * a.sK1;
+  const long b = z / a.zdiv;
+  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
+
+  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
+  int k_hi = a.nkeys, k_lo = 0;
+  if (a.causal) {
+    k_hi = min(k_hi, pos_hi + 1);
+    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
+  }
+  const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
+
+  // key masks: word 2t + h covers keys 64t + 32h .. +31
+  for (int tt = wave; tt < 2 * t_hi; tt += 8) {
+    const int key = tt * 32 + (lane & 31);
+    const bool ok = key < a.nkeys && (!kvl || kvl[min(key, a.nkeys - 1)] != 0);
+    const uint64_t m = __ballot(ok);
+    if (lane == 0) kmask_s[tt] = (uint32_t)m;
+  }
+
+  const int wrow0 = r0 + wave * 16;
+  const int qrow = wrow0 + c16;
+  const int qrow_c = min(qrow, a.rows - 1);
+  const int qpos = qrow_c / a.qdiv;
+  bf16x8_t qf[KS];
+  {
+    const bf16_t* qp = Q + map_row(a.qmap, qrow_c) * a.ldq + 8 * g;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * ks);
+  }
+#pragma unroll
+  for (int ks = 0; ks < KS; ++ks) fa_pin(qf[ks]);
+  __syncthreads();
+
+  const int causal = a.causal != 0, nowin = a.window <= 0;
+  const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
+  const int wpos_hi = min(wrow0 + 15, a.rows - 1) / a.qdiv;
+
+  // DMA: wave w stages rows 8w..8w+7 of each tile (one 1-KiB piece per tensor)
+  const fa_u32x4_t rsk = fa_rsrc(K, (uint32_t)((long)a.nkeys * a.ldk * 2));
+  const fa_u32x4_t rsv = fa_rsrc(V, (uint32_t)((long)a.nkeys * a.ldk * 2));
+  uint32_t dk, dv;
+  {
+    const int row = wave * 8 + (lane >> 3);
+    dk = (uint32_t)row * (uint32_t)a.ldk * 2u + 16u * ((lane & 7) ^ swz_k<D>(row));
+    dv = (uint32_t)row * (uint32_t)a.ldk * 2u + 16u * ((lane & 7) ^ swz_v<D>(row));
+  }
+  const uint32_t lds_k = __builtin_amdgcn_readfirstlane(fa_lds_addr(kring) + wave * 1024);
+  const uint32_t lds_v = __builtin_amdgcn_readfirstlane(fa_lds_addr(vring) + wave * 1024);
+  const uint32_t tile_bytes = __builtin_amdgcn_readfirstlane((uint32_t)KT * (uint32_t)a.ldk * 2u);
+  auto stage = [&](int bb, int t) __attribute__((always_inline)) {
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)t * tile_bytes);
+    FA_DMA(dk, so, rsk, lds_k + bb * TILE);
+    FA_DMA(dv, so, rsv, lds_v + bb * TILE);
+  };
+  // K rows 16ms + c16, chunk (4ks + g) ^ ((row >> 1) & 7): the swizzle does not depend on ms (immediate);
+  // V^T rows 16(2st + hh) + 4g + q4, chunk (2ds + (p4 >> 1)) ^ 2((row >> 1) & 3): independent of st, hh
+  int koff[KS];
+  const char* vaddr[DS];
+  {
+    const int q4 = c16 >> 2, p4 = c16 & 3, vrow = 4 * g + q4;
+#pragma unroll
+    for (int i = 0; i < KS; ++i) koff[i] = c16 * (D * 2) + ((i * 4 + g) ^ swz_k<D>(c16)) * 16;
+#pragma unroll
+    for (int i = 0; i < DS; ++i) {
+      const uint32_t va = fa_lds_addr(vring) + vrow * (D * 2) + ((2 * i + (p4 >> 1)) ^ swz_v<D>(vrow)) * 16 + 8 * (p4 & 1);
+      vaddr[i] = (const char*)(fa_lptr_t)(uintptr_t)__builtin_amdgcn_readfirstlane(0) + va;
+    }
+  }
+
+  f32x4_t o[DS];
+#pragma unroll
+  for (int i = 0; i < DS; ++i) o[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+  float m_run = -INFINITY, l_run = 0.f;
+  const float sl2 = a.scale * 1.4426950408889634f;
+  const float defer = FA_DEFER / sl2;
+  const bool idle = wrow0 >= a.rows;   // rows past the end (SigLIP's half-empty last block)
+
+  auto sync = [&](int bb, int t) __attribute__((always_inline)) {
+    if (t + 1 < t_hi) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    if (t + 2 < t_hi) stage((bb + 2) % NB, t + 2);
+  };
+  auto qk = [&](auto BUF, f32x4_t (&s)[MS]) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    const char* kb = kring + bb * TILE;
+#pragma unroll
+    for (int ms = 0; ms < MS; ++ms) {
+      s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int ks = 0; ks < KS; ++ks) {
+        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + koff[ks] + ms * 16 * (D * 2));
+        s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
+      }
+    }
+  };
+  // P for the k order of the P.V step st: {32st + 4g + 0..3, 32st + 16 + 4g + 0..3}
+  auto softmax = [&](int t, f32x4_t (&s)[MS], bf16x8_t (&pf)[ST]) __attribute__((always_inline)) {
+    const uint32_t km0 = kmask_s[2 * t], km1 = kmask_s[2 * t + 1];
+    const bool interior = (km0 & km1) == 0xffffffffu && (!causal || t * KT + KT - 1 <= wpos_lo) &&
+                          (nowin || t * KT > wpos_hi - a.window);
+    float mt = -INFINITY;
+    if (interior) {
+#pragma unroll
+      for (int ms = 0; ms < MS; ++ms)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) mt = fmaxf(mt, s[ms][j]);
+    } else {
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        uint32_t vis = h ? km1 : km0;
+        if (causal) {
+          const int d = qpos - (t * KT + 32 * h);
+          vis &= d >= 31 ? 0xffffffffu : (d < 0 ? 0u : (2u << d) - 1u);
+          if (!nowin) {
+            const int e = d - a.window;
+            vis &= e < 0 ? 0xffffffffu : (e >= 31 ? 0u : ~((2u << e) - 1u));
+          }
+        }
+#pragma unroll
+        for (int m2 = 0; m2 < 2; ++m2)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int ms = 2 * h + m2, kl = m2 * 16 + 4 * g + j;
+            const float v = ((vis >> kl) & 1u) ? s[ms][j] : -INFINITY;
+            s[ms][j] = v;
+            mt = fmaxf(mt, v);
+          }
+      }
+    }
+    mt = xor32_max(xor16_max(mt));
+    const bool up = mt > m_run + defer;
+    const float m_new = up ? mt : m_run;
+    const float alpha = (up && m_run != -INFINITY) ? __builtin_amdgcn_exp2f((m_run - m_new) * sl2) : 1.f;
+    const float mc = (m_new == -INFINITY) ? 0.f : m_new * sl2;
+    float rs = 0.f;
+#pragma unroll
+    for (int ms = 0; ms < MS; ++ms)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float p = __builtin_amdgcn_exp2f(fmaf(s[ms][j], sl2, -mc));
+        rs += p;
+        pf[ms >> 1][(ms & 1) * 4 + j] = (short)f2bf(p);
+      }
+    rs = xor32_sum(xor16_sum(rs));
+    l_run = l_run * alpha + rs;
+    m_run = m_new;
+    if (__any(alpha != 1.f)) {
+#pragma unroll
+      for (int i = 0; i < DS; ++i) o[i] *= alpha;
+    }
+  };
+  auto pv = [&](auto BUF, const bf16x8_t (&pf)[ST]) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds)
+#pragma unroll
+      for (int st = 0; st < ST; ++st) {
+        bf16x8_t vf;
+#pragma unroll
+        for (int hh = 0; hh < 2; ++hh) {
+          const char* addr = vaddr[ds] + bb * TILE + (2 * st + hh) * 16 * (D * 2);
+          const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
+          vf[4 * hh + 0] = r[0]; vf[4 * hh + 1] = r[1]; vf[4 * hh + 2] = r[2]; vf[4 * hh + 3] = r[3];
+        }
+        o[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf[st], o[ds], 0, 0, 0);
+      }
+  };
+  auto early = [&](auto BUF, int t) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    sync(bb, t);
+    if (idle) return;
+    f32x4_t s[MS];
+    bf16x8_t pf[ST];
+    qk(BUF, s);
+    softmax(t, s, pf);
+    pv(BUF, pf);
+  };
+  bf16x8_t pprev[ST];
+  auto late = [&](auto BUF, int t) __attribute__((always_inline)) {
+    constexpr int bb = decltype(BUF)::value;
+    if (t < t_hi) sync(bb, t);
+    if (idle) return;
+    if (t > t_lo) pv(fa_ic<(bb + NB - 1) % NB>{}, pprev);
+    if (t == t_hi) return;
+    f32x4_t s[MS];
+    qk(BUF, s);
+    softmax(t, s, pprev);
+  };
+  if (t_lo < t_hi) stage(0, t_lo);
+  if (t_lo + 1 < t_hi) stage(1, t_lo + 1);
+  if (wave < 4) {
+    for (int t = t_lo; t < t_hi;) {
+      early(fa_ic<0>{}, t);
+      if (++t >= t_hi) break;
+      early(fa_ic<1>{}, t);
+      if (++t >= t_hi) break;
+      early(fa_ic<2>{}, t);
+      if (++t >= t_hi) break;
+      early(fa_ic<3>{}, t);
+      ++t;
+    }
+  } else {
+    for (int t = t_lo; t <= t_hi;) {
+      late(fa_ic<0>{}, t);
+      if (++t > t_hi) break;
+      late(fa_ic<1>{}, t);
+      if (++t > t_hi) break;
+      late(fa_ic<2>{}, t);
+      if (++t > t_hi) break;
+      late(fa_ic<3>{}, t);
+      ++t;
+    }
+  }
+  if (qrow >= a.rows) return;
+  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
+  bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow) * a.ldo + 4 * g;
+#pragma unroll
+  for (int ds = 0; ds < DS; ++ds) {
+    u16x4_t u;
+    u[0] = f2bf(o[ds][0] * inv); u[1] = f2bf(o[ds][1] * inv);
+    u[2] = f2bf(o[ds][2] * inv); u[3] = f2bf(o[ds][3] * inv);
+    *reinterpret_cast<u16x4_t*>(op + 16 * ds) = u;
+  }
+  if (a.lse && g == 0)
+    a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_run)) * 0.6931471805599453f;
+}
+
 // ---------------------------------------------------------------- dQ, head_dim 256
 // The forward's structure (attn_fwd256_kernel) applied to the dQ pass: 8 waves x 16 query rows, K and V
 // tiles of 32 keys by buffer_load ... lds into separate 4-slot rings (K read by rows for S and transposed
 // for dQ, so its image uses the dual-use swizzle), the loop unrolled by the ring depth, per-tile key masks,
 // late waves one phase behind.  Per tile and wave: S^T = K Q^T, dP^T = V dO^T, P = exp(S scale - LSE),
-// dS = P (dP - delta), dQ^T += K^T dS^T.  Same arithmetic, in the same order, as attn_bwd_dq_kernel.
+// dS = P (dP - delta), dQ^T += K^T dS^T, as attn_bwd_dq_kernel.  It also computes delta = rowsum(dO O)
+// (attn_delta_kernel's job) from the dO fragments it holds anyway, and runs before the dK/dV kernel.
 __global__ void __launch_bounds__(512, 1) attn_bwd_dq256_kernel(FlashBwdArgs a) {
   constexpr int D = 256, KT = 32, KS = 8, DS = 16, NB = 4;
   constexpr int TILE = KT * D * 2;
@@ -927,7 +1178,23 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq256_kernel(FlashBwdArgs a) 
   }
   const float L2E = 1.4426950408889634f;
   float lse2 = a.lse[z * a.rows + qrow_c] * L2E;
-  float dlt = a.delta[z * a.rows + qrow_c];
+  // delta = rowsum(dO * O) for the wave's rows (this kernel runs before the dK/dV kernel, which reads it):
+  // the lane's 64 elements of its row, then the row's 4 lane groups
+  float dlt;
+  {
+    const long z0 = z / a.zin, z1 = z - z0 * a.zin;
+    const bf16_t* orow = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow_c) * a.ldo + 8 * g;
+    bf16x8_t of[KS];
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks) of[ks] = *reinterpret_cast<const bf16x8_t*>(orow + 32 * ks);
+    float acc0 = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < KS; ++ks)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc0 += bf2f((bf16_t)of[ks][e]) * bf2f((bf16_t)df[ks][e]);
+    dlt = xor32_sum(xor16_sum(acc0));
+    if (g == 0 && qrow < a.rows) a.delta[z * a.rows + qrow] = dlt;
+  }
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) {
     fa_pin(qf[ks]);
@@ -1934,7 +2201,12 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs*
         for (int s = 0; s < nslab && s < 128; ++s) { b.dkv_item_slab[s] = (unsigned char)s; b.dkv_item_piece[s] = 0; }
       }
       if (b.dkv_items > 128 || nslab > 128) return set_error("attn_bwd: %d dK/dV work items over %d key slabs (max 128)", b.dkv_items, nslab);
-      hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
+      // PTK_ATTN_DQ_OLD=1: the previous dQ kernel (A/B), after a separate delta pass and the dK/dV kernel;
+      // otherwise the dQ kernel computes delta and runs first
+      static const bool dq_old = getenv("PTK_ATTN_DQ_OLD") && atoi(getenv("PTK_ATTN_DQ_OLD")) == 1;
+      const bool dq_new = !dq_old && (a.nkeys + 31) / 32 <= FA_MAXT;
+      if (dq_new) hipLaunchKernelGGL(attn_bwd_dq256_kernel, gq, dim3(512), 0, st, b);
+      else hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
       // 32 keys per wave (one wave per SIMD) measured 209 us vs 252 us for 16 keys per wave (two per
       // SIMD, which spills the precomputed transposed-read addresses) at cfg2
       // PTK_ATTN_DKV_OLD=1: the previous dK/dV kernel (A/B)
@@ -1949,12 +2221,7 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs*
       } else if (ns > 0)
         hipLaunchKernelGGL(attn_dkv_reduce_kernel, dim3((unsigned)((nz * 2L * DKV_KEYS * 64 + 255) / 256), (unsigned)nslab),
                            dim3(256), 0, st, b);
-      // PTK_ATTN_DQ_OLD=1: the previous dQ kernel (A/B)
-      static const bool dq_old = getenv("PTK_ATTN_DQ_OLD") && atoi(getenv("PTK_ATTN_DQ_OLD")) == 1;
-      if (dq_old || (a.nkeys + 31) / 32 > FA_MAXT)
-        hipLaunchKernelGGL(attn_bwd_dq_kernel<256>, gq, dim3(512), 0, st, b);
-      else
-        hipLaunchKernelGGL(attn_bwd_dq256_kernel, gq, dim3(512), 0, st, b);
+      if (!dq_new) hipLaunchKernelGGL(attn_bwd_dq_kernel<256>, gq, dim3(512), 0, st, b);
       break;
     }
     default: return set_error("attn_bwd: head_dim %d unsupported (64, 256)", a.D);
@@ -1971,7 +2238,15 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
   if (nblk > 0x7fffffffL) return set_error("attn_fwd: too many blocks");
   dim3 grid((unsigned)nblk);
   switch (a.D) {
-    case 64: hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(512), 0, st, a); break;
+    case 64: {
+      // PTK_ATTN_FWD8W=1: the previous kernel (A/B); it also takes tables past FA_MAXT words
+      static const bool w8 = getenv("PTK_ATTN_FWD8W") && atoi(getenv("PTK_ATTN_FWD8W")) == 1;
+      if (w8 || (a.nkeys + 31) / 32 > FA_MAXT || (long)a.nkeys * a.ldk * 2 > 0x7fffffffL)
+        hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL(attn_fwd64_kernel, grid, dim3(512), 0, st, a);
+      break;
+    }
     // QG = 2 (256-row blocks) measured slower on the Gemma3 step: 352 blocks of double work on 256 CUs
     // quantise worse than 704 (110 vs 78 us per layer), and it spills
     case 256: {
