@@ -23,6 +23,9 @@ kw = {}
 if act == L.ACT_GEGLU:
     kw = dict(aux=torch.empty(m, n // 2, dtype=torch.bfloat16, device=dev),
               aux2=torch.empty(m, n // 2, dtype=torch.bfloat16, device=dev))
+elif act == L.ACT_GEGLU_BWD:   # dh GEMM: saved g, u [m, n] in, interleaved dg|du [m, 2n] out
+    kw = dict(aux_in=torch.randn(m, n, device=dev).to(torch.bfloat16),
+              aux_in2=torch.randn(m, n, device=dev).to(torch.bfloat16))
 L.lib().ptk_gemm_force_small_tiles(mode)
 C = K.gemm(A, B, act=act, **kw)
 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
