@@ -124,7 +124,8 @@ int ptk_gemm_timer_enable(int on);   /* 0 off, 1 every class, (1 << 8) | class m
    2 / 4 = every single-batch GEMM on the 256x256 / barrier-staggered 256x256 kernel,
    8 = every single-batch GEMM the persistent 4-wave 256x256 kernel supports on it. */
 int ptk_gemm_force_small_tiles(int mode);   /* tests: 0 auto, 1 128x128, 2 256x256, 4 staggered 256x256,
-                                              8 persistent 4-wave, 16 stream-K (needs desc scratch) */
+                                              8 persistent 4-wave, 16 stream-K (needs desc scratch),
+                                              32 ping-pong 8-wave (256x128 tiles) */
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
 
 /* Flash attention forward: O = softmax(scale * Q K^T + mask) V per z, bf16 in/out,

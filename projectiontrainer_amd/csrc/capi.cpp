@@ -108,8 +108,8 @@ size_t ptk_gemm_sk_workspace_bytes(void) { return (size_t)SK_MAX_BLOCKS * SK_SLA
 int ptk_gemm_sk_flag_count(void) { return SK_MAX_BLOCKS; }
 
 int ptk_gemm_force_small_tiles(int mode) {
-  if (mode != 0 && mode != 1 && mode != 2 && mode != 4 && mode != 8 && mode != 16)
-    return set_error("gemm tile mode %d not in {0, 1, 2, 4, 8, 16}", mode);
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 4 && mode != 8 && mode != 16 && mode != 32)
+    return set_error("gemm tile mode %d not in {0, 1, 2, 4, 8, 16, 32}", mode);
   force_small_tiles(mode);
   return 0;
 }

@@ -763,7 +763,8 @@ static int num_cus() {
 static bool g_timing = false;
 static int g_timing_mask = 0;   // activation classes whose launches are timed
 static int g_force_tiles = 0;   // tests: 1 = every GEMM on 128x128, 2 / 4 = single-batch GEMMs on 256x256 / staggered 256x256,
-                                // 8 = persistent 4-wave kernel, 16 = stream-K wherever scratch is given and tiles > CUs
+                                // 8 = persistent 4-wave kernel, 16 = stream-K wherever scratch is given and tiles > CUs,
+                                // 32 = ping-pong 8-wave kernel wherever it is supported
 void force_small_tiles(int mode) { g_force_tiles = mode; }
 static std::vector<hipEvent_t> g_ev[8];
 static size_t g_ev_used[8];
@@ -865,6 +866,19 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
                         ((act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32)) ||
                          (act == ACT_GELU_TANH && out == OUT_BF16)) &&
                             a.K <= 8192 && w4_round_fill(a.M, a.N) >= 0.8);
+  // ping-pong 8-wave kernel (forced mode 32; PTK_PP=1 puts the w4 shapes on it): bit-identical to the 4-wave
+  // kernel but measured slower on every step shape (gate|up 788 -> 946 us, dh 584 -> 786 us, plain N 1152 /
+  // 1536 / 3072 projections -8..-12 %, tools/pp_probe.sh): its 256x128 tiles fetch 1.5x the bytes per FLOP
+  // and the CU's global -> LDS stream saturates at ~20 B/clk, so it stays a measured alternative
+  static const bool pp_env = [] { const char* e = getenv("PTK_PP"); return e && e[0] == '1'; }();
+  if (batch == 1 && (g_force_tiles == 32 || (pp_env && w4_auto)) && pp_supported(a, act, out)) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
+    if (e0) (void)hipEventRecord(e0, st);
+    const int rc = launch_gemm_pp(a, act, out, st);
+    if (e1) (void)hipEventRecord(e1, st);
+    return rc;
+  }
   if (batch == 1 && (g_force_tiles == 8 || w4_auto) && w4_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }

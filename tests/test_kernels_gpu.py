@@ -448,3 +448,45 @@ def test_qknorm_rope_fwd_bwd(gpu, Hq, Hkv, D):
     cos = torch.nn.functional.cosine_similarity(dqkv.float().flatten(), ref.flatten(), dim=0)
     assert cos > 0.999, cos
     torch.testing.assert_close(dqkv.float(), ref, rtol=3e-2, atol=3e-2)
+
+
+@pytest.mark.parametrize("M,N,K", [(1000, 1024, 1152), (4096, 2304, 640), (2304, 3072, 1024), (513, 896, 1280),
+                                   (22528, 1152, 1152)])
+def test_gemm_pingpong_matches_w4(gpu, M, N, K):
+    """Ping-pong 8-wave kernel (forced mode 32; 256x128 tiles, several per workgroup, ragged M/N) against the
+    persistent 4-wave kernel (mode 8): same k-step order per output element, so every epilogue (plain bf16 /
+    fp32 / fp32-rounded, GEGLU with g, u side outputs, GEGLU backward into the interleaved dg|du layout) is
+    bit-identical; plain fp32 also against torch fp32.  The shapes give 1 to 3 tiles per workgroup (odd and
+    even counts: the last tile's epilogue falls to either wave group)."""
+    Kn, L = _k()
+    A, B = rnd(M, K, dev=gpu, seed=11), rnd(N, K, dev=gpu, seed=12, scale=0.05)
+    gin, uin = rnd(M, N, dev=gpu, seed=13), rnd(M, N, dev=gpu, seed=14)
+    outs = []
+    for md in (8, 32):
+        L.lib().ptk_gemm_force_small_tiles(md)
+        try:
+            o = {"f32": Kn.gemm(A, B, out_dtype=torch.float32), "bf16": Kn.gemm(A, B),
+                 "f32r": Kn.gemm(A, B, C=torch.empty(M, N, device=gpu), out_mode=L.OUT_F32_BF16ROUND)}
+            if N % 32 == 0:
+                g = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=gpu)
+                u = torch.zeros_like(g)
+                o["h"] = Kn.gemm(A, B, act=L.ACT_GEGLU, aux=g, aux2=u)
+                o["g"], o["u"] = g, u
+            o["dgdu"] = Kn.gemm(A, B, act=L.ACT_GEGLU_BWD, aux_in=gin, aux_in2=uin)
+            torch.cuda.synchronize()
+            outs.append(o)
+        finally:
+            L.lib().ptk_gemm_force_small_tiles(0)
+    ref = A.float() @ B.float().T
+    for k in outs[0]:
+        a, b = outs[0][k], outs[1][k]
+        if not torch.equal(a, b):
+            bad = (a != b).nonzero()
+            d = (a.float() - b.float()).abs()
+            msg = (f"{k}: {bad.shape[0]} of {a.numel()} differ, max |d| {d.max().item():.3g}; rows%256 "
+                   f"{sorted(set((bad[:, 0] % 256).tolist()))[:24]} cols%128 {sorted(set((bad[:, 1] % 128).tolist()))[:24]} "
+                   f"first {bad[:4].tolist()}")
+            if k == "f32":
+                msg += (f"; |w4 - ref| {(a - ref).abs().max().item():.3g} |pp - ref| {(b - ref).abs().max().item():.3g}")
+            raise AssertionError(msg)
+    torch.testing.assert_close(outs[1]["f32"], ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
