@@ -284,7 +284,7 @@ def main(argv=None):
     fpi = flops_per_image(cfg)["total"]
     geglu_ms = tot.value / max(cnt.value, 1)
     traffic = None
-    pmc = os.path.join(ROOT, "profiles", "r01_pmc_traffic_geglu.json")
+    pmc = os.path.join(ROOT, "profiles", "r02_pmc_traffic_geglu.json")
     if os.path.exists(pmc) and args.config == "cfg2" and cfg.batch_size == 32 and cfg.text_len == 128:
         traffic = json.load(open(pmc))["traffic_bytes_per_launch"]   # rocprofv3 --pmc passes (tools/pmc_traffic.py)
     # algorithmic FLOPs of every timed gate|up launch / their summed HIP-event time
