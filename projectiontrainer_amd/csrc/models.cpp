@@ -111,7 +111,8 @@ struct GemmaWs {
   std::vector<float*> x;          // L+1 residual-stream snapshots
   std::vector<GemmaLayerSave> L;
   bf16_t *P, *xn, *O, *h, *Vt, *Kt, *Qt, *dqkv, *dgu, *dao, *dO, *dS, *dST, *PT, *dOT, *dQ, *dK, *dV, *xf, *logits;
-  float *S, *dtmp, *rstd_f, *row_loss, *dxf, *dxf_part, *count, *gscale, *delta;
+  bf16_t* dtmp;             // bf16 dX of the q|k|v / gate|up projections (see the workspace layout)
+  float *S, *rstd_f, *row_loss, *dxf, *dxf_part, *count, *gscale, *delta;
   float* dkv_part;          // split-query dK/dV partials of the attention backward
   size_t dkv_part_bytes;
   int32_t* key_valid;
@@ -176,7 +177,10 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
   }
   w.dqkv = bp.take<bf16_t>(M * Dqkv);
   w.dgu = bp.take<bf16_t>(M * 2 * I);
-  w.dtmp = bp.take<float>(M * H);
+  // dX of the q|k|v and gate|up projections, bf16: the reference's autocast linear backward returns a bf16
+  // input grad (upcast to fp32 only where it meets the fp32 norm / residual stream), so the norm backward
+  // passes read bf16 values either way; stored as bf16 it moves half the bytes
+  w.dtmp = bp.take<bf16_t>(M * H);
   w.dao = bp.take<bf16_t>(M * H);
   w.dO = bp.take<bf16_t>(Z * SG * D);
   w.dS = nullptr;
@@ -534,20 +538,20 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
         CK(launch_gemm(g, ACT_GEGLU_BWD, OUT_BF16, 1, st));
       }
       if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, ident, H, M, w.TA, w.TB, GL->wgu, w.skpart, w.sk_floats, st));
-      CK(gemm_split(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), OUT_F32, w.skpart, w.sk_floats, st));
+      CK(gemm_split(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), OUT_BF16, w.skpart, w.sk_floats, st));
     } else {   // last layer: MLP gradient is non-zero on the loss rows only (compact h, g, u, dgu)
       GemmArgs g = gemm(w.dao, H, L.wd_t, H, w.h, I, R, I, H);
       g.amap = lossmap;
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
       CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, R, I, st));
       if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, lossmap, H, R, w.TA, w.TB, GL->wgu, w.skpart, w.sk_floats, st));
-      CKH(hipMemsetAsync(w.dtmp, 0, (size_t)M * H * sizeof(float), st));
+      CKH(hipMemsetAsync(w.dtmp, 0, (size_t)M * H * sizeof(bf16_t), st));
       GemmArgs g2 = gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, R, H, 2 * I);
       g2.cmap = lossmap;
-      CK(launch_gemm(g2, ACT_NONE, OUT_F32, 1, st));
+      CK(launch_gemm(g2, ACT_NONE, OUT_BF16, 1, st));
     }
-    if (train) CK(launch_rms_wgrad(sv.x2, H, ident, sv.rstd_pre, w.dtmp, H, 1, M, H, (bf16_t*)GL->ln_pre_ff, w.wpart, st));
-    CK(launch_residual_norm_bwd(sv.x2, L.ln_pre_ff, sv.rstd_pre, w.dtmp, dR, sv.ao, L.ln_post_attn, sv.rstd_ao, w.dao,
+    if (train) CK(launch_rms_wgrad_bdy(sv.x2, H, ident, sv.rstd_pre, w.dtmp, H, M, H, (bf16_t*)GL->ln_pre_ff, w.wpart, st));
+    CK(launch_residual_norm_bwd_bdn(sv.x2, L.ln_pre_ff, sv.rstd_pre, w.dtmp, dR, sv.ao, L.ln_post_attn, sv.rstd_ao, w.dao,
                                 M, H, st));
     if (train) {
       CK(launch_rms_wgrad_bx(sv.ao, H, ident, sv.rstd_ao, dR, H, 1, M, H, (bf16_t*)GL->ln_post_attn, w.wpart, st));
@@ -583,19 +587,19 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
                              (bf16_t*)GL->k_norm, w.wpart, st));
       CK(weight_grad(w.dqkv, Dqkv, ident, Dqkv, sv.xn_in, H, ident, H, M, w.TA, w.TB, GL->wqkv, w.skpart, w.sk_floats, st));
     }
-    CK(launch_gemm(gemm(w.dqkv, Dqkv, L.wqkv_t, Dqkv, w.dtmp, H, M, H, Dqkv), ACT_NONE, OUT_F32, 1, st));
-    if (train) CK(launch_rms_wgrad(w.x[l], H, ident, sv.rstd_in, w.dtmp, H, 1, M, H, (bf16_t*)GL->ln_in, w.wpart, st));
+    CK(launch_gemm(gemm(w.dqkv, Dqkv, L.wqkv_t, Dqkv, w.dtmp, H, M, H, Dqkv), ACT_NONE, OUT_BF16, 1, st));
+    if (train) CK(launch_rms_wgrad_bdy(w.x[l], H, ident, sv.rstd_in, w.dtmp, H, M, H, (bf16_t*)GL->ln_in, w.wpart, st));
     if (l > 0) {
       // dR += rms_bwd(x_l, ln_in, dtmp), then layer l-1's post-ff norm backward on the new dR -> dao
       const ptk_gemma3_layer& Lp = wt->layers[l - 1];
       const GemmaLayerSave& sp = w.L[l - 1];
-      CK(launch_residual_norm_bwd(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, sp.dn, Lp.ln_post_ff, sp.rstd_dn, w.dao,
+      CK(launch_residual_norm_bwd_bdn(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, sp.dn, Lp.ln_post_ff, sp.rstd_dn, w.dao,
                                   M, H, st));
       if (train)
         CK(launch_rms_wgrad_bx(sp.dn, H, ident, sp.rstd_dn, dR, H, 1, M, H, (bf16_t*)gr->layers[l - 1].ln_post_ff,
                                w.wpart, st));
     } else {
-      CK(launch_rmsnorm_bwd_f32(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, dR, M, H, st));
+      CK(launch_rmsnorm_bwd_bdn(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, dR, M, H, st));
     }
   }
   // input-embedding grads of every text token (tied with the lm_head grad above)

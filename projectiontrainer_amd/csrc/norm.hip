@@ -133,19 +133,31 @@ __global__ void __launch_bounds__(256) residual_norm_fwd_kernel(
     }                                                                         \
   }
 
-template <int NV>
-__global__ void __launch_bounds__(256) rmsnorm_bwd_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
-                                                              const float* __restrict__ rstd, const float* __restrict__ dn,
-                                                              const float* dacc, float* dx, long rows, int cols) {
+template <typename TD, int NV>
+PTK_DEV void rmsnorm_bwd_body(const float* __restrict__ x, const float* __restrict__ w, const float* __restrict__ rstd,
+                              const TD* __restrict__ dn, const float* dacc, float* dx, long rows, int cols) {
   ROW_SETUP
   float4 xv[NV], dv[NV];
 #pragma unroll
-  FOR_V { xv[v] = ld4(x + row * cols + COL); dv[v] = ld4(dn + row * cols + COL); }
+  FOR_V { xv[v] = ld4(x + row * cols + COL); dv[v] = ldx4(dn + row * cols + COL); }
   const float rs = rstd[row];
   RMS_BWD_BODY(xv, dv, rs, {
     float4 o = dacc ? add4(ld4(dacc + row * cols + COL), dxv) : dxv;
     st4(dx + row * cols + COL, o);
   })
+}
+template <int NV>
+__global__ void __launch_bounds__(256) rmsnorm_bwd_f32_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                              const float* __restrict__ rstd, const float* __restrict__ dn,
+                                                              const float* dacc, float* dx, long rows, int cols) {
+  rmsnorm_bwd_body<float, NV>(x, w, rstd, dn, dacc, dx, rows, cols);
+}
+// dn in bf16: the output grad of a bf16 linear (the reference's autocast linear backward returns bf16)
+template <int NV>
+__global__ void __launch_bounds__(256) rmsnorm_bwd_bdn_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                              const float* __restrict__ rstd, const bf16_t* __restrict__ dn,
+                                                              const float* dacc, float* dx, long rows, int cols) {
+  rmsnorm_bwd_body<bf16_t, NV>(x, w, rstd, dn, dacc, dx, rows, cols);
 }
 
 template <int NV>
@@ -174,10 +186,10 @@ PTK_DEV void post_norm_bwd_row(const float* dR, const bf16_t* t, const float* w,
   RMS_BWD_BODY(xv, dv, rs, { st4bf(dt + COL, dxv); })
 }
 
-template <int NV>
-__global__ void __launch_bounds__(256) residual_norm_bwd_kernel(
+template <typename TD, int NV>
+PTK_DEV void residual_norm_bwd_body(
     const float* __restrict__ x2, const float* __restrict__ w_pre, const float* __restrict__ rstd_pre,
-    const float* __restrict__ dn, float* __restrict__ dR, const bf16_t* __restrict__ t,
+    const TD* __restrict__ dn, float* __restrict__ dR, const bf16_t* __restrict__ t,
     const float* __restrict__ w_post, const float* __restrict__ rstd_t, bf16_t* __restrict__ dt, long rows,
     int cols) {
   ROW_SETUP
@@ -186,7 +198,7 @@ __global__ void __launch_bounds__(256) residual_norm_bwd_kernel(
     const float* w = w_pre;
     float4 xv[NV], dv[NV];
 #pragma unroll
-    FOR_V { xv[v] = ld4(x2 + row * cols + COL); dv[v] = ld4(dn + row * cols + COL); }
+    FOR_V { xv[v] = ld4(x2 + row * cols + COL); dv[v] = ldx4(dn + row * cols + COL); }
     const float rs = rstd_pre[row];
     RMS_BWD_BODY(xv, dv, rs, {
       nd[v] = add4(ld4(dR + row * cols + COL), dxv);
@@ -201,6 +213,22 @@ __global__ void __launch_bounds__(256) residual_norm_bwd_kernel(
     FOR_V { xv[v] = ld4bf(t + row * cols + COL); dv[v] = bfr4(nd[v]); }
     RMS_BWD_BODY(xv, dv, rs, { st4bf(dt + row * cols + COL, dxv); })
   }
+}
+template <int NV>
+__global__ void __launch_bounds__(256) residual_norm_bwd_kernel(
+    const float* __restrict__ x2, const float* __restrict__ w_pre, const float* __restrict__ rstd_pre,
+    const float* __restrict__ dn, float* __restrict__ dR, const bf16_t* __restrict__ t,
+    const float* __restrict__ w_post, const float* __restrict__ rstd_t, bf16_t* __restrict__ dt, long rows,
+    int cols) {
+  residual_norm_bwd_body<float, NV>(x2, w_pre, rstd_pre, dn, dR, t, w_post, rstd_t, dt, rows, cols);
+}
+template <int NV>
+__global__ void __launch_bounds__(256) residual_norm_bwd_bdn_kernel(
+    const float* __restrict__ x2, const float* __restrict__ w_pre, const float* __restrict__ rstd_pre,
+    const bf16_t* __restrict__ dn, float* __restrict__ dR, const bf16_t* __restrict__ t,
+    const float* __restrict__ w_post, const float* __restrict__ rstd_t, bf16_t* __restrict__ dt, long rows,
+    int cols) {
+  residual_norm_bwd_body<bf16_t, NV>(x2, w_pre, rstd_pre, dn, dR, t, w_post, rstd_t, dt, rows, cols);
 }
 
 template <int NV>
@@ -267,6 +295,21 @@ int launch_rmsnorm_bwd_f32(const float* x, const float* w, const float* rstd, co
   if (rows <= 0) return 0;
   NORM_DISPATCH(rmsnorm_bwd_f32_kernel, x, w, rstd, dn, dacc, dx, (long)rows, cols);
   RET_LAUNCH("rmsnorm_bwd");
+}
+int launch_rmsnorm_bwd_bdn(const float* x, const float* w, const float* rstd, const bf16_t* dn, const float* dacc,
+                           float* dx, int rows, int cols, hipStream_t st) {
+  if (check_cols(cols)) return -1;
+  if (rows <= 0) return 0;
+  NORM_DISPATCH(rmsnorm_bwd_bdn_kernel, x, w, rstd, dn, dacc, dx, (long)rows, cols);
+  RET_LAUNCH("rmsnorm_bwd_bdn");
+}
+int launch_residual_norm_bwd_bdn(const float* x2, const float* w_pre, const float* rstd_pre, const bf16_t* dn,
+                                 float* dR, const bf16_t* t, const float* w_post, const float* rstd_t, bf16_t* dt,
+                                 int rows, int cols, hipStream_t st) {
+  if (check_cols(cols)) return -1;
+  if (rows <= 0) return 0;
+  NORM_DISPATCH(residual_norm_bwd_bdn_kernel, x2, w_pre, rstd_pre, dn, dR, t, w_post, rstd_t, dt, (long)rows, cols);
+  RET_LAUNCH("residual_norm_bwd_bdn");
 }
 int launch_rmsnorm_bwd_scatter(const float* x, RowMap xmap, const float* w, const float* rstd, const float* dn,
                                float* dR, int rows, int cols, hipStream_t st) {

@@ -97,6 +97,12 @@ int launch_residual_norm_bwd(const float* x2, const float* w_pre, const float* r
 int launch_post_norm_bwd(const float* dR, const bf16_t* t, const float* w, const float* rstd_t, bf16_t* dt,
                          int rows, int cols, hipStream_t st);
 // final norm backward on gathered rows, scatter-add into dR rows given by map
+// the same two backward passes reading a bf16 dn (the bf16 output grad of the dX GEMMs)
+int launch_rmsnorm_bwd_bdn(const float* x, const float* w, const float* rstd, const bf16_t* dn, const float* dacc,
+                           float* dx, int rows, int cols, hipStream_t st);
+int launch_residual_norm_bwd_bdn(const float* x2, const float* w_pre, const float* rstd_pre, const bf16_t* dn,
+                                 float* dR, const bf16_t* t, const float* w_post, const float* rstd_t, bf16_t* dt,
+                                 int rows, int cols, hipStream_t st);
 int launch_rmsnorm_bwd_scatter(const float* x, RowMap xmap, const float* w, const float* rstd,
                                const float* dn, float* dR, int rows, int cols, hipStream_t st);
 
@@ -249,6 +255,8 @@ int launch_rms_wgrad(const float* x, long ldx, RowMap xmap, const float* rstd, c
                      int dy_round, int rows, int cols, bf16_t* grad, float* partial, hipStream_t st);
 int launch_rms_wgrad_bx(const bf16_t* x, long ldx, RowMap xmap, const float* rstd, const float* dy, long lddy,
                         int dy_round, int rows, int cols, bf16_t* grad, float* partial, hipStream_t st);
+int launch_rms_wgrad_bdy(const float* x, long ldx, RowMap xmap, const float* rstd, const bf16_t* dy, long lddy,
+                         int rows, int cols, bf16_t* grad, float* partial, hipStream_t st);
 // q_norm / k_norm weight grads from the attention-layout dQ / dK (partial >= 2 * ceil(B*S/64) * D floats)
 int launch_qknorm_wgrad(const bf16_t* qkv, const float* cos_t, const float* sin_t, AttnShape s, const float* rstd_q,
                         const float* rstd_k, const bf16_t* dQ, const bf16_t* dK, bf16_t* gq, bf16_t* gk,

@@ -192,6 +192,10 @@ int launch_rms_wgrad_bx(const bf16_t* x, long ldx, RowMap xmap, const float* rst
                         int dy_round, int rows, int cols, bf16_t* grad, float* partial, hipStream_t st) {
   return rms_wgrad_t<bf16_t, float>(x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, grad, partial, st);
 }
+int launch_rms_wgrad_bdy(const float* x, long ldx, RowMap xmap, const float* rstd, const bf16_t* dy, long lddy,
+                         int rows, int cols, bf16_t* grad, float* partial, hipStream_t st) {
+  return rms_wgrad_t<float, bf16_t>(x, ldx, xmap, rstd, dy, lddy, 0, rows, cols, grad, partial, st);
+}
 
 // ---------------------------------------------------------------- q_norm / k_norm weight grads
 // For every (token row, head): dn = RoPE^T(dr) (dr = grad of the rotated, normed head), x_hat = x * rstd;

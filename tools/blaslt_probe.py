@@ -16,7 +16,7 @@ SHAPES = [  # name, M, N, K, out dtype
     ("s1_qkv", M1, 1536, 1152, torch.bfloat16), ("s1_o", M1, 1152, 1024, torch.bfloat16),
     ("s1_down", M1, 1152, 6912, torch.bfloat16), ("s1_dX_gateup", M1, 1152, 13824, torch.float32),
     ("s1_dO", M1, 1024, 1152, torch.bfloat16), ("s1_dX_qkv", M1, 1152, 1536, torch.float32),
-    ("lm_head", 4096, 262144, 1152, torch.bfloat16),
+    ("lm_head", 4096, 262144, 1152, torch.bfloat16), ("s1_dX_lmhead", 4096, 1152, 262144, torch.float32),
     ("s2_qkv", M2, 1536, 1152, torch.bfloat16), ("s2_down", M2, 1152, 6912, torch.bfloat16),
     ("s2_dX_gateup", M2, 1152, 13824, torch.float32), ("s2_o", M2, 1152, 1024, torch.bfloat16),
     ("s2_dO", M2, 1024, 1152, torch.bfloat16), ("s2_dX_qkv", M2, 1152, 1536, torch.float32),
@@ -25,7 +25,10 @@ SHAPES = [  # name, M, N, K, out dtype
     ("dW_lmhead", 262144, 1152, 4096, torch.float32),
 ]
 tag = {"1": "blaslt", "0": "mfma"}.get(os.environ.get("PTK_BLASLT"), "rule")
+only = set(sys.argv[1:])
 for name, m, n, k, odt in SHAPES:
+    if only and name not in only:
+        continue
     A = torch.randn(m, k, device=dev).to(torch.bfloat16)
     B = (torch.randn(n, k, device=dev) * 0.05).to(torch.bfloat16)
     C = K.gemm(A, B, out_dtype=odt)
