@@ -17,6 +17,7 @@ SHAPES = [  # name, M, N, K, out dtype
     ("s1_down", M1, 1152, 6912, torch.bfloat16), ("s1_dX_gateup", M1, 1152, 13824, torch.float32),
     ("s1_dO", M1, 1024, 1152, torch.bfloat16), ("s1_dX_qkv", M1, 1152, 1536, torch.float32),
     ("lm_head", 4096, 262144, 1152, torch.bfloat16), ("s1_dX_lmhead", 4096, 1152, 262144, torch.float32),
+    ("s1_dX_qkv_b16", M1, 1152, 1536, torch.bfloat16), ("s1_dX_gateup_b16", M1, 1152, 13824, torch.bfloat16),
     ("s2_qkv", M2, 1536, 1152, torch.bfloat16), ("s2_down", M2, 1152, 6912, torch.bfloat16),
     ("s2_dX_gateup", M2, 1152, 13824, torch.float32), ("s2_o", M2, 1152, 1024, torch.bfloat16),
     ("s2_dO", M2, 1024, 1152, torch.bfloat16), ("s2_dX_qkv", M2, 1152, 1536, torch.float32),
