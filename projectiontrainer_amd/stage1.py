@@ -73,6 +73,9 @@ class Stage1Engine:
         self.vstream = None        # side stream of the vision prefetch
         self._prefetched = None    # event: the current buffer's features were computed ahead
         self._vision_ready = False  # encode_vision ran this step's tower on the main stream
+        self._graph = None         # graph_step: captured forward_backward, its input key and static inputs
+        self._graph_key = None
+        self._graph_in = None
 
     def _buffers(self, B, T):
         """Step buffers are allocated for the largest batch seen at this text length; a smaller batch
@@ -169,9 +172,10 @@ class Stage1Engine:
         L.check(L.lib().ptk_gather_vision_grad(self.dx.data_ptr(), B, self.N, self.Sp, self.llm.cfg.hidden_size,
                                                self.dy.data_ptr(), L.stream_ptr(self.device)), "gather_vision_grad")
         self.proj.bwd_into(self.vis, self.a, self.h, self.dy, self.proj_ws)
-        rel = torch.cuda.Event()
-        rel.record(main)
-        self._released[i] = rel
+        if not torch.cuda.is_current_stream_capturing():   # (graph_step never prefetches)
+            rel = torch.cuda.Event()
+            rel.record(main)
+            self._released[i] = rel
         return self.loss
 
     def encode_vision(self, pixel_values, token_ids):
@@ -210,6 +214,31 @@ class Stage1Engine:
         loss = self.forward_backward(pixel_values, token_ids, labels, next_pixel_values)
         self.optimizer_step()
         return loss
+
+    def graph_step(self, pixel_values, token_ids, labels):
+        """step() with forward_backward replayed from a HIP graph.  The ~900 kernel launches of the SigLIP,
+        projector and Gemma3 passes are captured once per input shape and then replayed as one launch: at a
+        small batch (cfg1: bs 2) the step is bound by launch latency, not by the kernels.  Capture needs every
+        lazy initialisation (hipBLASLt plans and workspace, step buffers) done, so at least one eager step()
+        at this shape must precede the first call.  Inputs are copied into static buffers that the graph reads.
+        The optimizer step stays eager: its learning rate and step count are kernel arguments that change every
+        step (and the DDP all-reduce runs there).  Same kernels in the same order: bit-identical to step()."""
+        key = (tuple(pixel_values.shape), pixel_values.dtype, tuple(token_ids.shape), tuple(labels.shape))
+        if self._prefetched is not None or self._vision_ready:
+            raise RuntimeError("Stage1Engine.graph_step: a vision prefetch / encode_vision is pending")
+        if self._graph is None or self._graph_key != key:
+            self._graph = None
+            static = (pixel_values.clone(), token_ids.clone(), labels.clone())
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):      # capture only: nothing runs until replay
+                self.forward_backward(*static)
+            self._graph, self._graph_key, self._graph_in = g, key, static
+        else:
+            for dst, src in zip(self._graph_in, (pixel_values, token_ids, labels)):
+                dst.copy_(src)
+        self._graph.replay()
+        self.optimizer_step()
+        return self.loss
 
     # ---------------------------------------------------------------- builders
     @classmethod

@@ -1,0 +1,43 @@
+"""Stage1Engine.graph_step (forward_backward replayed from a HIP graph) against step() (eager launches):
+same kernels in the same order, so loss, projector grads and post-AdamW parameters must be bit-identical
+over several steps with a new batch each step (the graph reads its inputs from static buffers)."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(cfg, dev):
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.gemma3 import Gemma3CausalLM
+    from projectiontrainer_amd.projectors import MLPProjector
+    from projectiontrainer_amd.siglip import SiglipVisionTower
+    from projectiontrainer_amd.stage1 import Stage1Engine
+    vp, lp = W.siglip_vision_params(cfg.vision), W.gemma3_params(cfg.text)
+    pp = W.projector_params(cfg.vision.hidden_size, cfg.text.hidden_size)
+    proj = MLPProjector(cfg.vision.hidden_size, cfg.text.hidden_size)
+    proj.load_state_dict({k: torch.from_numpy(v) for k, v in pp.items()})
+    proj.to(dev)
+    return Stage1Engine(SiglipVisionTower(cfg.vision, vp, dev),
+                        Gemma3CausalLM(cfg.text, lp, dev, max_pos=Gemma3CausalLM.seq_pad(cfg.seq_len)), proj,
+                        total_steps=100)
+
+
+@pytest.mark.parametrize("preset", ["tiny", "tiny_gqa"])
+def test_graph_step_bit_identical_to_eager(gpu, preset):
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    cfg = PRESETS[preset]
+    batches = []
+    for seed in range(4):
+        px, ids, labels = W.synthetic_batch(cfg, seed=20 + seed)
+        batches.append(tuple(torch.from_numpy(a).to(gpu) for a in (px, ids, labels)))
+    eager, graphed = _engine(cfg, gpu), _engine(cfg, gpu)
+    for k, b in enumerate(batches):
+        le = float(eager.step(*b))
+        lg = float(graphed.step(*b) if k == 0 else graphed.graph_step(*b))   # one eager step before capture
+        torch.cuda.synchronize()
+        assert le == lg, (k, le, lg)
+        assert torch.equal(eager.proj.flat_grad, graphed.proj.flat_grad), k
+        assert torch.equal(eager.proj.flat, graphed.proj.flat), k
+    assert graphed._graph is not None
