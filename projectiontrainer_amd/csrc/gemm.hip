@@ -868,8 +868,9 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
                             a.K <= 8192 && w4_round_fill(a.M, a.N) >= 0.8);
   // ping-pong 8-wave kernel (forced mode 32; PTK_PP=1 puts the w4 shapes on it): bit-identical to the 4-wave
   // kernel but measured slower on every step shape (gate|up 788 -> 946 us, dh 584 -> 786 us, plain N 1152 /
-  // 1536 / 3072 projections -8..-12 %, tools/pp_probe.sh): its 256x128 tiles fetch 1.5x the bytes per FLOP
-  // and the CU's global -> LDS stream saturates at ~20 B/clk, so it stays a measured alternative
+  // 1536 / 3072 projections -8..-12 %, tools/pp_probe.sh): its producer waves' instruction stream, sharing
+  // each SIMD's issue with the consumer's MFMAs, sets the k-step time, so it stays a measured
+  // alternative
   static const bool pp_env = [] { const char* e = getenv("PTK_PP"); return e && e[0] == '1'; }();
   if (batch == 1 && (g_force_tiles == 32 || (pp_env && w4_auto)) && pp_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
