@@ -560,6 +560,8 @@ static int num_cu() {
   return g_num_cu;
 }
 
+int device_cus() { return num_cu(); }
+
 double w4_round_fill(long M, long N) {
   const long ntile = ((M + W4 - 1) / W4) * ((N + W4 - 1) / W4), cu = num_cu();
   return (double)ntile / (double)(((ntile + cu - 1) / cu) * cu);

@@ -222,10 +222,17 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
 // 128x128 kernel as fp32 partials [S][M][N]; one pass sums them in slice order (deterministic).
 int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStream_t st) {
   const long nbig = (long)((a.M + 255) / 256) * ((a.N + 255) / 256);
-  int S = 1;
+  int S = 1, kmin = 1024;
   if (a.K >= 4096 && nbig <= 64) S = 4;
   else if (a.K >= 4096 && nbig <= 300) S = 2;
-  while (S > 1 && ((long)S * a.M * a.N > part_floats || a.K / S < 1024 || a.N % 4 || a.ldc % 4)) S /= 2;
+  // small M (cfg1, bs 2: M = 520): the 128x128 tile grid alone leaves most CUs idle, so split K until
+  // the slices fill about two blocks per CU (slices >= 256 deep)
+  const long n128 = (long)((a.M + 127) / 128) * ((a.N + 127) / 128), cus = device_cus();
+  if (n128 * 2 <= cus) {
+    kmin = 256;
+    while (n128 * S * 2 <= 2 * cus && a.K / (S * 2) >= kmin) S *= 2;
+  }
+  while (S > 1 && ((long)S * a.M * a.N > part_floats || a.K / S < kmin || a.N % 4 || a.ldc % 4)) S /= 2;
   const bool plain = !a.rowadd && !a.resid && !a.aux && !a.aux_in && a.amap.g == 0 && a.amap.off == 0 &&
                      a.cmap.g == 0 && a.cmap.off == 0 && a.bias == nullptr && a.alpha == 1.f;
   // few-tile weight grads (dW_qkv, dW_o: <= 64 tiles) split 4 ways on the MFMA kernels beat hipBLASLt
@@ -429,7 +436,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
     bf16_t* xin = train ? sv.xn_in : w.xn;
     bf16_t* xff = train ? sv.xn_ff : w.xn;
     bf16_t* hh = train ? sv.h : w.h;
-    CK(launch_gemm(gemm(xin, H, L.wqkv, H, sv.qkv, Dqkv, M, Dqkv, H), ACT_NONE, OUT_BF16, 1, st));
+    CK(gemm_split(gemm(xin, H, L.wqkv, H, sv.qkv, Dqkv, M, Dqkv, H), OUT_BF16, w.skpart, w.sk_floats, st));
     CK(launch_qknorm_rope_fwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, eps, sv.Q, sv.K, sv.V, sv.rstd_q, sv.rstd_k,
                               st));
     {  // causal / sliding-window GQA attention, flash; O token-major, LSE kept for the backward
@@ -447,7 +454,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
       fa.scale = scale;
       CK(launch_attn_fwd(fa, Z, st));
     }
-    CK(launch_gemm(gemm(sv.O, Dq, L.wo, Dq, sv.ao, H, M, H, Dq), ACT_NONE, OUT_BF16, 1, st));
+    CK(gemm_split(gemm(sv.O, Dq, L.wo, Dq, sv.ao, H, M, H, Dq), OUT_BF16, w.skpart, w.sk_floats, st));
     CK(launch_residual_norm_fwd(sv.ao, w.x[l], L.ln_post_attn, L.ln_pre_ff, sv.x2, xff, sv.rstd_ao, sv.rstd_pre, M,
                                 H, eps, st));
     if (l + 1 < nl) {
@@ -587,7 +594,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
                              (bf16_t*)GL->k_norm, w.wpart, st));
       CK(weight_grad(w.dqkv, Dqkv, ident, Dqkv, sv.xn_in, H, ident, H, M, w.TA, w.TB, GL->wqkv, w.skpart, w.sk_floats, st));
     }
-    CK(launch_gemm(gemm(w.dqkv, Dqkv, L.wqkv_t, Dqkv, w.dtmp, H, M, H, Dqkv), ACT_NONE, OUT_BF16, 1, st));
+    CK(gemm_split(gemm(w.dqkv, Dqkv, L.wqkv_t, Dqkv, w.dtmp, H, M, H, Dqkv), OUT_BF16, w.skpart, w.sk_floats, st));
     if (train) CK(launch_rms_wgrad_bdy(w.x[l], H, ident, sv.rstd_in, w.dtmp, H, M, H, (bf16_t*)GL->ln_in, w.wpart, st));
     if (l > 0) {
       // dR += rms_bwd(x_l, ln_in, dtmp), then layer l-1's post-ff norm backward on the new dR -> dao

@@ -64,6 +64,7 @@ bool w4_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid);
 // fraction of the persistent grid's tile rounds that hold work: ntile / (ceil(ntile / CUs) * CUs)
 double w4_round_fill(long M, long N);
+int device_cus();   // compute units of the current device (cached)
 // ping-pong 8-wave variant (gemm_w4.hip): two wave groups alternate K loop and epilogue on 256x128 tiles
 bool pp_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_pp(const GemmArgs& a, int act, int out, hipStream_t st);
