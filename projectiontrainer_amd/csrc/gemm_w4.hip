@@ -846,24 +846,27 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_
   } while (0)
 
   // consumer k-step: 8 groups of 4 MFMAs (row block q x column blocks 0..3).  With RD the next k-step's
-  // fragments (slot rslot) are read: B block q (q < 4) into NB before group q, A block q into fa[q] right
-  // after group q.  Issue order of one step's reads: B0 A0 B1 A1 B2 A2 B3 A3 A4 .. A7 (DS reads complete in
-  // order), so before group q of the next step lgkmcnt(n_q) leaves exactly the younger reads in flight:
-  // n_0 = 5 (B3 and older landed), n_1..3 = 10, n_4..7 = 11.
+  // fragments (slot rslot) are read: B block q (q < 4) into NB before group q, A block q into fa[q] one group
+  // after group q (A7 after the last group), so no read overwrites a register an MFMA just issued still
+  // reads.  Issue order of one step's reads: B0 B1 A0 B2 A1 B3 A2 A3 .. A7 (DS reads complete in order), so
+  // before group q of the next step lgkmcnt(n_q) leaves exactly the younger reads in flight: n_0 = 6 (B3 and
+  // older landed), n_1 = n_2 = 8, n_3 = 9, n_4..7 = 10.
   auto cstep = [&](auto first_c, auto read_c, bf16x8_t (&FB)[4], bf16x8_t (&NB)[4]) __attribute__((always_inline)) {
     constexpr bool first = decltype(first_c)::value, rd = decltype(read_c)::value;
     const uint32_t ba = frag_a + rslot, bb = frag_b + rslot;
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      if (q == 0) asm volatile("s_waitcnt lgkmcnt(5)" ::: "memory");
-      else if (q < 4) asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory");
-      else asm volatile("s_waitcnt lgkmcnt(11)" ::: "memory");
+      if (q == 0) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
+      else if (q < 3) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
+      else if (q == 3) asm volatile("s_waitcnt lgkmcnt(9)" ::: "memory");
+      else asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory");
       asm volatile("" : "+v"(fa[q]));
       if (q == 0) asm volatile("" : "+v"(FB[0]), "+v"(FB[1]), "+v"(FB[2]), "+v"(FB[3]));
       if (rd && q < 4) W4_DSREAD(NB[q], bb, q * 1024);
       PP_GROUP(FB, q, first);
-      if (rd) W4_DSREAD(fa[q], ba, q * 1024);
+      if (rd && q >= 1) W4_DSREAD(fa[q - 1], ba, (q - 1) * 1024);   // one group after its last reader
     }
+    if (rd) W4_DSREAD(fa[7], ba, 7 * 1024);
   };
   // all 12 fragments of position s+1 (the producer's last step: its next tile's first k-step)
   auto read_frags = [&](bf16x8_t (&NB)[4]) __attribute__((always_inline)) {
