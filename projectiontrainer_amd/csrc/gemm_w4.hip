@@ -34,6 +34,10 @@
 #ifndef PTK_W4_DMS
 #define PTK_W4_DMS 0      // diagnostic builds: DMA placement (1 = groups 8..15, 2 = groups 0..7, 3 = odd groups)
 #endif
+#ifndef PTK_PP_ABLATE
+#define PTK_PP_ABLATE 0   // diagnostic builds of the ping-pong kernel (make ppablate): 1 = no per-step barrier,
+                          // 2 = no DMA landing waits (wrong results by construction, timing only)
+#endif
 #ifndef PTK_W4_ABLATE
 #define PTK_W4_ABLATE 0   // diagnostic builds only: 1 = no DMA in the K loop, 2 = no fragment reads,
                           // 3 = the DMA re-reads one L2-resident K-tile, 4 = no K-loop barrier,
@@ -820,12 +824,16 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_
   uint32_t rslot = 0;             // ring slot of position s+1 (fragments read during step s)
   // end of step s: the issuer of position s+2 waits for it, then one barrier publishes it
   auto end_step = [&]() __attribute__((always_inline)) {
+#if PTK_PP_ABLATE != 2
     if (mk2 >= 0) pp_vm_wait(issued - mk2);
+#endif
     mk2 = mk3;
     mk3 = mk4;
     mk4 = mk5;
     rslot = rslot == (PP_NS - 1) * PP_SLOT ? 0u : rslot + PP_SLOT;
+#if PTK_PP_ABLATE != 1
     __builtin_amdgcn_s_barrier();
+#endif
   };
 
   // ---- fragments: A rows wr*128 + 16i + (lane&15), B rows wc*64 + 16j + (lane&15), logical chunk lane>>4
