@@ -629,17 +629,20 @@ constexpr int PP_EPI = 18;                 // producer steps that carry epilogue
 constexpr int PP_MIN_KS = 20;              // K >= 640
 template <int N> using pp_ic = std::integral_constant<int, N>;
 
-// s_waitcnt vmcnt(n) for a wave-uniform runtime n (n > 63 waits for more than needed: safe)
+// s_waitcnt vmcnt(n') with n' = n rounded down to a multiple of 6 (one step's DMA pieces), capped at 42:
+// waiting for a few more of the younger operations than needed is safe, and a 7-way compare chain keeps
+// the many inlined copies small (a 64-way jump table per copy made the kernel ~4x the 4-wave kernel's
+// code, and the code size itself cost 5-10 % of the ping-pong kernel's time)
 PTK_DEV void pp_vm_wait(int n) {
-  switch (n) {
-#define PP_VMW(k) case k: asm volatile("s_waitcnt vmcnt(" #k ")" ::: "memory"); break;
-    PP_VMW(0) PP_VMW(1) PP_VMW(2) PP_VMW(3) PP_VMW(4) PP_VMW(5) PP_VMW(6) PP_VMW(7) PP_VMW(8) PP_VMW(9) PP_VMW(10) PP_VMW(11) PP_VMW(12) PP_VMW(13) PP_VMW(14) PP_VMW(15) PP_VMW(16) PP_VMW(17) PP_VMW(18) PP_VMW(19) PP_VMW(20) PP_VMW(21) PP_VMW(22) PP_VMW(23) PP_VMW(24) PP_VMW(25) PP_VMW(26) PP_VMW(27) PP_VMW(28) PP_VMW(29) PP_VMW(30) PP_VMW(31) PP_VMW(32) PP_VMW(33) PP_VMW(34) PP_VMW(35) PP_VMW(36) PP_VMW(37) PP_VMW(38) PP_VMW(39) PP_VMW(40) PP_VMW(41) PP_VMW(42) PP_VMW(43) PP_VMW(44) PP_VMW(45) PP_VMW(46) PP_VMW(47) PP_VMW(48) PP_VMW(49) PP_VMW(50) PP_VMW(51) PP_VMW(52) PP_VMW(53) PP_VMW(54) PP_VMW(55) PP_VMW(56) PP_VMW(57) PP_VMW(58) PP_VMW(59) PP_VMW(60) PP_VMW(61) PP_VMW(62)
-#undef PP_VMW
-    default: asm volatile("s_waitcnt vmcnt(63)" ::: "memory"); break;
-  }
+  if (n >= 42) asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
+  else if (n >= 36) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
+  else if (n >= 30) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
+  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+  else if (n >= 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
+  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
+  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
 }
-// (s_nop 1: a VALU write of a >8-byte store's data VGPRs right after the store would corrupt the stored data;
-// hipcc's hazard recognizer does not cover stores issued from inline asm)
 #define PP_ST(ADDR, V) asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" :: "v"(ADDR), "v"(V) : "memory")
 #define PP_LD(DST, ADDR) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(DST) : "v"(ADDR) : "memory")
 
