@@ -755,6 +755,12 @@ PTK_DEV void pp_gbwd_load(const GemmArgs& p, long row0, long col0, int lane, bf1
 }
 }  // namespace
 
+#ifdef PTK_PP_STAMPS
+// diagnostic build only (make ppstamps): per wave, s_memtime cycles between barriers ("work": the consumer's
+// MFMA step or the producer's DMA + epilogue chunk) and inside end_step ("wait": landing wait + barrier),
+// per role, and the step counts
+__device__ unsigned long long g_pp_stamps[1024][8][6];
+#endif
 template <int ACT, int OUT>
 __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
   __shared__ __attribute__((aligned(16))) char smem[PP_NS * PP_SLOT];
@@ -826,7 +832,15 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_
   };
   uint32_t rslot = 0;             // ring slot of position s+1 (fragments read during step s)
   // end of step s: the issuer of position s+2 waits for it, then one barrier publishes it
+#ifdef PTK_PP_STAMPS
+  unsigned long long st_acc[2][2] = {{0, 0}, {0, 0}}, st_n[2] = {0, 0};
+  unsigned long long st_last = __builtin_amdgcn_s_memtime();
+  int st_role = 0;
+#endif
   auto end_step = [&]() __attribute__((always_inline)) {
+#ifdef PTK_PP_STAMPS
+    const unsigned long long st_a = __builtin_amdgcn_s_memtime();
+#endif
 #if PTK_PP_ABLATE != 2
     if (mk2 >= 0) pp_vm_wait(issued - mk2);
 #endif
@@ -836,6 +850,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_
     rslot = rslot == (PP_NS - 1) * PP_SLOT ? 0u : rslot + PP_SLOT;
 #if PTK_PP_ABLATE != 1
     __builtin_amdgcn_s_barrier();
+#endif
+#ifdef PTK_PP_STAMPS
+    const unsigned long long st_b = __builtin_amdgcn_s_memtime();
+    st_acc[st_role][0] += st_a - st_last;
+    st_acc[st_role][1] += st_b - st_a;
+    st_n[st_role] += 1;
+    st_last = st_b;
 #endif
   };
 
@@ -956,6 +977,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_
   for (int j = 0; j < ntw; ++j) {
     if ((j & 1) == grp) {
       // ---- consumer phase: tile j's K loop
+#ifdef PTK_PP_STAMPS
+      st_role = 0;
+#endif
       cstep(std::true_type{}, std::true_type{}, fb0, fb1);
       dma_step(false);
       end_step();
@@ -972,6 +996,9 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_
       end_step();
     } else {
       // ---- producer phase: the stream 5 k-steps ahead; tile j-1's epilogue (this wave's own tile)
+#ifdef PTK_PP_STAMPS
+      st_role = 1;
+#endif
       const bool drain = j >= 1;
       if (drain) epi_tile(j - 1);
       auto pstep = [&](auto ks_c) __attribute__((always_inline)) {
@@ -1007,6 +1034,13 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_
     last_rows(pp_ic<4>{}); last_rows(pp_ic<5>{}); last_rows(pp_ic<6>{}); last_rows(pp_ic<7>{});
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup exits
+#ifdef PTK_PP_STAMPS
+  if (lane == 0 && blockIdx.x < 1024) {
+    unsigned long long* o = g_pp_stamps[blockIdx.x][wave];
+    o[0] = st_acc[0][0]; o[1] = st_acc[0][1]; o[2] = st_n[0];
+    o[3] = st_acc[1][0]; o[4] = st_acc[1][1]; o[5] = st_n[1];
+  }
+#endif
 #undef PP_GROUP
 }
 
@@ -1019,6 +1053,11 @@ bool pp_supported(const GemmArgs& a, int act, int out) {
   return act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32 || out == OUT_F32_BFR);
 }
 
+#ifdef PTK_PP_STAMPS
+extern "C" int ptk_debug_pp_stamps_read(void* host, size_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pp_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif
 int launch_gemm_pp(const GemmArgs& a, int act, int out, hipStream_t st) {
   num_cu();
   const long ntile = (long)((a.M + PP_BM - 1) / PP_BM) * ((a.N + PP_BN - 1) / PP_BN);
