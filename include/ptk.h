@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTK_ABI_VERSION 2
+#define PTK_ABI_VERSION 3
 
 int ptk_abi_version(void);
 const char* ptk_last_error(void);
@@ -125,8 +125,13 @@ int ptk_gemm_timer_enable(int on);   /* 0 off, 1 every class, (1 << 8) | class m
    8 = every single-batch GEMM the persistent 4-wave 256x256 kernel supports on it. */
 int ptk_gemm_force_small_tiles(int mode);   /* tests: 0 auto, 1 128x128, 2 256x256, 4 staggered 256x256,
                                               8 persistent 4-wave, 16 stream-K (needs desc scratch),
-                                              32 ping-pong 8-wave (256x128 tiles) */
+                                              32 persistent 8-wave (two waves per SIMD) */
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
+/* Dispatch census (tests): counts[path * 8 + act] = GEMM launches since the last reset per kernel family
+ * (0 128x128, 1 256x256 8-wave, 2 staggered 256x256 8-wave, 3 persistent 4-wave, 4 ping-pong,
+ * 5 stream-K, 6 persistent 8-wave, 7 token-major weight grad) and epilogue class (PTK_ACT_*); counts may be
+ * NULL; reset != 0 zeroes them afterwards.  Host-side counters, no GPU work. */
+int ptk_gemm_path_counts(int64_t* counts, int reset);
 
 /* Flash attention forward: O = softmax(scale * Q K^T + mask) V per z, bf16 in/out,
  * LSE (natural log) per query row.  z -> (z0, z1) = (z / batch_inner, z % batch_inner);
@@ -274,6 +279,10 @@ typedef struct {
 size_t ptk_gemma3_workspace_bytes(const ptk_gemma3_config* c, int batch, int text_len, int seq_pad);
 int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_batch* b,
                             void* ws, size_t ws_bytes, void* stream);
+/* Forward + loss only (validation under torch.no_grad, Stage2/trainer.py:518-591): b->loss is written, b->dx
+ * is not touched; same workspace as ptk_gemma3_loss_fwd_bwd. */
+int ptk_gemma3_loss_fwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_batch* b,
+                        void* ws, size_t ws_bytes, void* stream);
 
 /* ------------------------------------------------------------------------ *
  * Gemma3 forward + loss + FULL backward (unfrozen LLM, Stage 2, cfg4)       *

@@ -120,7 +120,7 @@ class ImageDesc(C.Structure):
                 ("coef_off", c_int64), ("tmp_off", c_int64)]
 
 
-ABI_VERSION = 2      # include/ptk.h PTK_ABI_VERSION
+ABI_VERSION = 3      # include/ptk.h PTK_ABI_VERSION
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -144,6 +144,7 @@ SIGNATURES = {
     "ptk_gemm_sk_workspace_bytes": (c_size_t, []),
     "ptk_gemm_sk_flag_count": (c_int, []),
     "ptk_gemm_timer_read": (c_int, [c_int, C.POINTER(C.c_double), C.POINTER(c_int)]),
+    "ptk_gemm_path_counts": (c_int, [c_void_p, c_int]),
     "ptk_flash_attn_fwd": (c_int, [C.POINTER(FlashDesc), c_void_p]),
     "ptk_flash_attn_bwd": (c_int, [C.POINTER(FlashBwdDesc), c_void_p]),
     "ptk_flash_bwd_workspace_bytes": (c_size_t, [C.POINTER(FlashBwdDesc)]),
@@ -158,6 +159,8 @@ SIGNATURES = {
     "ptk_gemma3_workspace_bytes": (c_size_t, [C.POINTER(Gemma3ConfigC), c_int, c_int, c_int]),
     "ptk_gemma3_loss_fwd_bwd": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC),
                                         C.POINTER(Gemma3BatchC), c_void_p, c_size_t, c_void_p]),
+    "ptk_gemma3_loss_fwd": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC),
+                                    C.POINTER(Gemma3BatchC), c_void_p, c_size_t, c_void_p]),
     "ptk_gemma3_train_workspace_bytes": (c_size_t, [C.POINTER(Gemma3ConfigC), c_int, c_int, c_int]),
     "ptk_gemma3_train_fwd_bwd": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC),
                                          C.POINTER(Gemma3BatchC), C.POINTER(Gemma3GradsC), c_void_p, c_size_t,
@@ -207,6 +210,16 @@ def check(rc: int, what: str = ""):
 def ptr(t) -> int | None:
     """Device pointer of a torch tensor (None for None)."""
     return None if t is None else t.data_ptr()
+
+
+GEMM_PATHS = ("nt128", "big", "big2", "w4", "pingpong", "streamk", "p8", "tn")
+
+
+def gemm_path_counts(reset=False):
+    """{(path name, act class): launches} since the last reset (host-side census of launch_gemm)."""
+    buf = (C.c_int64 * (8 * len(GEMM_PATHS)))()
+    check(lib().ptk_gemm_path_counts(buf, int(reset)), "gemm_path_counts")
+    return {(GEMM_PATHS[i // 8], i % 8): int(v) for i, v in enumerate(buf) if v}
 
 
 def stream_ptr(device=None) -> int:

@@ -118,6 +118,7 @@ int ptk_gemm_timer_enable(int on) {
   return 0;
 }
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count) { return timer_read(act_class, total_ms, count); }
+int ptk_gemm_path_counts(int64_t* counts, int reset) { return path_counts(counts, reset); }
 
 int ptk_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float std, float mean, void* stream) {
   return launch_fill_normal_bf16((bf16_t*)out, n, seed, std, mean, ST);

@@ -804,33 +804,23 @@ int timer_read(int cls, double* total_ms, int* count) {
     hipEvent_t e0 = nullptr, e1 = nullptr;                                                     \
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }                              \
     if (e0) (void)hipEventRecord(e0, st);                                                          \
+    count_path(GEMM_PATH_NT, act);                                                             \
     hipLaunchKernelGGL((gemm_nt_kernel<ACT_, OUT_>), grid, dim3(256), 0, st, a);              \
     if (e1) (void)hipEventRecord(e1, st);                                                          \
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm launch failed");             \
   }
 
-// Plain GEMMs (no epilogue beyond the output cast) go to hipBLASLt (blaslt.cpp) where it measured ahead
-// of the MFMA kernels (tools/blaslt_probe.py, r02, same box): the q|k|v projection (+24 %), the down
-// projection (+14 %), dO (+19 %), the vocab-wide lm_head (+18 %) and every shape whose 256x256 grid
-// quantises badly (cfg4 M = 14336: down +74 %, d(gate|up) dX +53 %); not the K <= 1024 o projection
-// (-8 %), the d(gate|up) dX at 440 tiles and K = 13824 (-19 %: the staggered 256x256 kernel's K loop) or
-// K = 1536 (tie).  A fixed rule, so the choice (and the rounding) is the same in every process and rank.
-// PTK_BLASLT=0: every GEMM on the MFMA kernels; =1: every plain GEMM on hipBLASLt (A/B switches).
-static int blaslt_mode() {
-  static const int v = [] { const char* e = getenv("PTK_BLASLT"); return e ? (e[0] == '1' ? 1 : e[0] == '0' ? 0 : 2) : 2; }();
-  return v;
+// Dispatch census (tests assert which kernel family a model-level call ran): launches per (path, act)
+static long g_path_count[GEMM_NPATH][8];
+int path_counts(int64_t* out, int reset) {
+  for (int p = 0; p < GEMM_NPATH; ++p)
+    for (int c = 0; c < 8; ++c) {
+      if (out) out[p * 8 + c] = g_path_count[p][c];
+      if (reset) g_path_count[p][c] = 0;
+    }
+  return 0;
 }
-bool blaslt_preferred(const GemmArgs& a, int act, int out) {
-  const int mode = blaslt_mode();
-  if (mode == 0 || !blaslt_supported(a, act, out)) return false;
-  if (mode == 1) return true;
-  if (a.M < 1024 || a.N < 512) return false;
-  if (a.N >= 16384) return true;
-  if (a.K <= 1024) return false;
-  if (a.K >= 12288 && w4_round_fill(a.M, a.N) >= 0.8) return false;
-  if (a.K == 1536 && a.N == 1152) return false;
-  return true;
-}
+static inline void count_path(int path, int act) { ++g_path_count[path][act & 7]; }
 
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0 || batch <= 0) return 0;
@@ -838,15 +828,6 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   if ((a.lda % 8) || (a.ldb % 8)) return set_error("gemm: lda/ldb must be multiples of 8 (16-B rows)");
   if (((uintptr_t)a.A | (uintptr_t)a.B) & 15) return set_error("gemm: A/B must be 16-B aligned");
   if (a.zin <= 0) return set_error("gemm: zin must be >= 1");
-  if (batch == 1 && g_force_tiles == 0 && blaslt_preferred(a, act, out)) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
-    if (e0) (void)hipEventRecord(e0, st);
-    const int r = launch_gemm_blaslt(a, out, st);
-    if (e1) (void)hipEventRecord(e1, st);
-    if (r < 0) return -1;
-    if (r == 1) return 0;
-  }
   const long ntile = (long)((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   if (ntile > 0x7fffffffL) return set_error("gemm: too many tiles");
   // 256x256 (one block per CU) only where the K loop amortises its lock-step epilogue: long K or
@@ -863,20 +844,17 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // (r02: + the GELU-tanh epilogue with packed f32 math, SigLIP fc1 887 -> 936 TFLOP/s, tools/gemm_bench.py --all)
   const bool w4_auto = g_force_tiles == 0 && a.M >= 4096 && a.N <= 16384 &&
                        (act == ACT_GEGLU || act == ACT_GEGLU_BWD ||
-                        ((act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32)) ||
-                         (act == ACT_GELU_TANH && out == OUT_BF16)) &&
-                            a.K <= 8192 && w4_round_fill(a.M, a.N) >= 0.8);
-  // ping-pong 8-wave kernel (forced mode 32; PTK_PP=1 puts the w4 shapes on it): bit-identical to the 4-wave
-  // kernel but measured slower on every step shape (gate|up 788 -> 946 us, dh 584 -> 786 us, plain N 1152 /
-  // 1536 / 3072 projections -8..-12 %, tools/pp_probe.sh): its producer waves' instruction stream, sharing
-  // each SIMD's issue with the consumer's MFMAs, sets the k-step time, so it stays a measured
-  // alternative
-  static const bool pp_env = [] { const char* e = getenv("PTK_PP"); return e && e[0] == '1'; }();
-  if (batch == 1 && (g_force_tiles == 32 || (pp_env && w4_auto)) && pp_supported(a, act, out)) {
+                        (((act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32)) ||
+                          (act == ACT_GELU_TANH && out == OUT_BF16)) &&
+                         a.K <= 8192 && w4_round_fill(a.M, a.N) >= 0.8));
+  // persistent 8-wave kernel (forced mode 32; PTK_P8=1 puts the w4 shapes on it)
+  static const bool p8_env = [] { const char* e = getenv("PTK_P8"); return e && e[0] == '1'; }();
+  if (batch == 1 && (g_force_tiles == 32 || (p8_env && w4_auto)) && p8_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);
-    const int rc = launch_gemm_pp(a, act, out, st);
+    count_path(GEMM_PATH_P8, act);
+    const int rc = launch_gemm_p8(a, act, out, st);
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
   }
@@ -884,6 +862,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);
+    count_path(GEMM_PATH_W4, act);
     const int rc = launch_gemm_w4(a, act, out, st, 0);
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
@@ -901,6 +880,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
         hipEvent_t e0 = nullptr, e1 = nullptr;                                                  \
         if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); } \
         if (e0) (void)hipEventRecord(e0, st);                                                   \
+        count_path(GEMM_PATH_SK, act);                                                          \
         hipLaunchKernelGGL((gemm_sk_kernel<ACT_, OUT_>), dim3(G), dim3(512), 0, st, a);         \
         if (e1) (void)hipEventRecord(e1, st);                                                   \
         return hipGetLastError() == hipSuccess ? 0 : set_error("gemm launch failed");          \
@@ -925,6 +905,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
       hipEvent_t e0 = nullptr, e1 = nullptr;                                                    \
       if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }                             \
       if (e0) (void)hipEventRecord(e0, st);                                                     \
+      count_path(GEMM_PATH_BIG2, act);                                                          \
       hipLaunchKernelGGL((gemm_big2_kernel<ACT_, OUT_>), g4, dim3(512), 0, st, a);              \
       if (e1) (void)hipEventRecord(e1, st);                                                     \
       return hipGetLastError() == hipSuccess ? 0 : set_error("gemm launch failed");            \
@@ -949,6 +930,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
       hipEvent_t e0 = nullptr, e1 = nullptr;                                                    \
       if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }                             \
       if (e0) (void)hipEventRecord(e0, st);                                                     \
+      count_path(GEMM_PATH_BIG, act);                                                           \
       hipLaunchKernelGGL((gemm_big_kernel<ACT_, OUT_>), g2, dim3(512), 0, st, a);               \
       if (e1) (void)hipEventRecord(e1, st);                                                     \
       return hipGetLastError() == hipSuccess ? 0 : set_error("gemm launch failed");            \

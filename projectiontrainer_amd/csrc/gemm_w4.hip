@@ -34,10 +34,6 @@
 #ifndef PTK_W4_DMS
 #define PTK_W4_DMS 0      // diagnostic builds: DMA placement (1 = groups 8..15, 2 = groups 0..7, 3 = odd groups)
 #endif
-#ifndef PTK_PP_ABLATE
-#define PTK_PP_ABLATE 0   // diagnostic builds of the ping-pong kernel (make ppablate): 1 = no per-step barrier,
-                          // 2 = no DMA landing waits (wrong results by construction, timing only)
-#endif
 #ifndef PTK_W4_ABLATE
 #define PTK_W4_ABLATE 0   // diagnostic builds only: 1 = no DMA in the K loop, 2 = no fragment reads,
                           // 3 = the DMA re-reads one L2-resident K-tile, 4 = no K-loop barrier,
@@ -144,11 +140,11 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
 
 // row block I of the wave's tile: lane holds C[row0 + 16I + (lane&15)][col0 + 16j + 4(lane>>4) + e]
 // (one function per row block so every accumulator index is a compile-time constant)
-template <int ACT, int OUT, int I>
-PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, int lane, char* sink) {
+template <int ACT, int OUT, int I, int NJ = 8>
+PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, int lane, char* sink) {
   // pin the accumulator reads to this row block (otherwise hipcc reads all 256 up front and spills)
 #pragma unroll
-  for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
+  for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
   const int q = lane >> 4;
   const int cb = 16 * (q & 1) + 8 * (q >> 1);
   const long r = row0 + 16 * I + (lane & 15);
@@ -157,7 +153,7 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, i
     // GEMM columns: 16-wide gate / up groups alternate (interleaved weights); tiles 4pp, 4pp+2 are
     // gate and 4pp+1, 4pp+3 up for h columns [col0/2 + 32pp, +32)
 #pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
+    for (int pp = 0; pp < NJ / 4; ++pp) {
       f32x4_t g0 = a[4 * pp] * p.alpha, g1 = a[4 * pp + 2] * p.alpha;
       f32x4_t u0 = a[4 * pp + 1] * p.alpha, u1 = a[4 * pp + 3] * p.alpha;
       swap16(g0, g1);
@@ -184,7 +180,7 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, i
   } else {
     const W4Row w = w4_row(p, r);
 #pragma unroll
-    for (int pp = 0; pp < 4; ++pp) {
+    for (int pp = 0; pp < NJ / 2; ++pp) {
       f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
       swap16(x, y);
       float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
@@ -196,31 +192,31 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, i
 // GEGLU backward (GEMM output = dh [M, I]; writes dg, du into the interleaved [M, 2I] layout, as
 // geglu_bwd_kernel does): the saved g and u of row block I, 8 columns per lane and column pair pp,
 // loaded one row block ahead of their use so their latency runs under the previous block's math
-template <int I>
-PTK_DEV void w4_gbwd_load(const GemmArgs& p, long row0, long col0, int lane, u16x8_t (&G)[4], u16x8_t (&U)[4]) {
+template <int I, int NP = 4>
+PTK_DEV void w4_gbwd_load(const GemmArgs& p, long row0, long col0, int lane, u16x8_t (&G)[NP], u16x8_t (&U)[NP]) {
   const int q = lane >> 4;
   const int cb = 16 * (q & 1) + 8 * (q >> 1);
   const long r = row0 + 16 * I + (lane & 15);
   const long rl = r < p.M ? r : 0;
 #pragma unroll
-  for (int pp = 0; pp < 4; ++pp) {
+  for (int pp = 0; pp < NP; ++pp) {
     const long c = col0 + 32 * pp + cb;
     const long cl = c < p.N ? c : 0;
     G[pp] = *reinterpret_cast<const u16x8_t*>(p.aux_in + rl * p.ld_aux_in + cl);
     U[pp] = *reinterpret_cast<const u16x8_t*>(p.aux_in2 + rl * p.ld_aux_in + cl);
   }
 }
-template <int I>
-PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long col0, int lane, char* sink,
-                          const u16x8_t (&G)[4], const u16x8_t (&U)[4]) {
+template <int I, int NP = 4>
+PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[2 * NP], long row0, long col0, int lane, char* sink,
+                          const u16x8_t (&G)[NP], const u16x8_t (&U)[NP]) {
 #pragma unroll
-  for (int j = 0; j < 8; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
+  for (int j = 0; j < 2 * NP; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
   const int q = lane >> 4;
   const int cb = 16 * (q & 1) + 8 * (q >> 1);
   const long r = row0 + 16 * I + (lane & 15);
   const W4Row w = w4_row(p, r);
 #pragma unroll
-  for (int pp = 0; pp < 4; ++pp) {
+  for (int pp = 0; pp < NP; ++pp) {
     f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
     swap16(x, y);
     const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
@@ -246,37 +242,39 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[8], long row0, long co
   }
 }
 
-template <int ACT, int OUT>
-PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][8], long row0, long col0, int lane) {
+// the wave's 128 x 16NJ accumulator tile (8 row blocks of NJ 16x16 MFMA tiles)
+template <int ACT, int OUT, int NJ = 8>
+PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, long col0, int lane) {
   char* sink = g_w4_sink + lane * 64;
   if constexpr (ACT == ACT_GEGLU_BWD) {
-    u16x8_t G0[4], U0[4], G1[4], U1[4];
-    w4_gbwd_load<0>(p, row0, col0, lane, G0, U0);
-    w4_gbwd_load<1>(p, row0, col0, lane, G1, U1);
-    w4_gbwd_rows<0>(p, acc[0], row0, col0, lane, sink, G0, U0);
-    w4_gbwd_load<2>(p, row0, col0, lane, G0, U0);
-    w4_gbwd_rows<1>(p, acc[1], row0, col0, lane, sink, G1, U1);
-    w4_gbwd_load<3>(p, row0, col0, lane, G1, U1);
-    w4_gbwd_rows<2>(p, acc[2], row0, col0, lane, sink, G0, U0);
-    w4_gbwd_load<4>(p, row0, col0, lane, G0, U0);
-    w4_gbwd_rows<3>(p, acc[3], row0, col0, lane, sink, G1, U1);
-    w4_gbwd_load<5>(p, row0, col0, lane, G1, U1);
-    w4_gbwd_rows<4>(p, acc[4], row0, col0, lane, sink, G0, U0);
-    w4_gbwd_load<6>(p, row0, col0, lane, G0, U0);
-    w4_gbwd_rows<5>(p, acc[5], row0, col0, lane, sink, G1, U1);
-    w4_gbwd_load<7>(p, row0, col0, lane, G1, U1);
-    w4_gbwd_rows<6>(p, acc[6], row0, col0, lane, sink, G0, U0);
-    w4_gbwd_rows<7>(p, acc[7], row0, col0, lane, sink, G1, U1);
+    constexpr int NP = NJ / 2;
+    u16x8_t G0[NP], U0[NP], G1[NP], U1[NP];
+    w4_gbwd_load<0, NP>(p, row0, col0, lane, G0, U0);
+    w4_gbwd_load<1, NP>(p, row0, col0, lane, G1, U1);
+    w4_gbwd_rows<0, NP>(p, acc[0], row0, col0, lane, sink, G0, U0);
+    w4_gbwd_load<2, NP>(p, row0, col0, lane, G0, U0);
+    w4_gbwd_rows<1, NP>(p, acc[1], row0, col0, lane, sink, G1, U1);
+    w4_gbwd_load<3, NP>(p, row0, col0, lane, G1, U1);
+    w4_gbwd_rows<2, NP>(p, acc[2], row0, col0, lane, sink, G0, U0);
+    w4_gbwd_load<4, NP>(p, row0, col0, lane, G0, U0);
+    w4_gbwd_rows<3, NP>(p, acc[3], row0, col0, lane, sink, G1, U1);
+    w4_gbwd_load<5, NP>(p, row0, col0, lane, G1, U1);
+    w4_gbwd_rows<4, NP>(p, acc[4], row0, col0, lane, sink, G0, U0);
+    w4_gbwd_load<6, NP>(p, row0, col0, lane, G0, U0);
+    w4_gbwd_rows<5, NP>(p, acc[5], row0, col0, lane, sink, G1, U1);
+    w4_gbwd_load<7, NP>(p, row0, col0, lane, G1, U1);
+    w4_gbwd_rows<6, NP>(p, acc[6], row0, col0, lane, sink, G0, U0);
+    w4_gbwd_rows<7, NP>(p, acc[7], row0, col0, lane, sink, G1, U1);
     return;
   }
-  w4_rows<ACT, OUT, 0>(p, acc[0], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 1>(p, acc[1], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 2>(p, acc[2], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 3>(p, acc[3], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 4>(p, acc[4], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 5>(p, acc[5], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 6>(p, acc[6], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 7>(p, acc[7], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 0, NJ>(p, acc[0], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 1, NJ>(p, acc[1], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 2, NJ>(p, acc[2], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 3, NJ>(p, acc[3], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 4, NJ>(p, acc[4], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 5, NJ>(p, acc[5], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 6, NJ>(p, acc[6], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 7, NJ>(p, acc[7], row0, col0, lane, sink);
 }
 
 PTK_DEV void w4_tile_coords(int t, int nbm, int nbn, int& bm, int& bn) {
@@ -600,176 +598,29 @@ int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_
 }
 
 
-// ============================================================================ ping-pong variant
-// gemm_pp_kernel: 8 waves = two groups of 4, one wave of each group per SIMD.  Group g owns every other
-// 256x128 tile of the workgroup's persistent tile sequence (tiles j with j & 1 == g) and keeps that
-// tile's fp32 accumulators (128x64 per wave, 128 AGPRs) across phases.  Phase j: group j & 1 (the
-// consumer) runs tile j's K loop — MFMAs and LDS fragment reads only — while the other group (the
-// producer) issues the global -> LDS stream 5 k-steps ahead and drains its own previous tile's epilogue
-// (tile j-1) in row-block chunks.  The epilogue's HBM traffic and VALU work therefore run beside the
-// MFMAs instead of after them, and the MFMA waves carry none of the LDS-DMA issue cost that holds the
-// 4-wave kernel's K loop at ~64 % of the MFMA floor.
-//
-// Ring: 6 slots of one 32-deep k-step (A 256 x 64 B + B 128 x 64 B = 24 KiB; 144 KiB).  Stream position
-// s (k-step s % nks of the workgroup's tile s / nks) lands in slot s % 6.  During step s the consumer reads
-// the fragments of s+1 (slot (s+1) % 6) and the producer issues s+5 (slot (s+5) % 6 = that of s-1, whose
-// fragments were read during step s-2, before the barrier that ended step s-2).  Every step ends with one
-// barrier of all 8 waves; before it, the wave that issued position s+2 waits for it (vmcnt counted in
-// software: every memory instruction a wave issues is inline asm, so the count is exact), so the
-// fragments of s+2 can be read during step s+1.  At a tile boundary the producer also reads the first
-// fragments of its own next tile (it becomes the consumer).
+// ============================================================================ persistent 8-wave variant
+// gemm_p8_kernel: the w4 kernel's persistent 256x256 tiles, k-step ring and register epilogue with 8 waves,
+// two per SIMD.  Waves w and w + 4 share a SIMD; wave w computes rows wr*128 .. +128 and columns
+// wc*128 + 64*(w >> 2) .. +64 of the tile (wr, wc from w & 3): a 128x64 fp32 accumulator (128 AGPRs), so
+// each wave fits the 256-register budget of two waves per SIMD.  The LDS-DMA stream is split over all 8
+// waves (4 pieces per wave per k-step instead of w4's 8), and each wave's pieces issue while its SIMD
+// partner's MFMAs keep the matrix pipe busy: the per-piece issue cost that holds the 4-wave kernel's K loop
+// at ~64 % of the MFMA floor is paid beside the partner's MFMAs, not instead of them.
+// Fragments: B double-buffered (4 per k-step), A single-buffered and re-read in place one MFMA group after
+// its last reader (the ping-pong kernel's consumer stream).  The tile's last k-step reads no fragments, so
+// only the accumulators are live through the epilogue; the next tile's first fragments are read after it.
+// The ring, the DMA cursor and the one wait + barrier per pair of k-steps are w4's; the waits are vmcnt(4).
 namespace {
-constexpr int PP_BM = 256, PP_BN = 128, PP_KS = 32;
-constexpr int PP_SA = PP_BM * PP_KS * 2;   // A k-step image, 16 KiB
-constexpr int PP_SB = PP_BN * PP_KS * 2;   // B k-step image, 8 KiB
-constexpr int PP_SLOT = PP_SA + PP_SB;     // 24 KiB
-constexpr int PP_NS = 6;                   // ring slots (144 KiB)
-constexpr int PP_D = 5;                    // DMA distance in k-steps
-constexpr int PP_EPI = 18;                 // producer steps that carry epilogue work (compile-time schedule)
-constexpr int PP_MIN_KS = 20;              // K >= 640
-template <int N> using pp_ic = std::integral_constant<int, N>;
-
-// s_waitcnt vmcnt(n') with n' = n rounded down to a multiple of 6 (one step's DMA pieces), capped at 42:
-// waiting for a few more of the younger operations than needed is safe, and a 7-way compare chain keeps
-// the many inlined copies small (a 64-way jump table per copy made the kernel ~4x the 4-wave kernel's
-// code, and the code size itself cost 5-10 % of the ping-pong kernel's time)
-PTK_DEV void pp_vm_wait(int n) {
-  if (n >= 42) asm volatile("s_waitcnt vmcnt(42)" ::: "memory");
-  else if (n >= 36) asm volatile("s_waitcnt vmcnt(36)" ::: "memory");
-  else if (n >= 30) asm volatile("s_waitcnt vmcnt(30)" ::: "memory");
-  else if (n >= 24) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-  else if (n >= 18) asm volatile("s_waitcnt vmcnt(18)" ::: "memory");
-  else if (n >= 12) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
-  else if (n >= 6) asm volatile("s_waitcnt vmcnt(6)" ::: "memory");
-  else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+constexpr int P8_PIECES = 4;   // LDS-DMA pieces per wave per k-step
 }
-#define PP_ST(ADDR, V) asm volatile("global_store_dwordx4 %0, %1, off\n\ts_nop 1" :: "v"(ADDR), "v"(V) : "memory")
-#define PP_LD(DST, ADDR) asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(DST) : "v"(ADDR) : "memory")
 
-// memory instructions per row block of the epilogue (all inline asm: the software vmcnt needs exact counts)
 template <int ACT, int OUT>
-constexpr int pp_nst() {
-  return ACT == ACT_GEGLU ? 3 : ACT == ACT_GEGLU_BWD ? 4 : OUT == OUT_BF16 ? 2 : 4;
-}
-constexpr int PP_NLD = 4;   // GEGLU backward: g, u of two 8-column groups
-
-PTK_DEV uint32_t pk_bf(float a, float b) {
-  return __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{a, b}, bf16x2_t));
-}
-
-// row block I (16 rows) of the wave's 128x64 tile: lane holds C[row0 + 16I + (lane&15)][col0 + 16j + 4(lane>>4) + e]
-template <int ACT, int OUT, int I>
-PTK_DEV void pp_rows(const GemmArgs& p, f32x4_t (&a)[4], long row0, long col0, int lane, char* sink,
-                     const bf16x8_t& G0, const bf16x8_t& G1, const bf16x8_t& U0, const bf16x8_t& U1) {
-#pragma unroll
-  for (int j = 0; j < 4; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
-  const int q = lane >> 4;
-  const int cb = 16 * (q & 1) + 8 * (q >> 1);
-  const long r = row0 + 16 * I + (lane & 15);
-  const W4Row w = w4_row(p, r);
-  if constexpr (ACT == ACT_GEGLU) {
-    // GEMM columns: 16-wide gate / up groups alternate; tiles 0, 2 gate and 1, 3 up of h columns [col0/2, +32)
-    f32x4_t g0 = a[0] * p.alpha, g1 = a[2] * p.alpha, u0 = a[1] * p.alpha, u1 = a[3] * p.alpha;
-    swap16(g0, g1);
-    swap16(u0, u1);
-    const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
-    const float u[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-    uint32_t gp[4], up[4], hp[4];
-#pragma unroll
-    for (int e = 0; e < 8; e += 2) {
-      gp[e / 2] = pk_bf(g[e], g[e + 1]);
-      up[e / 2] = pk_bf(u[e], u[e + 1]);
-      const f32x2_t hh = bfround2(gelu_tanh2(bf2x2(gp[e / 2]))) * bf2x2(up[e / 2]);
-      hp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(hh, bf16x2_t));
-    }
-    const long hc = col0 / 2 + cb;
-    const bool cin = 2 * hc < p.N;
-    const bool rv = w.rv && cin, sv = w.cv && cin;
-    const void* pg = rv && p.aux ? (const void*)(p.aux + w.ro_aux + hc) : (const void*)sink;
-    const void* pu = rv && p.aux2 ? (const void*)(p.aux2 + w.ro_aux + hc) : (const void*)sink;
-    const void* ph = sv ? (const void*)(reinterpret_cast<bf16_t*>(p.C) + w.ro_c + hc) : (const void*)sink;
-    PP_ST(pg, (u32x4_t{gp[0], gp[1], gp[2], gp[3]}));
-    PP_ST(pu, (u32x4_t{up[0], up[1], up[2], up[3]}));
-    PP_ST(ph, (u32x4_t{hp[0], hp[1], hp[2], hp[3]}));
-  } else if constexpr (ACT == ACT_GEGLU_BWD) {
-#pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
-      swap16(x, y);
-      const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
-      const uint4 gw = __builtin_bit_cast(uint4, pp ? G1 : G0), uw = __builtin_bit_cast(uint4, pp ? U1 : U0);
-      const uint32_t gv[4] = {gw.x, gw.y, gw.z, gw.w}, uv[4] = {uw.x, uw.y, uw.z, uw.w};
-      uint32_t dg[4], du[4];
-#pragma unroll
-      for (int e = 0; e < 8; e += 2) {   // the same per-element math as w4_gbwd_rows / geglu_bwd_vec8
-        const f32x2_t d = bfround2(f32x2_t{v[e], v[e + 1]}), g = bf2x2(gv[e / 2]), u = bf2x2(uv[e / 2]);
-        f32x2_t f, df;
-        gelu_tanh_fg2(g, f, df);
-        const f32x2_t ga = bfround2(d * u) * df, ub = d * bfround2(f);
-        dg[e / 2] = pk_bf(ga.x, ga.y);
-        du[e / 2] = pk_bf(ub.x, ub.y);
-      }
-      const long c = col0 + 32 * pp + cb;
-      bf16_t* o = w.cv && c < p.N ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + (c >> 4) * 32 + (c & 15)
-                                  : reinterpret_cast<bf16_t*>(sink);
-      PP_ST((const void*)o, (u32x4_t{dg[0], dg[1], dg[2], dg[3]}));
-      PP_ST((const void*)(o + 16), (u32x4_t{du[0], du[1], du[2], du[3]}));
-    }
-  } else {
-#pragma unroll
-    for (int pp = 0; pp < 2; ++pp) {
-      f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
-      swap16(x, y);
-      const long c = col0 + 32 * pp + cb;
-      const bool sv = w.cv && c < p.N;
-      if constexpr (OUT == OUT_BF16) {
-        const void* d = sv ? (const void*)(reinterpret_cast<bf16_t*>(p.C) + w.ro_c + c) : (const void*)sink;
-        PP_ST(d, (u32x4_t{pk_bf(x[0], x[1]), pk_bf(x[2], x[3]), pk_bf(y[0], y[1]), pk_bf(y[2], y[3])}));
-      } else {
-        if constexpr (OUT == OUT_F32_BFR) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) { x[e] = bfround(x[e]); y[e] = bfround(y[e]); }
-        }
-        float* d = sv ? reinterpret_cast<float*>(p.C) + w.ro_c + c : reinterpret_cast<float*>(sink);
-        PP_ST((const void*)d, __builtin_bit_cast(u32x4_t, x));
-        PP_ST((const void*)(d + 4), __builtin_bit_cast(u32x4_t, y));
-      }
-    }
-  }
-}
-
-// GEGLU backward: saved g, u of row block I (two 8-column groups per lane)
-template <int I>
-PTK_DEV void pp_gbwd_load(const GemmArgs& p, long row0, long col0, int lane, bf16x8_t& G0, bf16x8_t& G1,
-                          bf16x8_t& U0, bf16x8_t& U1) {
-  const int q = lane >> 4;
-  const int cb = 16 * (q & 1) + 8 * (q >> 1);
-  const long r = row0 + 16 * I + (lane & 15);
-  const long rl = r < p.M ? r : 0;
-  const long c0 = col0 + cb, c1 = c0 + 32;
-  const long cl0 = c0 < p.N ? c0 : 0, cl1 = c1 < p.N ? c1 : 0;
-  PP_LD(G0, (const void*)(p.aux_in + rl * p.ld_aux_in + cl0));
-  PP_LD(U0, (const void*)(p.aux_in2 + rl * p.ld_aux_in + cl0));
-  PP_LD(G1, (const void*)(p.aux_in + rl * p.ld_aux_in + cl1));
-  PP_LD(U1, (const void*)(p.aux_in2 + rl * p.ld_aux_in + cl1));
-}
-}  // namespace
-
-#ifdef PTK_PP_STAMPS
-// diagnostic build only (make ppstamps): per wave, s_memtime cycles between barriers ("work": the consumer's
-// MFMA step or the producer's DMA + epilogue chunk) and inside end_step ("wait": landing wait + barrier),
-// per role, and the step counts
-__device__ unsigned long long g_pp_stamps[1024][8][6];
-#endif
-template <int ACT, int OUT>
-__global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
-  __shared__ __attribute__((aligned(16))) char smem[PP_NS * PP_SLOT];
-  constexpr bool BWD = ACT == ACT_GEGLU_BWD;
-  constexpr int NST = pp_nst<ACT, OUT>();
+__global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
+  __shared__ __attribute__((aligned(16))) char smem[W4_NSLOT * W4_SLOT];   // 160 KiB: the k-step ring
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int grp = wave >> 2, gw = wave & 3, wr = gw >> 1, wc = gw & 1;
-  const int nbm = (p.M + PP_BM - 1) / PP_BM, nbn = (p.N + PP_BN - 1) / PP_BN;
+  const int hf = wave >> 2, wq = wave & 3, wr = wq >> 1, wc = wq & 1;
+  const int nbm = (p.M + W4 - 1) / W4, nbn = (p.N + W4 - 1) / W4;
   const int ntile = nbm * nbn;
   const int G = gridDim.x;
   int loc;
@@ -778,114 +629,74 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_
     loc = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
   }
   if (loc >= ntile) return;
-  const int nks = p.K / PP_KS;
-  const int ntw = (ntile - loc + G - 1) / G;   // tiles of this workgroup
-  const int total = ntw * nks;                 // k-steps of its stream
-  char* const sink = g_w4_sink + lane * 64;
-
+  const int nt = p.K / W4_KT;                              // 64-deep K-tiles per output tile
+  const int nks = 2 * nt;                                  // 32-deep k-steps per output tile
+  const int total_ks = ((ntile - loc + G - 1) / G) * nks;
   const u32x4_t rsa = w4_rsrc(p.A, a_bytes), rsb = w4_rsrc(p.B, b_bytes);
-  // producer wave gw stages A rows 64gw..+63 (4 pieces of 16 rows x 64 B) and B rows 32gw..+31 (2 pieces);
-  // lane i of a piece writes LDS row 16j + (i>>2), chunk i&3, and fetches logical chunk (i&3) ^ ((row>>1)&2)
-  uint32_t offa[4], offb[2];
-  {
+
+  // global -> LDS: wave w fills rows 32w..32w+31 of both operands (2 + 2 pieces of 16 rows x 64 B), lane i of
+  // a piece writes LDS row 16j + (i>>2), chunk i&3 and fetches logical chunk (i&3) ^ ((row>>1)&2) (w4's swizzle)
+  uint32_t offa[2], offb[2];
+#pragma unroll
+  for (int j = 0; j < 2; ++j) {
+    const int lr = wave * 32 + 16 * j + (lane >> 2);
     const int lc = (lane & 3) ^ ((lane >> 3) & 2);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) offa[j] = (uint32_t)(gw * 64 + 16 * j + (lane >> 2)) * (uint32_t)p.lda * 2u + lc * 16;
-#pragma unroll
-    for (int j = 0; j < 2; ++j) offb[j] = (uint32_t)(gw * 32 + 16 * j + (lane >> 2)) * (uint32_t)p.ldb * 2u + lc * 16;
+    offa[j] = (uint32_t)lr * (uint32_t)p.lda * 2u + lc * 16;
+    offb[j] = (uint32_t)lr * (uint32_t)p.ldb * 2u + lc * 16;
   }
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem));
-  const uint32_t dma_a = lds_base + gw * 4096, dma_b = lds_base + PP_SA + gw * 2048;
-
-  // DMA cursor (every wave advances it every step; the producer issues): position dpos = tile dj,
-  // k-step dks, ring slot dslot, scalar offsets of the tile's row panels
-  int dpos = 0, dj = 0, dks = 0, dslot = 0;
+  const uint32_t lds_dma = lds_base + wave * 32 * 64;
+  int dt = loc, dks = 0, dcount = 0;
   uint32_t dsa = 0, dsb = 0;
-  auto dma_tile = [&](int jj) __attribute__((always_inline)) {
+  auto dma_tile = [&](int t) {
     int bm, bn;
-    w4_tile_coords(loc + jj * G, nbm, nbn, bm, bn);
-    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * PP_BM + (int)p.amap.off) * (uint32_t)p.lda * 2u);
-    dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * PP_BN) * (uint32_t)p.ldb * 2u);
+    w4_tile_coords(t, nbm, nbn, bm, bn);
+    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * W4 + (int)p.amap.off) * (uint32_t)p.lda * 2u);
+    dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * W4) * (uint32_t)p.ldb * 2u);
   };
-  int issued = 0;                 // memory instructions this wave has issued (software vmcnt)
-  int mk2 = -1, mk3 = -1, mk4 = -1, mk5 = -1;   // issued-count after the DMA of position s+2 .. s+5 (-1: not mine)
-  auto dma_step = [&](bool mine) __attribute__((always_inline)) {
-    mk5 = -1;
-    if (mine && dpos < total) {
-      const uint32_t sa = __builtin_amdgcn_readfirstlane(dsa + dks * (PP_KS * 2));
-      const uint32_t sb = __builtin_amdgcn_readfirstlane(dsb + dks * (PP_KS * 2));
-      const uint32_t la = __builtin_amdgcn_readfirstlane(dma_a + dslot * PP_SLOT);
-      const uint32_t lb = __builtin_amdgcn_readfirstlane(dma_b + dslot * PP_SLOT);
-#pragma unroll
-      for (int j = 0; j < 4; ++j) W4_DMA(rsa, offa[j], sa, la + j * 1024);
-#pragma unroll
-      for (int j = 0; j < 2; ++j) W4_DMA(rsb, offb[j], sb, lb + j * 1024);
-      issued += 6;
-      mk5 = issued;
-    }
-    ++dpos;
-    dslot = dslot == PP_NS - 1 ? 0 : dslot + 1;
-    if (++dks == nks) {
-      dks = 0;
-      if (++dj < ntw) dma_tile(dj);
+  auto dma_advance = [&]() {
+    if (++dcount < total_ks) {
+      if (++dks == nks) {
+        dks = 0;
+        dt += G;
+        dma_tile(dt);
+      }
     }
   };
-  uint32_t rslot = 0;             // ring slot of position s+1 (fragments read during step s)
-  // end of step s: the issuer of position s+2 waits for it, then one barrier publishes it
-#ifdef PTK_PP_STAMPS
-  unsigned long long st_acc[2][2] = {{0, 0}, {0, 0}}, st_n[2] = {0, 0};
-  unsigned long long st_last = __builtin_amdgcn_s_memtime();
-  int st_role = 0;
-#endif
-  auto end_step = [&]() __attribute__((always_inline)) {
-#ifdef PTK_PP_STAMPS
-    const unsigned long long st_a = __builtin_amdgcn_s_memtime();
-#endif
-#if PTK_PP_ABLATE != 2
-    if (mk2 >= 0) pp_vm_wait(issued - mk2);
-#endif
-    mk2 = mk3;
-    mk3 = mk4;
-    mk4 = mk5;
-    rslot = rslot == (PP_NS - 1) * PP_SLOT ? 0u : rslot + PP_SLOT;
-#if PTK_PP_ABLATE != 1
-    __builtin_amdgcn_s_barrier();
-#endif
-#ifdef PTK_PP_STAMPS
-    const unsigned long long st_b = __builtin_amdgcn_s_memtime();
-    st_acc[st_role][0] += st_a - st_last;
-    st_acc[st_role][1] += st_b - st_a;
-    st_n[st_role] += 1;
-    st_last = st_b;
-#endif
-  };
+  auto slot_next = [](uint32_t s) { s += W4_SLOT; return s == W4_NSLOT * W4_SLOT ? 0u : s; };
 
-  // ---- fragments: A rows wr*128 + 16i + (lane&15), B rows wc*64 + 16j + (lane&15), logical chunk lane>>4
   const int frag_off = (lane & 15) * 64 + (((lane >> 4) ^ ((lane >> 1) & 2)) << 4);
-  const uint32_t frag_a = lds_base + wr * 128 * 64 + frag_off;
-  const uint32_t frag_b = lds_base + PP_SA + wc * 64 * 64 + frag_off;
-  // A fragments single-buffered (each is re-read in place right after the 4 MFMAs of its row block have
-  // issued), B fragments double-buffered: 48 + 16 VGPRs, so the wave fits 128 VGPRs beside 128 AGPRs
+  const uint32_t frag_a = lds_addr(smem) + wr * 128 * 64 + frag_off;
+  const uint32_t frag_b = lds_addr(smem) + W4_SOPB + (wc * 128 + hf * 64) * 64 + frag_off;
   bf16x8_t fa[8], fb0[4], fb1[4];
   f32x4_t acc[8][4];
 
-#define PP_GROUP(FB, Q, FIRST)                                                      \
-  do {                                                                              \
-    _Pragma("unroll") for (int jj = 0; jj < 4; ++jj) {                              \
-      if (FIRST) W4_MFMA0(acc[Q][jj], FB[jj], fa[Q]);                               \
-      else W4_MFMA(acc[Q][jj], FB[jj], fa[Q]);                                      \
-    }                                                                               \
-  } while (0)
+  // all 12 fragments of the k-step in slot rs (after a barrier published it)
+  auto read_frags = [&](uint32_t rs) __attribute__((always_inline)) {
+    const uint32_t ba = frag_a + rs, bb = frag_b + rs;
+#pragma unroll
+    for (int r = 0; r < 8; ++r) W4_DSREAD(fa[r], ba, r * 1024);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) W4_DSREAD(fb0[r], bb, r * 1024);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    asm volatile("" : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]),
+                 "+v"(fa[6]), "+v"(fa[7]));
+    asm volatile("" : "+v"(fb0[0]), "+v"(fb0[1]), "+v"(fb0[2]), "+v"(fb0[3]));
+  };
 
-  // consumer k-step: 8 groups of 4 MFMAs (row block q x column blocks 0..3).  With RD the next k-step's
-  // fragments (slot rslot) are read: B block q (q < 4) into NB before group q, A block q into fa[q] one group
-  // after group q (A7 after the last group), so no read overwrites a register an MFMA just issued still
-  // reads.  Issue order of one step's reads: B0 B1 A0 B2 A1 B3 A2 A3 .. A7 (DS reads complete in order), so
-  // before group q of the next step lgkmcnt(n_q) leaves exactly the younger reads in flight: n_0 = 6 (B3 and
-  // older landed), n_1 = n_2 = 8, n_3 = 9, n_4..7 = 10.
-  auto cstep = [&](auto first_c, auto read_c, bf16x8_t (&FB)[4], bf16x8_t (&NB)[4]) __attribute__((always_inline)) {
+  // one k-step: 8 groups of 4 MFMAs (row block q x column blocks 0..3) on fa / FB.  RD: the next k-step's
+  // fragments (slot rs) are read, B block q (q < 4) into NB before group q and A block q into fa[q] one group
+  // after group q (A7 after the last group); issue order B0 B1 A0 B2 A1 B3 A2 .. A7, so before group q of the
+  // next k-step lgkmcnt(n_q) leaves exactly the younger reads in flight (n = 6, 8, 8, 9, 10, 10, 10, 10).
+  // The 4 LDS-DMA pieces of k-step +4 (slot ws) go out in the even groups (waves 0-3) or the odd groups
+  // (waves 4-7), so the two waves of a SIMD do not issue theirs side by side.
+  auto kstep = [&](auto first_c, auto read_c, auto half_c, bf16x8_t (&FB)[4], bf16x8_t (&NB)[4], uint32_t rs,
+                   uint32_t ws) __attribute__((always_inline)) {
     constexpr bool first = decltype(first_c)::value, rd = decltype(read_c)::value;
-    const uint32_t ba = frag_a + rslot, bb = frag_b + rslot;
+    constexpr int half = decltype(half_c)::value;
+    const uint32_t ba = frag_a + rs, bb = frag_b + rs;
+    const uint32_t da = lds_dma + ws, db = da + W4_SOPB;
+    const uint32_t sa = dsa + dks * (W4_KS * 2), sb = dsb + dks * (W4_KS * 2);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       if (q == 0) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
@@ -895,188 +706,100 @@ __global__ void __launch_bounds__(512, 1) gemm_pp_kernel(GemmArgs p, uint32_t a_
       asm volatile("" : "+v"(fa[q]));
       if (q == 0) asm volatile("" : "+v"(FB[0]), "+v"(FB[1]), "+v"(FB[2]), "+v"(FB[3]));
       if (rd && q < 4) W4_DSREAD(NB[q], bb, q * 1024);
-      PP_GROUP(FB, q, first);
+      if ((q & 1) == half) {
+        const int pc = q >> 1;   // pieces A0 B0 A1 B1
+        if (pc & 1) W4_DMA(rsb, offb[pc >> 1], sb, db + (pc >> 1) * 1024);
+        else W4_DMA(rsa, offa[pc >> 1], sa, da + (pc >> 1) * 1024);
+      }
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj) {
+        if (first) W4_MFMA0(acc[q][jj], FB[jj], fa[q]);
+        else W4_MFMA(acc[q][jj], FB[jj], fa[q]);
+      }
       if (rd && q >= 1) W4_DSREAD(fa[q - 1], ba, (q - 1) * 1024);   // one group after its last reader
     }
     if (rd) W4_DSREAD(fa[7], ba, 7 * 1024);
   };
-  // all 12 fragments of position s+1 (the producer's last step: its next tile's first k-step)
-  auto read_frags = [&](bf16x8_t (&NB)[4]) __attribute__((always_inline)) {
-    const uint32_t ba = frag_a + rslot, bb = frag_b + rslot;
+
+  auto run = [&](auto half_c) __attribute__((always_inline)) {
+    // prologue: k-steps 0..3 into slots 0..3; 0..2 landed and published; fragments of k-step 0 read
+    dma_tile(dt);
 #pragma unroll
-    for (int r = 0; r < 8; ++r) W4_DSREAD(fa[r], ba, r * 1024);
+    for (int b = 0; b < 4; ++b) {
+      const uint32_t da = lds_dma + b * W4_SLOT, db = da + W4_SOPB;
+      const uint32_t sa = dsa + dks * (W4_KS * 2), sb = dsb + dks * (W4_KS * 2);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) W4_DSREAD(NB[r], bb, r * 1024);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    asm volatile("" : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]),
-                 "+v"(fa[6]), "+v"(fa[7]));
-    asm volatile("" : "+v"(NB[0]), "+v"(NB[1]), "+v"(NB[2]), "+v"(NB[3]));
-  };
-
-  // the epilogue of one of this wave's tiles, row block R; the GEGLU backward's g, u loads go into the A
-  // fragment registers (dead in the producer phase until its last step re-reads them): set R & 1 = fa[4(R&1)..+3]
-  int ml0 = 0, ml1 = 0;           // issued-count after each load set
-  long erow = 0, ecol = 0;        // origin of the wave's part of the tile being drained
-  auto epi_tile = [&](int jj) __attribute__((always_inline)) {
-    int bm, bn;
-    w4_tile_coords(loc + jj * G, nbm, nbn, bm, bn);
-    erow = (long)bm * PP_BM + wr * 128;
-    ecol = (long)bn * PP_BN + wc * 64;
-  };
-  auto epi_load = [&](auto r_c) __attribute__((always_inline)) {
-    constexpr int R = decltype(r_c)::value;
-    constexpr int b = 4 * (R & 1);
-    int ln = lane;                // opaque copy: keeps the per-row-block address math here (not hoisted and
-    asm volatile("" : "+v"(ln));  // kept live through the consumer phase)
-    pp_gbwd_load<R>(p, erow, ecol, ln, fa[b], fa[b + 1], fa[b + 2], fa[b + 3]);
-    issued += PP_NLD;
-    if (R & 1) ml1 = issued; else ml0 = issued;
-  };
-  auto epi_rows = [&](auto r_c) __attribute__((always_inline)) {
-    constexpr int R = decltype(r_c)::value;
-    constexpr int b = 4 * (R & 1);
-    if constexpr (BWD) {
-      pp_vm_wait(issued - ((R & 1) ? ml1 : ml0));
-      asm volatile("" : "+v"(fa[b]), "+v"(fa[b + 1]), "+v"(fa[b + 2]), "+v"(fa[b + 3]));
-    }
-    int ln = lane;
-    asm volatile("" : "+v"(ln));
-    pp_rows<ACT, OUT, R>(p, acc[R], erow, ecol, ln, g_w4_sink + ln * 64, fa[b], fa[b + 1], fa[b + 2], fa[b + 3]);
-    issued += NST;
-  };
-  // producer step KS (< PP_EPI) of the epilogue schedule: plain epilogues drain row block r at step 2r+1;
-  // the GEGLU backward loads row block r's g, u at step 2r and drains it at step 2r+3
-  auto epi_chunk = [&](auto ks_c) __attribute__((always_inline)) {
-    constexpr int KS = decltype(ks_c)::value;
-    if constexpr (BWD) {
-      if constexpr (KS % 2 == 0 && KS / 2 < 8) epi_load(pp_ic<KS / 2>{});
-      if constexpr (KS % 2 == 1 && KS >= 3 && (KS - 3) / 2 < 8) epi_rows(pp_ic<(KS - 3) / 2>{});
-    } else {
-      if constexpr (KS % 2 == 1 && (KS - 1) / 2 < 8) epi_rows(pp_ic<(KS - 1) / 2>{});
-    }
-  };
-
-  // ---- prologue: group 1 (producer of phase 0) stages positions 0..4; 0 and 1 landed and published;
-  // group 0 reads the fragments of position 0
-  dma_tile(0);
-  dma_step(grp == 1);             // position 0
-  dma_step(grp == 1);             // position 1
-  const int mk_1 = mk5;
-  dma_step(grp == 1);             // positions 2..4: waited for at the ends of steps 0..2
-  mk2 = mk5;
-  dma_step(grp == 1);
-  mk3 = mk5;
-  dma_step(grp == 1);
-  mk4 = mk5;
-  if (mk_1 >= 0) pp_vm_wait(issued - mk_1);
-  else if (grp == 1) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __builtin_amdgcn_s_barrier();
-  if (grp == 0) read_frags(fb0);
-  rslot = PP_SLOT;                // step 0 reads position 1
-
-  for (int j = 0; j < ntw; ++j) {
-    if ((j & 1) == grp) {
-      // ---- consumer phase: tile j's K loop
-#ifdef PTK_PP_STAMPS
-      st_role = 0;
-#endif
-      cstep(std::true_type{}, std::true_type{}, fb0, fb1);
-      dma_step(false);
-      end_step();
-      for (int ks = 1; ks < nks - 1; ks += 2) {
-        cstep(std::false_type{}, std::true_type{}, fb1, fb0);
-        dma_step(false);
-        end_step();
-        cstep(std::false_type{}, std::true_type{}, fb0, fb1);
-        dma_step(false);
-        end_step();
+      for (int j = 0; j < 2; ++j) {
+        W4_DMA(rsa, offa[j], sa, da + j * 1024);
+        W4_DMA(rsb, offb[j], sb, db + j * 1024);
       }
-      cstep(std::false_type{}, std::false_type{}, fb1, fb0);
-      dma_step(false);
-      end_step();
-    } else {
-      // ---- producer phase: the stream 5 k-steps ahead; tile j-1's epilogue (this wave's own tile)
-#ifdef PTK_PP_STAMPS
-      st_role = 1;
-#endif
-      const bool drain = j >= 1;
-      if (drain) epi_tile(j - 1);
-      auto pstep = [&](auto ks_c) __attribute__((always_inline)) {
-        dma_step(true);
-        if (drain) epi_chunk(ks_c);
-        end_step();
-      };
-      pstep(pp_ic<0>{}); pstep(pp_ic<1>{}); pstep(pp_ic<2>{}); pstep(pp_ic<3>{}); pstep(pp_ic<4>{});
-      pstep(pp_ic<5>{}); pstep(pp_ic<6>{}); pstep(pp_ic<7>{}); pstep(pp_ic<8>{}); pstep(pp_ic<9>{});
-      pstep(pp_ic<10>{}); pstep(pp_ic<11>{}); pstep(pp_ic<12>{}); pstep(pp_ic<13>{}); pstep(pp_ic<14>{});
-      pstep(pp_ic<15>{}); pstep(pp_ic<16>{}); pstep(pp_ic<17>{});
-      static_assert(PP_EPI == 18, "producer schedule is unrolled for 18 steps");
-      for (int ks = PP_EPI; ks < nks - 1; ++ks) {
-        dma_step(true);
-        end_step();
-      }
-      // last step: the first fragments of this group's next tile (harmless reads when there is none)
-      dma_step(true);
-      read_frags(fb0);
-      end_step();
+      dma_advance();
     }
-  }
-
-  // ---- the last tile's epilogue (its consumer group; the other group drained its tile in the last phase)
-  if (((ntw - 1) & 1) == grp) {
-    asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");   // MFMA D -> accumulator read wait states
-    epi_tile(ntw - 1);
-    auto last_rows = [&](auto r_c) __attribute__((always_inline)) {
-      if constexpr (BWD) epi_load(r_c);
-      epi_rows(r_c);
+    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    read_frags(0);
+    __builtin_amdgcn_s_barrier();
+    // ring invariant as gemm_w4_kernel's (k-step i's fragments in registers, i+1 / i+2 published, i+3 in
+    // flight, i+4 issued into the slot of i-1); vmcnt(4) before each pair's barrier leaves only the youngest
+    // k-step's 4 pieces in flight
+    uint32_t rs = W4_SLOT, ws = 4 * W4_SLOT;
+    // one pair of k-steps, then the wait + barrier; the tile's first k-step initialises the accumulators
+    // (MFMA with C = 0) and its last reads no fragments.  Peeled per tile (no branch between MFMA forms),
+    // so the 128 accumulators keep their registers across the K loop.
+    auto pair = [&](auto first_c, auto last_c) __attribute__((always_inline)) {
+      constexpr bool lst = decltype(last_c)::value;
+      kstep(first_c, std::true_type{}, half_c, fb0, fb1, rs, ws);
+      dma_advance();
+      rs = slot_next(rs);
+      ws = slot_next(ws);
+      kstep(std::false_type{}, std::integral_constant<bool, !lst>{}, half_c, fb1, fb0, rs, ws);
+      dma_advance();
+      rs = slot_next(rs);
+      ws = slot_next(ws);
+      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      __builtin_amdgcn_s_barrier();
     };
-    last_rows(pp_ic<0>{}); last_rows(pp_ic<1>{}); last_rows(pp_ic<2>{}); last_rows(pp_ic<3>{});
-    last_rows(pp_ic<4>{}); last_rows(pp_ic<5>{}); last_rows(pp_ic<6>{}); last_rows(pp_ic<7>{});
-  }
+    for (int t = loc; t < ntile; t += G) {
+      pair(std::true_type{}, std::false_type{});
+      for (int kt = 1; kt < nt - 1; ++kt) pair(std::false_type{}, std::false_type{});
+      pair(std::false_type{}, std::true_type{});
+      asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");   // MFMA D -> accumulator read wait states
+      int bm, bn;
+      w4_tile_coords(t, nbm, nbn, bm, bn);
+      w4_epilogue<ACT, OUT, 4>(p, acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128 + hf * 64, lane);
+      read_frags(rs);   // the next tile's first k-step (published by the barrier; harmless after the last)
+    }
+  };
+  if (hf) run(std::integral_constant<int, 1>{});
+  else run(std::integral_constant<int, 0>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup exits
-#ifdef PTK_PP_STAMPS
-  if (lane == 0 && blockIdx.x < 1024) {
-    unsigned long long* o = g_pp_stamps[blockIdx.x][wave];
-    o[0] = st_acc[0][0]; o[1] = st_acc[0][1]; o[2] = st_n[0];
-    o[3] = st_acc[1][0]; o[4] = st_acc[1][1]; o[5] = st_n[1];
-  }
-#endif
-#undef PP_GROUP
 }
 
-// the ping-pong path: what the W4 path needs, K >= 640, and no epilogue inputs beyond the GEGLU backward's g, u
-bool pp_supported(const GemmArgs& a, int act, int out) {
-  if (!w4_supported(a, act, out)) return false;
-  if (a.K % 64 || a.K / PP_KS < PP_MIN_KS) return false;
-  if (a.bias || a.rowadd || a.resid || a.resid16 || a.bf16_linear) return false;
-  if (act == ACT_GEGLU || act == ACT_GEGLU_BWD) return out == OUT_BF16;
-  return act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32 || out == OUT_F32_BFR);
-}
+// the p8 path takes what the w4 path takes, at K >= 128 (a tile's first and last k-step pairs are peeled)
+bool p8_supported(const GemmArgs& a, int act, int out) { return a.K >= 128 && w4_supported(a, act, out); }
 
-#ifdef PTK_PP_STAMPS
-extern "C" int ptk_debug_pp_stamps_read(void* host, size_t bytes) {
-  return hipMemcpyFromSymbol(host, HIP_SYMBOL(g_pp_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
-}
-#endif
-int launch_gemm_pp(const GemmArgs& a, int act, int out, hipStream_t st) {
+int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st) {
   num_cu();
-  const long ntile = (long)((a.M + PP_BM - 1) / PP_BM) * ((a.N + PP_BN - 1) / PP_BN);
+  const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   const long grid = std::min<long>(ntile, g_num_cu);
   const long arows = a.M + a.amap.off;
   const uint32_t ab = (uint32_t)std::min<double>((double)arows * a.lda * 2, 2147483000.0);
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
-#define PTK_PP_CASE(ACT_, OUT_)                                                                   \
+#define PTK_P8_CASE(ACT_, OUT_)                                                                   \
   if (act == ACT_ && out == OUT_) {                                                               \
-    hipLaunchKernelGGL((gemm_pp_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb); \
-    return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_pp launch failed");              \
+    hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb); \
+    return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");              \
   }
-  PTK_PP_CASE(ACT_NONE, OUT_BF16)
-  PTK_PP_CASE(ACT_NONE, OUT_F32)
-  PTK_PP_CASE(ACT_NONE, OUT_F32_BFR)
-  PTK_PP_CASE(ACT_GEGLU, OUT_BF16)
-  PTK_PP_CASE(ACT_GEGLU_BWD, OUT_BF16)
-#undef PTK_PP_CASE
-  return set_error("gemm_pp: unsupported (act=%d, out=%d)", act, out);
+  PTK_P8_CASE(ACT_NONE, OUT_BF16)
+  PTK_P8_CASE(ACT_NONE, OUT_F32)
+  PTK_P8_CASE(ACT_NONE, OUT_F32_BFR)
+  PTK_P8_CASE(ACT_GELU_TANH, OUT_BF16)
+  PTK_P8_CASE(ACT_GELU_ERF, OUT_BF16)
+  PTK_P8_CASE(ACT_GEGLU, OUT_BF16)
+  PTK_P8_CASE(ACT_GELU_ERF_BWD, OUT_BF16)
+  PTK_P8_CASE(ACT_GEGLU_BWD, OUT_BF16)
+#undef PTK_P8_CASE
+  return set_error("gemm_p8: unsupported (act=%d, out=%d)", act, out);
 }
 
 }  // namespace ptk

@@ -235,21 +235,6 @@ int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStr
   while (S > 1 && ((long)S * a.M * a.N > part_floats || a.K / S < kmin || a.N % 4 || a.ldc % 4)) S /= 2;
   const bool plain = !a.rowadd && !a.resid && !a.aux && !a.aux_in && a.amap.g == 0 && a.amap.off == 0 &&
                      a.cmap.g == 0 && a.cmap.off == 0 && a.bias == nullptr && a.alpha == 1.f;
-  // few-tile weight grads (dW_qkv, dW_o: <= 64 tiles) split 4 ways on the MFMA kernels beat hipBLASLt
-  // (818 / 560 vs 638 / 519 TFLOP/s, tools/blaslt_probe.py r02); the larger ones go to hipBLASLt
-  if (S < 4 && plain && part && a.bf16_linear && a.resid16 && (long)a.M * a.N <= part_floats && a.N % 4 == 0) {
-    // the weight-grad accumulate: a plain fp32 GEMM (hipBLASLt where the shape rule prefers it) into the
-    // partial buffer, then bf16(grad + bf16(sum)) as autograd accumulates
-    GemmArgs b = a;
-    b.C = part; b.ldc = a.N;
-    b.bf16_linear = 0; b.resid16 = nullptr; b.ld_resid16 = 0;
-    if (blaslt_preferred(b, ACT_NONE, OUT_F32)) {
-      CK(launch_gemm(b, ACT_NONE, OUT_F32, 1, st));
-      return launch_splitk_reduce(part, 1, a.M, a.N, a.C, a.ldc, 1, a.resid16, a.ld_resid16, st);
-    }
-  } else if (plain && blaslt_preferred(a, ACT_NONE, out)) {
-    return launch_gemm(a, ACT_NONE, out, 1, st);
-  }
   if (S == 1 || !plain || !part) return launch_gemm(a, ACT_NONE, out, 1, st);
   const int kc = (a.K / S + 63) / 64 * 64;
   const int nfull = a.K / kc, rem = a.K - nfull * kc;
@@ -269,28 +254,12 @@ int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStr
                               bf ? a.resid16 : nullptr, a.ld_resid16, st);
 }
 
-// PTK_BLASLT_TN=0: the transpose + MFMA path for every weight grad (A/B)
-static bool blaslt_tn_enabled() {
-  static const int v = [] { const char* e = getenv("PTK_BLASLT_TN"); return e && e[0] == '0' ? 0 : 1; }();
-  return v != 0;
-}
-
 // dW (+)= dY^T X over K token rows: both operands are token-major, so each is first transposed to a
 // K-contiguous feature-major copy (rows gathered through a map, zero-padded to a multiple of 64), then one
 // MFMA GEMM accumulates into the bf16 .grad (bf16(grad + bf16(acc)), autograd's accumulation).
 int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* x, long ldx, RowMap xmap, int Nx,
                 int rows, bf16_t* TA, bf16_t* TB, void* grad, float* skpart, long sk_floats, hipStream_t st) {
   if (!grad) return 0;
-  // token-major operands straight into hipBLASLt's dY^T X (no transposes) for every contiguous-row weight
-  // grad that is not a few-tile one (those split-K on the MFMA kernels, see gemm_split); fp32 result,
-  // then the exact bf16 accumulate
-  const long nbig = (long)((Ny + 255) / 256) * ((Nx + 255) / 256);
-  const bool ident_rows = ymap.g == 0 && ymap.off == 0 && xmap.g == 0 && xmap.off == 0;
-  if (ident_rows && nbig > 64 && (long)Ny * Nx <= sk_floats && Nx % 4 == 0 && blaslt_tn_enabled()) {
-    const int r = launch_gemm_blaslt_tn((const bf16_t*)dy, lddy, Ny, (const bf16_t*)x, ldx, Nx, rows, skpart, Nx, st);
-    if (r < 0) return -1;
-    if (r == 1) return launch_splitk_reduce(skpart, 1, Ny, Nx, grad, Nx, 1, (const bf16_t*)grad, Nx, st);
-  }
   const int Kp = (rows + 63) / 64 * 64;
   CK(launch_transpose_rows(dy, lddy, ymap, rows, Ny, TA, Kp, Kp, st));
   CK(launch_transpose_rows(x, ldx, xmap, rows, Nx, TB, Kp, Kp, st));
@@ -391,7 +360,7 @@ namespace {
 // Gemma3 forward + causal-LM loss + backward.  gr == nullptr: the frozen LLM of Stage 1 (dX only);
 // otherwise every parameter's grad is accumulated into *gr as well (unfrozen LLM, Stage 2).
 int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,
-              const ptk_gemma3_grads* gr, void* ws, size_t ws_bytes, hipStream_t st) {
+              const ptk_gemma3_grads* gr, void* ws, size_t ws_bytes, hipStream_t st, bool fwd_only = false) {
   const bool train = gr != nullptr;
   const int B = bt->batch, T = bt->text_len, Nv = bt->num_vision, Sp = bt->seq_pad, S = Nv + T;
   const int lo = bt->label_offset;
@@ -487,6 +456,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
   CK(launch_count_valid(bt->labels, R, bt->loss_scale, w.gscale, w.count, st));
   CK(launch_ce_fwd_bwd(w.logits, V, R, V, bt->labels, w.row_loss, w.gscale, st));
   CK(launch_loss_reduce(w.row_loss, R, w.count, bt->loss, st));
+  if (fwd_only) return 0;   // validation loss (no_grad): the CE pass's d(logits) is left unused
   // tied lm_head weight grad: dE += dlogits^T . xf (the logits rows outside the loss rows have zero grad)
   if (train) CK(weight_grad(w.logits, V, ident, V, w.xf, H, ident, H, R, w.TL, w.TX, gr->embed, w.skpart, w.sk_floats, st));
   {  // d(xf) = dlogits . E, K = vocab: split-K over LM_SPLITK equal slices (fp32 partials, ordered sum);
@@ -621,6 +591,11 @@ extern "C" {
 int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,
                             void* ws, size_t ws_bytes, void* stream) {
   return gemma_run(c, wt, bt, nullptr, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int ptk_gemma3_loss_fwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,
+                        void* ws, size_t ws_bytes, void* stream) {
+  return gemma_run(c, wt, bt, nullptr, ws, ws_bytes, (hipStream_t)stream, true);
 }
 
 int ptk_gemma3_train_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,

@@ -52,22 +52,19 @@ constexpr int SK_MAX_BLOCKS = 512;
 constexpr long SK_SLAB_FLOATS = 256L * 256;
 
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
-// plain GEMMs on hipBLASLt (blaslt.cpp): 1 launched, 0 not available for the shape, < 0 error
-bool blaslt_supported(const GemmArgs& a, int act, int out);
-bool blaslt_preferred(const GemmArgs& a, int act, int out);   // the shape rule of gemm.hip
-int launch_gemm_blaslt(const GemmArgs& a, int out, hipStream_t st);
-// C[Ny, Nx] (fp32, ldc) = dY^T . X over K rows of the token-major dY [K, Ny] (lddy) and X [K, Nx] (ldx)
-int launch_gemm_blaslt_tn(const bf16_t* dy, long lddy, int Ny, const bf16_t* x, long ldx, int Nx, int K, float* C,
-                          long ldc, hipStream_t st);
+// kernel families launch_gemm dispatches to (census: path_counts, ptk_gemm_path_counts)
+enum GemmPath { GEMM_PATH_NT = 0, GEMM_PATH_BIG = 1, GEMM_PATH_BIG2 = 2, GEMM_PATH_W4 = 3, GEMM_PATH_PP = 4,
+                GEMM_PATH_SK = 5, GEMM_PATH_P8 = 6, GEMM_PATH_TN = 7, GEMM_NPATH = 8 };
+int path_counts(int64_t* out, int reset);   // out [GEMM_NPATH][8] launches per (path, act class)
 // persistent 256x256 4-wave GEMM (gemm_w4.hip): batch 1 only; w4_supported says whether a shape qualifies
 bool w4_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid);
 // fraction of the persistent grid's tile rounds that hold work: ntile / (ceil(ntile / CUs) * CUs)
 double w4_round_fill(long M, long N);
 int device_cus();   // compute units of the current device (cached)
-// ping-pong 8-wave variant (gemm_w4.hip): two wave groups alternate K loop and epilogue on 256x128 tiles
-bool pp_supported(const GemmArgs& a, int act, int out);
-int launch_gemm_pp(const GemmArgs& a, int act, int out, hipStream_t st);
+// persistent 8-wave variant (gemm_w4.hip): the w4 tiles and ring with two waves per SIMD
+bool p8_supported(const GemmArgs& a, int act, int out);
+int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st);
 // live GEMM timing per activation class (events recorded around each launch when enabled)
 void timer_enable(int on);
 void force_small_tiles(int mode);

@@ -127,6 +127,11 @@ class MLPProjector(nn.Module):
 
 
 class _ProjectorFn(torch.autograd.Function):
+    """Autograd of `self.model(x)` under the reference's bf16 autocast (Stage1/projectors.py:22-29):
+    the parameter grads accumulate into flat_grad (as `.grad` does), and the input grad is
+    dX = ((dY . W2) * gelu'(a)) . W1 -- the chain the reference's autograd takes through fc2, GELU and fc1,
+    with bf16 GEMM operands and the bf16 intermediate dA that autocast produces."""
+
     @staticmethod
     def forward(ctx, x, flat, mod: MLPProjector):
         shp = x.shape
@@ -137,7 +142,7 @@ class _ProjectorFn(torch.autograd.Function):
         out = torch.empty((R, mod.llm_dim), dtype=torch.float32, device=x.device)
         mod.fwd_into(xb, a, h, out)
         ctx.save_for_backward(xb, a, h)
-        ctx.mod = mod
+        ctx.mod, ctx.x_shape, ctx.x_dtype = mod, shp, x.dtype
         return out.view(*shp[:-1], mod.llm_dim)
 
     @staticmethod
@@ -149,4 +154,11 @@ class _ProjectorFn(torch.autograd.Function):
         prev = mod.flat_grad.clone()
         mod.bwd_into(xb, a, h, dy, ws)
         mod.flat_grad.add_(prev)           # accumulate like autograd would
-        return None, None, None
+        dx = None
+        if ctx.needs_input_grad[0]:
+            # dA = (dY . W2) * gelu'(a) (bf16, the fused GELU-backward epilogue), then dX = dA . W1
+            da = K.gemm(dy, mod._w2t, act=L.ACT_GELU_ERF_BWD, aux_in=a)
+            w1t = K.transpose(mod._w1b)   # [Dv, I]: W1 as the K-contiguous B operand
+            dx = K.gemm(da, w1t, out_dtype=torch.float32)
+            dx = dx.view(*ctx.x_shape).to(ctx.x_dtype)
+        return dx, None, None

@@ -223,9 +223,14 @@ class Stage1Engine:
         at this shape must precede the first call.  Inputs are copied into static buffers that the graph reads.
         The optimizer step stays eager: its learning rate and step count are kernel arguments that change every
         step (and the DDP all-reduce runs there).  Same kernels in the same order: bit-identical to step()."""
-        key = (tuple(pixel_values.shape), pixel_values.dtype, tuple(token_ids.shape), tuple(labels.shape))
         if self._prefetched is not None or self._vision_ready:
             raise RuntimeError("Stage1Engine.graph_step: a vision prefetch / encode_vision is pending")
+        self._buffers(*token_ids.shape)
+        # the graph replays the device pointers it was captured with: key it on every buffer it touches, so
+        # a reallocation in between (an eager step at a larger batch or another text length, a grown
+        # workspace) forces a new capture instead of replaying into freed memory
+        key = (tuple(pixel_values.shape), pixel_values.dtype, tuple(token_ids.shape), tuple(labels.shape),
+               self._buffer_fingerprint())
         if self._graph is None or self._graph_key != key:
             self._graph = None
             static = (pixel_values.clone(), token_ids.clone(), labels.clone())
@@ -239,6 +244,20 @@ class Stage1Engine:
         self._graph.replay()
         self.optimizer_step()
         return self.loss
+
+    def _buffer_fingerprint(self):
+        """Device addresses of everything forward_backward reads or writes (step buffers, workspaces,
+        projector shadows) and the vision double-buffer index."""
+        f = self._full
+        ptrs = [t.data_ptr() for k in ("px", "vis") for t in f[k]]
+        ptrs += [f[k].data_ptr() for k in ("a", "h", "x", "dx", "dy")]
+        p = self.proj
+        ptrs += [self.proj_ws.data_ptr(), self.loss.data_ptr(), p.flat.data_ptr(), p.flat_grad.data_ptr()]
+        ptrs += [t.data_ptr() if t is not None else 0 for t in (getattr(p, "_w1b", None), getattr(p, "_w2b", None),
+                                                               getattr(p, "_w2t", None))]
+        ptrs += [self.vision._ws.data_ptr() if self.vision._ws is not None else 0,
+                 self.llm._ws.data_ptr() if self.llm._ws is not None else 0]
+        return (self._cur, self._cap) + tuple(ptrs)
 
     # ---------------------------------------------------------------- builders
     @classmethod

@@ -159,20 +159,23 @@ class Stage2Engine:
     def __init__(self, vision: SiglipVisionTower, llm: Gemma3CausalLM, projector: MLPProjector, *,
                  learning_rate=1e-4, weight_decay=0.01, gradient_accumulation_steps=1, max_grad_norm=1.0,
                  warmup_steps=0, total_steps=1, betas=(0.9, 0.999), eps=1e-8, world_size=1, rank=0,
-                 process_group=None, pad_token_id=None):
+                 process_group=None, pad_token_id=None, zero1=None):
         self.vision, self.llm, self.proj = vision, llm, projector
         self.device = vision.device
         self.lr0, self.wd, self.gas, self.max_norm = learning_rate, weight_decay, gradient_accumulation_steps, max_grad_norm
         self.warmup, self.total, self.betas, self.eps = warmup_steps, total_steps, betas, eps
         self.world, self.rank, self.pg = world_size, rank, process_group
         self.pad_token_id = llm.cfg.pad_token_id if pad_token_id is None else pad_token_id
+        # zero1: reduce-scatter / sharded AdamW / all-gather through the process group (default: world > 1;
+        # True at world 1 runs the same collectives on a one-rank group, which tests the RCCL path on one GPU)
+        self.zero1 = world_size > 1 if zero1 is None else bool(zero1)
         self.state = Gemma3TrainState(llm, world_size)
         o, n = self.state.shard(rank)
         self.shard_lo, self.shard_n = o, n
         self.exp_avg = torch.zeros(n, dtype=torch.bfloat16, device=self.device)
         self.exp_avg_sq = torch.zeros(n, dtype=torch.bfloat16, device=self.device)
-        self._shard_grad = torch.empty(n, dtype=torch.bfloat16, device=self.device) if world_size > 1 else None
-        self._shard_param = torch.empty(n, dtype=torch.bfloat16, device=self.device) if world_size > 1 else None
+        self._shard_grad = torch.empty(n, dtype=torch.bfloat16, device=self.device) if self.zero1 else None
+        self._shard_param = torch.empty(n, dtype=torch.bfloat16, device=self.device) if self.zero1 else None
         self._partial = torch.empty(L.lib().ptk_bf16_sumsq_partial_floats(), dtype=torch.float32, device=self.device)
         self.sumsq = torch.zeros(1, dtype=torch.float32, device=self.device)
         self.grad_norm = torch.zeros(1, dtype=torch.float32, device=self.device)
@@ -203,9 +206,8 @@ class Stage2Engine:
             self._ws = torch.empty(n, dtype=torch.uint8, device=dev)
         self._shape = (B, T)
 
-    def forward_backward(self, pixel_values, question_ids, answer_ids):
-        """One micro-batch: loss (device [1], the mean CE over answer tokens) and grads accumulated
-        (scaled 1/gas^2: the trainer's loss / gas and Accelerator.backward's / gas)."""
+    def _inputs(self, pixel_values, question_ids, answer_ids):
+        """Vision + projector rows of x, token ids and labels, and the batch descriptor."""
         B, Tq = question_ids.shape
         Ta = answer_ids.shape[1]
         T = Tq + Ta
@@ -228,23 +230,36 @@ class Stage2Engine:
         bt = L.Gemma3BatchC(B, T, self.N - 1, self.Sp, ids.data_ptr(), labels.data_ptr(), self.x.data_ptr(),
                             self.dx.data_ptr(), 1.0 / float(self.gas * self.gas), self.loss.data_ptr(), Tq)
         self._ids, self._labels = ids, labels     # alive until the stream has consumed them
+        return cfg, bt
+
+    def forward_backward(self, pixel_values, question_ids, answer_ids):
+        """One micro-batch: loss (device [1], the mean CE over answer tokens) and grads accumulated
+        (scaled 1/gas^2: the trainer's loss / gas and Accelerator.backward's / gas)."""
+        cfg, bt = self._inputs(pixel_values, question_ids, answer_ids)
         L.check(L.lib().ptk_gemma3_train_fwd_bwd(cfg, self.llm.c_w, bt, self.state.c_grads, self._ws.data_ptr(),
                                                  self._ws.numel(), L.stream_ptr(self.device)),
                 "ptk_gemma3_train_fwd_bwd")
+        return self.loss
+
+    def forward_loss(self, pixel_values, question_ids, answer_ids):
+        """Validation loss under no_grad (Stage2/trainer.py:518-591): forward + CE only, no grads touched."""
+        cfg, bt = self._inputs(pixel_values, question_ids, answer_ids)
+        L.check(L.lib().ptk_gemma3_loss_fwd(cfg, self.llm.c_w, bt, self._ws.data_ptr(), self._ws.numel(),
+                                            L.stream_ptr(self.device)), "ptk_gemma3_loss_fwd")
         return self.loss
 
     def optimizer_step(self):
         """DDP grad average (ZeRO-1 reduce-scatter), clip_grad_norm_(max_norm), AdamW, all-gather, schedule."""
         st, stream = self.state, L.stream_ptr(self.device)
         lo, n = self.shard_lo, self.shard_n
-        if self.world > 1:
+        if self.zero1:
             reduce_scatter_(self._shard_grad, st.grad, self.world, self.rank, self.pg)
             g, scale = self._shard_grad, 1.0 / self.world
         else:
             g, scale = st.grad, 1.0
         L.check(L.lib().ptk_bf16_grad_scale_sumsq(g.data_ptr(), n, scale, self._partial.data_ptr(),
                                                   self.sumsq.data_ptr(), stream), "grad_scale_sumsq")
-        if self.world > 1:
+        if self.zero1:
             dist.all_reduce(self.sumsq, op=dist.ReduceOp.SUM, group=self.pg)
         lr = self.lr0 * cosine_lambda(self.sched_step, self.warmup, self.total)
         self.opt_step += 1
@@ -254,14 +269,37 @@ class Stage2Engine:
                                        self.exp_avg_sq.data_ptr(), n, self.sumsq.data_ptr(), self.max_norm, lr, b1,
                                        b2, self.eps, self.wd, self.opt_step, self.grad_norm.data_ptr(), stream),
                 "adamw_bf16")
-        if self.world > 1:
+        if self.zero1:
             self._shard_param.copy_(p)
             all_gather_(st.flat, self._shard_param, self.world, self.pg)
         st.refresh()
         st.zero_grad()
         self.sched_step += self.world
-        self.last_lr = lr
+        self.last_lr = lr       # the LR this optimizer step used (param_groups[0]["lr"] during .step())
         return lr
+
+    @property
+    def scheduler_lr(self):
+        """lr_scheduler.get_last_lr()[0]: the LR after the scheduler stepped num_processes times per optimizer
+        step, i.e. the next step's LR -- what the reference logs as train/learning_rate
+        (Stage2/trainer.py:446-452)."""
+        return self.lr0 * cosine_lambda(self.sched_step, self.warmup, self.total)
+
+    # ------------------------------------------------------------------ optimizer state (ZeRO-1 shards)
+    def optimizer_state(self):
+        """This rank's optimizer shard (moments of params [shard_lo, shard_lo + shard_n) of the flat store)
+        plus the step / schedule counters: every rank's file together is the full AdamW state."""
+        return {"exp_avg": self.exp_avg.cpu(), "exp_avg_sq": self.exp_avg_sq.cpu(), "step": self.opt_step,
+                "sched_step": self.sched_step, "shard": (self.shard_lo, self.shard_n), "world": self.world,
+                "rank": self.rank, "numel": self.state.numel}
+
+    def load_optimizer_state(self, sd):
+        if (sd["world"], sd["rank"], sd["numel"]) != (self.world, self.rank, self.state.numel):
+            raise ValueError(f"optimizer shard of world {sd['world']} rank {sd['rank']} (store {sd['numel']}) does "
+                             f"not match this engine (world {self.world} rank {self.rank} store {self.state.numel})")
+        self.exp_avg.copy_(sd["exp_avg"])
+        self.exp_avg_sq.copy_(sd["exp_avg_sq"])
+        self.opt_step, self.sched_step = int(sd["step"]), int(sd["sched_step"])
 
 
 def synthetic_engine(cfg, device="cuda", seed=0, **kw):

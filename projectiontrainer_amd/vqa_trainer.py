@@ -145,43 +145,67 @@ class VQATrainerStage2:
                     epoch_train_loss += avg_loss_step
                     log["train/step_loss"] = avg_loss_step
                 log.update({"train/batch_loss": float(acc.gather(loss).mean()),
-                            "train/learning_rate": self.engine.last_lr, "step": self.global_step})
+                            "train/learning_rate": self.engine.scheduler_lr, "step": self.global_step})
                 self._log(log, self.global_step)
             avg = epoch_train_loss / max(1, n_local)      # len(self.train_loader) (Stage2/trainer.py:468)
-            self._log({"train/loss": avg, "train/learning_rate": self.engine.last_lr, "epoch": epoch + 1},
+            self._log({"train/loss": avg, "train/learning_rate": self.engine.scheduler_lr, "epoch": epoch + 1},
                       self.global_step)
             if self.val_dataset is not None:
                 self.evaluate(epoch, self.global_step)
-            if acc.is_main_process:
-                self.save_model(os.path.join(self.output_dir, f"checkpoint-epoch_{epoch + 1}"))
+            # every rank: each writes its ZeRO-1 optimizer shard (the reference's save_state keeps the full
+            # optimizer); the main process writes the model and tokenizer
+            self.save_model(os.path.join(self.output_dir, f"checkpoint-epoch_{epoch + 1}"))
         logger.info("Process %d: Stage 2 training complete!", acc.process_index)
 
     def evaluate(self, epoch, global_step):
-        """Validation loss (Stage2/trainer.py:490-593; the sampled generate() is out of scope).  The grads the
-        loss pass accumulates are discarded."""
-        tot, n = 0.0, 0
-        for batch in self._batches(self.val_dataset, 0, shuffle=False):
-            loss = self.engine.forward_backward(batch["pixel_values"], batch["question_input_ids"],
+        """Validation loss (Stage2/trainer.py:490-593; the sampled generate() is out of scope): forward + CE
+        only, as under the reference's torch.no_grad (no grads touched).  As the reference, the batches are
+        collated with the tokenizer padding on the LEFT (restored afterwards) and a missing pad token falls
+        back to eos (:499-507)."""
+        tok = self.tokenizer
+        side = getattr(tok, "padding_side", "right")
+        pad0 = getattr(tok, "pad_token_id", None)
+        tok.padding_side = "left"
+        if pad0 is None:
+            logger.warning("Tokenizer pad_token_id is None. Setting to eos_token_id for evaluation.")
+            tok.pad_token_id = tok.eos_token_id
+        eng_pad = self.engine.pad_token_id
+        self.engine.pad_token_id = int(tok.pad_token_id)
+        try:
+            tot, n = 0.0, 0
+            for batch in self._batches(self.val_dataset, 0, shuffle=False):
+                loss = self.engine.forward_loss(batch["pixel_values"], batch["question_input_ids"],
                                                 batch["answer_input_ids"])
-            tot += float(self.accelerator.gather(loss).mean())
-            n += 1
-        self.engine.state.zero_grad()
+                tot += float(self.accelerator.gather(loss).mean())
+                n += 1
+        finally:
+            tok.padding_side = side
+            self.engine.pad_token_id = eng_pad
         avg = tot / max(1, n)
         self._log({"val/loss": avg, "epoch": epoch + 1}, global_step)
         return avg
 
     def save_model(self, path):
-        """language_model/model.safetensors (HF names, bf16) + this rank's optimizer state."""
-        if not self.accelerator.is_main_process:
-            return
-        from safetensors.torch import save_file
-        llm_dir = os.path.join(path, "language_model")
-        os.makedirs(llm_dir, exist_ok=True)
+        """Called on EVERY rank.  Main process: language_model/model.safetensors (HF names, bf16) and the
+        tokenizer (Stage2/trainer.py:740-742).  Every rank: optimizer_rank{r}.pt with its ZeRO-1 shard of the
+        AdamW moments and the step / schedule counters, so the files of all ranks hold the complete optimizer
+        state that the reference's accelerator.save_state writes (:718); load with load_optimizer_state."""
+        acc = self.accelerator
+        os.makedirs(path, exist_ok=True)
         torch.cuda.synchronize(self.device)
-        sd = {k: v.detach().contiguous().cpu() for k, v in self.engine.state.state_dict_hf().items()}
-        save_file(sd, os.path.join(llm_dir, "model.safetensors"))
-        eng = self.engine
-        torch.save({"exp_avg": eng.exp_avg.cpu(), "exp_avg_sq": eng.exp_avg_sq.cpu(), "step": eng.opt_step,
-                    "sched_step": eng.sched_step, "shard": (eng.shard_lo, eng.shard_n)},
-                   os.path.join(path, f"optimizer_rank{self.accelerator.process_index}.pt"))
-        logger.info("Full language model saved to %s", llm_dir)
+        torch.save(self.engine.optimizer_state(), os.path.join(path, f"optimizer_rank{acc.process_index}.pt"))
+        if acc.is_main_process:
+            from safetensors.torch import save_file
+            llm_dir = os.path.join(path, "language_model")
+            os.makedirs(llm_dir, exist_ok=True)
+            sd = {k: v.detach().contiguous().cpu() for k, v in self.engine.state.state_dict_hf().items()}
+            save_file(sd, os.path.join(llm_dir, "model.safetensors"))
+            if hasattr(self.tokenizer, "save_pretrained"):
+                self.tokenizer.save_pretrained(llm_dir)
+            logger.info("Full language model saved to %s", llm_dir)
+        acc.wait_for_everyone()
+
+    def load_optimizer_state(self, path):
+        """Restore this rank's ZeRO-1 optimizer shard written by save_model."""
+        sd = torch.load(os.path.join(path, f"optimizer_rank{self.accelerator.process_index}.pt"), weights_only=True)
+        self.engine.load_optimizer_state(sd)

@@ -200,4 +200,31 @@ def stage2_zero(rank, world, port, out_dir):
     torch.cuda.synchronize()
     np.save(os.path.join(out_dir, f"s2param{rank}.npy"), eng.state.flat.float().cpu().numpy())
     np.save(os.path.join(out_dir, f"s2norm{rank}.npy"), eng.grad_norm.cpu().numpy())
+    torch.save(eng.optimizer_state(), os.path.join(out_dir, f"opt{rank}.pt"))
+    dist.destroy_process_group()
+
+
+def stage2_rccl_world1(rank, world, port, out_dir):
+    """RCCL at world 1: Stage2Engine with zero1=True (reduce-scatter / all-gather / norm all-reduce through
+    the nccl process group) vs zero1=False, same batch, one optimizer step each."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.stage2 import synthetic_engine
+    cfg = PRESETS["tiny"].replace(batch_size=2, text_len=8 + 12, question_len=8)
+    px, q, a = (torch.from_numpy(t).to(dev) for t in W.synthetic_vqa_batch(cfg, seed=9))
+    out = []
+    for z in (True, False):
+        torch.manual_seed(0)
+        eng = synthetic_engine(cfg, dev, seed=3, learning_rate=1e-3, total_steps=10, zero1=z)
+        eng.forward_backward(px, q, a)
+        eng.optimizer_step()
+        torch.cuda.synchronize()
+        out.append((eng.state.flat.clone(), eng.exp_avg.clone(), eng.grad_norm.clone()))
+    ok = [dist.get_backend() == "nccl", torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1]),
+          torch.equal(out[0][2], out[1][2])]
+    np.save(os.path.join(out_dir, "rccl.npy"), np.array(ok, dtype=np.int64))
     dist.destroy_process_group()

@@ -41,3 +41,26 @@ def test_graph_step_bit_identical_to_eager(gpu, preset):
         assert torch.equal(eager.proj.flat_grad, graphed.proj.flat_grad), k
         assert torch.equal(eager.proj.flat, graphed.proj.flat), k
     assert graphed._graph is not None
+
+
+def test_graph_step_recaptures_after_reallocation(gpu):
+    """A graph captured at bs 2 must not be replayed after an eager step at bs 4 reallocated the step
+    buffers and workspaces (the captured pointers are freed): graph_step recaptures, and the sequence
+    graph(bs 2) -> eager(bs 4) -> graph(bs 2) stays bit-identical to the all-eager sequence."""
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    cfg2, cfg4 = PRESETS["tiny"].replace(batch_size=2), PRESETS["tiny"].replace(batch_size=4)
+    b2 = [tuple(torch.from_numpy(a).to(gpu) for a in W.synthetic_batch(cfg2, seed=40 + s)) for s in range(3)]
+    b4 = tuple(torch.from_numpy(a).to(gpu) for a in W.synthetic_batch(cfg4, seed=50))
+    eager, graphed = _engine(cfg2, gpu), _engine(cfg2, gpu)
+    seq = [("e", b2[0]), ("g", b2[1]), ("e", b4), ("g", b2[2]), ("g", b2[0])]
+    keys = []
+    for mode, b in seq:
+        le = float(eager.step(*b))
+        lg = float(graphed.step(*b) if mode == "e" else graphed.graph_step(*b))
+        torch.cuda.synchronize()
+        assert le == lg, (mode, le, lg)
+        assert torch.equal(eager.proj.flat, graphed.proj.flat)
+        keys.append(graphed._graph_key)
+    assert keys[1] is not None and keys[3] != keys[1], "bs-4 reallocation did not force a recapture"
+    assert keys[4] == keys[3]

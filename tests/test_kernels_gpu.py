@@ -112,6 +112,47 @@ def test_gemm_geglu_and_bwd(gpu):
     torch.testing.assert_close(du.float(), uu.grad, rtol=3e-2, atol=3e-2)
 
 
+@pytest.mark.parametrize("M", [4608, 5632])
+def test_gemm_geglu_and_bwd_persistent_vs_fp32(gpu, M):
+    """The GEGLU gate|up and dh + GEGLU-backward epilogues at the row counts where launch_gemm selects the
+    persistent kernels (M >= 4096, Gemma3-1B widths H 1152, I 2304 / 6912 cut to fit), vs torch fp32 of the
+    same math (modeling_gemma3.py:131-133: down(gelu_tanh(gate(x)) * up(x)) and its autograd); the census
+    asserts which kernel family ran."""
+    Kn, L = _k()
+    from projectiontrainer_amd.gemma3 import interleave_gate_up
+    H, I = 1152, 2304
+    x = rnd(M, H, dev=gpu, seed=81)
+    Wg, Wu = rnd(I, H, dev=gpu, seed=82, scale=0.03), rnd(I, H, dev=gpu, seed=83, scale=0.03)
+    Wgu = interleave_gate_up(Wg, Wu)
+    g = torch.empty(M, I, dtype=torch.bfloat16, device=gpu)
+    u = torch.empty_like(g)
+    L.gemm_path_counts(reset=True)
+    h = Kn.gemm(x, Wgu, act=L.ACT_GEGLU, aux=g, aux2=u)
+    torch.cuda.synchronize()
+    fwd_paths = L.gemm_path_counts(reset=True)
+    gr, ur = (x.float() @ Wg.float().T), (x.float() @ Wu.float().T)
+    torch.testing.assert_close(g.float(), gr, rtol=1e-2, atol=1e-2)
+    torch.testing.assert_close(u.float(), ur, rtol=1e-2, atol=1e-2)
+    href = F.gelu(g.float(), approximate="tanh").to(torch.bfloat16).float() * u.float()
+    torch.testing.assert_close(h.float(), href, rtol=2e-2, atol=2e-2)
+    y = rnd(M, H, dev=gpu, seed=84)
+    Wd = rnd(H, I, dev=gpu, seed=85, scale=0.03)
+    Wd_t = Wd.T.contiguous()
+    dgu = Kn.gemm(y, Wd_t, act=L.ACT_GEGLU_BWD, aux_in=g, aux_in2=u)
+    torch.cuda.synchronize()
+    bwd_paths = L.gemm_path_counts(reset=True)
+    dh = (y.float() @ Wd.float()).to(torch.bfloat16).float()
+    gg, uu = g.float().requires_grad_(True), u.float().requires_grad_(True)
+    (F.gelu(gg, approximate="tanh") * uu).backward(dh)
+    dg = dgu.view(M, I // 16, 2, 16)[:, :, 0].reshape(M, I)
+    du = dgu.view(M, I // 16, 2, 16)[:, :, 1].reshape(M, I)
+    torch.testing.assert_close(dg.float(), gg.grad, rtol=3e-2, atol=3e-2)
+    torch.testing.assert_close(du.float(), uu.grad, rtol=3e-2, atol=3e-2)
+    persistent = {"w4", "p8"}
+    assert any(p in persistent and a == L.ACT_GEGLU for p, a in fwd_paths), fwd_paths
+    assert any(p in persistent and a == L.ACT_GEGLU_BWD for p, a in bwd_paths), bwd_paths
+
+
 def test_gemm_batched_strided(gpu):
     Kn, L = _k()
     Bz, H, S, D = 3, 2, 96, 64
@@ -451,22 +492,33 @@ def test_qknorm_rope_fwd_bwd(gpu, Hq, Hkv, D):
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 1024, 1152), (4096, 2304, 640), (2304, 3072, 1024), (513, 896, 1280),
-                                   (22528, 1152, 1152)])
-def test_gemm_pingpong_matches_w4(gpu, M, N, K):
-    """Ping-pong 8-wave kernel (forced mode 32; 256x128 tiles, several per workgroup, ragged M/N) against the
-    persistent 4-wave kernel (mode 8): same k-step order per output element, so every epilogue (plain bf16 /
-    fp32 / fp32-rounded, GEGLU with g, u side outputs, GEGLU backward into the interleaved dg|du layout) is
-    bit-identical; plain fp32 also against torch fp32.  The shapes give 1 to 3 tiles per workgroup (odd and
-    even counts: the last tile's epilogue falls to either wave group)."""
+                                   (22528, 1152, 1152), (300, 256, 128), (4608, 13824, 1152)])
+def test_gemm_p8_matches_w4(gpu, M, N, K):
+    """Persistent 8-wave kernel (forced mode 32: two waves per SIMD, 128x64 per wave, several tiles per
+    workgroup, ragged M/N) against the persistent 4-wave kernel (mode 8): the same k-step order per output
+    element, so every epilogue -- plain bf16 / fp32 / fp32-rounded, bias + residual, GELU-tanh, GELU-erf
+    with its pre-activation, GELU-erf backward, GEGLU with g, u side outputs, GEGLU backward into the
+    interleaved dg|du layout -- is bit-identical; plain fp32 also against torch fp32."""
     Kn, L = _k()
     A, B = rnd(M, K, dev=gpu, seed=11), rnd(N, K, dev=gpu, seed=12, scale=0.05)
     gin, uin = rnd(M, N, dev=gpu, seed=13), rnd(M, N, dev=gpu, seed=14)
+    bias = rnd(N, dev=gpu, dtype=torch.float32, seed=15)
+    res = rnd(M, N, dev=gpu, dtype=torch.float32, seed=16)
     outs = []
     for md in (8, 32):
         L.lib().ptk_gemm_force_small_tiles(md)
+        L.gemm_path_counts(reset=True)
         try:
             o = {"f32": Kn.gemm(A, B, out_dtype=torch.float32), "bf16": Kn.gemm(A, B),
                  "f32r": Kn.gemm(A, B, C=torch.empty(M, N, device=gpu), out_mode=L.OUT_F32_BF16ROUND)}
+            C = res.clone()
+            Kn.gemm(A, B, C=C, bias=bias, resid=C)
+            o["resid"] = C
+            o["gelu_tanh"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_TANH)
+            aux = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
+            o["gelu_erf"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_ERF, aux=aux)
+            o["aux"] = aux
+            o["erf_bwd"] = Kn.gemm(A, B, act=L.ACT_GELU_ERF_BWD, aux_in=gin)
             if N % 32 == 0:
                 g = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=gpu)
                 u = torch.zeros_like(g)
@@ -474,19 +526,41 @@ def test_gemm_pingpong_matches_w4(gpu, M, N, K):
                 o["g"], o["u"] = g, u
             o["dgdu"] = Kn.gemm(A, B, act=L.ACT_GEGLU_BWD, aux_in=gin, aux_in2=uin)
             torch.cuda.synchronize()
+            paths = {p for p, _ in L.gemm_path_counts(reset=True)}
+            assert paths == {"w4" if md == 8 else "p8"}, paths
             outs.append(o)
         finally:
             L.lib().ptk_gemm_force_small_tiles(0)
-    ref = A.float() @ B.float().T
     for k in outs[0]:
-        a, b = outs[0][k], outs[1][k]
-        if not torch.equal(a, b):
-            bad = (a != b).nonzero()
-            d = (a.float() - b.float()).abs()
-            msg = (f"{k}: {bad.shape[0]} of {a.numel()} differ, max |d| {d.max().item():.3g}; rows%256 "
-                   f"{sorted(set((bad[:, 0] % 256).tolist()))[:24]} cols%128 {sorted(set((bad[:, 1] % 128).tolist()))[:24]} "
-                   f"first {bad[:4].tolist()}")
-            if k == "f32":
-                msg += (f"; |w4 - ref| {(a - ref).abs().max().item():.3g} |pp - ref| {(b - ref).abs().max().item():.3g}")
-            raise AssertionError(msg)
+        assert torch.equal(outs[0][k], outs[1][k]), (k, (outs[0][k].float() - outs[1][k].float()).abs().max())
+    ref = A.float() @ B.float().T
     torch.testing.assert_close(outs[1]["f32"], ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
+
+
+def test_projector_module_autograd(gpu):
+    """MLPProjector as an nn.Module under autograd (the public API, Stage1/projectors.py:22-29): output,
+    parameter grads and the INPUT grad vs torch fp32 autograd of the same Sequential(Linear, GELU, Linear);
+    bf16 GEMM operands (autocast semantics) bound the difference."""
+    from projectiontrainer_amd.projectors import MLPProjector
+    torch.manual_seed(0)
+    Dv, Dl = 64, 128
+    proj = MLPProjector(Dv, Dl, expansion_factor=4)
+    ref = torch.nn.Sequential(torch.nn.Linear(Dv, 4 * Dv), torch.nn.GELU(), torch.nn.Linear(4 * Dv, Dl))
+    ref.load_state_dict(proj.model.state_dict())
+    proj.to(gpu)
+    x = rnd(3, 40, Dv, dev=gpu, dtype=torch.float32, seed=91)
+    xr = x.detach().clone().requires_grad_(True)
+    x = x.detach().clone().requires_grad_(True)
+    out = proj(x)
+    w = rnd(3, 40, Dl, dev=gpu, dtype=torch.float32, seed=92)
+    (out * w).sum().backward()
+    ref = ref.to(gpu)
+    outr = ref(xr)
+    (outr * w).sum().backward()
+    torch.testing.assert_close(out, outr, rtol=3e-2, atol=3e-2)
+    assert x.grad is not None and x.grad.shape == x.shape
+    cos = F.cosine_similarity(x.grad.flatten(), xr.grad.flatten(), dim=0)
+    assert cos > 0.999, cos
+    torch.testing.assert_close(x.grad, xr.grad, rtol=5e-2, atol=5e-2 * xr.grad.abs().max().item())
+    for g, p in zip(proj.grads(), [ref[0].weight, ref[0].bias, ref[2].weight, ref[2].bias]):
+        assert F.cosine_similarity(g.flatten(), p.grad.flatten(), dim=0) > 0.999

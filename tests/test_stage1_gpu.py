@@ -157,14 +157,43 @@ def test_two_steps_vs_reference_golden(gpu, name):
             compare(d, f"s{s}_param.{k}", p, None, atol=2.5 * lr_sum + 1e-6, med=0.05 * meta["lr"], test=t)
 
 
+def _census(run):
+    """GEMM kernel families (path, act class) one call dispatches (ptk_gemm_path_counts)."""
+    from projectiontrainer_amd import _lib as L
+    L.gemm_path_counts(reset=True)
+    run()
+    torch.cuda.synchronize()
+    return set(L.gemm_path_counts(reset=True))
+
+
+def _bench_census(gpu):
+    """The dispatch of the benchmarked step (cfg2 at bs 32, bench.py's workload), HIP only."""
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.stage1 import Stage1Engine
+    cfg = PRESETS["cfg2"]
+    eng = Stage1Engine.synthetic(cfg, gpu, seed=0)
+    from projectiontrainer_amd import weights as W
+    px, ids, labels = W.synthetic_batch(cfg, seed=7, max_pad=40)
+    args = [torch.from_numpy(t).to(gpu) for t in (px, ids, labels)]
+    eng.forward_backward(*args)       # buffers allocated outside the census
+    got = _census(lambda: eng.forward_backward(*args))
+    del eng
+    torch.cuda.empty_cache()
+    return got
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("preset,bs,T,vl,tl", [("cfg2", 2, 128, None, None), ("cfg2", 1, 512, None, None),
-                                               ("cfg5", 1, 256, 2, 6)])
+                                               ("cfg2", 8, 128, None, None), ("cfg5", 1, 256, 2, 6)])
 def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
     """Full architecture vs the fp32 CPU oracle (the oracle is pinned to the reference by the fixtures).
     cfg2: SigLIP-L/16-384 (24 layers) + Gemma3-1B (26 layers) at bs 2, T 128 (S = 703 > window 512,
     left-padded captions), and at the reference's default caption length T = 512
     (train_projection_stage1.py:27; S = 1087, bs 1).
+    cfg2 at bs 8 (M = 5 632 token rows): the GEMM dispatch of the benchmarked bs-32 step -- the persistent
+    gate|up GEGLU and dh + GEGLU-backward kernels, the long-K d(gate|up) dX kernel -- which the small
+    batches never select; the test asserts that every kernel family (path, epilogue) the bs-32 step
+    launches also ran in this compared step.
     cfg5: Gemma3-4B dims (hidden 2560, GQA 8:4, window 1024, linear RoPE x8 on the full layer, vocab
     262 208 = 4 097 x 64, which leaves a remainder slice in the split-K lm_head backward) at 2 SigLIP and
     6 Gemma layers, bs 1, T 256.
@@ -193,8 +222,10 @@ def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
     proj.load_state_dict({k: torch.from_numpy(v) for k, v in pp.items()})
     proj.to(gpu)
     eng = Stage1Engine(vt, lm, proj, gradient_accumulation_steps=1)
-    loss = eng.forward_backward(torch.from_numpy(px).to(gpu), torch.from_numpy(ids).to(gpu),
-                                torch.from_numpy(labels).to(gpu))
+    run = lambda: eng.forward_backward(torch.from_numpy(px).to(gpu), torch.from_numpy(ids).to(gpu),
+                                       torch.from_numpy(labels).to(gpu))
+    paths = _census(run)
+    loss = eng.loss
     torch.cuda.synchronize()
     N, Nv = cfg.vision.num_patches, cfg.num_vision_tokens
     vis = eng.vis.view(bs, N, -1)[:, 1:].float().cpu()
@@ -204,6 +235,12 @@ def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
     loss = float(loss)
     del eng, lm, vt
     torch.cuda.empty_cache()
+    if bs == 8:
+        bench = _bench_census(gpu)
+        record(f"arch[{preset}-bs{bs}-T{T}]", "paths", n_bench=len(bench), n_here=len(paths),
+               missing=len(bench - paths))
+        assert bench <= paths, ("kernel families of the bs-32 step not exercised", sorted(bench - paths))
+        assert ("w4", 3) in paths and ("w4", 5) in paths, sorted(paths)   # gate|up GEGLU, dh + GEGLU bwd
     torch.set_num_threads(min(16, torch.get_num_threads()))
     st = R.init_state(pp)
     out = R.stage1_step(vp, cfg.vision, lp, cfg.text, st, (px, ids, labels), R.StepConfig(gradient_accumulation_steps=1),

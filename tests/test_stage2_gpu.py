@@ -170,6 +170,7 @@ def test_stage2_zero1_two_ranks_match_single_process(gpu):
         mp.spawn(dist_worker.stage2_zero, args=(2, _port(), td), nprocs=2, join=True)
         p0, p1 = np.load(f"{td}/s2param0.npy"), np.load(f"{td}/s2param1.npy")
         n0 = np.load(f"{td}/s2norm0.npy")
+        shards = [torch.load(f"{td}/opt{r}.pt", weights_only=True) for r in range(2)]
     np.testing.assert_array_equal(p0, p1)
     cfg = PRESETS["tiny"].replace(batch_size=4, text_len=8 + 12, question_len=8)
     torch.manual_seed(0)
@@ -195,6 +196,12 @@ def test_stage2_zero1_two_ranks_match_single_process(gpu):
     np.testing.assert_array_equal(flat[:n][mask], p0[:n][mask])
     assert np.abs(flat[e0:e1] - p0[e0:e1]).max() <= 2e-3
     np.testing.assert_allclose(float(eng.grad_norm), float(n0[0]), rtol=1e-6)
+    # the two ranks' saved optimizer shards together are the single process's AdamW moments
+    for key in ("exp_avg", "exp_avg_sq"):
+        both = torch.cat([sh[key] for sh in shards]).float().numpy()
+        one = getattr(eng, key).float().cpu().numpy()
+        np.testing.assert_array_equal(both[:n][mask], one[:n][mask])
+    assert [sh["shard"] for sh in shards] == [(0, p0.size // 2), (p0.size // 2, p0.size // 2)]
 
 
 def test_vqa_trainer_api_with_hf_models(gpu, tmp_path):
@@ -266,11 +273,116 @@ def test_vqa_trainer_api_with_hf_models(gpu, tmp_path):
                                  bt["answer_input_ids"].to(gpu))
             if (i + 1) % 2 == 0 or i + 1 == len(idx):
                 eng.optimizer_step()
-        # evaluate() runs a loss pass over the validation set and discards its grads
+        # evaluate() runs a forward + loss pass over the validation set (no grads)
+        vl = []
         for b in D.shard_batches(2, 2, 0, 1, 0, 0, False):
             bt = vqa_collate_fn([data[int(j)] for j in b], tok)
-            eng.forward_backward(bt["pixel_values"].to(gpu), bt["question_input_ids"].to(gpu),
-                                 bt["answer_input_ids"].to(gpu))
-        eng.state.zero_grad()
+            vl.append(float(eng.forward_loss(bt["pixel_values"].to(gpu), bt["question_input_ids"].to(gpu),
+                                             bt["answer_input_ids"].to(gpu))))
+        assert [x["val/loss"] for x in logs if "val/loss" in x][epoch] == sum(vl) / len(vl)
     torch.cuda.synchronize()
     assert torch.equal(eng.state.flat, tr.engine.state.flat)
+    # the optimizer shard (the whole state at world 1) is saved and restores into a fresh engine
+    st = torch.load(str(tmp_path / "checkpoint-epoch_2" / "optimizer_rank0.pt"), weights_only=True)
+    assert torch.equal(st["exp_avg"], tr.engine.exp_avg.cpu()) and torch.equal(st["exp_avg_sq"], tr.engine.exp_avg_sq.cpu())
+    assert (st["step"], st["sched_step"]) == (4, 4)
+    eng.exp_avg.zero_()
+    eng.load_optimizer_state(st)
+    assert torch.equal(eng.exp_avg, tr.engine.exp_avg) and eng.opt_step == 4
+    # the reference logs lr_scheduler.get_last_lr() (the next step's LR) as train/learning_rate
+    assert [x["train/learning_rate"] for x in logs if "train/loss" in x][-1] == tr.engine.scheduler_lr
+
+
+def test_stage2_forward_loss_matches_train_loss(gpu):
+    """ptk_gemma3_loss_fwd (validation, no grads) returns the same loss as the training pass and leaves the
+    grad store untouched."""
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.stage2 import synthetic_engine
+    cfg = PRESETS["tiny"].replace(batch_size=4, text_len=8 + 12, question_len=8)
+    eng = synthetic_engine(cfg, gpu, seed=3, learning_rate=1e-3, total_steps=10)
+    px, q, a = (torch.from_numpy(t).to(gpu) for t in W.synthetic_vqa_batch(cfg, seed=9))
+    lv = float(eng.forward_loss(px, q, a))
+    torch.cuda.synchronize()
+    assert not eng.state.grad.any()
+    lt = float(eng.forward_backward(px, q, a))
+    assert lv == lt, (lv, lt)
+
+
+def test_stage2_zero1_rccl_world1(gpu):
+    """The ZeRO-1 collectives on RCCL ("nccl" backend, bf16 reduce_scatter_tensor / all_gather_into_tensor,
+    fp32 all-reduce of the squared norm) at world 1 on the GPU: bit-identical to the collective-free step."""
+    import tempfile
+    import torch.multiprocessing as mp
+    from tests import dist_worker
+    from tests.test_dist import _port
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(dist_worker.stage2_rccl_world1, args=(1, _port(), td), nprocs=1, join=True)
+        r = np.load(f"{td}/rccl.npy")
+    assert r[0] == 1 and r[1] == 1 and r[2] == 1, r
+
+
+@pytest.mark.slow
+def test_stage2_architecture_scale_vs_oracle(gpu):
+    """Stage 2 at cfg4's architecture (SigLIP-L/16-384 + Gemma3-1B widths, full vocab 262 144, question 64
+    + answer 256 tokens, S = 895 > the 512-token window) at reduced depth (2 SigLIP, 6 Gemma layers: five
+    sliding and one global) and bs 2, one micro-batch and one optimizer step, vs oracle/stage2_ref.py (pinned
+    to the reference's VQATrainerStage2 by tests/test_stage2_oracle.py).  The oracle runs fp32 from the same
+    bf16-valued weights (the reference's bf16-loaded LLM, train_vqa_stage2.py:141-147); no twin fixture
+    exists at these sizes, so the bars are SURVEY.md:297's with rel-L2 on the weight grads widened to 6e-2
+    (the bf16-vs-fp32 distance the s2_tiny twins show, tests/golden/s2_tiny*.npz: up to 0.05); params
+    after AdamW within 2.5 lr + 1 bf16 ulp (Adam moves each weight by ~lr; bf16 parameters)."""
+    from oracle import stage2_ref as S
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.gemma3 import Gemma3CausalLM
+    from projectiontrainer_amd.projectors import MLPProjector
+    from projectiontrainer_amd.siglip import SiglipVisionTower
+    from projectiontrainer_amd.stage2 import Stage2Engine
+    cfg = PRESETS["cfg4"]
+    cfg = cfg.replace(vision=cfg.vision.__class__(**{**cfg.vision.__dict__, "num_hidden_layers": 2}),
+                      text=cfg.text.__class__(**{**cfg.text.__dict__, "num_hidden_layers": 6}), batch_size=2)
+    vp = {k: G.bf16_round(v) for k, v in W.siglip_vision_params(cfg.vision, seed=3).items()}
+    lp = {k: G.bf16_round(v) for k, v in W.gemma3_params(cfg.text, seed=4).items()}
+    pp = {k: G.bf16_round(v) for k, v in W.projector_params(cfg.vision.hidden_size, cfg.text.hidden_size,
+                                                            seed=5).items()}
+    px, q, a = W.synthetic_vqa_batch(cfg, seed=17, padding_side="left")
+    lr = 1e-4
+    proj = MLPProjector(cfg.vision.hidden_size, cfg.text.hidden_size)
+    proj.load_state_dict({k: torch.from_numpy(v) for k, v in pp.items()})
+    proj.to(gpu)
+    eng = Stage2Engine(SiglipVisionTower(cfg.vision, vp, gpu),
+                       Gemma3CausalLM(cfg.text, lp, gpu, max_pos=Gemma3CausalLM.seq_pad(cfg.seq_len)), proj,
+                       learning_rate=lr, weight_decay=0.01, max_grad_norm=1.0, warmup_steps=0, total_steps=10,
+                       pad_token_id=cfg.text.pad_token_id)
+    loss = float(eng.forward_backward(*(torch.from_numpy(t).to(gpu) for t in (px, q, a))))
+    torch.cuda.synchronize()
+    grads = {k: v.float().cpu() for k, v in eng.state.state_dict_hf(grads=True).items()}
+    eng.optimizer_step()
+    torch.cuda.synchronize()
+    params = {k: v.float().cpu() for k, v in eng.state.state_dict_hf().items()}
+    del eng
+    torch.cuda.empty_cache()
+    torch.set_num_threads(min(16, torch.get_num_threads()))
+    st = S.Stage2State(lp)
+    ref_loss = S.stage2_loss({k: torch.from_numpy(v) for k, v in vp.items()}, cfg.vision, st.params, cfg.text,
+                             {k: torch.from_numpy(v) for k, v in pp.items()},
+                             torch.from_numpy(px).bfloat16().float(),   # the tower's input cast (trainer.py:313-332)
+                             torch.from_numpy(q), torch.from_numpy(a), cfg.text.pad_token_id)
+    ref_loss.backward()
+    rec = S.optimizer_step(st, lr, 0, 10)
+    t = "stage2_arch[cfg4-L6-bs2]"
+    record(t, "loss", abs=abs(loss - float(ref_loss)))
+    assert abs(loss - float(ref_loss)) <= 2e-2, (loss, float(ref_loss))
+    worst = 0.0
+    for n, g in rec["grads"].items():
+        r, c = rel_l2(grads[n].numpy(), g.numpy()), cosine(grads[n].numpy(), g.numpy())
+        record(t, "grad." + n, rel_l2=r, cos=c, tol_rel_l2=6e-2, tol_cos=0.998)
+        worst = max(worst, r)
+        assert r <= 6e-2 and c >= 0.998, (n, r, c)
+    for n, p in st.params.items():
+        ref = p.detach().numpy()
+        ulp = 2.0 ** (np.floor(np.log2(max(np.abs(ref).max(), 1e-30))) - 7)
+        mx = np.abs(params[n].numpy() - ref).max()
+        record(t, "param." + n, max_abs=mx, atol=2.5 * lr + ulp)
+        assert mx <= 2.5 * lr + ulp, (n, mx)

@@ -1,0 +1,81 @@
+"""Persistent 4-wave (mode 8) vs persistent 8-wave (mode 32) vs the automatic dispatch (mode 0) on the GEMM
+shapes of the cfg2 / cfg4 steps: HIP-event time per launch, TFLOP/s, rounds interleaved (one process)."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from projectiontrainer_amd import kernels as K, _lib as L  # noqa: E402
+
+dev = torch.device("cuda:0")
+M1, M2, MS = 32 * 704, 16 * 896, 32 * 576
+SHAPES = [  # name, M, N, K, act, out dtype
+    ("g_gu_geglu", M1, 13824, 1152, L.ACT_GEGLU, torch.bfloat16),
+    ("g_dh_geglu_bwd", M1, 6912, 1152, L.ACT_GEGLU_BWD, torch.bfloat16),
+    ("g_down", M1, 1152, 6912, L.ACT_NONE, torch.bfloat16),
+    ("g_dgu_dx", M1, 1152, 13824, L.ACT_NONE, torch.bfloat16),
+    ("g_qkv", M1, 1536, 1152, L.ACT_NONE, torch.bfloat16),
+    ("g_o", M1, 1152, 1024, L.ACT_NONE, torch.bfloat16),
+    ("g_dO", M1, 1024, 1152, L.ACT_NONE, torch.bfloat16),
+    ("g_dqkv", M1, 1152, 1536, L.ACT_NONE, torch.bfloat16),
+    ("lm_head", 4096, 262144, 1152, L.ACT_NONE, torch.bfloat16),
+    ("sig_qkv", MS, 3072, 1024, L.ACT_NONE, torch.bfloat16),
+    ("sig_fc1", MS, 4096, 1024, L.ACT_GELU_TANH, torch.bfloat16),
+    ("sig_fc2", MS, 1024, 4096, L.ACT_NONE, torch.bfloat16),
+    ("proj_fc1", MS, 11520, 1024, L.ACT_GELU_ERF, torch.bfloat16),
+    ("proj_fc2", MS, 1152, 11520, L.ACT_NONE, torch.float32),
+    ("sq8192", 8192, 8192, 8192, L.ACT_NONE, torch.bfloat16),
+]
+
+
+def setup(m, n, k, act, odt):
+    A = torch.randn(m, k, device=dev).to(torch.bfloat16)
+    B = (torch.randn(n, k, device=dev) * 0.05).to(torch.bfloat16)
+    kw = {}
+    if act == L.ACT_GEGLU:
+        kw = dict(aux=torch.empty(m, n // 2, dtype=torch.bfloat16, device=dev),
+                  aux2=torch.empty(m, n // 2, dtype=torch.bfloat16, device=dev))
+    elif act == L.ACT_GEGLU_BWD:
+        kw = dict(aux_in=torch.randn(m, n, device=dev).to(torch.bfloat16),
+                  aux_in2=torch.randn(m, n, device=dev).to(torch.bfloat16))
+    elif act == L.ACT_GELU_ERF:
+        kw = dict(aux=torch.empty(m, n, dtype=torch.bfloat16, device=dev))
+    return A, B, kw
+
+
+def timed(A, B, kw, act, odt, C, reps):
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        K.gemm(A, B, C=C, out_dtype=odt, act=act, **kw)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / reps
+
+
+only = set(a for a in sys.argv[1:] if not a.startswith("-"))
+modes = (8, 32, 0)
+for name, m, n, k, act, odt in SHAPES:
+    if only and name not in only:
+        continue
+    A, B, kw = setup(m, n, k, act, odt)
+    C = K.gemm(A, B, out_dtype=odt, act=act, **kw)
+    reps = max(3, min(50, int(2e12 / (2.0 * m * n * k))))
+    res = {m_: [] for m_ in modes}
+    for rnd in range(3):
+        for md in modes:
+            L.lib().ptk_gemm_force_small_tiles(md)
+            timed(A, B, kw, act, odt, C, 1)
+            res[md].append(timed(A, B, kw, act, odt, C, reps))
+    L.lib().ptk_gemm_force_small_tiles(0)
+    fl = 2.0 * m * n * k
+    out = {"name": name, "M": m, "N": n, "K": k}
+    for md, tag in zip(modes, ("w4", "p8", "auto")):
+        ms = min(res[md])
+        out[tag + "_us"] = round(ms * 1e3, 1)
+        out[tag + "_TF"] = round(fl / ms / 1e9, 1)
+    print(json.dumps(out), flush=True)
+    del A, B, C, kw
+    torch.cuda.empty_cache()
