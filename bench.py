@@ -138,8 +138,13 @@ def cpu_baseline(cfg_name: str, seconds_budget: float = 45.0, min_steps: int = 3
     from projectiontrainer_amd.config import PRESETS
     info = _cpu_info()
     threads = info["affinity_physical_cores"]
-    if os.environ.get("OMP_NUM_THREADS", "").isdigit():
-        threads = min(threads, int(os.environ["OMP_NUM_THREADS"]))
+    limit = None
+    if os.environ.get("OMP_NUM_THREADS", "").isdigit() and int(os.environ["OMP_NUM_THREADS"]) < threads:
+        # the GPU box gives each GPU job a CPU share and says so through OMP_NUM_THREADS (16 per GPU there);
+        # more threads than that share would oversubscribe the cores the job is entitled to
+        threads = int(os.environ["OMP_NUM_THREADS"])
+        limit = (f"OMP_NUM_THREADS={threads}: the CPU share of this GPU job; the host has "
+                 f"{info['affinity_physical_cores']} physical cores in this process's affinity")
     threads = max(1, threads)
     prev = torch.get_num_threads()
     torch.set_num_threads(threads)
@@ -194,7 +199,21 @@ def cpu_baseline(cfg_name: str, seconds_budget: float = 45.0, min_steps: int = 3
             "sample": f"oracle/stage1_ref.py fp32 CPU restatement, {cfg_name} shapes at bs {cfg.batch_size} "
                       f"(T={cfg.text_len}): 1 warm-up + {len(times)} timed steps, median {med:.2f} s/step "
                       f"({', '.join(f'{x:.2f}' for x in times)}), {threads} threads",
-            **info}
+            "cores_limited_by": limit, **info}
+
+
+KERNEL_OF_PATH = {"nt128": "gemm_nt_kernel", "big": "gemm_big_kernel", "big2": "gemm_big2_kernel",
+                  "w4": "gemm_w4_kernel", "p8": "gemm_p8_kernel"}
+
+
+def geglu_label(census, steps):
+    """The timed launches as they were dispatched (ptk_gemm_path_counts over the timed steps): the Gemma3
+    gate|up projection with the GEGLU epilogue, per kernel family."""
+    from projectiontrainer_amd import _lib as L
+    per = {p: n for (p, a), n in census.items() if a == L.ACT_GEGLU}
+    mix = " + ".join(f"{n // max(steps, 1)} x {KERNEL_OF_PATH.get(p, p)}<ACT_GEGLU>" for p, n in sorted(per.items()))
+    return (f"Gemma3 gate|up projection, GEGLU epilogue, per step: {mix} (2*(B*S)*(2I)*H FLOP per launch; the last "
+            f"layer's launch on the B*T loss rows, 2*(B*T)*(2I)*H); achieved = summed FLOP / summed event time")
 
 
 def main(argv=None):
@@ -267,6 +286,7 @@ def main(argv=None):
     # the replayed launches being the same kernels on the same shapes)
     if not graph:
         L.lib().ptk_gemm_timer_enable((1 << 8) | (1 << L.ACT_GEGLU))
+    L.gemm_path_counts(reset=True)
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(args.steps + 1)]
     t_wall = time.perf_counter()
     ev[0].record()
@@ -283,6 +303,7 @@ def main(argv=None):
         L.lib().ptk_gemm_timer_enable((1 << 8) | (1 << L.ACT_GEGLU))
         eng.step(px, ids, labels)
         torch.cuda.synchronize()
+    census = L.gemm_path_counts(reset=True)
     elapsed = ev[0].elapsed_time(ev[-1]) / 1e3
     step_ms = [ev[k].elapsed_time(ev[k + 1]) for k in range(args.steps)]
     med_ms = float(np.median(step_ms))
@@ -317,8 +338,7 @@ def main(argv=None):
                                f"{lm_name} frozen fwd/bwd, {cfg.num_vision_tokens} vis + {cfg.text_len} text tokens",
                    "global_batch": world * cfg.batch_size, "per_gpu_batch": cfg.batch_size,
                    "seq_len": cfg.seq_len, "parallelism": f"dp{world}"},
-        "roofline": {"bound": "mfma", "kernel": "gemm_w4_kernel<ACT_GEGLU> (Gemma3 gate|up projection: 2*(B*S)*(2I)*H FLOP per launch, "
-                               "last layer 2*(B*T)*(2I)*H)",
+        "roofline": {"bound": "mfma", "kernel": geglu_label(census, args.steps),
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
                      "traffic_unit": "bytes/launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",

@@ -75,13 +75,7 @@ typedef struct {
   int64_t ld_aux_in;
   ptk_rowmap amap;
   ptk_rowmap cmap;
-  /* optional stream-K scratch (NULL: off): sk_workspace >= ptk_gemm_sk_workspace_bytes(), sk_flags >=
-   * ptk_gemm_sk_flag_count() int32 zeroed once before first use (each use leaves them zero) */
-  void* sk_workspace;
-  int32_t* sk_flags;
 } ptk_gemm_desc;
-size_t ptk_gemm_sk_workspace_bytes(void);
-int ptk_gemm_sk_flag_count(void);
 int ptk_gemm(const ptk_gemm_desc* d, void* stream);
 
 /* LayerNorm (SigLIP, modeling_siglip.py:329): x f32 [rows,cols] -> y bf16. */
@@ -122,10 +116,9 @@ int ptk_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float std, float m
 int ptk_gemm_timer_enable(int on);   /* 0 off, 1 every class, (1 << 8) | class mask: only those classes */
 /* Tile-path test hook: 0 = shape heuristic, 1 = every GEMM on the 128x128 kernel,
    2 / 4 = every single-batch GEMM on the 256x256 / barrier-staggered 256x256 kernel,
-   8 = every single-batch GEMM the persistent 4-wave 256x256 kernel supports on it. */
-int ptk_gemm_force_small_tiles(int mode);   /* tests: 0 auto, 1 128x128, 2 256x256, 4 staggered 256x256,
-                                              8 persistent 4-wave, 16 stream-K (needs desc scratch),
-                                              32 persistent 8-wave (two waves per SIMD) */
+   8 / 32 = every single-batch GEMM the persistent 4-wave / 8-wave (two waves per SIMD) 256x256 kernel
+   supports on it. */
+int ptk_gemm_force_small_tiles(int mode);
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
 /* Dispatch census (tests): counts[path * 8 + act] = GEMM launches since the last reset per kernel family
  * (0 128x128, 1 256x256 8-wave, 2 staggered 256x256 8-wave, 3 persistent 4-wave, 4 ping-pong,
@@ -330,6 +323,32 @@ int ptk_adamw_bf16(void* params, void* grads, void* exp_avg, void* exp_avg_sq, i
 int ptk_clip_adamw(float* params, const float* grads, float* exp_avg, float* exp_avg_sq, int64_t n,
                    float grad_scale, float max_norm, float lr, float beta1, float beta2, float eps,
                    float weight_decay, int step, float* partial, float* norm_out, void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * Data-parallel exchange over RCCL (SURVEY §8(b) ptk_comm_init /            *
+ * allreduce_avg, §8(e)): replaces the DDP reducer behind                    *
+ * accelerator.backward (Stage1/projector_trainer.py:237,                    *
+ * Stage1/accelerator_setup.py:12-16).  One process per GPU; RCCL is loaded  *
+ * at the first call (no link-time dependency).                              *
+ * ------------------------------------------------------------------------ */
+typedef struct ptk_comm ptk_comm;
+int ptk_comm_unique_id_bytes(void);              /* 128 */
+/* rank 0 creates the id; the caller hands the bytes to every rank (e.g. through torch.distributed) */
+int ptk_comm_get_unique_id(void* unique_id);
+/* collective over `world` ranks on the current HIP device */
+int ptk_comm_init(ptk_comm** comm, const void* unique_id, int world, int rank);
+int ptk_comm_destroy(ptk_comm* comm);
+int ptk_comm_world(const ptk_comm* comm);
+/* in place over ranks, n f32, on `stream`: the sum, or the average (DDP's gradient average) */
+int ptk_comm_allreduce_sum(ptk_comm* comm, float* buf, int64_t n, void* stream);
+int ptk_comm_allreduce_avg(ptk_comm* comm, float* buf, int64_t n, void* stream);
+/* ptk_projector_bwd into the flat grad buffer [dW1 | db1 | dW2 | db2] (the MLPProjector parameter order) with
+ * the ranks' SUM of it exchanged on comm_stream, overlapped: dW2 | db2 are computed first and all-reduced while
+ * the dA and dW1 GEMMs run on `stream`, then dW1 | db1; `stream` waits for the exchange before returning
+ * control to its next work.  The 1/world of DDP's average is folded into ptk_clip_adamw's grad_scale. */
+int ptk_projector_bwd_allreduce(const ptk_projector* p, int rows, const void* x, const void* a, const void* h,
+                                const void* dy, float* flat_grad, void* ws, size_t ws_bytes, ptk_comm* comm,
+                                void* comm_stream, void* stream);
 
 /* ------------------------------------------------------------------------ *
  * Host data step: image resize + normalise.              *

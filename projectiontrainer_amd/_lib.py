@@ -33,7 +33,7 @@ class GemmDesc(C.Structure):
                 ("ld_rowadd", c_int64), ("resid", c_void_p), ("ld_resid", c_int64),
                 ("aux", c_void_p), ("aux2", c_void_p), ("ld_aux", c_int64),
                 ("aux_in", c_void_p), ("aux_in2", c_void_p), ("ld_aux_in", c_int64),
-                ("amap", RowMap), ("cmap", RowMap), ("sk_workspace", c_void_p), ("sk_flags", c_void_p)]
+                ("amap", RowMap), ("cmap", RowMap)]
 
 
 class FlashDesc(C.Structure):
@@ -141,8 +141,6 @@ SIGNATURES = {
     "ptk_fill_normal_bf16": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_void_p]),
     "ptk_gemm_timer_enable": (c_int, [c_int]),
     "ptk_gemm_force_small_tiles": (c_int, [c_int]),
-    "ptk_gemm_sk_workspace_bytes": (c_size_t, []),
-    "ptk_gemm_sk_flag_count": (c_int, []),
     "ptk_gemm_timer_read": (c_int, [c_int, C.POINTER(C.c_double), C.POINTER(c_int)]),
     "ptk_gemm_path_counts": (c_int, [c_void_p, c_int]),
     "ptk_flash_attn_fwd": (c_int, [C.POINTER(FlashDesc), c_void_p]),
@@ -173,6 +171,15 @@ SIGNATURES = {
     "ptk_resize_coeffs": (c_int, [c_int, c_int, c_void_p, c_void_p]),
     "ptk_image_preprocess": (c_int, [c_void_p, c_void_p, c_void_p, c_int, c_int, c_int, c_int, c_void_p, c_int,
                                      c_void_p, c_void_p, c_void_p]),
+    "ptk_comm_unique_id_bytes": (c_int, []),
+    "ptk_comm_get_unique_id": (c_int, [c_void_p]),
+    "ptk_comm_init": (c_int, [C.POINTER(c_void_p), c_void_p, c_int, c_int]),
+    "ptk_comm_destroy": (c_int, [c_void_p]),
+    "ptk_comm_world": (c_int, [c_void_p]),
+    "ptk_comm_allreduce_sum": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "ptk_comm_allreduce_avg": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
+    "ptk_projector_bwd_allreduce": (c_int, [C.POINTER(ProjectorC), c_int] + [c_void_p] * 5 +
+                                    [c_void_p, c_size_t, c_void_p, c_void_p, c_void_p]),
     "ptk_clip_adamw": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_float, c_float, c_float,
                                c_float, c_float, c_float, c_float, c_int, c_void_p, c_void_p, c_void_p]),
 }

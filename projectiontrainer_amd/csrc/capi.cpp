@@ -33,7 +33,6 @@ GemmArgs to_args(const ptk_gemm_desc* d) {
   a.aux = (bf16_t*)d->aux; a.aux2 = (bf16_t*)d->aux2; a.ld_aux = d->ld_aux;
   a.aux_in = (const bf16_t*)d->aux_in; a.aux_in2 = (const bf16_t*)d->aux_in2; a.ld_aux_in = d->ld_aux_in;
   a.amap = to_map(d->amap); a.cmap = to_map(d->cmap);
-  a.sk_part = (float*)d->sk_workspace; a.sk_flags = (int*)d->sk_flags;
   return a;
 }
 
@@ -104,12 +103,9 @@ int ptk_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream) {
   return launch_cast_f32_bf16(in, (bf16_t*)out, n, ST);
 }
 
-size_t ptk_gemm_sk_workspace_bytes(void) { return (size_t)SK_MAX_BLOCKS * SK_SLAB_FLOATS * sizeof(float); }
-int ptk_gemm_sk_flag_count(void) { return SK_MAX_BLOCKS; }
-
 int ptk_gemm_force_small_tiles(int mode) {
-  if (mode != 0 && mode != 1 && mode != 2 && mode != 4 && mode != 8 && mode != 16 && mode != 32)
-    return set_error("gemm tile mode %d not in {0, 1, 2, 4, 8, 16, 32}", mode);
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 4 && mode != 8 && mode != 32)
+    return set_error("gemm tile mode %d not in {0, 1, 2, 4, 8, 32}", mode);
   force_small_tiles(mode);
   return 0;
 }
@@ -179,7 +175,9 @@ int ptk_projector_fwd(const ptk_projector* p, int rows, const void* x, void* a, 
   return launch_gemm(g2, ACT_NONE, round_bf16 ? OUT_F32_BFR : OUT_F32, 1, ST);
 }
 
+}  // extern "C"
 static size_t align256(size_t v) { return (v + 255) & ~(size_t)255; }
+extern "C" {
 
 size_t ptk_projector_workspace_bytes(const ptk_projector* p, int rows) {
   const size_t Dv = p->vision_dim, I = p->inter_dim, Dl = p->llm_dim, R = ((size_t)rows + 63) / 64 * 64;
@@ -192,8 +190,14 @@ size_t ptk_projector_workspace_bytes(const ptk_projector* p, int rows) {
   return s;
 }
 
-int ptk_projector_bwd(const ptk_projector* p, int rows, const void* x, const void* a, const void* h, const void* dy,
-                      float* dw1, float* db1, float* dw2, float* db2, void* ws, size_t ws_bytes, void* stream) {
+}  // extern "C"
+
+namespace ptk {
+// stage 0: db2 = colsum(dy), dW2 = dy^T . h;  stage 1: dA = (dy . W2) * gelu'(a), db1 = colsum(dA), dW1 = dA^T . x
+// (the projector backward in the order comm.cpp overlaps with the DDP exchange)
+int projector_bwd_stage(const ptk_projector* p, int rows, const void* x, const void* a, const void* h, const void* dy,
+                        float* dw1, float* db1, float* dw2, float* db2, void* ws, size_t ws_bytes, int stage,
+                        hipStream_t st) {
   // weight grads contract over tokens: transposed operands are zero-padded to Rp = roundup(R, 64)
   const int Dv = p->vision_dim, I = p->inter_dim, Dl = p->llm_dim, R = rows, Rp = (rows + 63) / 64 * 64;
   if (ws_bytes < ptk_projector_workspace_bytes(p, rows)) return set_error("projector_bwd: workspace too small");
@@ -203,25 +207,36 @@ int ptk_projector_bwd(const ptk_projector* p, int rows, const void* x, const voi
   bf16_t* dA = (bf16_t*)w; w += align256((size_t)Rp * I * 2);
   bf16_t* xT = (bf16_t*)w; w += align256((size_t)Dv * Rp * 2);
   float* part = (float*)w;
-  // db2 = colsum(dy); dW2 = dy^T . h  (contraction over tokens)
-  if (launch_colsum_bf16((const bf16_t*)dy, R, Dl, db2, part, ST)) return -1;
-  if (launch_transpose((const bf16_t*)dy, Dl, 0, 0, 1, dyT, Rp, 0, 0, 1, R, Dl, Rp, ST)) return -1;
-  if (launch_transpose((const bf16_t*)h, I, 0, 0, 1, T, Rp, 0, 0, 1, R, I, Rp, ST)) return -1;
-  GemmArgs g;
-  g.A = dyT; g.B = T; g.C = dw2; g.M = Dl; g.N = I; g.K = Rp; g.lda = Rp; g.ldb = Rp; g.ldc = I;
-  if (launch_gemm(g, ACT_NONE, OUT_F32, 1, ST)) return -1;
+  if (stage == 0) {
+    // db2 = colsum(dy); dW2 = dy^T . h  (contraction over tokens)
+    if (launch_colsum_bf16((const bf16_t*)dy, R, Dl, db2, part, st)) return -1;
+    if (launch_transpose((const bf16_t*)dy, Dl, 0, 0, 1, dyT, Rp, 0, 0, 1, R, Dl, Rp, st)) return -1;
+    if (launch_transpose((const bf16_t*)h, I, 0, 0, 1, T, Rp, 0, 0, 1, R, I, Rp, st)) return -1;
+    GemmArgs g;
+    g.A = dyT; g.B = T; g.C = dw2; g.M = Dl; g.N = I; g.K = Rp; g.lda = Rp; g.ldb = Rp; g.ldc = I;
+    return launch_gemm(g, ACT_NONE, OUT_F32, 1, st);
+  }
   // dA = (dy . W2) * gelu'(a)
   GemmArgs g2;
   g2.A = (const bf16_t*)dy; g2.B = (const bf16_t*)p->w2t; g2.C = dA; g2.M = R; g2.N = I; g2.K = Dl;
   g2.lda = Dl; g2.ldb = Dl; g2.ldc = I; g2.aux_in = (const bf16_t*)a; g2.ld_aux_in = I;
-  if (launch_gemm(g2, ACT_GELU_ERF_BWD, OUT_BF16, 1, ST)) return -1;
+  if (launch_gemm(g2, ACT_GELU_ERF_BWD, OUT_BF16, 1, st)) return -1;
   // db1 = colsum(dA); dW1 = dA^T . x
-  if (launch_colsum_bf16(dA, R, I, db1, part, ST)) return -1;
-  if (launch_transpose(dA, I, 0, 0, 1, T, Rp, 0, 0, 1, R, I, Rp, ST)) return -1;
-  if (launch_transpose((const bf16_t*)x, Dv, 0, 0, 1, xT, Rp, 0, 0, 1, R, Dv, Rp, ST)) return -1;
+  if (launch_colsum_bf16(dA, R, I, db1, part, st)) return -1;
+  if (launch_transpose(dA, I, 0, 0, 1, T, Rp, 0, 0, 1, R, I, Rp, st)) return -1;
+  if (launch_transpose((const bf16_t*)x, Dv, 0, 0, 1, xT, Rp, 0, 0, 1, R, Dv, Rp, st)) return -1;
   GemmArgs g3;
   g3.A = T; g3.B = xT; g3.C = dw1; g3.M = I; g3.N = Dv; g3.K = Rp; g3.lda = Rp; g3.ldb = Rp; g3.ldc = Dv;
-  return launch_gemm(g3, ACT_NONE, OUT_F32, 1, ST);
+  return launch_gemm(g3, ACT_NONE, OUT_F32, 1, st);
+}
+}  // namespace ptk
+
+extern "C" {
+
+int ptk_projector_bwd(const ptk_projector* p, int rows, const void* x, const void* a, const void* h, const void* dy,
+                      float* dw1, float* db1, float* dw2, float* db2, void* ws, size_t ws_bytes, void* stream) {
+  if (projector_bwd_stage(p, rows, x, a, h, dy, dw1, db1, dw2, db2, ws, ws_bytes, 0, ST)) return -1;
+  return projector_bwd_stage(p, rows, x, a, h, dy, dw1, db1, dw2, db2, ws, ws_bytes, 1, ST);
 }
 
 int ptk_gather_vision_grad(const float* dx_llm, int batch, int num_patches, int seq_pad, int llm_dim, void* dy,

@@ -2201,17 +2201,15 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs*
         for (int s = 0; s < nslab && s < 128; ++s) { b.dkv_item_slab[s] = (unsigned char)s; b.dkv_item_piece[s] = 0; }
       }
       if (b.dkv_items > 128 || nslab > 128) return set_error("attn_bwd: %d dK/dV work items over %d key slabs (max 128)", b.dkv_items, nslab);
-      // PTK_ATTN_DQ_OLD=1: the previous dQ kernel (A/B), after a separate delta pass and the dK/dV kernel;
-      // otherwise the dQ kernel computes delta and runs first
-      static const bool dq_old = getenv("PTK_ATTN_DQ_OLD") && atoi(getenv("PTK_ATTN_DQ_OLD")) == 1;
-      const bool dq_new = !dq_old && (a.nkeys + 31) / 32 <= FA_MAXT;
+      // the dQ kernel computes delta and runs first; past the 4096-key mask table the generic dQ kernel runs
+      // after a separate delta pass and the dK/dV kernel
+      const bool dq_new = (a.nkeys + 31) / 32 <= FA_MAXT;
       if (dq_new) hipLaunchKernelGGL(attn_bwd_dq256_kernel, gq, dim3(512), 0, st, b);
       else hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
       // 32 keys per wave (one wave per SIMD) measured 209 us vs 252 us for 16 keys per wave (two per
       // SIMD, which spills the precomputed transposed-read addresses) at cfg2
-      // PTK_ATTN_DKV_OLD=1: the previous dK/dV kernel (A/B)
-      static const bool dkv_old = getenv("PTK_ATTN_DKV_OLD") && atoi(getenv("PTK_ATTN_DKV_OLD")) == 1;
-      if (dkv_old || (b.qdiv & (b.qdiv - 1)) || (long)b.rows * 256 * 2 > 0x7fffffffL)
+      // the generic dK/dV kernel for GQA groups that are not a power of two and for very long query rows
+      if ((b.qdiv & (b.qdiv - 1)) || (long)b.rows * 256 * 2 > 0x7fffffffL)
         hipLaunchKernelGGL(attn_bwd_dkv256_kernel<32>, dim3((unsigned)(np * nz)), dim3(256), 0, st, b);
       else
         hipLaunchKernelGGL(attn_bwd_dkv256b_kernel, dim3((unsigned)(np * nz)), dim3(256), 0, st, b);
@@ -2239,9 +2237,8 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
   dim3 grid((unsigned)nblk);
   switch (a.D) {
     case 64: {
-      // PTK_ATTN_FWD8W=1: the previous kernel (A/B); it also takes tables past FA_MAXT words
-      static const bool w8 = getenv("PTK_ATTN_FWD8W") && atoi(getenv("PTK_ATTN_FWD8W")) == 1;
-      if (w8 || (a.nkeys + 31) / 32 > FA_MAXT || (long)a.nkeys * a.ldk * 2 > 0x7fffffffL)
+      // the generic kernel past the 4096-key mask table
+      if ((a.nkeys + 31) / 32 > FA_MAXT || (long)a.nkeys * a.ldk * 2 > 0x7fffffffL)
         hipLaunchKernelGGL((attn_fwd_kernel<64, 1>), grid, dim3(512), 0, st, a);
       else
         hipLaunchKernelGGL(attn_fwd64_kernel, grid, dim3(512), 0, st, a);
@@ -2250,18 +2247,11 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
     // QG = 2 (256-row blocks) measured slower on the Gemma3 step: 352 blocks of double work on 256 CUs
     // quantise worse than 704 (110 vs 78 us per layer), and it spills
     case 256: {
-      // PTK_ATTN_FWD8W=1: the 8-wave, 16-rows-per-wave form (A/B)
-      static const bool w8 = getenv("PTK_ATTN_FWD8W") && atoi(getenv("PTK_ATTN_FWD8W")) == 1;
-      if (w8) hipLaunchKernelGGL((attn_fwd_kernel<256, 1>), grid, dim3(512), 0, st, a);
-      else if ((a.nkeys + 31) / 32 > FA_MAXT || (long)a.nkeys * a.ldk * 2 > 0x7fffffffL)
+      // the generic kernel past the 4096-key mask table
+      if ((a.nkeys + 31) / 32 > FA_MAXT || (long)a.nkeys * a.ldk * 2 > 0x7fffffffL)
         hipLaunchKernelGGL((attn_fwd_kernel<256, 1>), grid, dim3(512), 0, st, a);
-      else {
-        // PTK_ATTN_NOSTAGGER=1: every wave in the early order (A/B)
-        static const bool nst = getenv("PTK_ATTN_NOSTAGGER") && atoi(getenv("PTK_ATTN_NOSTAGGER")) == 1;
-        FlashArgs b = a;
-        b.variant = nst ? 1 : 0;
-        hipLaunchKernelGGL(attn_fwd256_kernel, grid, dim3(512), 0, st, b);
-      }
+      else
+        hipLaunchKernelGGL(attn_fwd256_kernel, grid, dim3(512), 0, st, a);
       break;
     }
     default: return set_error("attn_fwd: head_dim %d unsupported (64, 256)", a.D);

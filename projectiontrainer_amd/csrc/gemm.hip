@@ -662,92 +662,6 @@ __global__ void __launch_bounds__(512, 1) gemm_big2_kernel(GemmArgs p) {
   big_epilogue<ACT, OUT>(p, smem, bm, bn, acc, threadIdx.x);
 }
 
-// ---------------------------------------------------------------- stream-K over the 256x256 tiles
-// A tile grid that quantises badly onto the CUs (Gemma3's N = 1152 projections: 440 tiles = 1.72
-// waves of 256 CUs) runs as a persistent grid of G blocks, block v owning the K-tile iterations
-// [v*T/G, (v+1)*T/G) of the T = tiles x K-tiles iteration space (every range >= one tile's K loop, so a
-// tile is split between at most two neighbouring blocks).  Block v's range starts with the tail of a
-// tile whose head block v-1 computes LAST: the tail block writes its fp32 partial (256 KiB slab, MFMA
-// register order, 1 KiB per wave instruction), publishes it (agent-scope release + flag), and the head
-// block, finishing its range, acquires it, adds it to its registers and runs the fused epilogue.  The
-// head never waits on a block that could be waiting on it (block v depends only on v+1's FIRST segment).
-template <int ACT, int OUT>
-__global__ void __launch_bounds__(512, 1) gemm_sk_kernel(GemmArgs p) {
-  __shared__ __attribute__((aligned(16))) char smem[8 * EPI_WAVE_BYTES];
-  const int tid = threadIdx.x;
-  const int G = gridDim.x;
-  // segment control in scalar registers (32-bit: the launcher bounds tiles x K-tiles below 2^31)
-  const int v = __builtin_amdgcn_readfirstlane(xcd_remap(blockIdx.x, G));   // consecutive v share an XCD
-  const int nt = __builtin_amdgcn_readfirstlane(p.K / BK);
-  const int ntile = __builtin_amdgcn_readfirstlane(((p.M + BIG - 1) / BIG) * ((p.N + BIG - 1) / BIG));
-  const long total = (long)ntile * nt;
-  const int g0 = __builtin_amdgcn_readfirstlane((int)((long)v * total / G));
-  const int g1 = __builtin_amdgcn_readfirstlane((int)((long)(v + 1) * total / G));
-  f32x4_t acc[8][4];
-  for (int g = g0; g < g1;) {
-    const int tile = __builtin_amdgcn_readfirstlane(g / nt);
-    const int k0 = __builtin_amdgcn_readfirstlane(g - tile * nt);
-    const int k1 = __builtin_amdgcn_readfirstlane(min(nt, k0 + (g1 - g)));
-    g += k1 - k0;
-    int bm, bn;
-    big_tile_coords(p, tile, bm, bn);
-    bm = __builtin_amdgcn_readfirstlane(bm);
-    bn = __builtin_amdgcn_readfirstlane(bn);
-    // an opaque copy of the thread index per segment: keeps the per-lane address arithmetic of the
-    // K loop and the epilogue inside the segment (hoisted out of this loop it stays live through the
-    // MFMA loop and spills)
-    int ltid = tid;
-    asm volatile("" : "+v"(ltid));
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-    big2_kloop(p, smem, bm, bn, k0, k1, acc, ltid);
-    if (k0 > 0) {
-      // tail of a tile whose head is block v-1's last segment: publish the partial in slot v-1
-      float4* slab = reinterpret_cast<float4*>(p.sk_part + (long)(v - 1) * SK_SLAB_FLOATS) + ltid * 1 + (ltid >> 6) * 31 * 64;
-#pragma unroll
-      for (int i = 0; i < 8; ++i)
-#pragma unroll
-        for (int j = 0; j < 4; ++j)
-          slab[(i * 4 + j) * 64] = make_float4(acc[i][j][0], acc[i][j][1], acc[i][j][2], acc[i][j][3]);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (tid == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(p.sk_flags + (v - 1), 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      continue;   // k1 == nt: the head block finishes this tile
-    }
-    if (k1 < nt) {
-      // head of a tile whose tail is block v+1's first segment: take its partial
-      if (tid == 0) {
-        while (__hip_atomic_load(p.sk_flags + v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
-          __builtin_amdgcn_s_sleep(4);
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        __hip_atomic_store(p.sk_flags + v, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);   // ready for the next launch
-      }
-      __syncthreads();
-      const float4* slab = reinterpret_cast<const float4*>(p.sk_part + (long)v * SK_SLAB_FLOATS) + ltid + (ltid >> 6) * 31 * 64;
-#pragma unroll
-      for (int i = 0; i < 8; ++i) {
-        float4 t[4];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) t[j] = slab[(i * 4 + j) * 64];
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          acc[i][j][0] += t[j].x; acc[i][j][1] += t[j].y; acc[i][j][2] += t[j].z; acc[i][j][3] += t[j].w;
-        }
-        __builtin_amdgcn_sched_barrier(0);   // four slab loads in flight at a time (register pressure)
-      }
-    }
-    big_epilogue<ACT, OUT>(p, smem, bm, bn, acc, ltid);
-    __syncthreads();   // epilogue staging done before the next segment's DMA reuses the LDS
-  }
-}
-
 static int g_num_cu = 0;
 static int num_cus() {
   if (!g_num_cu) {
@@ -763,8 +677,7 @@ static int num_cus() {
 static bool g_timing = false;
 static int g_timing_mask = 0;   // activation classes whose launches are timed
 static int g_force_tiles = 0;   // tests: 1 = every GEMM on 128x128, 2 / 4 = single-batch GEMMs on 256x256 / staggered 256x256,
-                                // 8 = persistent 4-wave kernel, 16 = stream-K wherever scratch is given and tiles > CUs,
-                                // 32 = ping-pong 8-wave kernel wherever it is supported
+                                // 8 = persistent 4-wave kernel, 32 = persistent 8-wave kernel wherever they are supported
 void force_small_tiles(int mode) { g_force_tiles = mode; }
 static std::vector<hipEvent_t> g_ev[8];
 static size_t g_ev_used[8];
@@ -866,36 +779,6 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
     const int rc = launch_gemm_w4(a, act, out, st, 0);
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
-  }
-  // stream-K (forced mode 16 only): measured on the step's N = 1152 projections (440 tiles = 1.72 waves of
-  // 256 CUs) it balances the CUs but runs each K-tile ~1.5x slower — blocks enter their tiles at
-  // different K offsets, so neighbouring tiles no longer stream the same A/B panels through L2 in
-  // lock-step and the launch becomes bound by L2-miss traffic (g_dgu 643 -> 832 us)
-  if (batch == 1 && a.sk_part && a.sk_flags && g_force_tiles == 16) {
-    const int nbig = ((a.M + BIG - 1) / BIG) * ((a.N + BIG - 1) / BIG);
-    const int G = std::min(num_cus(), SK_MAX_BLOCKS);
-    if (nbig > G && (long)nbig * (a.K / BK) < 0x7fffffffL) {
-#define PTK_SK_CASE(ACT_, OUT_)                                                                 \
-      if (act == ACT_ && out == OUT_) {                                                         \
-        hipEvent_t e0 = nullptr, e1 = nullptr;                                                  \
-        if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); } \
-        if (e0) (void)hipEventRecord(e0, st);                                                   \
-        count_path(GEMM_PATH_SK, act);                                                          \
-        hipLaunchKernelGGL((gemm_sk_kernel<ACT_, OUT_>), dim3(G), dim3(512), 0, st, a);         \
-        if (e1) (void)hipEventRecord(e1, st);                                                   \
-        return hipGetLastError() == hipSuccess ? 0 : set_error("gemm launch failed");          \
-      }
-      PTK_SK_CASE(ACT_NONE, OUT_BF16)
-      PTK_SK_CASE(ACT_NONE, OUT_F32)
-      PTK_SK_CASE(ACT_NONE, OUT_F32_BFR)
-      PTK_SK_CASE(ACT_GELU_TANH, OUT_BF16)
-      PTK_SK_CASE(ACT_GELU_ERF, OUT_BF16)
-      PTK_SK_CASE(ACT_GEGLU, OUT_BF16)
-      PTK_SK_CASE(ACT_GELU_ERF_BWD, OUT_BF16)
-      PTK_SK_CASE(ACT_GEGLU_BWD, OUT_BF16)
-#undef PTK_SK_CASE
-      return set_error("gemm: unsupported (act=%d, out=%d)", act, out);
-    }
   }
   if (batch == 1 && (g_force_tiles == 4 || (g_force_tiles == 0 && big_shape && a.K >= 4096))) {
     const long nb = (long)((a.M + BIG - 1) / BIG) * ((a.N + BIG - 1) / BIG);

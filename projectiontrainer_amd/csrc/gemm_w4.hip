@@ -313,8 +313,7 @@ PTK_DEV u32x4_t w4_rsrc(const void* base, uint32_t bytes) {
 PTK_DEV uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_ptr_t)p; }
 
 template <int ACT, int OUT>
-__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes,
-                                                          uint32_t stagger) {
+__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
   __shared__ __attribute__((aligned(16))) char smem[W4_NSLOT * W4_SLOT];   // 160 KiB: the k-step ring
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -328,10 +327,6 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
     loc = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
   }
   if (loc >= ntile) return;
-  // stagger > 0: every other CU of an XCD starts ~stagger/1024 x 1k cycles late, so half the CUs run
-  // their epilogue (stores) while the other half runs MFMAs
-  if (stagger && ((blockIdx.x >> 3) & 1))
-    for (uint32_t i = 0; i < stagger; ++i) __builtin_amdgcn_s_sleep(16);
   const int nt = p.K / W4_KT;                              // 64-deep K-tiles per output tile
   const int nks = 2 * nt;                                  // 32-deep k-steps per output tile
   const int total_ks = ((ntile - loc + G - 1) / G) * nks;
@@ -571,10 +566,6 @@ double w4_round_fill(long M, long N) {
 
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid) {
   num_cu();
-  static const uint32_t stagger = [] {   // diagnostic: PTK_W4_STAGGER=<units of ~1k cycles> (default 0)
-    const char* e = getenv("PTK_W4_STAGGER");
-    return e ? (uint32_t)atoi(e) : 0u;
-  }();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   long grid = std::min<long>(ntile, max_grid > 0 ? max_grid : g_num_cu);
   const long arows = a.M + a.amap.off;
@@ -582,7 +573,7 @@ int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
 #define PTK_W4_CASE(ACT_, OUT_)                                                                   \
   if (act == ACT_ && out == OUT_) {                                                               \
-    hipLaunchKernelGGL((gemm_w4_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb, stagger); \
+    hipLaunchKernelGGL((gemm_w4_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb); \
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_w4 launch failed");              \
   }
   PTK_W4_CASE(ACT_NONE, OUT_BF16)
@@ -754,7 +745,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       ws = slot_next(ws);
       kstep(std::false_type{}, std::integral_constant<bool, !lst>{}, half_c, fb1, fb0, rs, ws);
       dma_advance();
-      rs = slot_next(rs);
+      if (!lst) rs = slot_next(rs);   // last pair: rs stays on the next tile's first k-step (read after the epilogue)
       ws = slot_next(ws);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       __builtin_amdgcn_s_barrier();
@@ -767,7 +758,12 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       int bm, bn;
       w4_tile_coords(t, nbm, nbn, bm, bn);
       w4_epilogue<ACT, OUT, 4>(p, acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128 + hf * 64, lane);
-      read_frags(rs);   // the next tile's first k-step (published by the barrier; harmless after the last)
+      // the next tile's first k-step (published by the barrier; harmless after the last).  Its slot is the
+      // one the NEXT pair's second k-step restages (k-step i+6 lands in the slot of i+1), so a barrier keeps
+      // a wave that finished its epilogue early from overwriting it before every wave has read it
+      read_frags(rs);
+      __builtin_amdgcn_s_barrier();
+      rs = slot_next(rs);
     }
   };
   if (hf) run(std::integral_constant<int, 1>{});

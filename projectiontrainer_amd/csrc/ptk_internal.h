@@ -42,14 +42,7 @@ struct GemmArgs {
   long ld_aux_in = 0;
   RowMap amap{0, 0, 0, 0};                       // A row remap (gather)
   RowMap cmap{0, 0, 0, 0};                       // C row remap (scatter / skip)
-  // stream-K scratch (launch_gemm may then balance a poorly quantised tile grid over the CUs):
-  // sk_part >= SK_MAX_BLOCKS * 256 KiB, sk_flags >= SK_MAX_BLOCKS ints, zero before the first use
-  // (every split tile's consumer resets its flag)
-  float* sk_part = nullptr;
-  int* sk_flags = nullptr;
 };
-constexpr int SK_MAX_BLOCKS = 512;
-constexpr long SK_SLAB_FLOATS = 256L * 256;
 
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
 // kernel families launch_gemm dispatches to (census: path_counts, ptk_gemm_path_counts)
@@ -271,4 +264,11 @@ int launch_adamw_bf16(bf16_t* p, bf16_t* g, bf16_t* m, bf16_t* v, long n, const 
                       double lr, double b1, double b2, double eps, double wd, int step, float* norm_out,
                       hipStream_t st);
 
+}  // namespace ptk
+#include "../../include/ptk.h"
+namespace ptk {
+// projector backward in two stages (capi.cpp): 0 = db2, dW2; 1 = dA, db1, dW1 (comm.cpp overlaps the DDP exchange)
+int projector_bwd_stage(const ptk_projector* p, int rows, const void* x, const void* a, const void* h, const void* dy,
+                        float* dw1, float* db1, float* dw2, float* db2, void* ws, size_t ws_bytes, int stage,
+                        hipStream_t st);
 }  // namespace ptk

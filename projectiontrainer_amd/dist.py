@@ -135,3 +135,59 @@ def allreduce_grads_(flat_grad, world: int, group=None):
     if world > 1:
         dist.all_reduce(flat_grad, op=dist.ReduceOp.SUM, group=group)
     return 1.0 / world
+
+
+def grad_exchange_chunks(proj):
+    """(offset, count) pieces of the projector's flat grad [dW1 | db1 | dW2 | db2] in exchange order: dW2 | db2
+    (computed first by the backward, so its all-reduce overlaps the dA / dW1 GEMMs), then dW1 | db1
+    (ptk_projector_bwd_allreduce; SURVEY §8(e): the 89 MB all-reduce split to pipeline with the dW GEMMs)."""
+    Dv, I, Dl = proj.vision_dim, proj.inter_dim, proj.llm_dim
+    n1 = I * Dv + I
+    return [(n1, Dl * I + Dl), (0, n1)]
+
+
+def allreduce_grads_chunked_(flat_grad, chunks, world: int, group=None):
+    """allreduce_grads_ piece by piece in the given order (the collective-library path of the overlapped
+    RCCL exchange; gloo on CPU): the same sums, element for element."""
+    if world > 1:
+        for off, n in chunks:
+            dist.all_reduce(flat_grad[off:off + n], op=dist.ReduceOp.SUM, group=group)
+    return 1.0 / world
+
+
+class RcclComm:
+    """libptk's RCCL communicator (ptk_comm_*) over the ranks of an initialised torch process group: rank 0
+    creates the unique id, the group broadcasts it, every rank joins on its current device."""
+
+    def __init__(self, group=None):
+        import ctypes
+        from . import _lib as L
+        self._L = L
+        lib = L.lib()
+        nb = lib.ptk_comm_unique_id_bytes()
+        world, rank = dist.get_world_size(group), dist.get_rank(group)
+        uid = (ctypes.c_char * nb)()
+        if rank == 0:
+            L.check(lib.ptk_comm_get_unique_id(uid), "ptk_comm_get_unique_id")
+        obj = [bytes(uid) if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
+        uid = (ctypes.c_char * nb).from_buffer_copy(obj[0])
+        self.handle = ctypes.c_void_p()
+        L.check(lib.ptk_comm_init(ctypes.byref(self.handle), uid, world, rank), "ptk_comm_init")
+        self.world, self.rank = world, rank
+
+    def allreduce_sum_(self, t, stream):
+        self._L.check(self._L.lib().ptk_comm_allreduce_sum(self.handle, t.data_ptr(), t.numel(), stream),
+                      "ptk_comm_allreduce_sum")
+        return t
+
+    def close(self):
+        if getattr(self, "handle", None) is not None and self.handle.value:
+            self._L.lib().ptk_comm_destroy(self.handle)
+            self.handle = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

@@ -23,9 +23,8 @@ def _bits(t):
 def gemm(A, B, *, C=None, out_dtype=torch.bfloat16, act=L.ACT_NONE, alpha=1.0, bias=None, rowadd=None,
          resid=None, aux=None, aux2=None, aux_in=None, aux_in2=None, M=None, N=None, K=None,
          lda=None, ldb=None, ldc=None, batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0),
-         amap=(0, 0, 0, 0), cmap=(0, 0, 0, 0), out_mode=None, stream_k=False):
-    """C = epi(alpha * A . B^T) with A [M,K], B [N,K] bf16 (K-contiguous).  stream_k: hand the library
-    stream-K scratch (it then balances badly quantised 256x256 tile grids over the CUs)."""
+         amap=(0, 0, 0, 0), cmap=(0, 0, 0, 0), out_mode=None):
+    """C = epi(alpha * A . B^T) with A [M,K], B [N,K] bf16 (K-contiguous)."""
     _require_cuda(A, B)
     M = A.shape[-2] if M is None else M
     K = A.shape[-1] if K is None else K
@@ -57,24 +56,8 @@ def gemm(A, B, *, C=None, out_dtype=torch.bfloat16, act=L.ACT_NONE, alpha=1.0, b
     d.aux_in2 = ptr(aux_in2)
     d.amap = L.RowMap(*amap)
     d.cmap = L.RowMap(*cmap)
-    if stream_k:
-        part, flags = sk_scratch(A.device)
-        d.sk_workspace, d.sk_flags = ptr(part), ptr(flags)
     check(L.lib().ptk_gemm(d, L.stream_ptr(A.device)), "ptk_gemm")
     return C
-
-
-_SK = {}
-
-
-def sk_scratch(device):
-    """Per-device stream-K scratch: fp32 partial slabs and zeroed flags (left zero by every launch)."""
-    key = str(device)
-    if key not in _SK:
-        lib = L.lib()
-        _SK[key] = (torch.empty(lib.ptk_gemm_sk_workspace_bytes(), dtype=torch.uint8, device=device),
-                    torch.zeros(lib.ptk_gemm_sk_flag_count(), dtype=torch.int32, device=device))
-    return _SK[key]
 
 
 def layernorm(x, w, b, eps):

@@ -8,7 +8,8 @@ The body of `for batch in progress_bar:` (Stage1/projector_trainer.py:152-245):
   embed + cat + mask + labels (:183-220)  inside ptk_gemma3_loss_fwd_bwd
   Gemma3 fwd + loss + backward (:226-237) ptk_gemma3_loss_fwd_bwd (loss scaled 1/gas^2)
   projector bwd                         ptk_gather_vision_grad + ptk_projector_bwd
-  DDP grad all-reduce                   torch.distributed.all_reduce (RCCL) on the flat fp32 grads
+  DDP grad all-reduce                   ptk_projector_bwd_allreduce (RCCL via libptk, overlapped with the
+                                        projector backward); gloo: torch.distributed, same pieces
   clip_grad_norm_(5) + AdamW (:240-242) ptk_clip_adamw, then bf16 shadow refresh
   lr_scheduler.step() x num_processes   host-side cosine lambda (no device sync)
 
@@ -33,7 +34,7 @@ import torch
 from . import _lib as L
 from . import kernels as K
 from .config import Stage1Config
-from .dist import allreduce_grads_
+from .dist import RcclComm, allreduce_grads_chunked_, grad_exchange_chunks
 from .gemma3 import Gemma3CausalLM
 from .projectors import MLPProjector
 from .siglip import SiglipVisionTower
@@ -51,7 +52,7 @@ class Stage1Engine:
     def __init__(self, vision: SiglipVisionTower, llm: Gemma3CausalLM, projector: MLPProjector, *,
                  learning_rate=1e-4, weight_decay=0.01, gradient_accumulation_steps=1, max_grad_norm=5.0,
                  warmup_steps=0, total_steps=1, betas=(0.9, 0.999), eps=1e-8, process_group=None,
-                 world_size=1):
+                 world_size=1, comm="auto"):
         self.vision, self.llm, self.proj = vision, llm, projector
         self.device = vision.device
         self.lr0, self.wd, self.gas, self.max_norm = learning_rate, weight_decay, gradient_accumulation_steps, max_grad_norm
@@ -76,6 +77,16 @@ class Stage1Engine:
         self._graph = None         # graph_step: captured forward_backward, its input key and static inputs
         self._graph_key = None
         self._graph_in = None
+        # DDP exchange of the projector grads.  RCCL process group: libptk's communicator, the all-reduce
+        # overlapped with the projector backward (ptk_projector_bwd_allreduce).  Otherwise (gloo): the
+        # collective library, piece by piece in the same order, after the backward.  comm=True forces the
+        # RCCL path (e.g. at world 1, to exercise it on one GPU); False disables it.
+        self.comm, self._comm_stream, self._exchanged = None, None, False
+        use = comm is True or (comm == "auto" and world_size > 1 and torch.distributed.is_initialized()
+                               and torch.distributed.get_backend(process_group) == "nccl")
+        if use:
+            self.comm = RcclComm(process_group)
+            self._comm_stream = torch.cuda.Stream(self.device)
 
     def _buffers(self, B, T):
         """Step buffers are allocated for the largest batch seen at this text length; a smaller batch
@@ -171,7 +182,17 @@ class Stage1Engine:
                                      1.0 / float(self.gas * self.gas), self.loss, pad_token_id=self.pad_token_id)
         L.check(L.lib().ptk_gather_vision_grad(self.dx.data_ptr(), B, self.N, self.Sp, self.llm.cfg.hidden_size,
                                                self.dy.data_ptr(), L.stream_ptr(self.device)), "gather_vision_grad")
-        self.proj.bwd_into(self.vis, self.a, self.h, self.dy, self.proj_ws)
+        if self.comm is not None:
+            L.check(L.lib().ptk_projector_bwd_allreduce(self.proj.desc(), self.vis.shape[0], self.vis.data_ptr(),
+                                                        self.a.data_ptr(), self.h.data_ptr(), self.dy.data_ptr(),
+                                                        self.proj.flat_grad.data_ptr(), self.proj_ws.data_ptr(),
+                                                        self.proj_ws.numel(), self.comm.handle,
+                                                        self._comm_stream.cuda_stream, L.stream_ptr(self.device)),
+                    "ptk_projector_bwd_allreduce")
+            self._exchanged = True
+        else:
+            self.proj.bwd_into(self.vis, self.a, self.h, self.dy, self.proj_ws)
+            self._exchanged = False
         if not torch.cuda.is_current_stream_capturing():   # (graph_step never prefetches)
             rel = torch.cuda.Event()
             rel.record(main)
@@ -196,7 +217,12 @@ class Stage1Engine:
 
     def optimizer_step(self):
         """DDP all-reduce (sum; 1/W folded into the update), clip + AdamW, schedule."""
-        grad_scale = allreduce_grads_(self.proj.flat_grad, self.world, self.pg)
+        if self._exchanged:      # summed over the ranks inside the backward (RCCL, overlapped)
+            grad_scale = 1.0 / self.world
+        else:
+            grad_scale = allreduce_grads_chunked_(self.proj.flat_grad, grad_exchange_chunks(self.proj), self.world,
+                                                  self.pg)
+        self._exchanged = False
         lr = self.lr0 * cosine_lambda(self.sched_step, self.warmup, self.total)
         self.opt_step += 1
         b1, b2 = self.betas
@@ -225,6 +251,8 @@ class Stage1Engine:
         step (and the DDP all-reduce runs there).  Same kernels in the same order: bit-identical to step()."""
         if self._prefetched is not None or self._vision_ready:
             raise RuntimeError("Stage1Engine.graph_step: a vision prefetch / encode_vision is pending")
+        if self.comm is not None:
+            raise RuntimeError("Stage1Engine.graph_step: not with the RCCL exchange inside the backward")
         self._buffers(*token_ids.shape)
         # the graph replays the device pointers it was captured with: key it on every buffer it touches, so
         # a reallocation in between (an eager step at a larger batch or another text length, a grown

@@ -228,3 +228,66 @@ def stage2_rccl_world1(rank, world, port, out_dir):
           torch.equal(out[0][2], out[1][2])]
     np.save(os.path.join(out_dir, "rccl.npy"), np.array(ok, dtype=np.int64))
     dist.destroy_process_group()
+
+
+def chunked_exchange(rank, world, port, out_dir):
+    """CPU/gloo: the projector grad exchange piece by piece (grad_exchange_chunks order) vs one all-reduce."""
+    _init(rank, world, port, "gloo")
+    from projectiontrainer_amd import dist as D
+    from projectiontrainer_amd.projectors import MLPProjector
+    proj = MLPProjector(32, 48, expansion_factor=3)
+    g = torch.Generator().manual_seed(100 + rank)
+    flat = torch.randn(proj.flat.numel(), generator=g)
+    a, b = flat.clone(), flat.clone()
+    s1 = D.allreduce_grads_(a, world)
+    s2 = D.allreduce_grads_chunked_(b, D.grad_exchange_chunks(proj), world)
+    chunks = D.grad_exchange_chunks(proj)
+    covered = sorted((o, o + n) for o, n in chunks)
+    ok = [torch.equal(a, b), s1 == s2, covered == [(0, covered[0][1]), (covered[0][1], flat.numel())]]
+    np.save(os.path.join(out_dir, f"chunk{rank}.npy"), np.array(ok, dtype=np.int64))
+    dist.destroy_process_group()
+
+
+def rccl_comm_world1(rank, world, port, out_dir):
+    """RCCL at world 1 through libptk's communicator: ptk_comm_allreduce_sum / _avg on a buffer, and a
+    Stage1Engine step with the exchange overlapped inside the projector backward (comm=True) against the
+    same step without it (comm=False)."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port), RANK="0", WORLD_SIZE="1", LOCAL_RANK="0")
+    dev = torch.device("cuda:0")
+    torch.cuda.set_device(dev)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=dev)
+    from projectiontrainer_amd import _lib as L
+    from projectiontrainer_amd import dist as D
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.gemma3 import Gemma3CausalLM
+    from projectiontrainer_amd.projectors import MLPProjector
+    from projectiontrainer_amd.siglip import SiglipVisionTower
+    from projectiontrainer_amd.stage1 import Stage1Engine
+    comm = D.RcclComm()
+    t = torch.arange(1000, dtype=torch.float32, device=dev)
+    u = t.clone()
+    comm.allreduce_sum_(u, L.stream_ptr(dev))
+    L.check(L.lib().ptk_comm_allreduce_avg(comm.handle, u.data_ptr(), u.numel(), L.stream_ptr(dev)), "avg")
+    torch.cuda.synchronize()
+    ok = [L.lib().ptk_comm_world(comm.handle) == 1, torch.equal(t, u)]
+    comm.close()
+    cfg = PRESETS["tiny"]
+    vp, lp = W.siglip_vision_params(cfg.vision), W.gemma3_params(cfg.text)
+    pp = W.projector_params(cfg.vision.hidden_size, cfg.text.hidden_size)
+    px, ids, labels = (torch.from_numpy(x).to(dev) for x in W.synthetic_batch(cfg, seed=5))
+    res = []
+    for use in (True, False):
+        proj = MLPProjector(cfg.vision.hidden_size, cfg.text.hidden_size)
+        proj.load_state_dict({k: torch.from_numpy(v) for k, v in pp.items()})
+        proj.to(dev)
+        eng = Stage1Engine(SiglipVisionTower(cfg.vision, vp, dev),
+                           Gemma3CausalLM(cfg.text, lp, dev, max_pos=Gemma3CausalLM.seq_pad(cfg.seq_len)), proj,
+                           world_size=1, comm=use, total_steps=10)
+        for _ in range(2):
+            eng.step(px, ids, labels)
+        torch.cuda.synchronize()
+        res.append((eng.proj.flat.clone(), eng.proj.flat_grad.clone(), eng.comm is not None))
+    ok += [res[0][2] and not res[1][2], torch.equal(res[0][0], res[1][0]), torch.equal(res[0][1], res[1][1])]
+    np.save(os.path.join(out_dir, "rcclcomm.npy"), np.array(ok, dtype=np.int64))
+    dist.destroy_process_group()

@@ -108,6 +108,26 @@ def test_ddp_grad_average_gloo_cpu():
     np.testing.assert_allclose(g0, (gs[0] + gs[1]) / 2, rtol=1e-5, atol=1e-9)
 
 
+def test_chunked_exchange_matches_single_allreduce_gloo_cpu():
+    """world 2, gloo: the projector grads exchanged in the overlapped path's pieces (dW2 | db2, then dW1 | db1;
+    SURVEY §8(e)) equal one all-reduce of the whole buffer bit for bit, and the pieces tile the buffer."""
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(dist_worker.chunked_exchange, args=(2, _port(), td), nprocs=2, join=True)
+        r = [np.load(f"{td}/chunk{k}.npy") for k in range(2)]
+    assert all(x.all() for x in r), r
+
+
+@pytest.mark.gpu
+def test_rccl_comm_world1(gpu):
+    """libptk's RCCL communicator (ptk_comm_*) at world 1 on the GPU: sum / average are the identity, and a
+    Stage1Engine whose exchange runs inside the projector backward on the comm stream
+    (ptk_projector_bwd_allreduce) trains bit-identically to the engine without it."""
+    with tempfile.TemporaryDirectory() as td:
+        mp.spawn(dist_worker.rccl_comm_world1, args=(1, _port(), td), nprocs=1, join=True)
+        r = np.load(f"{td}/rcclcomm.npy")
+    assert r.all(), r
+
+
 @pytest.mark.gpu
 def test_engine_ddp_two_ranks_one_gpu(gpu):
     """The real Stage1Engine at world size 2 (gloo over one device): replicas stay
