@@ -760,9 +760,19 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
                         (((act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32)) ||
                           (act == ACT_GELU_TANH && out == OUT_BF16)) &&
                          a.K <= 8192 && w4_round_fill(a.M, a.N) >= 0.8));
-  // persistent 8-wave kernel (forced mode 32; PTK_P8=1 puts the w4 shapes on it)
+  // persistent 8-wave kernel (two waves per SIMD, gemm_w4.hip) where it measured ahead of the 4-wave one
+  // (tools/p8_probe.py, same box, interleaved, r03): the w4 plain / GELU-tanh shapes at K <= 2048 (Gemma q|k|v
+  // 90 -> 87 us, o 58 -> 56, SigLIP q|k|v 111 -> 109, fc1 157 -> 151), the projector fc1 with the GELU-erf
+  // epilogue (674 -> 583 us) and its backward (dA, 858 -> 703 us) and the long-K d(gate|up) dX (K 13 824, N <= 2048: 700 -> 672 us); w4 keeps the
+  // GEGLU / GEGLU-backward epilogues and the K 6 912 down projection (697 / 486 / 330 us vs 723 / 500 / 342).
+  // PTK_P8=1 puts every w4 shape on it (A/B)
   static const bool p8_env = [] { const char* e = getenv("PTK_P8"); return e && e[0] == '1'; }();
-  if (batch == 1 && (g_force_tiles == 32 || (p8_env && w4_auto)) && p8_supported(a, act, out)) {
+  const bool p8_auto = g_force_tiles == 0 && a.M >= 4096 && a.N <= 16384 &&
+                       ((w4_auto && (p8_env || (act != ACT_GEGLU && act != ACT_GEGLU_BWD && a.K <= 2048))) ||
+                        ((act == ACT_GELU_ERF || act == ACT_GELU_ERF_BWD) && out == OUT_BF16 && a.K <= 2048 &&
+                         w4_round_fill(a.M, a.N) >= 0.8) ||
+                        (act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32) && a.K >= 12288 && a.N <= 2048));
+  if (batch == 1 && (g_force_tiles == 32 || p8_auto) && p8_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);

@@ -77,6 +77,7 @@ class Stage1Engine:
         self._graph = None         # graph_step: captured forward_backward, its input key and static inputs
         self._graph_key = None
         self._graph_in = None
+        self._retired_graphs = []
         # DDP exchange of the projector grads.  RCCL process group: libptk's communicator, the all-reduce
         # overlapped with the projector backward (ptk_projector_bwd_allreduce).  Otherwise (gloo): the
         # collective library, piece by piece in the same order, after the backward.  comm=True forces the
@@ -260,6 +261,12 @@ class Stage1Engine:
         key = (tuple(pixel_values.shape), pixel_values.dtype, tuple(token_ids.shape), tuple(labels.shape),
                self._buffer_fingerprint())
         if self._graph is None or self._graph_key != key:
+            # a replaced graph is kept, not destroyed: on this ROCm (7.2 / torch 2.10) destroying a captured
+            # graph and capturing another made the NEW graph's second and later replays compute garbage
+            # (tools/graph_debug.py: NaN grads; kept alive, every replay is bit-identical to eager).  Only a
+            # shape or buffer change retires one, so the list stays short.
+            if self._graph is not None:
+                self._retired_graphs.append((self._graph, self._graph_in))
             self._graph = None
             static = (pixel_values.clone(), token_ids.clone(), labels.clone())
             g = torch.cuda.CUDAGraph()

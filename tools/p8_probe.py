@@ -26,6 +26,9 @@ SHAPES = [  # name, M, N, K, act, out dtype
     ("sig_fc2", MS, 1024, 4096, L.ACT_NONE, torch.bfloat16),
     ("proj_fc1", MS, 11520, 1024, L.ACT_GELU_ERF, torch.bfloat16),
     ("proj_fc2", MS, 1152, 11520, L.ACT_NONE, torch.float32),
+    ("proj_dW2", 1152, 11520, 18432, L.ACT_NONE, torch.float32),
+    ("proj_dW1", 11520, 1024, 18432, L.ACT_NONE, torch.float32),
+    ("proj_dA", 18432, 11520, 1152, L.ACT_GELU_ERF_BWD, torch.bfloat16),
     ("sq8192", 8192, 8192, 8192, L.ACT_NONE, torch.bfloat16),
 ]
 
@@ -42,6 +45,8 @@ def setup(m, n, k, act, odt):
                   aux_in2=torch.randn(m, n, device=dev).to(torch.bfloat16))
     elif act == L.ACT_GELU_ERF:
         kw = dict(aux=torch.empty(m, n, dtype=torch.bfloat16, device=dev))
+    elif act == L.ACT_GELU_ERF_BWD:
+        kw = dict(aux_in=torch.randn(m, n, device=dev).to(torch.bfloat16))
     return A, B, kw
 
 
