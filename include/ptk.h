@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTK_ABI_VERSION 4
+#define PTK_ABI_VERSION 3
 
 int ptk_abi_version(void);
 const char* ptk_last_error(void);
@@ -75,18 +75,8 @@ typedef struct {
   int64_t ld_aux_in;
   ptk_rowmap amap;
   ptk_rowmap cmap;
-  /* Optional split-tail scratch (NULL = off) of ptk_gemm_split_workspace_bytes() bytes whose first
-   * PTK_GEMM_SPLIT_COUNTER_BYTES are zero before its first use (every GEMM leaves them zero again).  With it a
-   * persistent-kernel GEMM whose 256x256 tiles fill the last round of the CUs badly splits that round's tiles
-   * over K (fp32 partials, summed in a fixed order: deterministic).  One GEMM at a time per scratch. */
-  void* split_ws;
-  size_t split_ws_bytes;
 } ptk_gemm_desc;
 int ptk_gemm(const ptk_gemm_desc* d, void* stream);
-#define PTK_GEMM_SPLIT_COUNTER_BYTES 16384
-size_t ptk_gemm_split_workspace_bytes(void);
-/* K-chunks the split-tail plan gives the last round of this GEMM's tiles (0: no split), for tests. */
-int ptk_gemm_split_ways(const ptk_gemm_desc* d);
 
 /* LayerNorm (SigLIP, modeling_siglip.py:329): x f32 [rows,cols] -> y bf16. */
 int ptk_layernorm(const float* x, const float* w, const float* b, void* y, int rows, int cols, float eps,

@@ -33,8 +33,7 @@ class GemmDesc(C.Structure):
                 ("ld_rowadd", c_int64), ("resid", c_void_p), ("ld_resid", c_int64),
                 ("aux", c_void_p), ("aux2", c_void_p), ("ld_aux", c_int64),
                 ("aux_in", c_void_p), ("aux_in2", c_void_p), ("ld_aux_in", c_int64),
-                ("amap", RowMap), ("cmap", RowMap),
-                ("split_ws", c_void_p), ("split_ws_bytes", C.c_size_t)]
+                ("amap", RowMap), ("cmap", RowMap)]
 
 
 class FlashDesc(C.Structure):
@@ -121,7 +120,7 @@ class ImageDesc(C.Structure):
                 ("coef_off", c_int64), ("tmp_off", c_int64)]
 
 
-ABI_VERSION = 4      # include/ptk.h PTK_ABI_VERSION
+ABI_VERSION = 3      # include/ptk.h PTK_ABI_VERSION
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -144,8 +143,6 @@ SIGNATURES = {
     "ptk_gemm_force_small_tiles": (c_int, [c_int]),
     "ptk_gemm_timer_read": (c_int, [c_int, C.POINTER(C.c_double), C.POINTER(c_int)]),
     "ptk_gemm_path_counts": (c_int, [c_void_p, c_int]),
-    "ptk_gemm_split_workspace_bytes": (C.c_size_t, []),
-    "ptk_gemm_split_ways": (c_int, [C.POINTER(GemmDesc)]),
     "ptk_flash_attn_fwd": (c_int, [C.POINTER(FlashDesc), c_void_p]),
     "ptk_flash_attn_bwd": (c_int, [C.POINTER(FlashBwdDesc), c_void_p]),
     "ptk_flash_bwd_workspace_bytes": (c_size_t, [C.POINTER(FlashBwdDesc)]),

@@ -33,7 +33,6 @@ GemmArgs to_args(const ptk_gemm_desc* d) {
   a.aux = (bf16_t*)d->aux; a.aux2 = (bf16_t*)d->aux2; a.ld_aux = d->ld_aux;
   a.aux_in = (const bf16_t*)d->aux_in; a.aux_in2 = (const bf16_t*)d->aux_in2; a.ld_aux_in = d->ld_aux_in;
   a.amap = to_map(d->amap); a.cmap = to_map(d->cmap);
-  if (d->split_ws && d->split_ws_bytes >= split_scratch_bytes()) split_scratch_attach(a, d->split_ws);
   return a;
 }
 
@@ -52,9 +51,6 @@ int ptk_gemm(const ptk_gemm_desc* d, void* stream) {
   if (d->act == PTK_ACT_GEGLU && (d->N % 32)) return set_error("ptk_gemm: GEGLU needs N %% 32 == 0");
   return launch_gemm(to_args(d), d->act, d->out, d->batch > 0 ? d->batch : 1, ST);
 }
-
-size_t ptk_gemm_split_workspace_bytes(void) { return split_scratch_bytes(); }
-int ptk_gemm_split_ways(const ptk_gemm_desc* d) { return d ? p8_split_ways(to_args(d)) : 0; }
 
 int ptk_layernorm(const float* x, const float* w, const float* b, void* y, int rows, int cols, float eps,
                   void* stream) {
@@ -191,7 +187,6 @@ size_t ptk_projector_workspace_bytes(const ptk_projector* p, int rows) {
   s += align256(R * I * 2);       // dA
   s += align256(Dv * R * 2);      // x^T
   s += align256(64 * (I > Dl ? I : Dl) * 4);   // colsum partials
-  s += align256(split_scratch_bytes());         // split-tail GEMM scratch
   return s;
 }
 
@@ -211,10 +206,7 @@ int projector_bwd_stage(const ptk_projector* p, int rows, const void* x, const v
   bf16_t* T = (bf16_t*)w; w += align256((size_t)I * Rp * 2);
   bf16_t* dA = (bf16_t*)w; w += align256((size_t)Rp * I * 2);
   bf16_t* xT = (bf16_t*)w; w += align256((size_t)Dv * Rp * 2);
-  float* part = (float*)w; w += align256(64 * (size_t)(I > Dl ? I : Dl) * 4);
-  void* split = w;
-  if (hipMemsetAsync(split, 0, PTK_GEMM_SPLIT_COUNTER_BYTES, st) != hipSuccess)
-    return set_error("projector_bwd: split counters memset failed");
+  float* part = (float*)w;
   if (stage == 0) {
     // db2 = colsum(dy); dW2 = dy^T . h  (contraction over tokens)
     if (launch_colsum_bf16((const bf16_t*)dy, R, Dl, db2, part, st)) return -1;
@@ -222,14 +214,12 @@ int projector_bwd_stage(const ptk_projector* p, int rows, const void* x, const v
     if (launch_transpose((const bf16_t*)h, I, 0, 0, 1, T, Rp, 0, 0, 1, R, I, Rp, st)) return -1;
     GemmArgs g;
     g.A = dyT; g.B = T; g.C = dw2; g.M = Dl; g.N = I; g.K = Rp; g.lda = Rp; g.ldb = Rp; g.ldc = I;
-    split_scratch_attach(g, split);
     return launch_gemm(g, ACT_NONE, OUT_F32, 1, st);
   }
   // dA = (dy . W2) * gelu'(a)
   GemmArgs g2;
   g2.A = (const bf16_t*)dy; g2.B = (const bf16_t*)p->w2t; g2.C = dA; g2.M = R; g2.N = I; g2.K = Dl;
   g2.lda = Dl; g2.ldb = Dl; g2.ldc = I; g2.aux_in = (const bf16_t*)a; g2.ld_aux_in = I;
-  split_scratch_attach(g2, split);
   if (launch_gemm(g2, ACT_GELU_ERF_BWD, OUT_BF16, 1, st)) return -1;
   // db1 = colsum(dA); dW1 = dA^T . x
   if (launch_colsum_bf16(dA, R, I, db1, part, st)) return -1;
@@ -237,7 +227,6 @@ int projector_bwd_stage(const ptk_projector* p, int rows, const void* x, const v
   if (launch_transpose((const bf16_t*)x, Dv, 0, 0, 1, xT, Rp, 0, 0, 1, R, Dv, Rp, st)) return -1;
   GemmArgs g3;
   g3.A = T; g3.B = xT; g3.C = dw1; g3.M = I; g3.N = Dv; g3.K = Rp; g3.lda = Rp; g3.ldb = Rp; g3.ldc = Dv;
-  split_scratch_attach(g3, split);
   return launch_gemm(g3, ACT_NONE, OUT_F32, 1, st);
 }
 }  // namespace ptk

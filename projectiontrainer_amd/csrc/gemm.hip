@@ -772,11 +772,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
                         ((act == ACT_GELU_ERF || act == ACT_GELU_ERF_BWD) && out == OUT_BF16 && a.K <= 2048 &&
                          w4_round_fill(a.M, a.N) >= 0.8) ||
                         (act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32) && a.K >= 12288 && a.N <= 2048));
-  // split tail (gemm_w4.hip P8Split): a persistent-kernel shape whose last round of 256x256 tiles fills the CUs
-  // badly goes to the 8-wave kernel with that round split over K when the caller gave split scratch
-  const bool split_auto = g_force_tiles == 0 && a.M >= 4096 && a.N <= 16384 && a.split_ws &&
-                          (w4_auto || p8_auto) && p8_split_ways(a) > 0;
-  if (batch == 1 && (g_force_tiles == 32 || p8_auto || split_auto) && p8_supported(a, act, out)) {
+  if (batch == 1 && (g_force_tiles == 32 || p8_auto) && p8_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);

@@ -601,73 +601,12 @@ int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_
 // its last reader (the ping-pong kernel's consumer stream).  The tile's last k-step reads no fragments, so
 // only the accumulators are live through the epilogue; the next tile's first fragments are read after it.
 // The ring, the DMA cursor and the one wait + barrier per pair of k-steps are w4's; the waits are vmcnt(4).
-// split-tail epilogue (P8Split) of the wave that arrived last: row block I of the S <= 4 chunks' partials
-// (chunk cc of this wave's part at src + cc * cstride floats; fragment (I, j) of a lane at +(4I + j) * 256) is
-// loaded with all 4S loads in flight, summed in chunk order (deterministic whichever chunk arrived last) and
-// handed to the epilogue of that row block
-template <int ACT, int OUT, int I>
-PTK_DEV void p8_tail_rows(const GemmArgs& p, const float* src, size_t cstride, int S, long row0, long col0,
-                          int lane, char* sink) {
-  f32x4_t v[4][4];
-#pragma unroll
-  for (int cc = 0; cc < 4; ++cc) {
-    if (cc < S) {
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj)
-        asm volatile("global_load_dwordx4 %0, %1, off sc1"
-                     : "=v"(v[cc][jj]) : "v"(src + cc * cstride + (4 * I + jj) * 256) : "memory");
-    }
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  f32x4_t sum[4];
-#pragma unroll
-  for (int jj = 0; jj < 4; ++jj) {
-    sum[jj] = v[0][jj] + v[1][jj];
-    if (S > 2) sum[jj] += v[2][jj];
-    if (S > 3) sum[jj] += v[3][jj];
-  }
-  if constexpr (ACT == ACT_GEGLU_BWD) {
-    u16x8_t G[2], U[2];
-    w4_gbwd_load<I, 2>(p, row0, col0, lane, G, U);
-    w4_gbwd_rows<I, 2>(p, sum, row0, col0, lane, sink, G, U);
-  } else {
-    w4_rows<ACT, OUT, I, 4>(p, sum, row0, col0, lane, sink);
-  }
-}
-template <int ACT, int OUT>
-PTK_DEV void p8_tail_epilogue(const GemmArgs& p, const float* src, size_t cstride, int S, long row0, long col0,
-                              int lane) {
-  char* sink = g_w4_sink + lane * 64;
-  p8_tail_rows<ACT, OUT, 0>(p, src, cstride, S, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 1>(p, src, cstride, S, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 2>(p, src, cstride, S, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 3>(p, src, cstride, S, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 4>(p, src, cstride, S, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 5>(p, src, cstride, S, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 6>(p, src, cstride, S, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 7>(p, src, cstride, S, row0, col0, lane, sink);
+namespace {
+constexpr int P8_PIECES = 4;   // LDS-DMA pieces per wave per k-step
 }
 
-// Split tail (P8Split, all zero = off): a tile grid that fills the persistent grid's last round badly (Gemma3's
-// N = 1152 projections: 440 tiles = 1.72 rounds of 256 CUs; q|k|v 528 = 2.06) runs its first R full rounds
-// data-parallel (every workgroup R whole tiles, the lock-step L2 sharing of the plain kernel) and splits each of
-// the Tt remaining tiles into S K-chunks, so the last round's Tt x S items spread over every CU.  Items go out
-// chunk-major (chunk c of every tail tile, then c + 1), so the workgroups of an XCD stream neighbouring tiles at
-// the same K offset.  Each wave writes its 128x64 fp32 partial (32 KiB, write-through `sc1` stores) to the
-// item's slab, drains it (vmcnt(0)) and adds 1 to the (tail tile, wave) arrival counter (agent scope); the wave
-// whose add returns S - 1 loads the other chunks' partials (`sc1` loads: the hand-off of MI355X_MICROARCH.md's
-// "one lane per storing wave, agent atomic add, sc1 stores and loads" row), sums the S partials in chunk order
-// (deterministic: the same result whichever chunk arrives last), resets the counter for the next launch and runs
-// the fused epilogue.  No wave ever waits for another workgroup.
-struct P8Split {
-  int R = 0, Tt = 0, S = 0;      // full data-parallel rounds, tail tiles, K-chunks per tail tile
-  float* slab = nullptr;         // Tt * S * 8 waves * 32 KiB of partials
-  uint32_t* cnt = nullptr;       // Tt * 8 arrival counters, zero at launch (each launch leaves them zero)
-};
-
 template <int ACT, int OUT>
-__global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes,
-                                                         P8Split sp) {
+__global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
   __shared__ __attribute__((aligned(16))) char smem[W4_NSLOT * W4_SLOT];   // 160 KiB: the k-step ring
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -680,33 +619,10 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     const int b = blockIdx.x, q = G >> 3, rr = G & 7, x = b & 7;
     loc = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
   }
+  if (loc >= ntile) return;
   const int nt = p.K / W4_KT;                              // 64-deep K-tiles per output tile
-  // this workgroup's segments: whole tiles loc, loc + G, .. below the data-parallel range, then tail items
-  // loc, loc + G, .. of the Tt x S chunk-major items
-  const int dp_tiles = sp.S ? sp.R * G : ntile;
-  const int n_dp = loc < dp_tiles ? (dp_tiles - loc + G - 1) / G : 0;
-  const int n_items = sp.S ? sp.Tt * sp.S : 0;
-  const int n_tail = loc < n_items ? (n_items - loc + G - 1) / G : 0;
-  const int nseg = n_dp + n_tail;
-  if (nseg == 0) return;
-  // segment s -> tile, K-tile range [k0, k1), tail item (-1: whole tile)
-  auto segment = [&](int s, int& t, int& k0, int& k1, int& item) __attribute__((always_inline)) {
-    if (s < n_dp) {
-      t = loc + s * G; k0 = 0; k1 = nt; item = -1;
-    } else {
-      item = loc + (s - n_dp) * G;
-      const int c = item / sp.Tt, u = item - c * sp.Tt;
-      t = dp_tiles + u;
-      k0 = c * nt / sp.S;
-      k1 = (c + 1) * nt / sp.S;
-    }
-  };
-  int total_ks = 0;
-  for (int s = 0; s < nseg; ++s) {
-    int t, k0, k1, it;
-    segment(s, t, k0, k1, it);
-    total_ks += 2 * (k1 - k0);
-  }
+  const int nks = 2 * nt;                                  // 32-deep k-steps per output tile
+  const int total_ks = ((ntile - loc + G - 1) / G) * nks;
   const u32x4_t rsa = w4_rsrc(p.A, a_bytes), rsb = w4_rsrc(p.B, b_bytes);
 
   // global -> LDS: wave w fills rows 32w..32w+31 of both operands (2 + 2 pieces of 16 rows x 64 B), lane i of
@@ -721,25 +637,20 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
   }
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   const uint32_t lds_dma = lds_base + wave * 32 * 64;
-  // DMA cursor: segment dseg, k-step dks of it (past the last k-step it stays put and re-loads that k-step into
-  // a free slot, never read, so every k-step issues the same instructions)
-  int dseg = 0, dks = 0, dlen = 0, dcount = 0;
+  int dt = loc, dks = 0, dcount = 0;
   uint32_t dsa = 0, dsb = 0;
-  auto dma_seg = [&](int s) {
-    int t, k0, k1, it;
-    segment(s, t, k0, k1, it);
+  auto dma_tile = [&](int t) {
     int bm, bn;
     w4_tile_coords(t, nbm, nbn, bm, bn);
-    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * W4 + (int)p.amap.off) * (uint32_t)p.lda * 2u +
-                                         (uint32_t)k0 * (W4_KT * 2));
-    dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * W4) * (uint32_t)p.ldb * 2u + (uint32_t)k0 * (W4_KT * 2));
-    dlen = 2 * (k1 - k0);
+    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * W4 + (int)p.amap.off) * (uint32_t)p.lda * 2u);
+    dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * W4) * (uint32_t)p.ldb * 2u);
   };
   auto dma_advance = [&]() {
     if (++dcount < total_ks) {
-      if (++dks == dlen) {
+      if (++dks == nks) {
         dks = 0;
-        dma_seg(++dseg);
+        dt += G;
+        dma_tile(dt);
       }
     }
   };
@@ -801,30 +712,9 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     if (rd) W4_DSREAD(fa[7], ba, 7 * 1024);
   };
 
-  // split-tail hand-off of one wave's 128x64 partial (see P8Split).  Returns true when this wave arrived last
-  // and must sum the partials and run the epilogue (p8_tail_epilogue).
-  auto tail_finish = [&](int item) __attribute__((always_inline)) -> bool {
-    const int u = item % sp.Tt;
-    const size_t wave_floats = 128 * 64;
-    float* mine = sp.slab + ((size_t)item * 8 + wave) * wave_floats;
-#pragma unroll
-    for (int q = 0; q < 8; ++q)
-#pragma unroll
-      for (int jj = 0; jj < 4; ++jj) {
-        float* d = mine + ((q * 4 + jj) * 64 + lane) * 4;
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(d), "v"(acc[q][jj]) : "memory");
-      }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t old = 0;
-    if (lane == 0)
-      old = __hip_atomic_fetch_add(sp.cnt + u * 8 + wave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __builtin_amdgcn_readfirstlane(old);
-    return (int)old == sp.S - 1;
-  };
-
   auto run = [&](auto half_c) __attribute__((always_inline)) {
     // prologue: k-steps 0..3 into slots 0..3; 0..2 landed and published; fragments of k-step 0 read
-    dma_seg(0);
+    dma_tile(dt);
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const uint32_t da = lds_dma + b * W4_SLOT, db = da + W4_SOPB;
@@ -844,8 +734,8 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     // flight, i+4 issued into the slot of i-1); vmcnt(4) before each pair's barrier leaves only the youngest
     // k-step's 4 pieces in flight
     uint32_t rs = W4_SLOT, ws = 4 * W4_SLOT;
-    // one pair of k-steps, then the wait + barrier; the segment's first k-step initialises the accumulators
-    // (MFMA with C = 0) and its last reads no fragments.  Peeled per segment (no branch between MFMA forms),
+    // one pair of k-steps, then the wait + barrier; the tile's first k-step initialises the accumulators
+    // (MFMA with C = 0) and its last reads no fragments.  Peeled per tile (no branch between MFMA forms),
     // so the 128 accumulators keep their registers across the K loop.
     auto pair = [&](auto first_c, auto last_c) __attribute__((always_inline)) {
       constexpr bool lst = decltype(last_c)::value;
@@ -855,30 +745,20 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       ws = slot_next(ws);
       kstep(std::false_type{}, std::integral_constant<bool, !lst>{}, half_c, fb1, fb0, rs, ws);
       dma_advance();
-      if (!lst) rs = slot_next(rs);   // last pair: rs stays on the next segment's first k-step
+      if (!lst) rs = slot_next(rs);   // last pair: rs stays on the next tile's first k-step (read after the epilogue)
       ws = slot_next(ws);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     };
-    for (int s = 0; s < nseg; ++s) {
-      int t, k0, k1, item;
-      segment(s, t, k0, k1, item);
+    for (int t = loc; t < ntile; t += G) {
       pair(std::true_type{}, std::false_type{});
-      for (int kt = k0 + 1; kt < k1 - 1; ++kt) pair(std::false_type{}, std::false_type{});
+      for (int kt = 1; kt < nt - 1; ++kt) pair(std::false_type{}, std::false_type{});
       pair(std::false_type{}, std::true_type{});
       asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");   // MFMA D -> accumulator read wait states
       int bm, bn;
       w4_tile_coords(t, nbm, nbn, bm, bn);
-      const long row0 = (long)bm * W4 + wr * 128, col0 = (long)bn * W4 + wc * 128 + hf * 64;
-      if (item < 0) {
-        w4_epilogue<ACT, OUT, 4>(p, acc, row0, col0, lane);
-      } else if (tail_finish(item)) {
-        const int u = item % sp.Tt;
-        const float* src = sp.slab + ((size_t)u * 8 + wave) * (128 * 64) + lane * 4;
-        p8_tail_epilogue<ACT, OUT>(p, src, (size_t)sp.Tt * 8 * (128 * 64), sp.S, row0, col0, lane);
-        if (lane == 0) __hip_atomic_store(sp.cnt + u * 8 + wave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      }
-      // the next segment's first k-step (published by the barrier; harmless after the last).  Its slot is the
+      w4_epilogue<ACT, OUT, 4>(p, acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128 + hf * 64, lane);
+      // the next tile's first k-step (published by the barrier; harmless after the last).  Its slot is the
       // one the NEXT pair's second k-step restages (k-step i+6 lands in the slot of i+1), so a barrier keeps
       // a wave that finished its epilogue early from overwriting it before every wave has read it
       read_frags(rs);
@@ -894,46 +774,6 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
 // the p8 path takes what the w4 path takes, at K >= 128 (a tile's first and last k-step pairs are peeled)
 bool p8_supported(const GemmArgs& a, int act, int out) { return a.K >= 128 && w4_supported(a, act, out); }
 
-// the split-tail plan (P8Split) for a launch, or S = 0: the last round must fill < 85 % of the CUs, every
-// chunk >= 2 K-tiles, and the split must cut the last round's time (ceil(Tt S / G) / S of a round) by >= 15 %
-static P8Split p8_split_plan(const GemmArgs& a, long ntile, long G) {
-  P8Split sp;
-  if (!a.split_ws || !a.split_cnt || ntile <= G) return sp;
-  const long R = ntile / G, Tt = ntile - R * G, nt = a.K / W4_KT;
-  if (Tt == 0 || Tt >= (G * 85) / 100 || Tt * 8 > a.split_cnt_n) return sp;
-  double best = 1.0;
-  int bestS = 0;
-  for (int S = 2; S <= 4; ++S) {
-    if (nt / S < 2) break;
-    if ((double)Tt * S * 8 * 128 * 64 > (double)a.split_ws_floats) break;
-    const double cost = (double)((Tt * S + G - 1) / G) / S;
-    if (cost < best - 1e-9) { best = cost; bestS = S; }
-  }
-  if (bestS == 0 || best > 0.85) return sp;
-  sp.R = (int)R; sp.Tt = (int)Tt; sp.S = bestS;
-  sp.slab = a.split_ws;
-  sp.cnt = a.split_cnt;
-  return sp;
-}
-
-constexpr size_t P8_CNT_BYTES = 16384;   // = PTK_GEMM_SPLIT_COUNTER_BYTES
-size_t split_scratch_bytes() {
-  num_cu();
-  return P8_CNT_BYTES + (size_t)((g_num_cu * 85) / 100) * 4 * 8 * 128 * 64 * sizeof(float);
-}
-void split_scratch_attach(GemmArgs& a, void* ws) {
-  num_cu();
-  a.split_cnt = (uint32_t*)ws;
-  a.split_cnt_n = (int)(P8_CNT_BYTES / sizeof(uint32_t));
-  a.split_ws = (float*)((char*)ws + P8_CNT_BYTES);
-  a.split_ws_floats = (long)((split_scratch_bytes() - P8_CNT_BYTES) / sizeof(float));
-}
-int p8_split_ways(const GemmArgs& a) {
-  num_cu();
-  const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
-  return p8_split_plan(a, ntile, std::min<long>(ntile, g_num_cu)).S;
-}
-
 int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st) {
   num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
@@ -941,10 +781,9 @@ int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st) {
   const long arows = a.M + a.amap.off;
   const uint32_t ab = (uint32_t)std::min<double>((double)arows * a.lda * 2, 2147483000.0);
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
-  const P8Split sp = p8_split_plan(a, ntile, grid);
 #define PTK_P8_CASE(ACT_, OUT_)                                                                   \
   if (act == ACT_ && out == OUT_) {                                                               \
-    hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb, sp); \
+    hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb); \
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");              \
   }
   PTK_P8_CASE(ACT_NONE, OUT_BF16)

@@ -72,36 +72,17 @@ static bool dkv_reduce_split() {
   return v != 0;
 }
 
-// split-tail scratch (gemm_w4.hip P8Split) of the model run on this thread: every GEMM it builds carries it.
-// PTK_P8_SPLIT=0 leaves it off (A/B).
-static thread_local void* tl_split = nullptr;
-static bool split_enabled() {
-  static const int v = [] { const char* e = getenv("PTK_P8_SPLIT"); return e && e[0] == '0' ? 0 : 1; }();
-  return v != 0;
-}
-struct SplitScope {
-  void* prev;
-  SplitScope(void* ws, hipStream_t st) : prev(tl_split) {
-    tl_split = nullptr;
-    if (ws && split_enabled() && hipMemsetAsync(ws, 0, PTK_GEMM_SPLIT_COUNTER_BYTES, st) == hipSuccess)
-      tl_split = ws;
-  }
-  ~SplitScope() { tl_split = prev; }
-};
-
 GemmArgs gemm(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K) {
   GemmArgs g;
   g.A = (const bf16_t*)A; g.B = (const bf16_t*)B; g.C = C;
   g.lda = lda; g.ldb = ldb; g.ldc = ldc;
   g.M = M; g.N = N; g.K = K;
-  if (tl_split) split_scratch_attach(g, tl_split);
   return g;
 }
 
 // ------------------------------------------------------------------ SigLIP
 struct SiglipWs {
   bf16_t *patches, *h, *a, *qkv, *o, *mlp;
-  void* split;   // split-tail GEMM scratch
 };
 
 SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
@@ -114,7 +95,6 @@ SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
   w.qkv = bp.take<bf16_t>(M * 3 * D);
   w.o = bp.take<bf16_t>(M * D);
   w.mlp = bp.take<bf16_t>(M * I);
-  w.split = bp.take<char>(split_scratch_bytes());
   return w;
 }
 
@@ -141,7 +121,6 @@ struct GemmaWs {
   float* wpart = nullptr;
   float* skpart = nullptr;     // split-K partials (gemm_split)
   long sk_floats = 0;
-  void* split = nullptr;       // split-tail GEMM scratch
 };
 
 GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp, bool train = false) {
@@ -232,7 +211,6 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
   w.sk_floats = std::max(std::max(2 * M * H, 2 * 2 * I * H), 4 * std::max(Dqkv, H) * H);
   if (train) w.sk_floats = std::max(w.sk_floats, V * H);   // the tied embedding's fp32 dW before its accumulate
   w.skpart = bp.take<float>(w.sk_floats);
-  w.split = bp.take<char>(split_scratch_bytes());
   return w;
 }
 
@@ -313,7 +291,6 @@ int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int
   if (Kp % 64 || hd % 64) return set_error("siglip_fwd: patch dim %d and head dim %d must be multiples of 64", Kp, hd);
   Bump bp(ws);
   SiglipWs w = siglip_layout(bp, c, B);
-  SplitScope split_scope(w.split, st);
 
   // K1 patch embed: im2col + GEMM; bf16(conv + bias) + pos -> bf16 residual stream (modeling_siglip.py:175-186)
   CK(launch_im2col((const bf16_t*)pixels, w.patches, B, c->channels, c->image_size, c->image_size, P, st));
@@ -402,7 +379,6 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
   const float eps = c->eps, scale = 1.0f / sqrtf(c->query_pre_attn_scalar);
   Bump bp(ws);
   GemmaWs w = gemma_layout(bp, c, B, T, Sp, train);
-  SplitScope split_scope(w.split, st);
   AttnShape ash{B, Sp, Hq, Hkv, D};
   const RowMap ident{0, 0, 0, 0};
   const int Rp = (R + 63) / 64 * 64;

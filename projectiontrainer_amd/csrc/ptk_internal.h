@@ -42,12 +42,6 @@ struct GemmArgs {
   long ld_aux_in = 0;
   RowMap amap{0, 0, 0, 0};                       // A row remap (gather)
   RowMap cmap{0, 0, 0, 0};                       // C row remap (scatter / skip)
-  // optional split-tail scratch of the persistent 8-wave kernel (gemm_w4.hip P8Split): fp32 partial slabs and
-  // arrival counters (zero before the first use; every launch leaves them zero)
-  float* split_ws = nullptr;
-  long split_ws_floats = 0;
-  uint32_t* split_cnt = nullptr;
-  int split_cnt_n = 0;
 };
 
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
@@ -60,11 +54,6 @@ bool w4_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid);
 // fraction of the persistent grid's tile rounds that hold work: ntile / (ceil(ntile / CUs) * CUs)
 double w4_round_fill(long M, long N);
-// split-tail scratch of the persistent 8-wave kernel: bytes (counters first, then the partial slabs) and
-// attaching it to a GEMM; p8_split_ways = the K-chunks its plan gives a GEMM's last-round tiles (0: no split)
-size_t split_scratch_bytes();
-void split_scratch_attach(GemmArgs& a, void* ws);
-int p8_split_ways(const GemmArgs& a);
 int device_cus();   // compute units of the current device (cached)
 // persistent 8-wave variant (gemm_w4.hip): the w4 tiles and ring with two waves per SIMD
 bool p8_supported(const GemmArgs& a, int act, int out);

@@ -23,11 +23,8 @@ def _bits(t):
 def gemm(A, B, *, C=None, out_dtype=torch.bfloat16, act=L.ACT_NONE, alpha=1.0, bias=None, rowadd=None,
          resid=None, aux=None, aux2=None, aux_in=None, aux_in2=None, M=None, N=None, K=None,
          lda=None, ldb=None, ldc=None, batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0),
-         amap=(0, 0, 0, 0), cmap=(0, 0, 0, 0), out_mode=None, split=False):
-    """C = epi(alpha * A . B^T) with A [M,K], B [N,K] bf16 (K-contiguous).
-
-    split: give the GEMM this device's split-tail scratch (ptk_gemm_desc.split_ws), so a persistent-kernel
-    shape whose last round of tiles fills the CUs badly splits that round over K."""
+         amap=(0, 0, 0, 0), cmap=(0, 0, 0, 0), out_mode=None):
+    """C = epi(alpha * A . B^T) with A [M,K], B [N,K] bf16 (K-contiguous)."""
     _require_cuda(A, B)
     M = A.shape[-2] if M is None else M
     K = A.shape[-1] if K is None else K
@@ -59,24 +56,8 @@ def gemm(A, B, *, C=None, out_dtype=torch.bfloat16, act=L.ACT_NONE, alpha=1.0, b
     d.aux_in2 = ptr(aux_in2)
     d.amap = L.RowMap(*amap)
     d.cmap = L.RowMap(*cmap)
-    if split:
-        ws = split_workspace(A.device)
-        d.split_ws, d.split_ws_bytes = ptr(ws), ws.numel()
     check(L.lib().ptk_gemm(d, L.stream_ptr(A.device)), "ptk_gemm")
     return C
-
-
-_split_ws = {}
-
-
-def split_workspace(device):
-    """The per-device split-tail GEMM scratch (counters zeroed once; every GEMM leaves them zero)."""
-    key = torch.device(device)
-    ws = _split_ws.get(key)
-    if ws is None:
-        ws = torch.zeros(int(L.lib().ptk_gemm_split_workspace_bytes()), dtype=torch.uint8, device=key)
-        _split_ws[key] = ws
-    return ws
 
 
 def layernorm(x, w, b, eps):

@@ -505,67 +505,6 @@ def test_gemm_p8_matches_w4(gpu, M, N, K):
     torch.testing.assert_close(outs[1]["f32"], ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
 
 
-@pytest.mark.parametrize("M,N,K,ways", [(4352, 4096, 1024, 4), (4500, 4000, 640, 4), (22528, 1024, 1152, 2),
-                                        (22528, 1152, 6912, 4), (1000, 1024, 1152, 0)])
-def test_gemm_p8_split_tail(gpu, M, N, K, ways):
-    """Split tail of the persistent 8-wave kernel (gemm_w4.hip P8Split): the last, badly filled round of
-    256x256 tiles split over K into fp32 partials that the last-arriving wave sums in chunk order.  Every
-    epilogue against the unsplit kernel (the same math on a differently ordered fp32 sum: bf16-ulp level),
-    plain fp32 against torch fp32, two runs bit-identical (the fixed summation order), the arrival counters
-    back at zero after every GEMM, the plan's K-chunk count as computed for 256 CUs."""
-    Kn, L = _k()
-    A, B = rnd(M, K, dev=gpu, seed=21), rnd(N, K, dev=gpu, seed=22, scale=0.05)
-    gin, uin = rnd(M, N, dev=gpu, seed=23), rnd(M, N, dev=gpu, seed=24)
-    bias = rnd(N, dev=gpu, dtype=torch.float32, seed=25)
-    res = rnd(M, N, dev=gpu, dtype=torch.float32, seed=26)
-    ws = Kn.split_workspace(gpu)
-    d = L.GemmDesc()
-    d.M, d.N, d.K, d.lda, d.ldb = M, N, K, K, K
-    d.split_ws, d.split_ws_bytes = ws.data_ptr(), ws.numel()
-    if torch.cuda.get_device_properties(gpu).multi_processor_count == 256:
-        assert L.lib().ptk_gemm_split_ways(d) == ways
-
-    def run(split):
-        o = {"f32": Kn.gemm(A, B, out_dtype=torch.float32, split=split), "bf16": Kn.gemm(A, B, split=split)}
-        C = res.clone()
-        Kn.gemm(A, B, C=C, bias=bias, resid=C, split=split)
-        o["resid"] = C
-        o["gelu_tanh"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_TANH, split=split)
-        aux = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
-        o["gelu_erf"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_ERF, aux=aux, split=split)
-        o["aux"] = aux
-        o["erf_bwd"] = Kn.gemm(A, B, act=L.ACT_GELU_ERF_BWD, aux_in=gin, split=split)
-        if N % 32 == 0:
-            g = torch.zeros(M, N // 2, dtype=torch.bfloat16, device=gpu)
-            u = torch.zeros_like(g)
-            o["h"] = Kn.gemm(A, B, act=L.ACT_GEGLU, aux=g, aux2=u, split=split)
-            o["g"], o["u"] = g, u
-        o["dgdu"] = Kn.gemm(A, B, act=L.ACT_GEGLU_BWD, aux_in=gin, aux_in2=uin, split=split)
-        torch.cuda.synchronize()
-        return o
-
-    L.lib().ptk_gemm_force_small_tiles(32)
-    try:
-        base = run(False)
-        s1 = run(True)
-        assert int(ws[:16384].count_nonzero()) == 0
-        s2 = run(True)
-    finally:
-        L.lib().ptk_gemm_force_small_tiles(0)
-    for k in base:
-        assert torch.equal(s1[k], s2[k]), k
-        if ways == 0:
-            assert torch.equal(s1[k], base[k]), k
-        else:
-            torch.testing.assert_close(s1[k].float(), base[k].float(), rtol=1.6e-2, atol=2e-2, msg=k)
-    ref = A.float() @ B.float().T
-    torch.testing.assert_close(s1["f32"], ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
-    if ways:
-        # the split changes the fp32 sum order only: fp32 outputs within a few fp32 ulps of the sum's size
-        err = (s1["f32"] - base["f32"]).abs().max().item()
-        assert err <= 1e-5 * math.sqrt(K) * float(ref.abs().max()), err
-
-
 def test_projector_module_autograd(gpu):
     """MLPProjector as an nn.Module under autograd (the public API, Stage1/projectors.py:22-29): output,
     parameter grads and the INPUT grad vs torch fp32 autograd of the same Sequential(Linear, GELU, Linear);

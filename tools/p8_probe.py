@@ -1,6 +1,5 @@
-"""Persistent 4-wave (mode 8) vs persistent 8-wave (mode 32) vs the 8-wave kernel with its split tail vs the
-automatic dispatch without / with split scratch (mode 0) on the GEMM shapes of the cfg2 / cfg4 steps: HIP-event
-time per launch, TFLOP/s, rounds interleaved (one process)."""
+"""Persistent 4-wave (mode 8) vs persistent 8-wave (mode 32) vs the automatic dispatch (mode 0) on the GEMM
+shapes of the cfg2 / cfg4 steps: HIP-event time per launch, TFLOP/s, rounds interleaved (one process)."""
 import json
 import os
 import sys
@@ -51,19 +50,18 @@ def setup(m, n, k, act, odt):
     return A, B, kw
 
 
-def timed(A, B, kw, act, odt, C, reps, split=False):
+def timed(A, B, kw, act, odt, C, reps):
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
-        K.gemm(A, B, C=C, out_dtype=odt, act=act, split=split, **kw)
+        K.gemm(A, B, C=C, out_dtype=odt, act=act, **kw)
     e1.record()
     torch.cuda.synchronize()
     return e0.elapsed_time(e1) / reps
 
 
 only = set(a for a in sys.argv[1:] if not a.startswith("-"))
-modes = ((8, False), (32, False), (32, True), (0, False), (0, True))
-tags = ("w4", "p8", "p8split", "auto", "autosplit")
+modes = (8, 32, 0)
 for name, m, n, k, act, odt in SHAPES:
     if only and name not in only:
         continue
@@ -73,18 +71,13 @@ for name, m, n, k, act, odt in SHAPES:
     res = {m_: [] for m_ in modes}
     for rnd in range(3):
         for md in modes:
-            L.lib().ptk_gemm_force_small_tiles(md[0])
-            timed(A, B, kw, act, odt, C, 1, md[1])
-            res[md].append(timed(A, B, kw, act, odt, C, reps, md[1]))
+            L.lib().ptk_gemm_force_small_tiles(md)
+            timed(A, B, kw, act, odt, C, 1)
+            res[md].append(timed(A, B, kw, act, odt, C, reps))
     L.lib().ptk_gemm_force_small_tiles(0)
     fl = 2.0 * m * n * k
     out = {"name": name, "M": m, "N": n, "K": k}
-    d = L.GemmDesc()
-    d.M, d.N, d.K, d.lda, d.ldb = m, n, k, k, k
-    ws = K.split_workspace(dev)
-    d.split_ws, d.split_ws_bytes = ws.data_ptr(), ws.numel()
-    out["ways"] = L.lib().ptk_gemm_split_ways(d)
-    for md, tag in zip(modes, tags):
+    for md, tag in zip(modes, ("w4", "p8", "auto")):
         ms = min(res[md])
         out[tag + "_us"] = round(ms * 1e3, 1)
         out[tag + "_TF"] = round(fl / ms / 1e9, 1)
