@@ -121,8 +121,8 @@ int ptk_gemm_timer_enable(int on);   /* 0 off, 1 every class, (1 << 8) | class m
 int ptk_gemm_force_small_tiles(int mode);
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
 /* Dispatch census (tests): counts[path * 8 + act] = GEMM launches since the last reset per kernel family
- * (0 128x128, 1 256x256 8-wave, 2 staggered 256x256 8-wave, 3 persistent 4-wave, 4 ping-pong,
- * 5 stream-K, 6 persistent 8-wave, 7 token-major weight grad) and epilogue class (PTK_ACT_*); counts may be
+ * (0 128x128, 1 256x256 8-wave, 2 staggered 256x256 8-wave, 3 persistent 4-wave, 4 and 5 retired (the
+ * ping-pong and stream-K kernels, removed), 6 persistent 8-wave, 7 token-major weight grad) and epilogue class (PTK_ACT_*); counts may be
  * NULL; reset != 0 zeroes them afterwards.  Host-side counters, no GPU work. */
 int ptk_gemm_path_counts(int64_t* counts, int reset);
 

@@ -352,6 +352,25 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
 constexpr float FA_DEFER = 8.f;
 constexpr int FA_MAXT = 128;   // key tiles (of 32) the mask table holds: nkeys <= 4096
 
+// diagnostic build (make fastamps): s_memtime stamps of the 32-row d-256 kernels' phases per workgroup, kept in
+// registers and written by lane 0 of wave 0 at the end (no extra memory op inside the counted-vmcnt pipeline)
+#ifdef PTK_FA_STAMPS
+__device__ unsigned long long g_fa_stamps[1 << 14][8];
+#define FA_STAMP(i) st_[i] = __builtin_amdgcn_s_memtime()
+#define FA_STAMPS_DECL unsigned long long st_[8] = {}; st_[5] = __builtin_amdgcn_s_memrealtime(); FA_STAMP(0)
+#define FA_STAMPS_WRITE(ntiles)                                                                    \
+  if (threadIdx.x == 0) {                                                                          \
+    FA_STAMP(4);                                                                                   \
+    st_[6] = __builtin_amdgcn_s_memrealtime();                                                     \
+    st_[7] = (unsigned long long)(ntiles);                                                         \
+    for (int i_ = 0; i_ < 8; ++i_) g_fa_stamps[blockIdx.x & ((1 << 14) - 1)][i_] = st_[i_];        \
+  }
+#else
+#define FA_STAMP(i) (void)0
+#define FA_STAMPS_DECL (void)0
+#define FA_STAMPS_WRITE(ntiles) (void)0
+#endif
+
 #define FA_DMA(VOFF, SOFF, RSRC, LDS)                                                                      \
   asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen lds"                   \
                :: "v"(VOFF), "s"(LDS), "s"(RSRC), "s"(SOFF) : "memory")
@@ -663,6 +682,348 @@ __global__ void __launch_bounds__(512, 1) attn_fwd256_kernel(FlashArgs a) {
   }
   if (a.lse && g == 0)
     a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_run)) * 0.6931471805599453f;
+}
+
+// ---------------------------------------------------------------- forward, head_dim 256, 32 rows per wave
+// One workgroup = 4 waves (one per SIMD, the whole 512-entry register file each) = 128 query rows of one z;
+// each wave owns 32 rows and runs v_mfma_f32_32x32x16_bf16 (32 cycles, 32x32 outputs), so every K / V^T
+// fragment read from LDS feeds twice the FLOPs of the 16-row form (whose 8 waves read 256 KiB of LDS per
+// 32-key tile, the LDS array's whole 256 B/clk at the MFMA rate).  Per 32-key tile and wave:
+//   S^T[32 keys x 32 q] = K Q^T        16 MFMAs, one accumulator chain; A = K rows (ds_read_b128), B = Q
+//                                      fragments held in registers for the whole block
+//   online softmax                     lane = query column c32, 16 keys (8i + 4h + j) per lane: 15 max + one
+//                                      permlane32 swap; the running sum stays per lane half (summed once at
+//                                      the end), the running max moves only by more than FA_DEFER
+//   O^T[256 d x 32 q] += V^T P^T       16 MFMAs (8 d blocks x 2 key steps); B = P straight from the S^T
+//                                      accumulators (registers 8kk..8kk+7 = keys 16kk + 8(j>>2) + 4h + (j&3)),
+//                                      A = V^T by ds_read_b64_tr_b16 in that same key order
+// Software pipeline inside the wave: iteration t issues QK^T of tile t+1 beside the softmax of tile t, then
+// P.V of tile t, so the MFMA pipe has independent work while the softmax VALU runs.  K / V tiles by LDS-DMA
+// (8 x 1 KiB pieces per wave per tile) into 4-deep rings, one counted vmcnt + barrier per tile.
+// LDS images (32 rows x 512 B, chunk c of row r at chunk c ^ swz(r)): K swz = r & 15 (the b128 row reads of
+// 16 distinct keys per lane group hit 16 distinct bank quads), V swz = 4 (r & 3) (each 32-lane half of a
+// transposed read takes 4 rows r..r+3 x 64 B: 4 distinct bank quads of 16).
+__global__ void __launch_bounds__(256, 1) attn_fwd256w_kernel(FlashArgs a) {
+  constexpr int D = 256, KT = 32, NB = 4;
+  constexpr int TILE = KT * D * 2;   // 16 KiB
+  __shared__ __attribute__((aligned(16))) char smem[2 * NB * TILE + FA_MAXT * 4];
+  char* const kring = smem;
+  char* const vring = smem + NB * TILE;
+  uint32_t* const kmask_s = reinterpret_cast<uint32_t*>(smem + 2 * NB * TILE);
+  FA_STAMPS_DECL;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, c32 = lane & 31;
+  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
+  const int z = blockIdx.x % nz, z0 = z / a.zin, z1 = z - z0 * a.zin;
+  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;   // heaviest (latest) row blocks first
+  const bf16_t* Q = a.Q + z0 * a.sQ0 + z1 * a.sQ1;
+  const bf16_t* K = a.K + z0 * a.sK0 + z1 * a.sK1;
+  const bf16_t* V = a.V + z0 * a.sK0 + z1 * a.sK1;
+  const long b = z / a.zdiv;
+  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
+
+  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
+  int k_hi = a.nkeys, k_lo = 0;
+  if (a.causal) {
+    k_hi = min(k_hi, pos_hi + 1);
+    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
+  }
+  const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
+
+  // ---- per-tile key masks (valid and < nkeys), written before any DMA is in flight
+  for (int tt = t_lo + wave; tt < t_hi; tt += 4) {
+    const int key = tt * KT + c32;
+    const bool ok = key < a.nkeys && (!kvl || kvl[min(key, a.nkeys - 1)] != 0);
+    const uint64_t m = __ballot(ok);
+    if (lane == 0) kmask_s[tt] = (uint32_t)m;
+  }
+
+  // ---- Q fragments: B operand of S^T = K Q^T for k-step ks, lane holds Q[row c32][16 ks + 8 h .. +7]
+  const int wrow0 = r0 + wave * 32;
+  const int qrow = wrow0 + c32;
+  const int qrow_c = min(qrow, a.rows - 1);
+  const int qpos = qrow_c / a.qdiv;
+  bf16x8_t qf[16];
+  {
+    const bf16_t* qp = Q + map_row(a.qmap, qrow_c) * a.ldq + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + 16 * ks);
+  }
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) fa_pin(qf[ks]);
+  __syncthreads();   // key masks published (no LDS-DMA in flight yet)
+  FA_STAMP(1);
+
+  const int causal = a.causal != 0, nowin = a.window <= 0;
+  const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
+  const int wpos_hi = min(wrow0 + 31, a.rows - 1) / a.qdiv;
+  const bool idle = wrow0 >= a.rows;   // rows past the end: stage and keep the barriers only
+
+  // ---- DMA: wave w stages rows 8w..8w+7 of each tile (4 pieces of 2 rows x 512 B per tensor); lane i of a
+  // piece writes LDS row 8w + 2j + (i >> 5), chunk i & 31, fetched from logical chunk (i & 31) ^ swz(row)
+  const fa_u32x4_t rsk = fa_rsrc(K, (uint32_t)((long)a.nkeys * a.ldk * 2));
+  const fa_u32x4_t rsv = fa_rsrc(V, (uint32_t)((long)a.nkeys * a.ldk * 2));
+  uint32_t dk[4], dv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wave * 8 + 2 * j + h;
+    dk[j] = (uint32_t)row * (uint32_t)a.ldk * 2u + 16u * (c32 ^ (row & 15));
+    dv[j] = (uint32_t)row * (uint32_t)a.ldk * 2u + 16u * (c32 ^ (4 * (row & 3)));
+  }
+  const uint32_t lds_k = __builtin_amdgcn_readfirstlane(fa_lds_addr(kring) + wave * 4096);
+  const uint32_t lds_v = __builtin_amdgcn_readfirstlane(fa_lds_addr(vring) + wave * 4096);
+  const uint32_t tile_bytes = __builtin_amdgcn_readfirstlane((uint32_t)KT * (uint32_t)a.ldk * 2u);
+  auto stage = [&](int bb, int t) __attribute__((always_inline)) {
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)t * tile_bytes);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) FA_DMA(dk[j], so, rsk, lds_k + bb * TILE + j * 1024);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) FA_DMA(dv[j], so, rsv, lds_v + bb * TILE + j * 1024);
+  };
+
+  // ---- LDS read addresses (lane part; the ring slot and the rest are immediates).
+  // K: row c32, logical chunk 2ks + h -> (2ks + h) ^ (c32 & 15): 8 bases for ks & 7, ks >> 3 = +256 B.
+  // V^T (tr read, key step kk, half r, d block db): lane 4q+p of group G = lane >> 4 reads row
+  // 16kk + 8r + 4h + q, logical chunk 4db + 2(G & 1) + (p >> 1), byte 8 (p & 1); swz = 4q, so the chunk is
+  // 4 ((db & 3) ^ q) + 2(G & 1) + (p >> 1) + 16 (db >> 2): 4 bases for db & 3, kk / r / db >> 2 immediates.
+  uint32_t kaddr[8], vaddr[4];   // LDS byte addresses
+  {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+      kaddr[i] = fa_lds_addr(kring) + c32 * (D * 2) + (((2 * i + h) ^ (c32 & 15)) * 16);
+    const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+    const int vrow = 4 * h + q;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+      vaddr[i] = fa_lds_addr(vring) + vrow * (D * 2) + (4 * (i ^ q) + 2 * (G & 1) + (p >> 1)) * 16 + 8 * (p & 1);
+  }
+
+  typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+  f32x16_t o[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) o[i] = (f32x16_t){};
+  float m_run = -INFINITY, l_run = 0.f;   // l_run: this lane half's partial row sum
+  const float sl2 = a.scale * 1.4426950408889634f;   // scores in log2 units
+  const float defer = FA_DEFER / sl2;                 // the deferral in raw score units
+
+  // ---- MFMA and LDS helpers.  The P.V MFMAs are inline asm with O tied to VGPRs (with the builtin, hipcc
+  // keeps O in AGPRs and moves it through VGPRs around the rescale, 256 moves per pair of tiles); QK^T uses
+  // the builtin, so hipcc sees its operands and results.  Volatile asm keeps its source order, and no LDS
+  // read moves across it, so the loops below place every read, MFMA and softmax piece themselves (one slot
+  // per MFMA, pinned by sched_barrier): reads run 3 (K) or 2 (V) MFMAs ahead of their use.  Hazards hipcc
+  // does not see through the asm: each asm MFMA opens with s_nop 2, the wait states of a VALU write (P, the
+  // rescaled O, or any copy the compiler places) right before it; O is read by VALU only in the next
+  // iteration's rescale, after the barrier and 16 MFMAs, and in the epilogue, after its own s_nops
+  // (tests/test_asm_hazards.py checks the emitted code for both).
+  auto kload = [&](uint32_t so, int ks) __attribute__((always_inline)) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) bf16x8_t*>(
+        (uintptr_t)(kaddr[ks & 7] + so + (ks >> 3) * 256));
+  };
+  // V^T fragment of key step kk, d block db: two transposed reads (keys 16kk + 8r + 4h + 0..3)
+  auto vload = [&](uint32_t so, int kk, int db) __attribute__((always_inline)) {
+    bf16x8_t vf;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t addr = vaddr[db & 3] + so + (16 * kk + 8 * r) * (D * 2) + (db >> 2) * 256;
+      const s16x4_t x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(uintptr_t)addr);
+      vf[4 * r + 0] = x[0]; vf[4 * r + 1] = x[1]; vf[4 * r + 2] = x[2]; vf[4 * r + 3] = x[3];
+    }
+    return vf;
+  };
+  auto vmax3 = [](float x, float y, float z) __attribute__((always_inline)) {
+    float r;   // (plain fmaxf adds a canonicalising v_max per MFMA-produced operand)
+    asm("v_max3_f32 %0, %1, %2, %3" : "=v"(r) : "v"(x), "v"(y), "v"(z));
+    return r;
+  };
+
+  // the mask of tile t on its scores (tiles every key of which every row of the wave sees skip it: all keys
+  // valid, below the causal diagonal, inside the window).  Run at the top of the iteration, in a block of its
+  // own, so the softmax pieces below have no branch.
+  auto mask = [&](int t, f32x16_t& s) __attribute__((always_inline)) {
+    const uint32_t km = kmask_s[t];
+    const bool interior = km == 0xffffffffu && (!causal || t * KT + KT - 1 <= wpos_lo) &&
+                          (nowin || t * KT > wpos_hi - a.window);
+    if (interior) return;
+    // this row's visible keys of the tile as a 32-bit mask: valid, kl <= qpos - t KT (causal),
+    // kl > qpos - W - t KT (window); lane half h holds keys 8i + 4h + j
+    uint32_t vis = km;
+    if (causal) {
+      const int d = qpos - t * KT;
+      vis &= d >= 31 ? 0xffffffffu : (d < 0 ? 0u : (2u << d) - 1u);
+      if (!nowin) {
+        const int e = d - a.window;
+        vis &= e < 0 ? 0xffffffffu : (e >= 31 ? 0u : ~((2u << e) - 1u));
+      }
+    }
+    vis >>= 4 * h;
+#pragma unroll
+    for (int r = 0; r < 16; ++r) {
+      const int kl = (r & 3) + 8 * (r >> 2);
+      s[r] = ((vis >> kl) & 1u) ? s[r] : -INFINITY;
+    }
+  };
+
+  // Phase A of an iteration: QK^T of the next tile (16 MFMAs, if QK) beside the online softmax of the
+  // current tile's masked scores (if SM) in 16 slots: 0-3 the row max (v_max3), 4 the half-wave max swap and
+  // the running max / rescale factor, 5-12 two exponentials each (P to bf16, fp32 row sum), 13 the running
+  // sum.  The running max moves only by more than FA_DEFER; the row sum stays per lane half.
+  float alpha = 1.f;
+  auto phase_a = [&](auto QK, auto SM, uint32_t so, f32x16_t& s_next, const f32x16_t& s, bf16x8_t (&pf)[2])
+      __attribute__((always_inline)) {
+    constexpr bool qk = decltype(QK)::value, sm = decltype(SM)::value;
+    bf16x8_t kf[4];
+    if (qk) {
+      kf[0] = kload(so, 0);
+      kf[1] = kload(so, 1);
+      kf[2] = kload(so, 2);
+    }
+    float mt = 0.f, m_new = 0.f, mc = 0.f, rs = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      if (qk) {
+        if (ks + 3 < 16) kf[(ks + 3) & 3] = kload(so, ks + 3);
+        s_next = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks & 3], qf[ks], ks == 0 ? (f32x16_t){} : s_next, 0, 0, 0);
+      }
+      if (sm) {
+        if (ks == 0) mt = vmax3(vmax3(s[0], s[1], s[2]), s[3], s[4]);
+        else if (ks < 3) mt = vmax3(vmax3(mt, s[4 * ks + 1], s[4 * ks + 2]), s[4 * ks + 3], s[4 * ks + 4]);
+        else if (ks == 3) mt = vmax3(mt, s[13], vmax3(s[14], s[15], s[15]));
+        else if (ks == 4) {
+          // the half-wave swap in asm: hipcc does not see that the v_max3 asm above is the VALU write the
+          // permlane reads, so the 2 wait states of that hazard are written out here
+          float mt2 = mt;
+          asm volatile("s_nop 1\n\tv_permlane32_swap_b32 %0, %1" : "+v"(mt), "+v"(mt2));
+          mt = fmaxf(mt, mt2);
+          const bool up = mt > m_run + defer;   // m_run = -inf: any finite tile max moves it
+          m_new = up ? mt : m_run;
+          alpha = (up && m_run != -INFINITY) ? __builtin_amdgcn_exp2f((m_run - m_new) * sl2) : 1.f;
+          mc = (m_new == -INFINITY) ? 0.f : m_new * sl2;
+        } else if (ks <= 12) {
+          const int r = 2 * (ks - 5);
+          const float p0 = __builtin_amdgcn_exp2f(fmaf(s[r], sl2, -mc));   // exp2(-inf) = 0 for masked keys
+          const float p1 = __builtin_amdgcn_exp2f(fmaf(s[r + 1], sl2, -mc));
+          rs += p0 + p1;
+          pf[r >> 3][r & 7] = (short)f2bf(p0);
+          pf[r >> 3][(r & 7) + 1] = (short)f2bf(p1);
+          // pin the pair here: otherwise hipcc sinks the exponentials past the rescale branch to their use
+          asm volatile("" : "+v"(pf[r >> 3]));
+        } else if (ks == 13) {
+          l_run = l_run * alpha + rs;
+          m_run = m_new;
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  auto rescale = [&]() __attribute__((always_inline)) {
+    if (__any(alpha != 1.f)) {
+#pragma unroll
+      for (int i = 0; i < 8; ++i) o[i] *= alpha;
+    }
+  };
+  // Phase B: O^T += V^T P^T (16 MFMAs, key step outer so one accumulator's two MFMAs are 8 apart), V^T reads
+  // two MFMAs ahead; the next tile's 8 LDS-DMA pieces (if ST) go out one per two MFMAs.
+  auto phase_b = [&](auto ST, uint32_t so, const bf16x8_t (&pf)[2], int bb_st, int t_st)
+      __attribute__((always_inline)) {
+    constexpr bool st = decltype(ST)::value;
+    bf16x8_t vf[3];
+    vf[0] = vload(so, 0, 0);
+    vf[1] = vload(so, 0, 1);
+    uint32_t sso = 0;
+    if (st) sso = __builtin_amdgcn_readfirstlane((uint32_t)t_st * tile_bytes);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kk = i >> 3, db = i & 7;
+      if (i + 2 < 16) vf[(i + 2) % 3] = vload(so, (i + 2) >> 3, (i + 2) & 7);
+      asm volatile("s_nop 2\n\tv_mfma_f32_32x32x16_bf16 %0, %1, %2, %0" : "+v"(o[db]) : "v"(vf[i % 3]), "v"(pf[kk]));
+      if (st && (i & 1) == 0) {
+        const int j = i >> 1;   // pieces K0..K3, V0..V3
+        if (j < 4) FA_DMA(dk[j], sso, rsk, lds_k + bb_st * TILE + j * 1024);
+        else FA_DMA(dv[j - 4], sso, rsv, lds_v + bb_st * TILE + (j - 4) * 1024);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  // Tile t lives in ring slot (t - t_lo) % NB.  At iteration t the wave waits for tile t+1 (tile t+2 may
+  // stay in flight), the barrier publishes it, and tile t+3 is staged into the slot of tile t-1, whose last
+  // readers (QK^T of t-1 at iteration t-2, P.V of t-1 at iteration t-1) every wave has passed.  Past the last
+  // tile the stage re-loads tile t_hi - 1 into that free slot (never read), so every iteration issues the
+  // same 8 pieces and waits with the same count.  Fully masked tiles are computed like the others
+  // (exp2(-inf) = 0).  The loop body is unrolled by two so the two score accumulators swap roles without a
+  // copy.
+  if (t_lo < t_hi) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) stage(i, min(t_lo + i, t_hi - 1));
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  f32x16_t sa, sb = (f32x16_t){};
+  bf16x8_t pf[2];
+  phase_a(T_{}, F_{}, 0, sa, sb, pf);   // QK^T of tile t_lo (t_lo == t_hi: slot 0 holds nothing, unused)
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // its MFMA results -> the first VALU reads
+  FA_STAMP(2);
+  auto slot = [&](int t) { return (uint32_t)((t - t_lo) & (NB - 1)) * (uint32_t)TILE; };
+  auto iter = [&](int t, f32x16_t& s_cur, f32x16_t& s_next) __attribute__((always_inline)) {
+    mask(t, s_cur);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    phase_a(T_{}, T_{}, slot(t + 1), s_next, s_cur, pf);
+    rescale();
+    phase_b(T_{}, slot(t), pf, (t - t_lo + 3) & (NB - 1), min(t + 3, t_hi - 1));
+  };
+  int t = t_lo;
+  for (; t + 2 < t_hi; t += 2) {
+    iter(t, sa, sb);
+    iter(t + 1, sb, sa);
+  }
+  if (t + 1 < t_hi) {
+    iter(t, sa, sb);
+    ++t;
+    sa = sb;
+  }
+  if (t < t_hi) {   // the last tile: softmax and P.V only
+    mask(t, sa);
+    phase_a(F_{}, T_{}, 0, sb, sa, pf);
+    rescale();
+    phase_b(F_{}, slot(t), pf, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup exits
+  FA_STAMP(3);
+
+  // ---- epilogue: O[q][d] = O^T[d][q] / l.  Lane half h holds d = 32db + 8i + 4h + (0..3) for query c32;
+  // one permlane32 swap per register pair (i = 2m, 2m + 1) gives the lower half d 32db + 16m + 0..7 and the
+  // upper half 32db + 16m + 8..15, stored 16 B per lane.
+  const float l_tot = l_run + xor32_get(l_run);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // the last P.V MFMAs -> VALU reads of O
+  if (qrow >= a.rows) return;
+  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+  bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow) * a.ldo + 8 * h;
+#pragma unroll
+  for (int db = 0; db < 8; ++db) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      uint32_t w[4];   // packed bf16 pairs: registers (i = 2m: 0-1, i = 2m + 1: 2-3)
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = 8 * m + 2 * k;
+        w[k] = (uint32_t)f2bf(o[db][r] * inv) | ((uint32_t)f2bf(o[db][r + 1] * inv) << 16);
+      }
+      // lower half keeps registers of i = 2m and takes the upper half's i = 2m; the upper half keeps i = 2m+1
+      const auto s0 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+      *reinterpret_cast<uint4*>(op + 32 * db + 16 * m) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+  }
+  if (a.lse && h == 0)
+    a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_tot)) * 0.6931471805599453f;
+  FA_STAMPS_WRITE(t_hi - t_lo);
 }
 
 // ============================================================================ backward
@@ -1124,6 +1485,292 @@ __global__ void __launch_bounds__(512, 2) attn_fwd64_kernel(FlashArgs a) {
   }
   if (a.lse && g == 0)
     a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_run)) * 0.6931471805599453f;
+}
+
+// ---------------------------------------------------------------- dQ, head_dim 256, 32 rows per wave
+// attn_fwd256w_kernel's structure applied to the dQ pass: 4 waves (one per SIMD) x 32 query rows, 32x32x16
+// MFMAs, K / V tiles of 32 keys by LDS-DMA into 4-deep rings, one counted vmcnt + barrier per tile.  Per tile
+// and wave:
+//   S^T = K Q^T, dP^T = V dO^T   32 MFMAs, A = K / V rows (ds_read_b128), B = the wave's Q / dO fragments,
+//                                held in registers for the whole block
+//   P = exp2(S scale log2e - LSE log2e) (bf16), dS = P (dP - delta) (bf16)   lane = query column: the row's
+//                                LSE and delta are per lane, no cross-lane work at all
+//   dQ^T[256 d x 32 q] += K^T dS^T   16 MFMAs, A = K^T by ds_read_b64_tr_b16 from the same K tile, B = dS^T
+//                                straight from the accumulator layout (keys 16kk + 8(j>>2) + 4h + (j&3)),
+//                                dQ^T accumulated in AGPRs
+// Software pipeline: iteration t issues S / dP of tile t+1 (phase A) beside dS of tile t, then dQ of tile t
+// (phase B) with the next DMA pieces.  The K image serves row reads and transposed reads: chunk c of row r at
+// c ^ (4 (r & 3) | ((r >> 2) & 3)) (16 distinct chunk quads for the b128 lane groups, 4 distinct bank quads
+// for the 4 rows of a transposed read); the V image uses it too (row reads only).  It also computes delta = rowsum(dO O) (attn_delta_kernel's job)
+// from the dO fragments it holds, and runs before the dK/dV kernel, which reads it.  Same arithmetic as
+// attn_bwd_dq256_kernel (P rounded to bf16 before the product, as the dK/dV kernel does).
+PTK_DEV int swz_dual(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
+
+__global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a) {
+  constexpr int D = 256, KT = 32, NB = 4;
+  constexpr int TILE = KT * D * 2;
+  typedef __attribute__((ext_vector_type(16))) float f32x16_t;
+  // ring slot b: the K tile at 2b TILE, the V tile at (2b + 1) TILE, so one base register addresses both
+  __shared__ __attribute__((aligned(16))) char smem[2 * NB * TILE + FA_MAXT * 4];
+  char* const kring = smem;
+  uint32_t* const kmask_s = reinterpret_cast<uint32_t*>(smem + 2 * NB * TILE);
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int h = lane >> 5, c32 = lane & 31;
+  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
+  const long z = blockIdx.x % nz;
+  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;   // heaviest (latest) row blocks first
+  const bf16_t* K = a.K + z * (long)a.nkeys * D;
+  const bf16_t* V = a.V + z * (long)a.nkeys * D;
+  const long b = z / a.zdiv;
+  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
+  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
+  int k_hi = a.nkeys, k_lo = 0;
+  if (a.causal) {
+    k_hi = min(k_hi, pos_hi + 1);
+    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
+  }
+  const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
+
+  for (int tt = t_lo + wave; tt < t_hi; tt += 4) {
+    const int key = tt * KT + c32;
+    const bool ok = key < a.nkeys && (!kvl || kvl[min(key, a.nkeys - 1)] != 0);
+    const uint64_t m = __ballot(ok);
+    if (lane == 0) kmask_s[tt] = (uint32_t)m;
+  }
+
+  // ---- Q, dO fragments (B operands, k-step ks: lane holds row c32, d 16 ks + 8 h .. +7), LSE, delta
+  const int wrow0 = r0 + wave * 32;
+  const int qrow = wrow0 + c32;
+  const int qrow_c = min(qrow, a.rows - 1);
+  const int qpos = qrow_c / a.qdiv;
+  bf16x8_t qf[16], df[16];
+  const long qoff = (z * a.rows + qrow_c) * (long)D + 8 * h;
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    qf[ks] = *reinterpret_cast<const bf16x8_t*>(a.Q + qoff + 16 * ks);
+    df[ks] = *reinterpret_cast<const bf16x8_t*>(a.dO + qoff + 16 * ks);
+  }
+  const float L2E = 1.4426950408889634f;
+  const float lse2 = a.lse[z * a.rows + qrow_c] * L2E;
+  float dlt;
+  {
+    const long z0 = z / a.zin, z1 = z - z0 * a.zin;
+    const bf16_t* orow = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow_c) * a.ldo + 8 * h;
+    float acc0 = 0.f;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      const bf16x8_t of = *reinterpret_cast<const bf16x8_t*>(orow + 16 * ks);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc0 += bf2f((bf16_t)of[e]) * bf2f((bf16_t)df[ks][e]);
+    }
+    dlt = xor32_sum(acc0);
+    if (h == 0 && qrow < a.rows) a.delta[z * a.rows + qrow] = dlt;
+  }
+#pragma unroll
+  for (int ks = 0; ks < 16; ++ks) {
+    fa_pin(qf[ks]);
+    fa_pin(df[ks]);
+  }
+  __syncthreads();   // key masks published (no LDS-DMA in flight yet)
+  const float sl2 = a.scale * L2E;
+  const int causal = a.causal != 0, nowin = a.window <= 0;
+  const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
+  const int wpos_hi = min(wrow0 + 31, a.rows - 1) / a.qdiv;
+
+  // ---- DMA: wave w stages rows 8w..8w+7 of each tile (4 pieces of 2 rows x 512 B per tensor)
+  const fa_u32x4_t rsk = fa_rsrc(K, (uint32_t)((long)a.nkeys * D * 2));
+  const fa_u32x4_t rsv = fa_rsrc(V, (uint32_t)((long)a.nkeys * D * 2));
+  uint32_t dk[4], dv[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int row = wave * 8 + 2 * j + h;
+    dk[j] = (uint32_t)row * (D * 2) + 16u * (c32 ^ swz_dual(row));
+    dv[j] = dk[j];
+  }
+  const uint32_t lds_k = __builtin_amdgcn_readfirstlane(fa_lds_addr(kring) + wave * 4096);
+  const uint32_t lds_v = lds_k + TILE;
+  constexpr uint32_t tile_bytes = KT * D * 2;
+  auto stage = [&](int bb, int t) __attribute__((always_inline)) {
+    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)t * tile_bytes);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) FA_DMA(dk[j], so, rsk, lds_k + bb * 2 * TILE + j * 1024);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) FA_DMA(dv[j], so, rsv, lds_v + bb * 2 * TILE + j * 1024);
+  };
+
+  // ---- LDS read addresses.  Row reads (K and V, k-step ks): row c32, logical chunk 2ks + h: 8 bases for
+  // ks & 7 (both tiles use swz_dual), ks >> 3 = +256 B, the V tile +TILE.  Transposed K reads (key step kk, half r, d block db): lane 4q+p of group
+  // G reads row 16kk + 8r + 4h + q, logical chunk 4db + 2(G & 1) + (p >> 1); with swz_dual the physical chunk
+  // is 4((db & 3) ^ q) + ((2(G & 1) + (p >> 1)) ^ ((2r + h) & 3)) + 16 (db >> 2): 8 bases for (db & 3, r).
+  uint32_t kaddr[8], taddr[8];
+  {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) kaddr[i] = fa_lds_addr(kring) + c32 * (D * 2) + (((2 * i + h) ^ swz_dual(c32)) * 16);
+    const int G = lane >> 4, q = (lane >> 2) & 3, p = lane & 3;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int dbl = i & 3, r = i >> 2;
+      const int row = 8 * r + 4 * h + q;
+      const int ch = (4 * dbl + 2 * (G & 1) + (p >> 1)) ^ swz_dual(row);
+      taddr[i] = fa_lds_addr(kring) + row * (D * 2) + ch * 16 + 8 * (p & 1);
+    }
+  }
+  auto rload = [&](int tensor, uint32_t so, int ks) __attribute__((always_inline)) {
+    return *reinterpret_cast<const __attribute__((address_space(3))) bf16x8_t*>(
+        (uintptr_t)(kaddr[ks & 7] + so + tensor * TILE + (ks >> 3) * 256));
+  };
+  auto tload = [&](uint32_t so, int kk, int db) __attribute__((always_inline)) {
+    bf16x8_t vf;
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      const uint32_t addr = taddr[(db & 3) + 4 * r] + so + 16 * kk * (D * 2) + (db >> 2) * 256;
+      const s16x4_t x = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(uintptr_t)addr);
+      vf[4 * r + 0] = x[0]; vf[4 * r + 1] = x[1]; vf[4 * r + 2] = x[2]; vf[4 * r + 3] = x[3];
+    }
+    return vf;
+  };
+
+  f32x16_t acc[8];   // dQ^T: d block db, lane = query column
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc[i] = (f32x16_t){};
+
+  // visibility of tile t for this row (all ones when the tile is interior for the wave)
+  auto vis_of = [&](int t) __attribute__((always_inline)) {
+    const uint32_t km = kmask_s[t];
+    const bool interior = km == 0xffffffffu && (!causal || t * KT + KT - 1 <= wpos_lo) &&
+                          (nowin || t * KT > wpos_hi - a.window);
+    uint32_t vis = km;
+    if (!interior && causal) {
+      const int d = qpos - t * KT;
+      vis &= d >= 31 ? 0xffffffffu : (d < 0 ? 0u : (2u << d) - 1u);
+      if (!nowin) {
+        const int e = d - a.window;
+        vis &= e < 0 ? 0xffffffffu : (e >= 31 ? 0u : ~((2u << e) - 1u));
+      }
+    }
+    return interior ? 0xffffffffu : (vis >> (4 * h));
+  };
+
+  // Phase A: S^T, dP^T of the next tile (32 MFMAs, if MM) beside dS of the current tile (if DS) in the
+  // slots of the first 16 MFMAs: two keys per slot (P = exp2, bf16 round, dS = P (dP - delta), bf16).
+  auto phase_a = [&](auto MM, auto DSC, uint32_t so, f32x16_t& s_n, f32x16_t& p_n, const f32x16_t& s,
+                     const f32x16_t& dp, uint32_t vis, bf16x8_t (&dsf)[2]) __attribute__((always_inline)) {
+    constexpr bool mm = decltype(MM)::value, dsc = decltype(DSC)::value;
+    bf16x8_t kf[3], vf[3];
+    if (mm) {
+      kf[0] = rload(0, so, 0); vf[0] = rload(1, so, 0);
+      kf[1] = rload(0, so, 1); vf[1] = rload(1, so, 1);
+    }
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      if (mm) {
+        if (ks + 2 < 16) {
+          kf[(ks + 2) % 3] = rload(0, so, ks + 2);
+          vf[(ks + 2) % 3] = rload(1, so, ks + 2);
+        }
+        s_n = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks % 3], qf[ks], ks == 0 ? (f32x16_t){} : s_n, 0, 0, 0);
+        p_n = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks % 3], df[ks], ks == 0 ? (f32x16_t){} : p_n, 0, 0, 0);
+      }
+      if (dsc && ks < 8) {
+        const int r = 2 * ks;
+        float d2[2];
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const int kl = ((r + e) & 3) + 8 * ((r + e) >> 2);
+          const float pe = __builtin_amdgcn_exp2f(((vis >> kl) & 1u) ? fmaf(s[r + e], sl2, -lse2) : -INFINITY);
+          d2[e] = bfround(pe) * (dp[r + e] - dlt);
+        }
+        dsf[r >> 3][r & 7] = (short)f2bf(d2[0]);
+        dsf[r >> 3][(r & 7) + 1] = (short)f2bf(d2[1]);
+        asm volatile("" : "+v"(dsf[r >> 3]));   // keep the pair here (not sunk to the dQ MFMAs)
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+  // Phase B: dQ^T += K^T dS^T (16 MFMAs, key step outer), K^T reads two MFMAs ahead, the next DMA pieces
+  // (if ST) one per two MFMAs.  (All MFMAs of this kernel are builtins: no VALU touches dQ^T before the
+  // epilogue, so hipcc has no reason to move it between register files, and it inserts the hazard waits.)
+  auto phase_b = [&](auto ST, uint32_t so, const bf16x8_t (&dsf)[2], int bb_st, int t_st)
+      __attribute__((always_inline)) {
+    constexpr bool st = decltype(ST)::value;
+    bf16x8_t tf[3];
+    tf[0] = tload(so, 0, 0);
+    tf[1] = tload(so, 0, 1);
+    uint32_t sso = 0;
+    if (st) sso = __builtin_amdgcn_readfirstlane((uint32_t)t_st * tile_bytes);
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int kk = i >> 3, db = i & 7;
+      if (i + 2 < 16) tf[(i + 2) % 3] = tload(so, (i + 2) >> 3, (i + 2) & 7);
+      acc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[i % 3], dsf[kk], acc[db], 0, 0, 0);
+      if (st && (i & 1) == 0) {
+        const int j = i >> 1;
+        if (j < 4) FA_DMA(dk[j], sso, rsk, lds_k + bb_st * 2 * TILE + j * 1024);
+        else FA_DMA(dv[j - 4], sso, rsv, lds_v + bb_st * 2 * TILE + (j - 4) * 1024);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+  };
+
+  if (t_lo < t_hi) {
+#pragma unroll
+    for (int i = 0; i < 3; ++i) stage(i, min(t_lo + i, t_hi - 1));
+    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+  }
+  using T_ = std::true_type;
+  using F_ = std::false_type;
+  f32x16_t sa, pa, sb = (f32x16_t){}, pb = (f32x16_t){};
+  bf16x8_t dsf[2];
+  phase_a(T_{}, F_{}, 0, sa, pa, sb, pb, 0u, dsf);
+  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // its MFMA results -> the first VALU reads
+  auto slot = [&](int t) { return (uint32_t)((t - t_lo) & (NB - 1)) * (uint32_t)(2 * TILE); };
+  auto iter = [&](int t, f32x16_t& s_c, f32x16_t& p_c, f32x16_t& s_n, f32x16_t& p_n) __attribute__((always_inline)) {
+    const uint32_t vis = vis_of(t);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    phase_a(T_{}, T_{}, slot(t + 1), s_n, p_n, s_c, p_c, vis, dsf);
+    phase_b(T_{}, slot(t), dsf, (t - t_lo + 3) & (NB - 1), min(t + 3, t_hi - 1));
+  };
+  int t = t_lo;
+  for (; t + 2 < t_hi; t += 2) {
+    iter(t, sa, pa, sb, pb);
+    iter(t + 1, sb, pb, sa, pa);
+  }
+  if (t + 1 < t_hi) {
+    iter(t, sa, pa, sb, pb);
+    ++t;
+    sa = sb;
+    pa = pb;
+  }
+  if (t < t_hi) {
+    phase_a(F_{}, T_{}, 0, sb, pb, sa, pa, vis_of(t), dsf);
+    phase_b(F_{}, slot(t), dsf, 0, 0);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup exits
+
+  // ---- dQ[q][d] = scale dQ^T[d][q] (bf16), 16-B stores after one permlane32 swap per register pair
+  if (qrow >= a.rows) return;
+  bf16_t* op = a.dQ + (z * a.rows + qrow) * (long)D + 8 * h;
+#pragma unroll
+  for (int db = 0; db < 8; ++db) {
+#pragma unroll
+    for (int m = 0; m < 2; ++m) {
+      uint32_t w[4];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const int r = 8 * m + 2 * k;
+        w[k] = (uint32_t)f2bf(acc[db][r] * a.scale) | ((uint32_t)f2bf(acc[db][r + 1] * a.scale) << 16);
+      }
+      const auto s0 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+      const auto s1 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+      *reinterpret_cast<uint4*>(op + 32 * db + 16 * m) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+    }
+  }
 }
 
 // ---------------------------------------------------------------- dQ, head_dim 256
@@ -2204,7 +2851,9 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs*
       // the dQ kernel computes delta and runs first; past the 4096-key mask table the generic dQ kernel runs
       // after a separate delta pass and the dK/dV kernel
       const bool dq_new = (a.nkeys + 31) / 32 <= FA_MAXT;
-      if (dq_new) hipLaunchKernelGGL(attn_bwd_dq256_kernel, gq, dim3(512), 0, st, b);
+      static const bool dq_old = [] { const char* e = getenv("PTK_ATTN_DQ_OLD"); return e && e[0] == '1'; }();
+      if (dq_new && dq_old) hipLaunchKernelGGL(attn_bwd_dq256_kernel, gq, dim3(512), 0, st, b);
+      else if (dq_new) hipLaunchKernelGGL(attn_bwd_dq256w_kernel, gq, dim3(256), 0, st, b);
       else hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
       // 32 keys per wave (one wave per SIMD) measured 209 us vs 252 us for 16 keys per wave (two per
       // SIMD, which spills the precomputed transposed-read addresses) at cfg2
@@ -2248,10 +2897,13 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
     // quantise worse than 704 (110 vs 78 us per layer), and it spills
     case 256: {
       // the generic kernel past the 4096-key mask table
+      static const bool old = [] { const char* e = getenv("PTK_ATTN_FWD_OLD"); return e && e[0] == '1'; }();
       if ((a.nkeys + 31) / 32 > FA_MAXT || (long)a.nkeys * a.ldk * 2 > 0x7fffffffL)
         hipLaunchKernelGGL((attn_fwd_kernel<256, 1>), grid, dim3(512), 0, st, a);
-      else
+      else if (old)
         hipLaunchKernelGGL(attn_fwd256_kernel, grid, dim3(512), 0, st, a);
+      else
+        hipLaunchKernelGGL(attn_fwd256w_kernel, grid, dim3(256), 0, st, a);
       break;
     }
     default: return set_error("attn_fwd: head_dim %d unsupported (64, 256)", a.D);
@@ -2260,3 +2912,9 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
 }
 
 }  // namespace ptk
+
+#ifdef PTK_FA_STAMPS
+extern "C" int ptk_debug_fa_stamps_read(void* host, size_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ptk::g_fa_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+#endif

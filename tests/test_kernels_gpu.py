@@ -331,11 +331,14 @@ def test_flash_fwd_siglip_layout(gpu, N):
     torch.testing.assert_close(O.float(), ref, rtol=2e-2, atol=2e-2)
 
 
-@pytest.mark.parametrize("Hkv,G,window", [(1, 4, 0), (1, 4, 100), (2, 2, 64)])
-def test_flash_fwd_gemma_layout(gpu, Hkv, G, window):
-    """Causal GQA, head_dim 256, key padding, sliding window, token-major O via row map, LSE."""
+@pytest.mark.parametrize("Hkv,G,window,S", [(1, 4, 0, 320), (1, 4, 100, 320), (2, 2, 64, 320), (1, 4, 512, 704),
+                                            (1, 3, 0, 300), (1, 1, 0, 100), (1, 1, 0, 36)])
+def test_flash_fwd_gemma_layout(gpu, Hkv, G, window, S):
+    """Causal GQA, head_dim 256, key padding, sliding window, token-major O via row map, LSE.  S 704 with
+    window 512 = the cfg2 step's sliding layers; G 3 / S 300 and S 100 / 36: query rows that are not a
+    multiple of the 128-row block (idle waves, partial tiles)."""
     Kn, L = _k()
-    B, S, hd = 2, 320, 256
+    B, hd = 2, 256
     Hq = Hkv * G
     Q = rnd(B, Hkv, S, G, hd, dev=gpu, seed=41)
     Kt = rnd(B, Hkv, S, hd, dev=gpu, seed=42)

@@ -184,16 +184,18 @@ def _bench_census(gpu):
 
 @pytest.mark.slow
 @pytest.mark.parametrize("preset,bs,T,vl,tl", [("cfg2", 2, 128, None, None), ("cfg2", 1, 512, None, None),
-                                               ("cfg2", 16, 128, None, None), ("cfg5", 1, 256, 2, 6)])
+                                               ("cfg2", 30, 128, 2, 6), ("cfg5", 1, 256, 2, 6)])
 def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
     """Full architecture vs the fp32 CPU oracle (the oracle is pinned to the reference by the fixtures).
     cfg2: SigLIP-L/16-384 (24 layers) + Gemma3-1B (26 layers) at bs 2, T 128 (S = 703 > window 512,
     left-padded captions), and at the reference's default caption length T = 512
     (train_projection_stage1.py:27; S = 1087, bs 1).
-    cfg2 at bs 16 (M = 11 264 token rows, 9 216 SigLIP rows; the smallest batch whose 256x256 tile rounds send
-    every plain projection to the same kernel family as bs 32): the GEMM dispatch of the benchmarked bs-32 step -- the persistent
-    gate|up GEGLU and dh + GEGLU-backward kernels, the long-K d(gate|up) dX kernel -- which the small
-    batches never select; the test asserts that every kernel family (path, epilogue) the bs-32 step
+    cfg2 at bs 30, 2 SigLIP + 6 Gemma layers (one of them global): the GEMM dispatch of the benchmarked
+    bs-32 step -- the persistent gate|up GEGLU and dh + GEGLU-backward kernels, the 8-wave persistent plain and
+    GELU-tanh kernels, the long-K d(gate|up) dX kernel -- which the small batches never select.  Every layer
+    of a tower has the same shapes, so depth does not change the dispatch; bs 30 is the smallest batch whose
+    256x256 tile rounds send every projection to the same kernel family as bs 32 (tools/census_probe.py:
+    bs 16-28 each miss one).  The test asserts that every kernel family (path, epilogue) the bs-32 step
     launches also ran in this compared step.
     cfg5: Gemma3-4B dims (hidden 2560, GQA 8:4, window 1024, linear RoPE x8 on the full layer, vocab
     262 208 = 4 097 x 64, which leaves a remainder slice in the split-K lm_head backward) at 2 SigLIP and
@@ -236,7 +238,7 @@ def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
     loss = float(loss)
     del eng, lm, vt
     torch.cuda.empty_cache()
-    if bs == 16:
+    if bs == 30:
         bench = _bench_census(gpu)
         record(f"arch[{preset}-bs{bs}-T{T}]", "paths", n_bench=len(bench), n_here=len(paths),
                missing=len(bench - paths))
