@@ -684,6 +684,28 @@ __global__ void __launch_bounds__(512, 1) attn_fwd256_kernel(FlashArgs a) {
     a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_run)) * 0.6931471805599453f;
 }
 
+// per-tile 32-bit key masks (key valid and < nkeys) of tiles [t_lo, t_hi) into LDS, tile tt by wave tt % NW:
+// every key_valid load of the wave issued before the first ballot waits (8 tiles at a time), so the table
+// costs one memory latency, not one per tile
+template <int NW>
+PTK_DEV void fa_key_masks(const int* kvl, int nkeys, int t_lo, int t_hi, int wave, int lane, uint32_t* kmask_s) {
+  constexpr int KT = 32;
+  for (int base = t_lo + wave; base < t_hi; base += 8 * NW) {
+    int v[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int key = (base + NW * j) * KT + (lane & 31);
+      v[j] = (kvl && base + NW * j < t_hi) ? kvl[min(key, nkeys - 1)] : 1;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int tt = base + NW * j;
+      const uint64_t m = __ballot(tt * KT + (lane & 31) < nkeys && v[j] != 0);
+      if (tt < t_hi && lane == 0) kmask_s[tt] = (uint32_t)m;
+    }
+  }
+}
+
 // ---------------------------------------------------------------- forward, head_dim 256, 32 rows per wave
 // One workgroup = 4 waves (one per SIMD, the whole 512-entry register file each) = 128 query rows of one z;
 // each wave owns 32 rows and runs v_mfma_f32_32x32x16_bf16 (32 cycles, 32x32 outputs), so every K / V^T
@@ -732,15 +754,8 @@ __global__ void __launch_bounds__(256, 1) attn_fwd256w_kernel(FlashArgs a) {
   }
   const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
 
-  // ---- per-tile key masks (valid and < nkeys), written before any DMA is in flight
-  for (int tt = t_lo + wave; tt < t_hi; tt += 4) {
-    const int key = tt * KT + c32;
-    const bool ok = key < a.nkeys && (!kvl || kvl[min(key, a.nkeys - 1)] != 0);
-    const uint64_t m = __ballot(ok);
-    if (lane == 0) kmask_s[tt] = (uint32_t)m;
-  }
-
-  // ---- Q fragments: B operand of S^T = K Q^T for k-step ks, lane holds Q[row c32][16 ks + 8 h .. +7]
+  // ---- Q fragments: B operand of S^T = K Q^T for k-step ks, lane holds Q[row c32][16 ks + 8 h .. +7]; the
+  // loads are issued first and stay in flight while the key masks are built
   const int wrow0 = r0 + wave * 32;
   const int qrow = wrow0 + c32;
   const int qrow_c = min(qrow, a.rows - 1);
@@ -751,6 +766,7 @@ __global__ void __launch_bounds__(256, 1) attn_fwd256w_kernel(FlashArgs a) {
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + 16 * ks);
   }
+  fa_key_masks<4>(kvl, a.nkeys, t_lo, t_hi, wave, lane, kmask_s);
 #pragma unroll
   for (int ks = 0; ks < 16; ++ks) fa_pin(qf[ks]);
   __syncthreads();   // key masks published (no LDS-DMA in flight yet)
@@ -1533,13 +1549,6 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
   }
   const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
 
-  for (int tt = t_lo + wave; tt < t_hi; tt += 4) {
-    const int key = tt * KT + c32;
-    const bool ok = key < a.nkeys && (!kvl || kvl[min(key, a.nkeys - 1)] != 0);
-    const uint64_t m = __ballot(ok);
-    if (lane == 0) kmask_s[tt] = (uint32_t)m;
-  }
-
   // ---- Q, dO fragments (B operands, k-step ks: lane holds row c32, d 16 ks + 8 h .. +7), LSE, delta
   const int wrow0 = r0 + wave * 32;
   const int qrow = wrow0 + c32;
@@ -1558,13 +1567,15 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
   {
     const long z0 = z / a.zin, z1 = z - z0 * a.zin;
     const bf16_t* orow = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow_c) * a.ldo + 8 * h;
+    bf16x8_t of[16];
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) of[ks] = *reinterpret_cast<const bf16x8_t*>(orow + 16 * ks);
+    fa_key_masks<4>(kvl, a.nkeys, t_lo, t_hi, wave, lane, kmask_s);   // (its loads join those in flight)
     float acc0 = 0.f;
 #pragma unroll
-    for (int ks = 0; ks < 16; ++ks) {
-      const bf16x8_t of = *reinterpret_cast<const bf16x8_t*>(orow + 16 * ks);
+    for (int ks = 0; ks < 16; ++ks)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) acc0 += bf2f((bf16_t)of[e]) * bf2f((bf16_t)df[ks][e]);
-    }
+      for (int e = 0; e < 8; ++e) acc0 += bf2f((bf16_t)of[ks][e]) * bf2f((bf16_t)df[ks][e]);
     dlt = xor32_sum(acc0);
     if (h == 0 && qrow < a.rows) a.delta[z * a.rows + qrow] = dlt;
   }
