@@ -355,20 +355,20 @@ constexpr int FA_MAXT = 128;   // key tiles (of 32) the mask table holds: nkeys 
 // diagnostic build (make fastamps): s_memtime stamps of the 32-row d-256 kernels' phases per workgroup, kept in
 // registers and written by lane 0 of wave 0 at the end (no extra memory op inside the counted-vmcnt pipeline)
 #ifdef PTK_FA_STAMPS
-__device__ unsigned long long g_fa_stamps[1 << 14][8];
+__device__ unsigned long long g_fa_stamps[3][1 << 13][8];   // [kernel: fwd, dQ, dK/dV][workgroup][stamp]
 #define FA_STAMP(i) st_[i] = __builtin_amdgcn_s_memtime()
 #define FA_STAMPS_DECL unsigned long long st_[8] = {}; st_[5] = __builtin_amdgcn_s_memrealtime(); FA_STAMP(0)
-#define FA_STAMPS_WRITE(ntiles)                                                                    \
+#define FA_STAMPS_WRITE(kid, ntiles)                                                               \
   if (threadIdx.x == 0) {                                                                          \
     FA_STAMP(4);                                                                                   \
     st_[6] = __builtin_amdgcn_s_memrealtime();                                                     \
     st_[7] = (unsigned long long)(ntiles);                                                         \
-    for (int i_ = 0; i_ < 8; ++i_) g_fa_stamps[blockIdx.x & ((1 << 14) - 1)][i_] = st_[i_];        \
+    for (int i_ = 0; i_ < 8; ++i_) g_fa_stamps[kid][blockIdx.x & ((1 << 13) - 1)][i_] = st_[i_];   \
   }
 #else
 #define FA_STAMP(i) (void)0
 #define FA_STAMPS_DECL (void)0
-#define FA_STAMPS_WRITE(ntiles) (void)0
+#define FA_STAMPS_WRITE(kid, ntiles) (void)0
 #endif
 
 #define FA_DMA(VOFF, SOFF, RSRC, LDS)                                                                      \
@@ -1039,7 +1039,7 @@ __global__ void __launch_bounds__(256, 1) attn_fwd256w_kernel(FlashArgs a) {
   }
   if (a.lse && h == 0)
     a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_tot)) * 0.6931471805599453f;
-  FA_STAMPS_WRITE(t_hi - t_lo);
+  FA_STAMPS_WRITE(0, t_hi - t_lo);
 }
 
 // ============================================================================ backward
@@ -1530,6 +1530,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
   __shared__ __attribute__((aligned(16))) char smem[2 * NB * TILE + FA_MAXT * 4];
   char* const kring = smem;
   uint32_t* const kmask_s = reinterpret_cast<uint32_t*>(smem + 2 * NB * TILE);
+  FA_STAMPS_DECL;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1585,6 +1586,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
     fa_pin(df[ks]);
   }
   __syncthreads();   // key masks published (no LDS-DMA in flight yet)
+  FA_STAMP(1);
   const float sl2 = a.scale * L2E;
   const int causal = a.causal != 0, nowin = a.window <= 0;
   const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
@@ -1738,6 +1740,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
   bf16x8_t dsf[2];
   phase_a(T_{}, F_{}, 0, sa, pa, sb, pb, 0u, dsf);
   asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // its MFMA results -> the first VALU reads
+  FA_STAMP(2);
   auto slot = [&](int t) { return (uint32_t)((t - t_lo) & (NB - 1)) * (uint32_t)(2 * TILE); };
   auto iter = [&](int t, f32x16_t& s_c, f32x16_t& p_c, f32x16_t& s_n, f32x16_t& p_n) __attribute__((always_inline)) {
     const uint32_t vis = vis_of(t);
@@ -1763,6 +1766,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
     phase_b(F_{}, slot(t), dsf, 0, 0);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup exits
+  FA_STAMP(3);
 
   // ---- dQ[q][d] = scale dQ^T[d][q] (bf16), 16-B stores after one permlane32 swap per register pair
   if (qrow >= a.rows) return;
@@ -1782,6 +1786,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
       *reinterpret_cast<uint4*>(op + 32 * db + 16 * m) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
     }
   }
+  FA_STAMPS_WRITE(1, t_hi - t_lo);
 }
 
 // ---------------------------------------------------------------- dQ, head_dim 256
@@ -2443,6 +2448,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256b_kernel(FlashBwdArgs a
   char* const qring = smem;
   char* const oring = smem + NB * TILE;
   const float* const ldring = reinterpret_cast<const float*>(smem + 2 * NB * TILE);
+  FA_STAMPS_DECL;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -2490,6 +2496,8 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256b_kernel(FlashBwdArgs a
       fa_pin(kf[kg][ks]);
       fa_pin(vf[kg][ks]);
     }
+  FA_STAMP(1);
+  FA_STAMP(2);
   const float L2E = 1.4426950408889634f;
   const float sl2 = a.scale * L2E;
   const int qshift = __builtin_ctz(a.qdiv);   // host guarantees a power of two
@@ -2652,6 +2660,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256b_kernel(FlashBwdArgs a
     ++c;
   }
 
+  FA_STAMP(3);
   // ---- outputs: lane holds dV^T[16ds + 4g + j][key]
   if (P == 1) {
 #pragma unroll
@@ -2685,6 +2694,7 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256b_kernel(FlashBwdArgs a
       }
     }
   }
+  FA_STAMPS_WRITE(2, c1 - c0);
 }
 
 // sums the partials of every split slab in piece order -> bf16 dK (x scale), dV

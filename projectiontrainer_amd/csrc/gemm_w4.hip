@@ -297,8 +297,18 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 #define W4_DSREAD(DST, ADDR, OFF) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(DST) : "v"(ADDR), "i"(OFF))
 // one 1-KiB LDS-DMA piece: M0 = wave-uniform LDS destination.  hipcc emits no M0 use of its own in
 // these kernels (no LDS-DMA builtins, gfx950 ds_* do not read M0), so M0 is not saved / restored.
+// PTK_W4_DMA_POL (diagnostic builds, make w4pol): cache-policy bits on the pieces (1 sc1, 2 sc0, 3 nt)
+#if PTK_W4_DMA_POL == 1
+#define W4_POL " sc1"
+#elif PTK_W4_DMA_POL == 2
+#define W4_POL " sc0"
+#elif PTK_W4_DMA_POL == 3
+#define W4_POL " nt"
+#else
+#define W4_POL ""
+#endif
 #define W4_DMA(RSRC, VOFF, SOFF, LDS)                                                                      \
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen lds"                   \
+  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen" W4_POL " lds"        \
                :: "v"(VOFF), "s"(LDS), "s"(RSRC), "s"(SOFF) : "memory")
 
 PTK_DEV u32x4_t w4_rsrc(const void* base, uint32_t bytes) {
