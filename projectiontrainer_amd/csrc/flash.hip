@@ -27,9 +27,6 @@
 #include <vector>
 #include "common.h"
 #include "ptk_internal.h"
-#ifndef PTK_FA_ABL
-#define PTK_FA_ABL 0   // diagnostic ablation builds of attn_fwd256_kernel (make faabl): wrong results by construction
-#endif
 
 namespace ptk {
 
@@ -337,18 +334,10 @@ __global__ void __launch_bounds__(512, 1) attn_fwd_kernel(FlashArgs a) {
   }
 }
 
-// ---------------------------------------------------------------- forward, head_dim 256
-// The 8-wave, 16-rows-per-wave structure of attn_fwd_kernel, re-cut for instruction count (the loop was
-// issue-bound: ~190 non-MFMA VALU + ~115 SALU per 32 MFMAs):
-//   * K/V tiles by buffer_load ... lds: one descriptor per tensor, a per-lane 32-bit offset fixed for the
-//     whole kernel and the tile's byte offset in an SGPR, so a DMA piece costs no VALU;
-//   * separate K and V rings (4 x 16 KiB each) and the tile loop unrolled by the ring depth, so every LDS
-//     read address is a lane offset + an immediate (no per-tile address arithmetic);
-//   * the key-valid flags compressed once per block into one 32-bit mask per key tile (LDS), read as a
-//     scalar per tile: the interior test is a compare, the mask one bit test per score;
-//   * online softmax with a deferred running max: it moves only when a tile's max exceeds it by more than
-//     FA_DEFER (log2 units; P <= 2^FA_DEFER is exact enough in fp32 sums and bf16 operands), so the O
-//     rescale runs a few times per row block instead of on most tiles.
+// ---------------------------------------------------------------- d-256 helpers
+// online softmax with a deferred running max: it moves only when a tile's max exceeds it by more than
+// FA_DEFER (log2 units; P <= 2^FA_DEFER is exact enough in fp32 sums and bf16 operands), so the O rescale
+// runs a few times per row block instead of on most tiles
 constexpr float FA_DEFER = 8.f;
 constexpr int FA_MAXT = 128;   // key tiles (of 32) the mask table holds: nkeys <= 4096
 
@@ -386,303 +375,6 @@ PTK_DEV fa_u32x4_t fa_rsrc(const void* base, uint32_t bytes) {
 }
 PTK_DEV uint32_t fa_lds_addr(const void* p) { return (uint32_t)(uintptr_t)(fa_lptr_t)p; }
 template <int N> using fa_ic = std::integral_constant<int, N>;
-
-__global__ void __launch_bounds__(512, 1) attn_fwd256_kernel(FlashArgs a) {
-  constexpr int D = 256, KT = 32, KS = 8, DS = 16, NB = 4;
-  constexpr int TILE = KT * D * 2;   // one K or V tile, 16 KiB
-  __shared__ __attribute__((aligned(16))) char smem[2 * NB * TILE + FA_MAXT * 4];   // K ring, V ring, key masks
-  char* const kring = smem;
-  char* const vring = smem + NB * TILE;
-  uint32_t* const kmask_s = reinterpret_cast<uint32_t*>(smem + 2 * NB * TILE);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, c16 = lane & 15;
-  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
-  const int z = blockIdx.x % nz, z0 = z / a.zin, z1 = z - z0 * a.zin;
-  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;   // heaviest (latest) row blocks first
-  const bf16_t* Q = a.Q + z0 * a.sQ0 + z1 * a.sQ1;
-  const bf16_t* K = a.K + z0 * a.sK0 + z1 * a.sK1;
-  const bf16_t* V = a.V + z0 * a.sK0 + z1 * a.sK1;
-  const long b = z / a.zdiv;
-  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
-
-  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
-  int k_hi = a.nkeys, k_lo = 0;
-  if (a.causal) {
-    k_hi = min(k_hi, pos_hi + 1);
-    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
-  }
-  const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
-
-  // ---- per-tile key masks (valid and < nkeys), written before any DMA is in flight
-  for (int tt = wave; tt < t_hi; tt += 8) {
-    const int key = tt * KT + (lane & 31);
-    const bool ok = key < a.nkeys && (!kvl || kvl[min(key, a.nkeys - 1)] != 0);
-    const uint64_t m = __ballot(ok);
-    if (lane == 0) kmask_s[tt] = (uint32_t)m;
-  }
-
-  // ---- Q fragments: B operand of S^T = K Q^T, lane holds Q[row c16][8g + 32ks .. +7]
-  const int wrow0 = r0 + wave * 16;
-  const int qrow = wrow0 + c16;
-  const int qrow_c = min(qrow, a.rows - 1);
-  const int qpos = qrow_c / a.qdiv;
-  bf16x8_t qf[KS];
-  {
-    const bf16_t* qp = Q + map_row(a.qmap, qrow_c) * a.ldq + 8 * g;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + 32 * ks);
-  }
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) fa_pin(qf[ks]);
-  __syncthreads();   // key masks published (no LDS-DMA in flight yet)
-
-  const int causal = a.causal != 0, nowin = a.window <= 0;
-  const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
-  const int wpos_hi = min(wrow0 + 15, a.rows - 1) / a.qdiv;
-
-  // ---- DMA: wave w stages rows 4w..4w+3 of each tile (2 pieces of 2 rows x 512 B per tensor); lane i of
-  // a piece writes LDS row 2j + (i >> 5), chunk i & 31, and fetches logical chunk (i & 31) ^ swz(row)
-  const fa_u32x4_t rsk = fa_rsrc(K, (uint32_t)((long)a.nkeys * a.ldk * 2));
-  const fa_u32x4_t rsv = fa_rsrc(V, (uint32_t)((long)a.nkeys * a.ldk * 2));
-  uint32_t dk[2], dv[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = (wave * 2 + j) * 2 + (lane >> 5);
-    dk[j] = (uint32_t)row * (uint32_t)a.ldk * 2u + 16u * ((lane & 31) ^ swz_k<D>(row));
-    dv[j] = (uint32_t)row * (uint32_t)a.ldk * 2u + 16u * ((lane & 31) ^ swz_v<D>(row));
-  }
-  const uint32_t lds_k = __builtin_amdgcn_readfirstlane(fa_lds_addr(kring) + wave * 2048);
-  const uint32_t lds_v = __builtin_amdgcn_readfirstlane(fa_lds_addr(vring) + wave * 2048);
-  const uint32_t tile_bytes = __builtin_amdgcn_readfirstlane((uint32_t)KT * (uint32_t)a.ldk * 2u);
-  auto stage = [&](int bb, int t) __attribute__((always_inline)) {
-    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)t * tile_bytes);
-    FA_DMA(dk[0], so, rsk, lds_k + bb * TILE);
-    FA_DMA(dk[1], so, rsk, lds_k + bb * TILE + 1024);
-    FA_DMA(dv[0], so, rsv, lds_v + bb * TILE);
-    FA_DMA(dv[1], so, rsv, lds_v + bb * TILE + 1024);
-  };
-
-  // ---- LDS read offsets.  K rows 16ms + c16, chunk (4ks + g) ^ (row & 15): ks bit 2 and ms untouched by
-  // the swizzle (immediates).  V^T rows 16hh + 4g + q4, chunk (2ds + (p4 >> 1)) ^ 2(row & 7): ds bit 3, hh
-  // untouched (immediates).
-  // (lane addresses include the ring base, so the per-read immediates stay below 64 KiB)
-  int koff[4];
-  const char* vaddr[8];
-  {
-    const int q4 = c16 >> 2, p4 = c16 & 3, vrow = 4 * g + q4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) koff[i] = c16 * (D * 2) + ((i * 4 + g) ^ swz_k<D>(c16)) * 16;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) {
-      const uint32_t va = fa_lds_addr(vring) + vrow * (D * 2) + ((2 * i + (p4 >> 1)) ^ swz_v<D>(vrow)) * 16 + 8 * (p4 & 1);
-      vaddr[i] = (const char*)(fa_lptr_t)(uintptr_t)__builtin_amdgcn_readfirstlane(0) + va;
-    }
-  }
-
-  f32x4_t o[DS];
-#pragma unroll
-  for (int i = 0; i < DS; ++i) o[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-  float m_run = -INFINITY, l_run = 0.f;
-  const float sl2 = a.scale * 1.4426950408889634f;   // scores in log2 units
-  const float defer = FA_DEFER / sl2;                 // the deferral in raw score units
-  const bool idle = wrow0 >= a.rows;                  // rows past the end: stage and keep the barriers only
-
-  // Tile t lives in ring slot (t - t_lo) % NB (compile-time in each unrolled copy); tile t + 2 is staged at
-  // iteration t into the slot of tile t - 2.  Waves 4-7 (the second wave of each SIMD) run one phase behind
-  // waves 0-3: between two barriers a SIMD's early wave runs S(t), softmax(t), P(t)V(t) while its late wave
-  // runs P(t-1)V(t-1), S(t), softmax(t), so one wave's softmax and LDS waits face the other's MFMAs instead
-  // of both waves contending for the same pipe in lockstep.  Same operations on O in the same order: results
-  // are identical for both orders.
-  auto sync = [&](int bb, int t) __attribute__((always_inline)) {
-    // tile t landed (this wave's 4 pieces; tile t+1 may stay in flight), then the barrier publishes every
-    // wave's share; the slot restaged below held tile t-2, whose last reader (a late wave's P.V of tile t-2)
-    // ran before this barrier
-    if (t + 1 < t_hi) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#if PTK_FA_ABL != 1
-    __builtin_amdgcn_s_barrier();
-#endif
-#if PTK_FA_ABL != 2
-    if (t + 2 < t_hi) stage((bb + 2) % NB, t + 2);
-#endif
-  };
-  // S^T = K Q^T for tile t: s[ms] holds keys 16ms + 4g + j, query column c16
-  auto qk = [&](auto BUF, f32x4_t (&s)[2]) __attribute__((always_inline)) {
-    constexpr int bb = decltype(BUF)::value;
-    const char* kb = kring + bb * TILE;
-#pragma unroll
-    for (int ms = 0; ms < 2; ++ms) {
-      s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-#if PTK_FA_ABL == 6
-        const bf16x8_t kf = qf[(ks + 1) & 7];
-#else
-        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + koff[ks & 3] + (ks >> 2) * 256 + ms * 16 * (D * 2));
-#endif
-#if PTK_FA_ABL == 3
-        s[ms][ks & 3] += (float)kf[ks];
-#else
-        s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
-#endif
-      }
-    }
-  };
-  // mask + online softmax (running max deferred) -> P (bf16); rescales O when the max moved.  A tile whose
-  // every key is valid and visible to every row of the wave (below the causal diagonal, inside the window)
-  // skips the mask.
-  auto softmax = [&](int t, f32x4_t (&s)[2], bf16x8_t& pf) __attribute__((always_inline)) {
-#if PTK_FA_ABL == 5
-#pragma unroll
-    for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) pf[ms * 4 + j] = (short)f2bf(s[ms][j]);
-    l_run += s[0][0];
-    return;
-#endif
-    const uint32_t km = kmask_s[t];
-    const bool interior = km == 0xffffffffu && (!causal || t * KT + KT - 1 <= wpos_lo) &&
-                          (nowin || t * KT > wpos_hi - a.window);
-    float mt = -INFINITY;
-    if (interior) {
-#pragma unroll
-      for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) mt = fmaxf(mt, s[ms][j]);
-    } else {
-      // the row's visible keys of this tile as a 32-bit mask: valid, kl <= qpos - t KT (causal),
-      // kl > qpos - W - t KT (window)
-      uint32_t vis = km;
-      if (causal) {
-        const int d = qpos - t * KT;
-        vis &= d >= 31 ? 0xffffffffu : (d < 0 ? 0u : (2u << d) - 1u);
-        if (!nowin) {
-          const int e = d - a.window;
-          vis &= e < 0 ? 0xffffffffu : (e >= 31 ? 0u : ~((2u << e) - 1u));
-        }
-      }
-#pragma unroll
-      for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int kl = ms * 16 + 4 * g + j;
-          const float v = ((vis >> kl) & 1u) ? s[ms][j] : -INFINITY;
-          s[ms][j] = v;
-          mt = fmaxf(mt, v);
-        }
-    }
-    mt = xor32_max(xor16_max(mt));
-    const bool up = mt > m_run + defer;   // m_run = -inf: any finite tile max moves it
-    const float m_new = up ? mt : m_run;
-    const float alpha = (up && m_run != -INFINITY) ? __builtin_amdgcn_exp2f((m_run - m_new) * sl2) : 1.f;
-    const float mc = (m_new == -INFINITY) ? 0.f : m_new * sl2;
-    float rs = 0.f;
-#pragma unroll
-    for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const float p = __builtin_amdgcn_exp2f(fmaf(s[ms][j], sl2, -mc));   // exp2(-inf) = 0 for masked keys
-        rs += p;   // fp32 row sum (P itself enters P.V in bf16)
-        pf[ms * 4 + j] = (short)f2bf(p);
-      }
-    rs = xor32_sum(xor16_sum(rs));
-    l_run = l_run * alpha + rs;
-    m_run = m_new;
-    if (__any(alpha != 1.f)) {
-#pragma unroll
-      for (int i = 0; i < DS; ++i) o[i] *= alpha;
-    }
-  };
-  // O^T += V^T P^T : k order {4g+0..3, 16+4g+0..3} on both operands
-  auto pv = [&](auto BUF, const bf16x8_t& pf) __attribute__((always_inline)) {
-    constexpr int bb = decltype(BUF)::value;
-#pragma unroll
-    for (int ds = 0; ds < DS; ++ds) {
-      bf16x8_t vf;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const char* addr = vaddr[ds & 7] + bb * TILE + (ds >> 3) * 256 + hh * 16 * (D * 2);
-#if PTK_FA_ABL == 7
-        const s16x4_t r = {qf[ds & 7][hh], qf[ds & 7][hh + 2], qf[ds & 7][hh + 4], qf[ds & 7][hh + 6]};
-#else
-        const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
-#endif
-        vf[4 * hh + 0] = r[0]; vf[4 * hh + 1] = r[1]; vf[4 * hh + 2] = r[2]; vf[4 * hh + 3] = r[3];
-      }
-#if PTK_FA_ABL == 4
-      o[ds][0] += (float)vf[ds & 7] * (float)pf[1];
-#else
-      o[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, pf, o[ds], 0, 0, 0);
-#endif
-    }
-  };
-  auto early = [&](auto BUF, int t) __attribute__((always_inline)) {
-    constexpr int bb = decltype(BUF)::value;
-    sync(bb, t);
-    if (idle) return;
-    f32x4_t s[2];
-    bf16x8_t pf;
-    qk(BUF, s);
-    softmax(t, s, pf);
-    pv(BUF, pf);
-  };
-  bf16x8_t pprev;   // late waves: P of the previous tile, applied after the next barrier
-  // (called for t = t_lo .. t_hi: the call at t_hi only applies the last tile's P.V, whose slot nothing
-  // restages after the last barrier)
-  auto late = [&](auto BUF, int t) __attribute__((always_inline)) {
-    constexpr int bb = decltype(BUF)::value;
-    if (t < t_hi) sync(bb, t);
-    if (idle) return;
-    if (t > t_lo) pv(fa_ic<(bb + NB - 1) % NB>{}, pprev);
-    if (t == t_hi) return;
-    f32x4_t s[2];
-    qk(BUF, s);
-    softmax(t, s, pprev);
-  };
-
-  if (t_lo < t_hi) stage(0, t_lo);
-  if (t_lo + 1 < t_hi) stage(1, t_lo + 1);
-  if (wave < 4 || a.variant == 1) {
-    for (int t = t_lo; t < t_hi;) {
-      early(fa_ic<0>{}, t);
-      if (++t >= t_hi) break;
-      early(fa_ic<1>{}, t);
-      if (++t >= t_hi) break;
-      early(fa_ic<2>{}, t);
-      if (++t >= t_hi) break;
-      early(fa_ic<3>{}, t);
-      ++t;
-    }
-  } else {
-    for (int t = t_lo; t <= t_hi;) {
-      late(fa_ic<0>{}, t);
-      if (++t > t_hi) break;
-      late(fa_ic<1>{}, t);
-      if (++t > t_hi) break;
-      late(fa_ic<2>{}, t);
-      if (++t > t_hi) break;
-      late(fa_ic<3>{}, t);
-      ++t;
-    }
-    // the last tile's P.V: its slot is still intact (nothing restages after the last barrier)
-  }
-
-  // ---- epilogue: O[q][d] = O^T[d][q] / l ; lane holds d = 16ds + 4g + j for query c16
-  if (qrow >= a.rows) return;
-  const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
-  bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow) * a.ldo + 4 * g;
-#pragma unroll
-  for (int ds = 0; ds < DS; ++ds) {
-    u16x4_t u;
-    u[0] = f2bf(o[ds][0] * inv); u[1] = f2bf(o[ds][1] * inv);
-    u[2] = f2bf(o[ds][2] * inv); u[3] = f2bf(o[ds][3] * inv);
-    *reinterpret_cast<u16x4_t*>(op + 16 * ds) = u;
-  }
-  if (a.lse && g == 0)
-    a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_run)) * 0.6931471805599453f;
-}
 
 // per-tile 32-bit key masks (key valid and < nkeys) of tiles [t_lo, t_hi) into LDS, tile tt by wave tt % NW:
 // every key_valid load of the wave issued before the first ballot waits (8 tiles at a time), so the table
@@ -1254,7 +946,7 @@ __global__ void __launch_bounds__(512, 1) attn_bwd_dq_kernel(FlashBwdArgs a) {
 }
 
 // ---------------------------------------------------------------- forward, head_dim 64 (SigLIP)
-// attn_fwd256_kernel's structure at head_dim 64: 64-key tiles (8 KiB per tensor: one LDS-DMA piece per
+// The 16-rows-per-wave, 8-wave structure at head_dim 64: 64-key tiles (8 KiB per tensor: one LDS-DMA piece per
 // tensor per wave), K/V rings of 4 slots (64 KiB, so two blocks can share a CU), the loop unrolled by
 // the ring depth, per-tile key masks, deferred running max, late waves one phase behind.  Per tile and
 // wave: S^T = K Q^T (8 MFMAs), 16 scores per lane, O^T += V^T P^T (8 MFMAs).
@@ -1519,7 +1211,7 @@ __global__ void __launch_bounds__(512, 2) attn_fwd64_kernel(FlashArgs a) {
 // c ^ (4 (r & 3) | ((r >> 2) & 3)) (16 distinct chunk quads for the b128 lane groups, 4 distinct bank quads
 // for the 4 rows of a transposed read); the V image uses it too (row reads only).  It also computes delta = rowsum(dO O) (attn_delta_kernel's job)
 // from the dO fragments it holds, and runs before the dK/dV kernel, which reads it.  Same arithmetic as
-// attn_bwd_dq256_kernel (P rounded to bf16 before the product, as the dK/dV kernel does).
+// the generic attn_bwd_dq_kernel (P rounded to bf16 before the product, as the dK/dV kernel does).
 PTK_DEV int swz_dual(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
 __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a) {
@@ -1789,247 +1481,6 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
   FA_STAMPS_WRITE(1, t_hi - t_lo);
 }
 
-// ---------------------------------------------------------------- dQ, head_dim 256
-// The forward's structure (attn_fwd256_kernel) applied to the dQ pass: 8 waves x 16 query rows, K and V
-// tiles of 32 keys by buffer_load ... lds into separate 4-slot rings (K read by rows for S and transposed
-// for dQ, so its image uses the dual-use swizzle), the loop unrolled by the ring depth, per-tile key masks,
-// late waves one phase behind.  Per tile and wave: S^T = K Q^T, dP^T = V dO^T, P = exp(S scale - LSE),
-// dS = P (dP - delta), dQ^T += K^T dS^T, as attn_bwd_dq_kernel.  It also computes delta = rowsum(dO O)
-// (attn_delta_kernel's job) from the dO fragments it holds anyway, and runs before the dK/dV kernel.
-__global__ void __launch_bounds__(512, 1) attn_bwd_dq256_kernel(FlashBwdArgs a) {
-  constexpr int D = 256, KT = 32, KS = 8, DS = 16, NB = 4;
-  constexpr int TILE = KT * D * 2;
-  __shared__ __attribute__((aligned(16))) char smem[2 * NB * TILE + FA_MAXT * 4];
-  char* const kring = smem;
-  char* const vring = smem + NB * TILE;
-  uint32_t* const kmask_s = reinterpret_cast<uint32_t*>(smem + 2 * NB * TILE);
-
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int g = lane >> 4, c16 = lane & 15;
-  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
-  const long z = blockIdx.x % nz;
-  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;
-  const bf16_t* K = a.K + z * (long)a.nkeys * D;
-  const bf16_t* V = a.V + z * (long)a.nkeys * D;
-  const long b = z / a.zdiv;
-  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
-  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
-  int k_hi = a.nkeys, k_lo = 0;
-  if (a.causal) {
-    k_hi = min(k_hi, pos_hi + 1);
-    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
-  }
-  const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
-
-  for (int tt = wave; tt < t_hi; tt += 8) {
-    const int key = tt * KT + (lane & 31);
-    const bool ok = key < a.nkeys && (!kvl || kvl[min(key, a.nkeys - 1)] != 0);
-    const uint64_t m = __ballot(ok);
-    if (lane == 0) kmask_s[tt] = (uint32_t)m;
-  }
-
-  const int wrow0 = r0 + wave * 16;
-  const int qrow = wrow0 + c16;
-  const int qrow_c = min(qrow, a.rows - 1);
-  const long qoff = (z * a.rows + qrow_c) * (long)D + 8 * g;
-  bf16x8_t qf[KS], df[KS];
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    qf[ks] = *reinterpret_cast<const bf16x8_t*>(a.Q + qoff + 32 * ks);
-    df[ks] = *reinterpret_cast<const bf16x8_t*>(a.dO + qoff + 32 * ks);
-  }
-  const float L2E = 1.4426950408889634f;
-  float lse2 = a.lse[z * a.rows + qrow_c] * L2E;
-  // delta = rowsum(dO * O) for the wave's rows (this kernel runs before the dK/dV kernel, which reads it):
-  // the lane's 64 elements of its row, then the row's 4 lane groups
-  float dlt;
-  {
-    const long z0 = z / a.zin, z1 = z - z0 * a.zin;
-    const bf16_t* orow = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow_c) * a.ldo + 8 * g;
-    bf16x8_t of[KS];
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks) of[ks] = *reinterpret_cast<const bf16x8_t*>(orow + 32 * ks);
-    float acc0 = 0.f;
-#pragma unroll
-    for (int ks = 0; ks < KS; ++ks)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) acc0 += bf2f((bf16_t)of[ks][e]) * bf2f((bf16_t)df[ks][e]);
-    dlt = xor32_sum(xor16_sum(acc0));
-    if (g == 0 && qrow < a.rows) a.delta[z * a.rows + qrow] = dlt;
-  }
-#pragma unroll
-  for (int ks = 0; ks < KS; ++ks) {
-    fa_pin(qf[ks]);
-    fa_pin(df[ks]);
-  }
-  fa_pin(lse2);
-  fa_pin(dlt);
-  __syncthreads();   // key masks published (no LDS-DMA in flight yet)
-  const int qpos = qrow_c / a.qdiv;
-  const float sl2 = a.scale * L2E;
-  const int causal = a.causal != 0, nowin = a.window <= 0;
-  const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
-  const int wpos_hi = min(wrow0 + 15, a.rows - 1) / a.qdiv;
-  const bool idle = wrow0 >= a.rows;
-
-  const fa_u32x4_t rsk = fa_rsrc(K, (uint32_t)((long)a.nkeys * D * 2));
-  const fa_u32x4_t rsv = fa_rsrc(V, (uint32_t)((long)a.nkeys * D * 2));
-  uint32_t dof[2];
-#pragma unroll
-  for (int j = 0; j < 2; ++j) {
-    const int row = (wave * 2 + j) * 2 + (lane >> 5);
-    dof[j] = (uint32_t)row * (D * 2) + 16u * ((lane & 31) ^ swz_rt(row));
-  }
-  const uint32_t lds_k = __builtin_amdgcn_readfirstlane(fa_lds_addr(kring) + wave * 2048);
-  const uint32_t lds_v = __builtin_amdgcn_readfirstlane(fa_lds_addr(vring) + wave * 2048);
-  auto stage = [&](int bb, int t) __attribute__((always_inline)) {
-    const uint32_t so = __builtin_amdgcn_readfirstlane((uint32_t)t * (uint32_t)(KT * D * 2));
-    FA_DMA(dof[0], so, rsk, lds_k + bb * TILE);
-    FA_DMA(dof[1], so, rsk, lds_k + bb * TILE + 1024);
-    FA_DMA(dof[0], so, rsv, lds_v + bb * TILE);
-    FA_DMA(dof[1], so, rsv, lds_v + bb * TILE + 1024);
-  };
-  // row reads (K for S, V for dP): rows 16ms + c16, chunk (4ks + g) ^ 2(row & 7): ks bit 2, ms untouched;
-  // transposed K reads (dQ): rows 16hh + 4g + q4, chunk (2ds + (p4 >> 1)) ^ 2(row & 7): ds bit 3, hh untouched
-  int roff[4], toff[8];
-  const char* vrow_base;
-  {
-    const int q4 = c16 >> 2, p4 = c16 & 3, trow = 4 * g + q4;
-#pragma unroll
-    for (int i = 0; i < 4; ++i) roff[i] = c16 * (D * 2) + ((i * 4 + g) ^ swz_rt(c16)) * 16;
-#pragma unroll
-    for (int i = 0; i < 8; ++i) toff[i] = trow * (D * 2) + ((2 * i + (p4 >> 1)) ^ swz_rt(trow)) * 16 + 8 * (p4 & 1);
-    vrow_base = (const char*)(fa_lptr_t)(uintptr_t)__builtin_amdgcn_readfirstlane(0) + fa_lds_addr(vring);
-  }
-
-  f32x4_t acc[DS];
-#pragma unroll
-  for (int i = 0; i < DS; ++i) acc[i] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-
-  auto sync = [&](int bb, int t) __attribute__((always_inline)) {
-    if (t + 1 < t_hi) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    if (t + 2 < t_hi) stage((bb + 2) % NB, t + 2);
-  };
-  // S^T, dP^T for tile t, then dS^T (bf16, k order 4g+j / 16+4g+j as the dQ product's B operand)
-  auto sdp = [&](auto BUF, int t, bf16x8_t& dsf) __attribute__((always_inline)) {
-    constexpr int bb = decltype(BUF)::value;
-    const char* kb = kring + bb * TILE;
-    const char* vb = vrow_base + bb * TILE;
-    f32x4_t s[2], dp[2];
-#pragma unroll
-    for (int ms = 0; ms < 2; ++ms) {
-      s[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-      dp[ms] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int off = roff[ks & 3] + (ks >> 2) * 256 + ms * 16 * (D * 2);
-        const bf16x8_t kf = *reinterpret_cast<const bf16x8_t*>(kb + off);
-        const bf16x8_t vf = *reinterpret_cast<const bf16x8_t*>(vb + off);
-        s[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kf, qf[ks], s[ms], 0, 0, 0);
-        dp[ms] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(vf, df[ks], dp[ms], 0, 0, 0);
-      }
-    }
-    const uint32_t km = kmask_s[t];
-    const bool interior = km == 0xffffffffu && (!causal || t * KT + KT - 1 <= wpos_lo) &&
-                          (nowin || t * KT > wpos_hi - a.window);
-    if (interior) {
-#pragma unroll
-      for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float p = __builtin_amdgcn_exp2f(fmaf(s[ms][j], sl2, -lse2));
-          dsf[ms * 4 + j] = (short)f2bf(bfround(p) * (dp[ms][j] - dlt));
-        }
-    } else {
-      uint32_t vis = km;
-      if (causal) {
-        const int d = qpos - t * KT;
-        vis &= d >= 31 ? 0xffffffffu : (d < 0 ? 0u : (2u << d) - 1u);
-        if (!nowin) {
-          const int e = d - a.window;
-          vis &= e < 0 ? 0xffffffffu : (e >= 31 ? 0u : ~((2u << e) - 1u));
-        }
-      }
-#pragma unroll
-      for (int ms = 0; ms < 2; ++ms)
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int kl = ms * 16 + 4 * g + j;
-          const float p = __builtin_amdgcn_exp2f(((vis >> kl) & 1u) ? fmaf(s[ms][j], sl2, -lse2) : -INFINITY);
-          dsf[ms * 4 + j] = (short)f2bf(bfround(p) * (dp[ms][j] - dlt));
-        }
-    }
-  };
-  auto dq = [&](auto BUF, const bf16x8_t& dsf) __attribute__((always_inline)) {
-    constexpr int bb = decltype(BUF)::value;
-    const char* kb = kring + bb * TILE;
-#pragma unroll
-    for (int ds = 0; ds < DS; ++ds) {
-      bf16x8_t kt;
-#pragma unroll
-      for (int hh = 0; hh < 2; ++hh) {
-        const char* addr = kb + toff[ds & 7] + (ds >> 3) * 256 + hh * 16 * (D * 2);
-        const s16x4_t r = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(addr));
-        kt[4 * hh + 0] = r[0]; kt[4 * hh + 1] = r[1]; kt[4 * hh + 2] = r[2]; kt[4 * hh + 3] = r[3];
-      }
-      acc[ds] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(kt, dsf, acc[ds], 0, 0, 0);
-    }
-  };
-  auto early = [&](auto BUF, int t) __attribute__((always_inline)) {
-    constexpr int bb = decltype(BUF)::value;
-    sync(bb, t);
-    if (idle) return;
-    bf16x8_t dsf;
-    sdp(BUF, t, dsf);
-    dq(BUF, dsf);
-  };
-  bf16x8_t dprev;
-  auto late = [&](auto BUF, int t) __attribute__((always_inline)) {
-    constexpr int bb = decltype(BUF)::value;
-    if (t < t_hi) sync(bb, t);
-    if (idle) return;
-    if (t > t_lo) dq(fa_ic<(bb + NB - 1) % NB>{}, dprev);
-    if (t == t_hi) return;
-    sdp(BUF, t, dprev);
-  };
-  if (t_lo < t_hi) stage(0, t_lo);
-  if (t_lo + 1 < t_hi) stage(1, t_lo + 1);
-  if (wave < 4) {
-    for (int t = t_lo; t < t_hi;) {
-      early(fa_ic<0>{}, t);
-      if (++t >= t_hi) break;
-      early(fa_ic<1>{}, t);
-      if (++t >= t_hi) break;
-      early(fa_ic<2>{}, t);
-      if (++t >= t_hi) break;
-      early(fa_ic<3>{}, t);
-      ++t;
-    }
-  } else {
-    for (int t = t_lo; t <= t_hi;) {
-      late(fa_ic<0>{}, t);
-      if (++t > t_hi) break;
-      late(fa_ic<1>{}, t);
-      if (++t > t_hi) break;
-      late(fa_ic<2>{}, t);
-      if (++t > t_hi) break;
-      late(fa_ic<3>{}, t);
-      ++t;
-    }
-  }
-  if (qrow >= a.rows) return;
-  bf16_t* op = a.dQ + (z * a.rows + qrow) * (long)D + 4 * g;
-#pragma unroll
-  for (int ds = 0; ds < DS; ++ds) {
-    u16x4_t u;
-    u[0] = f2bf(acc[ds][0] * a.scale); u[1] = f2bf(acc[ds][1] * a.scale);
-    u[2] = f2bf(acc[ds][2] * a.scale); u[3] = f2bf(acc[ds][3] * a.scale);
-    *reinterpret_cast<u16x4_t*>(op + 16 * ds) = u;
-  }
-}
 
 template <int D>
 __global__ void __launch_bounds__(256, 1) attn_bwd_dkv_kernel(FlashBwdArgs a) {
@@ -2872,9 +2323,7 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs*
       // the dQ kernel computes delta and runs first; past the 4096-key mask table the generic dQ kernel runs
       // after a separate delta pass and the dK/dV kernel
       const bool dq_new = (a.nkeys + 31) / 32 <= FA_MAXT;
-      static const bool dq_old = [] { const char* e = getenv("PTK_ATTN_DQ_OLD"); return e && e[0] == '1'; }();
-      if (dq_new && dq_old) hipLaunchKernelGGL(attn_bwd_dq256_kernel, gq, dim3(512), 0, st, b);
-      else if (dq_new) hipLaunchKernelGGL(attn_bwd_dq256w_kernel, gq, dim3(256), 0, st, b);
+      if (dq_new) hipLaunchKernelGGL(attn_bwd_dq256w_kernel, gq, dim3(256), 0, st, b);
       else hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
       // 32 keys per wave (one wave per SIMD) measured 209 us vs 252 us for 16 keys per wave (two per
       // SIMD, which spills the precomputed transposed-read addresses) at cfg2
@@ -2918,11 +2367,8 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
     // quantise worse than 704 (110 vs 78 us per layer), and it spills
     case 256: {
       // the generic kernel past the 4096-key mask table
-      static const bool old = [] { const char* e = getenv("PTK_ATTN_FWD_OLD"); return e && e[0] == '1'; }();
       if ((a.nkeys + 31) / 32 > FA_MAXT || (long)a.nkeys * a.ldk * 2 > 0x7fffffffL)
         hipLaunchKernelGGL((attn_fwd_kernel<256, 1>), grid, dim3(512), 0, st, a);
-      else if (old)
-        hipLaunchKernelGGL(attn_fwd256_kernel, grid, dim3(512), 0, st, a);
       else
         hipLaunchKernelGGL(attn_fwd256w_kernel, grid, dim3(256), 0, st, a);
       break;

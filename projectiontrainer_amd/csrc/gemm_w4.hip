@@ -297,7 +297,8 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 #define W4_DSREAD(DST, ADDR, OFF) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(DST) : "v"(ADDR), "i"(OFF))
 // one 1-KiB LDS-DMA piece: M0 = wave-uniform LDS destination.  hipcc emits no M0 use of its own in
 // these kernels (no LDS-DMA builtins, gfx950 ds_* do not read M0), so M0 is not saved / restored.
-// PTK_W4_DMA_POL (diagnostic builds, make w4pol): cache-policy bits on the pieces (1 sc1, 2 sc0, 3 nt)
+// PTK_W4_DMA_POL (diagnostic builds, make w4pol): cache-policy bits on the pieces (1 sc1, 2 sc0, 3 nt);
+// measured (tools/gemm_ab.sh, r03): sc1 / sc0 within +-1 % of none on every step shape, nt 2x slower
 #if PTK_W4_DMA_POL == 1
 #define W4_POL " sc1"
 #elif PTK_W4_DMA_POL == 2

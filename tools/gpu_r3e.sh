@@ -8,5 +8,5 @@ grep -E "passed|failed" gpurun_out/r3e_attn.log | tail -1; grep FAILED gpurun_ou
 [ $rc -eq 0 ] || exit $rc
 for i in 1 2; do
   echo "new"; timeout -k 10 60 python tools/attn_bench.py --what fwd,bwd 2>&1 | grep kernel || exit 1
-  echo "old"; PTK_ATTN_FWD_OLD=1 PTK_ATTN_DQ_OLD=1 timeout -k 10 60 python tools/attn_bench.py --what fwd,bwd 2>&1 | grep kernel || exit 1
+
 done
