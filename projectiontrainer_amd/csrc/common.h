@@ -134,6 +134,10 @@ PTK_DEV void gelu_tanh_fg2(f32x2_t x, f32x2_t& f, f32x2_t& df) {
 }
 // bf16 round trip of two lanes: one v_cvt_pk_bf16_f32 and two unpacks
 typedef __attribute__((ext_vector_type(2))) __bf16 bf16x2_t;
+// IEEE 754-2019 maximum (NaN-propagating): v_maximum3_f32 / v_maximum_f32 on gfx950, without the operand
+// canonicalisation fmaxf (maxNum) costs in IEEE mode
+PTK_DEV float fmaxe(float a, float b) { return __builtin_elementwise_maximum(a, b); }
+PTK_DEV float fmax3e(float a, float b, float c) { return fmaxe(fmaxe(a, b), c); }
 PTK_DEV f32x2_t bfround2(f32x2_t v) {
   const uint32_t u = __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t));
   return f32x2_t{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};

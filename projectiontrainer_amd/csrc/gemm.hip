@@ -122,13 +122,63 @@ PTK_DEV void epilogue(const GemmArgs& p, char* smem, int wave, int lane, f32x4_t
     // 8 lanes per row, each 8 columns (16-B stores); 8 rows per pass
     const int rr = lane >> 3, c8 = (lane & 7) * 8;
     const long c = col0 + c8;
+    if (ACT == ACT_NONE && p.row_stats) {
+      // softmax statistics (max, sum exp(x - max)) of each row's 64 columns, from the bf16-rounded values the
+      // logits store holds.  This runs with the MFMAs idle (one workgroup per CU, lock-step epilogue), so it is
+      // written for VALU issue slots: NaN-propagating v_maximum3 (no operand canonicalisation), packed f32 FMAs
+      // and adds, the 8 rows' max all-reduced over the row's 8 lanes by DPP, the 8 rows' sums reduce-scattered
+      // (partners 7 - j, j ^ 1, j ^ 2: 7 DPP adds instead of 24), after which lane j holds the row
+      // 4 (j >= 4) + 2 (j & 1) + ((j >> 1) & 1) of its row group and stores that row's pair: one 8-B store per lane.
+      constexpr float L2E = 1.4426950408889634f;
+      const f32x2_t l2e = {L2E, L2E};
+      float mx[8], sm[8];
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const float* tr = T + (it * 8 + rr) * EPI_LD + c8;
+        const float4 v0 = *reinterpret_cast<const float4*>(tr);
+        const float4 v1 = *reinterpret_cast<const float4*>(tr + 4);
+        const f32x2_t x0 = bfround2(f32x2_t{v0.x, v0.y}), x1 = bfround2(f32x2_t{v0.z, v0.w});
+        const f32x2_t x2 = bfround2(f32x2_t{v1.x, v1.y}), x3 = bfround2(f32x2_t{v1.z, v1.w});
+        float m = fmax3e(fmax3e(x0[0], x0[1], x1[0]), fmax3e(x1[1], x2[0], x2[1]), fmaxe(x3[0], x3[1]));
+        m = fmaxe(m, dpp<0xB1>(m));
+        m = fmaxe(m, dpp<0x4E>(m));
+        m = fmaxe(m, dpp<0x141>(m));
+        const float nm = -m * L2E;
+        const f32x2_t nm2 = {nm, nm};
+        const f32x2_t a0 = x0 * l2e + nm2, a1 = x1 * l2e + nm2, a2 = x2 * l2e + nm2, a3 = x3 * l2e + nm2;
+        const f32x2_t e0 = {__builtin_amdgcn_exp2f(a0[0]), __builtin_amdgcn_exp2f(a0[1])};
+        const f32x2_t e1 = {__builtin_amdgcn_exp2f(a1[0]), __builtin_amdgcn_exp2f(a1[1])};
+        const f32x2_t e2 = {__builtin_amdgcn_exp2f(a2[0]), __builtin_amdgcn_exp2f(a2[1])};
+        const f32x2_t e3 = {__builtin_amdgcn_exp2f(a3[0]), __builtin_amdgcn_exp2f(a3[1])};
+        const f32x2_t s2 = (e0 + e1) + (e2 + e3);
+        mx[it] = m;
+        sm[it] = s2[0] + s2[1];
+      }
+      const int j = lane & 7;
+      const bool b1 = j >= 4, b2 = j & 1, b3 = (j >> 1) & 1;
+      float s4[4], m4[4], s2[2], m2[2];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        s4[i] = (b1 ? sm[i + 4] : sm[i]) + dpp<0x141>(b1 ? sm[i] : sm[i + 4]);
+        m4[i] = b1 ? mx[i + 4] : mx[i];
+      }
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        s2[i] = (b2 ? s4[i + 2] : s4[i]) + dpp<0xB1>(b2 ? s4[i] : s4[i + 2]);
+        m2[i] = b2 ? m4[i + 2] : m4[i];
+      }
+      const float ss = (b3 ? s2[1] : s2[0]) + dpp<0x4E>(b3 ? s2[0] : s2[1]);
+      const float ms = b3 ? m2[1] : m2[0];
+      const long rs = row0 + (4 * b1 + 2 * b2 + b3) * 8 + rr;
+      if (rs < p.M) *reinterpret_cast<float2*>(p.row_stats + rs * p.ld_stats + 2 * (col0 >> 6)) = make_float2(ms, ss);
+    }
 #pragma unroll
     for (int it = 0; it < 8; ++it) {
       const int lr = it * 8 + rr;
       const long r = row0 + lr;
-      if (r >= p.M) continue;
       const float4 v0 = *reinterpret_cast<const float4*>(T + lr * EPI_LD + c8);
       const float4 v1 = *reinterpret_cast<const float4*>(T + lr * EPI_LD + c8 + 4);
+      if (r >= p.M) continue;
       epi_vec8_bf16<ACT>(p, Cz, r, c, v0, v1);
     }
   } else {

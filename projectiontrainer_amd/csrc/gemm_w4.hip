@@ -539,6 +539,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 // N % 8 == 0, byte extents of A and B below 2^31 (32-bit buffer offsets)
 bool w4_supported(const GemmArgs& a, int act, int out) {
   if (a.N % 8 || a.K % W4_KT) return false;
+  if (a.row_stats) return false;   // the softmax-statistics epilogue lives in gemm.hip's epilogue only
   if (a.resid16 || a.bf16_linear) return false;
   if ((a.ldc % 8) || (a.resid && a.ld_resid % 4) || (a.rowadd && a.ld_rowadd % 4)) return false;
   if ((a.aux || a.aux2) && a.ld_aux % 8) return false;

@@ -150,6 +150,31 @@ int launch_build_llm_inputs(const bf16_t* embed, const int64_t* ids, int B, int 
 }
 
 // ---------------------------------------------------------------- cross entropy
+// dlogits = (softmax - onehot) * g in place over one row, 256 threads x 8 columns per 16-B access.  The
+// loads of a group of 8 accesses go out before its stores (the compiler cannot move a load of the row above
+// a store to it), so each thread keeps 8 loads in flight instead of 1.
+PTK_DEV void ce_write_dlogits(bf16_t* __restrict__ lr, int V, float lse, long tgt, float g) {
+  auto one = [&](int c, const u16x8_t& u) {
+    u16x8_t o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float p = __expf(bf2f(u[e]) - lse);
+      if (c + e == tgt) p -= 1.f;
+      o[e] = f2bf(p * g);
+    }
+    *reinterpret_cast<u16x8_t*>(lr + c) = o;
+  };
+  int c = threadIdx.x * 8;
+  for (; c + 7 * 2048 < V; c += 8 * 2048) {
+    u16x8_t u[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j) u[j] = *reinterpret_cast<const u16x8_t*>(lr + c + j * 2048);
+#pragma unroll
+    for (int j = 0; j < 8; ++j) one(c + j * 2048, u[j]);
+  }
+  for (; c < V; c += 2048) one(c, *reinterpret_cast<const u16x8_t*>(lr + c));
+}
+
 // ForCausalLMLoss (TF/loss/loss_utils.py:49-67): logits (bf16, as the reference's
 // autocast lm_head produces) upcast to fp32, CE mean over valid targets.
 // One block per row: pass 1 online max/sum-exp, pass 2 writes
@@ -180,18 +205,44 @@ __global__ void __launch_bounds__(256) ce_kernel(bf16_t* __restrict__ logits, lo
   const bool valid = tgt >= 0;
   if (threadIdx.x == 0) row_loss[r] = valid ? lse - bf2f(lr[tgt]) : 0.f;
   __syncthreads();   // target logit read before it is overwritten
-  const float g = valid ? gscale[0] : 0.f;
-  for (int c = threadIdx.x * 8; c < V; c += 2048) {
-    u16x8_t u = *reinterpret_cast<const u16x8_t*>(lr + c);
-    u16x8_t o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      float p = __expf(bf2f(u[e]) - lse);
-      if (c + e == tgt) p -= 1.f;
-      o[e] = f2bf(p * g);
-    }
-    *reinterpret_cast<u16x8_t*>(lr + c) = o;
+  ce_write_dlogits(lr, V, lse, tgt, valid ? gscale[0] : 0.f);
+}
+// The same loss and d(logits) from the lm_head GEMM's softmax statistics (GemmArgs::row_stats: per row and
+// 64-column chunk the max and sum exp(x - max) of the bf16 logits): the row's log-sum-exp is combined from
+// its V / 64 chunk statistics, so the logits are read once (and d(logits) written in place) instead of
+// twice.  Same arithmetic per element as ce_kernel; the sum over the row is taken in a different order.
+__global__ void __launch_bounds__(256) ce_stats_kernel(bf16_t* __restrict__ logits, long ld, int V,
+                                                       const float* __restrict__ stats, long ld_stats,
+                                                       const int64_t* __restrict__ targets,
+                                                       float* __restrict__ row_loss, const float* __restrict__ gscale) {
+  __shared__ float red[8];
+  const long r = blockIdx.x;
+  bf16_t* lr = logits + r * ld;
+  const float* st = stats + r * ld_stats;
+  const int nch = V >> 6;
+  const long tgt = targets[r];
+  float m = -INFINITY, s = 0.f;
+  for (int k = threadIdx.x; k < nch; k += 256) {
+    const float2 ms = *reinterpret_cast<const float2*>(st + 2 * k);
+    const float mn = fmaxf(m, ms.x);
+    s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (ms.x == -INFINITY ? 0.f : ms.y * __expf(ms.x - mn));
+    m = mn;
   }
+  const float M = block_max<256>(m, red);
+  const float Ssum = block_sum<256>(m == -INFINITY ? 0.f : s * __expf(m - M), red);
+  const float lse = M + __logf(Ssum);
+  const bool valid = tgt >= 0;
+  if (threadIdx.x == 0) row_loss[r] = valid ? lse - bf2f(lr[tgt]) : 0.f;
+  __syncthreads();   // target logit read before it is overwritten
+  ce_write_dlogits(lr, V, lse, tgt, valid ? gscale[0] : 0.f);
+}
+int launch_ce_stats_fwd_bwd(bf16_t* logits, long ld, int R, int V, const float* stats, long ld_stats,
+                            const int64_t* targets, float* row_loss, const float* gscale, hipStream_t st) {
+  if (V % 64 || ld % 8) return set_error("ce_stats: vocab %% 64");
+  if (R <= 0) return 0;
+  hipLaunchKernelGGL(ce_stats_kernel, dim3(R), dim3(256), 0, st, logits, ld, V, stats, ld_stats, targets, row_loss,
+                     gscale);
+  RET_OK("ce_stats");
 }
 int launch_ce_fwd_bwd(bf16_t* logits, long ld, int R, int V, const int64_t* targets, float* row_loss,
                       const float* gscale, hipStream_t st) {

@@ -72,6 +72,13 @@ static bool dkv_reduce_split() {
   return v != 0;
 }
 
+// PTK_CE_TWO_PASS=1: the cross-entropy pass computes its own row statistics (two reads of the logits) instead
+// of taking them from the lm_head GEMM's epilogue (A/B; tests/test_stage1_gpu.py checks both agree)
+static bool ce_two_pass() {
+  static const int v = [] { const char* e = getenv("PTK_CE_TWO_PASS"); return e && e[0] == '1' ? 1 : 0; }();
+  return v != 0;
+}
+
 GemmArgs gemm(const void* A, long lda, const void* B, long ldb, void* C, long ldc, int M, int N, int K) {
   GemmArgs g;
   g.A = (const bf16_t*)A; g.B = (const bf16_t*)B; g.C = C;
@@ -113,6 +120,7 @@ struct GemmaWs {
   bf16_t *P, *xn, *O, *h, *Vt, *Kt, *Qt, *dqkv, *dgu, *dao, *dO, *dS, *dST, *PT, *dOT, *dQ, *dK, *dV, *xf, *logits;
   bf16_t* dtmp;             // bf16 dX of the q|k|v / gate|up projections (see the workspace layout)
   float *S, *rstd_f, *row_loss, *dxf, *dxf_part, *count, *gscale, *delta;
+  float* ce_stats = nullptr;   // the lm_head epilogue's softmax statistics [R][V / 64] (float2)
   float* dkv_part;          // split-query dK/dV partials of the attention backward
   size_t dkv_part_bytes;
   int32_t* key_valid;
@@ -193,6 +201,7 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
   w.xf = bp.take<bf16_t>(R * H);
   w.rstd_f = bp.take<float>(R);
   w.logits = bp.take<bf16_t>(R * V);
+  if (V % 64 == 0) w.ce_stats = bp.take<float>(R * (V / 64) * 2);
   w.row_loss = bp.take<float>(R);
   w.dxf = bp.take<float>(R * H);
   w.dxf_part = bp.take<float>((long)(LM_SPLITK + 1) * R * H);   // + one slot for a vocab remainder
@@ -452,9 +461,21 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
 
   // ---------------- loss (text-predicting rows only)
   CK(launch_rmsnorm_fwd(w.x[nl], H, lossmap, wt->final_norm, w.xf, w.rstd_f, R, H, eps, st));
-  CK(launch_gemm(gemm(w.xf, H, wt->embed, H, w.logits, V, R, V, H), ACT_NONE, OUT_BF16, 1, st));
-  CK(launch_count_valid(bt->labels, R, bt->loss_scale, w.gscale, w.count, st));
-  CK(launch_ce_fwd_bwd(w.logits, V, R, V, bt->labels, w.row_loss, w.gscale, st));
+  {
+    // lm_head: logits (bf16) plus, from the GEMM epilogue, each row's softmax statistics per 64 columns, so
+    // the cross-entropy pass reads the 2 GB of logits once (loss_utils.py:49-67)
+    GemmArgs g = gemm(w.xf, H, wt->embed, H, w.logits, V, R, V, H);
+    if (w.ce_stats && !ce_two_pass()) {
+      g.row_stats = w.ce_stats;
+      g.ld_stats = (V / 64) * 2;
+    }
+    CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
+    CK(launch_count_valid(bt->labels, R, bt->loss_scale, w.gscale, w.count, st));
+    if (g.row_stats)
+      CK(launch_ce_stats_fwd_bwd(w.logits, V, R, V, w.ce_stats, g.ld_stats, bt->labels, w.row_loss, w.gscale, st));
+    else
+      CK(launch_ce_fwd_bwd(w.logits, V, R, V, bt->labels, w.row_loss, w.gscale, st));
+  }
   CK(launch_loss_reduce(w.row_loss, R, w.count, bt->loss, st));
   if (fwd_only) return 0;   // validation loss (no_grad): the CE pass's d(logits) is left unused
   // tied lm_head weight grad: dE += dlogits^T . xf (the logits rows outside the loss rows have zero grad)

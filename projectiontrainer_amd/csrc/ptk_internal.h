@@ -42,6 +42,11 @@ struct GemmArgs {
   long ld_aux_in = 0;
   RowMap amap{0, 0, 0, 0};                       // A row remap (gather)
   RowMap cmap{0, 0, 0, 0};                       // C row remap (scatter / skip)
+  // optional (256x256 8-wave kernel, ACT_NONE, bf16 out, N % 64 == 0): per (row, 64-column chunk) the max and
+  // the sum of exp(x - max) of the bf16-rounded outputs, float2 at row_stats[r * ld_stats + 2 * (c / 64)]
+  // (the lm_head's softmax statistics: the cross-entropy pass then reads the logits once)
+  float* row_stats = nullptr;
+  long ld_stats = 0;
 };
 
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
@@ -222,6 +227,8 @@ int launch_build_llm_inputs(const bf16_t* embed, const int64_t* ids, int B, int 
                             hipStream_t st);
 int launch_ce_fwd_bwd(bf16_t* logits, long ld, int R, int V, const int64_t* targets, float* row_loss,
                       const float* gscale, hipStream_t st);
+int launch_ce_stats_fwd_bwd(bf16_t* logits, long ld, int R, int V, const float* stats, long ld_stats,
+                            const int64_t* targets, float* row_loss, const float* gscale, hipStream_t st);
 int launch_count_valid(const int64_t* labels, int n, float loss_scale, float* gscale, float* count,
                        hipStream_t st);
 int launch_loss_reduce(const float* row_loss, int R, const float* count, float* loss, hipStream_t st);

@@ -1,6 +1,7 @@
 """One Stage-1 forward/backward at architecture-true Gemma3-1B dims (bs 2, S 703, 2 layers: one sliding-window and
 one full-attention layer, so both dK/dV split plans run), results
-saved to argv[1]. Run by tests/test_dkv_fused_gpu.py under PTK_DKV_REDUCE_SPLIT=0/1 (the switch is read
+saved to argv[1]. Run by tests/test_dkv_fused_gpu.py under PTK_DKV_REDUCE_SPLIT=0/1 and tests/test_ce_stats_gpu.py
+under PTK_CE_TWO_PASS=0/1 (each switch is read
 once per process, so each setting needs its own process)."""
 import os
 import sys
