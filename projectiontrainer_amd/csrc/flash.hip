@@ -1214,6 +1214,9 @@ __global__ void __launch_bounds__(512, 2) attn_fwd64_kernel(FlashArgs a) {
 // the generic attn_bwd_dq_kernel (P rounded to bf16 before the product, as the dK/dV kernel does).
 PTK_DEV int swz_dual(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 
+#ifndef DQ_RA
+#define DQ_RA 2   // dQ kernel: LDS fragment reads issued this many MFMAs ahead of their use
+#endif
 __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a) {
   constexpr int D = 256, KT = 32, NB = 4;
   constexpr int TILE = KT * D * 2;
@@ -1363,20 +1366,21 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
   auto phase_a = [&](auto MM, auto DSC, uint32_t so, f32x16_t& s_n, f32x16_t& p_n, const f32x16_t& s,
                      const f32x16_t& dp, uint32_t vis, bf16x8_t (&dsf)[2]) __attribute__((always_inline)) {
     constexpr bool mm = decltype(MM)::value, dsc = decltype(DSC)::value;
-    bf16x8_t kf[3], vf[3];
+    constexpr int RA = DQ_RA, RN = DQ_RA + 1;   // K / V row reads RA k-steps ahead of their MFMAs
+    bf16x8_t kf[RN], vf[RN];
     if (mm) {
-      kf[0] = rload(0, so, 0); vf[0] = rload(1, so, 0);
-      kf[1] = rload(0, so, 1); vf[1] = rload(1, so, 1);
+#pragma unroll
+      for (int i = 0; i < RA; ++i) { kf[i] = rload(0, so, i); vf[i] = rload(1, so, i); }
     }
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) {
       if (mm) {
-        if (ks + 2 < 16) {
-          kf[(ks + 2) % 3] = rload(0, so, ks + 2);
-          vf[(ks + 2) % 3] = rload(1, so, ks + 2);
+        if (ks + RA < 16) {
+          kf[(ks + RA) % RN] = rload(0, so, ks + RA);
+          vf[(ks + RA) % RN] = rload(1, so, ks + RA);
         }
-        s_n = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks % 3], qf[ks], ks == 0 ? (f32x16_t){} : s_n, 0, 0, 0);
-        p_n = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks % 3], df[ks], ks == 0 ? (f32x16_t){} : p_n, 0, 0, 0);
+        s_n = __builtin_amdgcn_mfma_f32_32x32x16_bf16(kf[ks % RN], qf[ks], ks == 0 ? (f32x16_t){} : s_n, 0, 0, 0);
+        p_n = __builtin_amdgcn_mfma_f32_32x32x16_bf16(vf[ks % RN], df[ks], ks == 0 ? (f32x16_t){} : p_n, 0, 0, 0);
       }
       if (dsc && ks < 8) {
         const int r = 2 * ks;
@@ -1400,16 +1404,17 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
   auto phase_b = [&](auto ST, uint32_t so, const bf16x8_t (&dsf)[2], int bb_st, int t_st)
       __attribute__((always_inline)) {
     constexpr bool st = decltype(ST)::value;
-    bf16x8_t tf[3];
-    tf[0] = tload(so, 0, 0);
-    tf[1] = tload(so, 0, 1);
+    constexpr int RA = DQ_RA, RN = DQ_RA + 1;
+    bf16x8_t tf[RN];
+#pragma unroll
+    for (int i = 0; i < RA; ++i) tf[i] = tload(so, i >> 3, i & 7);
     uint32_t sso = 0;
     if (st) sso = __builtin_amdgcn_readfirstlane((uint32_t)t_st * tile_bytes);
 #pragma unroll
     for (int i = 0; i < 16; ++i) {
       const int kk = i >> 3, db = i & 7;
-      if (i + 2 < 16) tf[(i + 2) % 3] = tload(so, (i + 2) >> 3, (i + 2) & 7);
-      acc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[i % 3], dsf[kk], acc[db], 0, 0, 0);
+      if (i + RA < 16) tf[(i + RA) % RN] = tload(so, (i + RA) >> 3, (i + RA) & 7);
+      acc[db] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(tf[i % RN], dsf[kk], acc[db], 0, 0, 0);
       if (st && (i & 1) == 0) {
         const int j = i >> 1;
         if (j < 4) FA_DMA(dk[j], sso, rsk, lds_k + bb_st * 2 * TILE + j * 1024);
@@ -1892,6 +1897,9 @@ __global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel
 // immediate); the causal / window position test by shift (query heads per kv head a power of two); a wave
 // whose 32 keys are all invisible to a chunk's rows (the causal diagonal and the window edge of the slab)
 // skips that chunk's MFMAs.
+#ifndef DKV_PD
+#define DKV_PD 2   // dK/dV kernel: LDS fragment groups read ahead of their MFMAs (0 = hipcc's own placement)
+#endif
 __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256b_kernel(FlashBwdArgs a) {
   constexpr int D = 256, KS = D / 32, DS = D / 16, KPW = 32, KG = 2, NB = 4;
   constexpr int TILE = DKV_CH * D * 2;   // 16 KiB: 32 rows of Q or dO
@@ -2030,19 +2038,31 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256b_kernel(FlashBwdArgs a
         sc[qt][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
         dp[qt][kg] = (f32x4_t){0.f, 0.f, 0.f, 0.f};
       }
+    // group i = (qt, ks): Q and dO fragments read DKV_PD groups ahead of their MFMAs (as in the dV/dK loop)
+    bf16x8_t qar[DKV_PD + 1], oar[DKV_PD + 1];
+    auto ldr = [&](int i) __attribute__((always_inline)) {
+      const int qt = i / KS, ks = i % KS;
+      const int off = roff[ks & 3] + (ks >> 2) * 256 + qt * 16 * (D * 2);
+      qar[i % (DKV_PD + 1)] = *reinterpret_cast<const bf16x8_t*>(qb + off);
+      oar[i % (DKV_PD + 1)] = *reinterpret_cast<const bf16x8_t*>(ob + off);
+    };
 #pragma unroll
-    for (int qt = 0; qt < 2; ++qt) {
+    for (int i = 0; i < DKV_PD; ++i) ldr(i);
 #pragma unroll
-      for (int ks = 0; ks < KS; ++ks) {
-        const int off = roff[ks & 3] + (ks >> 2) * 256 + qt * 16 * (D * 2);
-        const bf16x8_t qa = *reinterpret_cast<const bf16x8_t*>(qb + off);
-        const bf16x8_t oa = *reinterpret_cast<const bf16x8_t*>(ob + off);
-#pragma unroll
-        for (int kg = 0; kg < KG; ++kg) {
-          sc[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qa, kf[kg][ks], sc[qt][kg], 0, 0, 0);
-          dp[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oa, vf[kg][ks], dp[qt][kg], 0, 0, 0);
-        }
+    for (int i = 0; i < 2 * KS; ++i) {
+      const int qt = i / KS, ks = i % KS;
+      if (DKV_PD > 0) {
+        if (i + DKV_PD < 2 * KS) ldr(i + DKV_PD);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        ldr(i);
       }
+#pragma unroll
+      for (int kg = 0; kg < KG; ++kg) {
+        sc[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qar[i % (DKV_PD + 1)], kf[kg][ks], sc[qt][kg], 0, 0, 0);
+        dp[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oar[i % (DKV_PD + 1)], vf[kg][ks], dp[qt][kg], 0, 0, 0);
+      }
+      if (DKV_PD > 0) __builtin_amdgcn_sched_barrier(0);
     }
     // ---- P = exp(S*scale - LSE) (bf16), dS = P (dP - delta) (bf16); slot 4qt + j of lane group g <-> row 16qt + 4g + j
     bf16x8_t pf[KG], dsf[KG];
@@ -2076,23 +2096,38 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256b_kernel(FlashBwdArgs a
         }
       }
     }
-    // ---- dV^T += dO^T P, dK^T += Q^T dS (A operands by transposed LDS reads)
-#pragma unroll
-    for (int ds = 0; ds < DS; ++ds) {
-      bf16x8_t ot, qt_;
+    // ---- dV^T += dO^T P, dK^T += Q^T dS (A operands by transposed LDS reads), the reads of group ds + DKV_PD
+    // issued before the MFMAs of group ds (a ring of DKV_PD + 1 fragment pairs; sched_barrier keeps hipcc from
+    // sinking the reads to just before their use, which left each group's LDS latency exposed)
+    bf16x8_t otr[DKV_PD + 1], qtr[DKV_PD + 1];
+    auto ldt = [&](int ds) __attribute__((always_inline)) {
 #pragma unroll
       for (int hh = 0; hh < 2; ++hh) {
         const int off = toff[ds & 7] + (ds >> 3) * 256 + hh * 16 * (D * 2);
         const s16x4_t ro = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(ob + off));
         const s16x4_t rq = __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) s16x4_t*)(qb + off));
+        bf16x8_t& ot = otr[ds % (DKV_PD + 1)];
+        bf16x8_t& qt_ = qtr[ds % (DKV_PD + 1)];
         ot[4 * hh + 0] = ro[0]; ot[4 * hh + 1] = ro[1]; ot[4 * hh + 2] = ro[2]; ot[4 * hh + 3] = ro[3];
         qt_[4 * hh + 0] = rq[0]; qt_[4 * hh + 1] = rq[1]; qt_[4 * hh + 2] = rq[2]; qt_[4 * hh + 3] = rq[3];
       }
+    };
+#pragma unroll
+    for (int ds = 0; ds < DKV_PD; ++ds) ldt(ds);
+#pragma unroll
+    for (int ds = 0; ds < DS; ++ds) {
+      if (DKV_PD > 0) {
+        if (ds + DKV_PD < DS) ldt(ds + DKV_PD);
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        ldt(ds);
+      }
 #pragma unroll
       for (int kg = 0; kg < KG; ++kg) {
-        dv[ds][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ot, pf[kg], dv[ds][kg], 0, 0, 0);
-        dk[ds][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qt_, dsf[kg], dk[ds][kg], 0, 0, 0);
+        dv[ds][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(otr[ds % (DKV_PD + 1)], pf[kg], dv[ds][kg], 0, 0, 0);
+        dk[ds][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qtr[ds % (DKV_PD + 1)], dsf[kg], dk[ds][kg], 0, 0, 0);
       }
+      if (DKV_PD > 0) __builtin_amdgcn_sched_barrier(0);
     }
   };
 
