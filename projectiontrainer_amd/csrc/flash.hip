@@ -1897,6 +1897,9 @@ __global__ void __launch_bounds__(DKV_KEYS / KPW * 64, 1) attn_bwd_dkv256_kernel
 // immediate); the causal / window position test by shift (query heads per kv head a power of two); a wave
 // whose 32 keys are all invisible to a chunk's rows (the causal diagonal and the window edge of the slab)
 // skips that chunk's MFMAs.
+#ifndef DKV_VACC
+#define DKV_VACC 1   // dK/dV kernel: S / dP MFMAs from inline asm with VGPR accumulators (0 = builtins)
+#endif
 #ifndef DKV_PD
 #define DKV_PD 2   // dK/dV kernel: LDS fragment groups read ahead of their MFMAs (0 = hipcc's own placement)
 #endif
@@ -2059,10 +2062,31 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dkv256b_kernel(FlashBwdArgs a
       }
 #pragma unroll
       for (int kg = 0; kg < KG; ++kg) {
-        sc[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qar[i % (DKV_PD + 1)], kf[kg][ks], sc[qt][kg], 0, 0, 0);
-        dp[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oar[i % (DKV_PD + 1)], vf[kg][ks], dp[qt][kg], 0, 0, 0);
+        if (DKV_VACC) {
+          // S and dP accumulate in VGPRs (asm): with the builtin, hipcc put them in AGPRs and moved 32 of
+          // the dK/dV accumulators out to VGPRs and back around every chunk
+          if (ks == 0) {
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
+                         : "=&v"(sc[qt][kg]) : "v"(qar[i % (DKV_PD + 1)]), "v"(kf[kg][ks]));
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0"
+                         : "=&v"(dp[qt][kg]) : "v"(oar[i % (DKV_PD + 1)]), "v"(vf[kg][ks]));
+          } else {
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                         : "+v"(sc[qt][kg]) : "v"(qar[i % (DKV_PD + 1)]), "v"(kf[kg][ks]));
+            asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0"
+                         : "+v"(dp[qt][kg]) : "v"(oar[i % (DKV_PD + 1)]), "v"(vf[kg][ks]));
+          }
+        } else {
+          sc[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(qar[i % (DKV_PD + 1)], kf[kg][ks], sc[qt][kg], 0, 0, 0);
+          dp[qt][kg] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(oar[i % (DKV_PD + 1)], vf[kg][ks], dp[qt][kg], 0, 0, 0);
+        }
       }
       if (DKV_PD > 0) __builtin_amdgcn_sched_barrier(0);
+    }
+    if (DKV_VACC) {
+      // the last asm MFMAs' results -> the softmax VALU reads (10 wait states for 16x16x32; 12 here)
+      asm volatile("s_nop 7\n\ts_nop 3" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
     }
     // ---- P = exp(S*scale - LSE) (bf16), dS = P (dP - delta) (bf16); slot 4qt + j of lane group g <-> row 16qt + 4g + j
     bf16x8_t pf[KG], dsf[KG];

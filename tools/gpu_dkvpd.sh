@@ -9,8 +9,8 @@ timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method threa
 grep -E "passed|failed" gpurun_out/dkvpd_tests.log | tail -1; grep FAILED gpurun_out/dkvpd_tests.log | head
 [ $rc -eq 0 ] || exit $rc
 cd /tmp && export TMPDIR=/tmp
-for rep in 1; do
-for lib in build/libptk_dkvpd0.so new build/libptk_dkvpd3.so build/libptk_dqra3.so build/libptk_dqra4.so; do
+for rep in 1 2; do
+for lib in ${DKV_LIBS:-new}; do
   tag=$(basename $lib .so)
   l=$lib; [ "$l" = new ] && l=""
   PTK_LIB=$l timeout -k 10 200 rocprofv3 --kernel-trace -d $R/gpurun_out/dkvpd_$tag -o run -- python3 $R/bench.py --no-cpu-baseline --steps 2 --warmup 1 > $R/gpurun_out/dkvpd_$tag.log 2>&1 || { echo "prof failed $tag"; tail -3 $R/gpurun_out/dkvpd_$tag.log; exit 1; }
