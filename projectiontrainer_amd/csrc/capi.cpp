@@ -207,9 +207,10 @@ int projector_bwd_stage(const ptk_projector* p, int rows, const void* x, const v
   bf16_t* dA = (bf16_t*)w; w += align256((size_t)Rp * I * 2);
   bf16_t* xT = (bf16_t*)w; w += align256((size_t)Dv * Rp * 2);
   float* part = (float*)w;
+  const long part_floats = 64L * (I > Dl ? I : Dl);   // the colsum partials of ptk_projector_workspace_bytes
   if (stage == 0) {
     // db2 = colsum(dy); dW2 = dy^T . h  (contraction over tokens)
-    if (launch_colsum_bf16((const bf16_t*)dy, R, Dl, db2, part, st)) return -1;
+    if (launch_colsum_bf16((const bf16_t*)dy, R, Dl, db2, part, part_floats, st)) return -1;
     if (launch_transpose((const bf16_t*)dy, Dl, 0, 0, 1, dyT, Rp, 0, 0, 1, R, Dl, Rp, st)) return -1;
     if (launch_transpose((const bf16_t*)h, I, 0, 0, 1, T, Rp, 0, 0, 1, R, I, Rp, st)) return -1;
     GemmArgs g;
@@ -222,7 +223,7 @@ int projector_bwd_stage(const ptk_projector* p, int rows, const void* x, const v
   g2.lda = Dl; g2.ldb = Dl; g2.ldc = I; g2.aux_in = (const bf16_t*)a; g2.ld_aux_in = I;
   if (launch_gemm(g2, ACT_GELU_ERF_BWD, OUT_BF16, 1, st)) return -1;
   // db1 = colsum(dA); dW1 = dA^T . x
-  if (launch_colsum_bf16(dA, R, I, db1, part, st)) return -1;
+  if (launch_colsum_bf16(dA, R, I, db1, part, part_floats, st)) return -1;
   if (launch_transpose(dA, I, 0, 0, 1, T, Rp, 0, 0, 1, R, I, Rp, st)) return -1;
   if (launch_transpose((const bf16_t*)x, Dv, 0, 0, 1, xT, Rp, 0, 0, 1, R, Dv, Rp, st)) return -1;
   GemmArgs g3;

@@ -233,7 +233,8 @@ int launch_count_valid(const int64_t* labels, int n, float loss_scale, float* gs
                        hipStream_t st);
 int launch_loss_reduce(const float* row_loss, int R, const float* count, float* loss, hipStream_t st);
 int launch_gather_dy(const float* dx, int B, int N, int Spad, int H, bf16_t* dy, hipStream_t st);
-int launch_colsum_bf16(const bf16_t* x, int rows, int cols, float* out, float* partial, hipStream_t st);
+int launch_colsum_bf16(const bf16_t* x, int rows, int cols, float* out, float* partial, long part_floats,
+                       hipStream_t st);
 int launch_sumsq_partial(const float* x, long n, float* partial, int nparts, hipStream_t st);
 int launch_clip_adamw(float* p, const float* g, float* m, float* v, long n, const float* partial,
                       int nparts, float grad_scale, float max_norm, float lr, float b1, float b2,
