@@ -15,6 +15,7 @@ Rank 0 prints one JSON line.
 from __future__ import annotations
 
 import argparse
+import glob
 import json
 import os
 import socket
@@ -236,7 +237,7 @@ def main(argv=None):
     from projectiontrainer_amd import _lib as L
     from projectiontrainer_amd import weights as W
     from projectiontrainer_amd.config import PRESETS
-    from projectiontrainer_amd.flops import flops_per_image, geglu_step_flops
+    from projectiontrainer_amd.flops import flops_per_image, geglu_algo_bytes, geglu_step_flops
     from projectiontrainer_amd.stage1 import Stage1Engine
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -319,10 +320,12 @@ def main(argv=None):
     value = imgs / elapsed
     fpi = flops_per_image(cfg)["total"]
     geglu_ms = tot.value / max(cnt.value, 1)
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "r02_pmc_traffic_geglu.json")
-    if os.path.exists(pmc) and args.config == "cfg2" and cfg.batch_size == 32 and cfg.text_len == 128:
-        traffic = json.load(open(pmc))["traffic_bytes_per_launch"]   # rocprofv3 --pmc passes (tools/pmc_traffic.py)
+    traffic, traffic_src = None, None
+    # the newest profiles/rNN_pmc_traffic_geglu.json (two rocprofv3 --pmc passes, tools/pmc_traffic.py)
+    pmcs = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]_pmc_traffic_geglu.json")))
+    if pmcs and args.config == "cfg2" and cfg.batch_size == 32 and cfg.text_len == 128:
+        traffic = json.load(open(pmcs[-1]))["traffic_bytes_per_launch"]
+        traffic_src = os.path.relpath(pmcs[-1], ROOT)
     # algorithmic FLOPs of every timed gate|up launch / their summed HIP-event time
     achieved = geglu_step_flops(cfg) * (1 if graph else args.steps) / (tot.value / 1e3) / 1e12
     lm_name = {2560: "Gemma3-4B", 1152: "Gemma3-1B"}.get(cfg.text.hidden_size, f"Gemma3(h{cfg.text.hidden_size})")
@@ -341,7 +344,8 @@ def main(argv=None):
         "roofline": {"bound": "mfma", "kernel": geglu_label(census, args.steps),
                      "achieved": round(achieved, 1), "peak": MFMA_BF16_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": round(achieved / MFMA_BF16_PEAK_TFLOPS, 4), "traffic": traffic,
-                     "traffic_unit": "bytes/launch (PMC FETCH_SIZEx2 + WRITE_SIZE)",
+                     "traffic_unit": "bytes/launch (PMC FETCH_SIZEx2 + WRITE_SIZE)", "traffic_src": traffic_src,
+                     "traffic_algorithmic": geglu_algo_bytes(cfg),
                      "launches": cnt.value, "avg_ms": round(geglu_ms, 4)},
         "median_ms_per_step": round(med_ms, 3),
         "value_at_median_step": round(world * cfg.batch_size / (med_ms / 1e3), 3),

@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTK_ABI_VERSION 3
+#define PTK_ABI_VERSION 4
 
 int ptk_abi_version(void);
 const char* ptk_last_error(void);
@@ -75,8 +75,23 @@ typedef struct {
   int64_t ld_aux_in;
   ptk_rowmap amap;
   ptk_rowmap cmap;
+  /* bf16 residual (SigLIP's pure-bf16 tower, PTK_OUT_BF16 only): out = bf16(resid16 + bf16(linear)) when
+   * bf16_linear != 0 rounds alpha*acc + bias to bf16 first (may alias C) */
+  const void* resid16;
+  int64_t ld_resid16;
+  int bf16_linear;
+  /* Optional stream-K tail scratch (NULL = off) of ptk_gemm_tail_scratch_bytes() bytes whose first
+   * PTK_GEMM_TAIL_COUNTER_BYTES are zero before its first use (every GEMM leaves them zero again).  With it a
+   * plain (PTK_ACT_NONE) GEMM on the persistent 8-wave kernel whose 256x256 tiles fill the last round of the
+   * CUs badly spreads that round's K-tiles evenly over the CUs (fp32 partials of the tiles cut in pieces,
+   * summed in K order: deterministic).  One GEMM at a time per scratch (stream order). */
+  void* tail_ws;
 } ptk_gemm_desc;
 int ptk_gemm(const ptk_gemm_desc* d, void* stream);
+#define PTK_GEMM_TAIL_COUNTER_BYTES 16384
+size_t ptk_gemm_tail_scratch_bytes(void);
+/* Workgroups the stream-K plan spreads this GEMM's last tile round over (0: no split), for tests. */
+int ptk_gemm_tail_split(const ptk_gemm_desc* d);
 
 /* LayerNorm (SigLIP, modeling_siglip.py:329): x f32 [rows,cols] -> y bf16. */
 int ptk_layernorm(const float* x, const float* w, const float* b, void* y, int rows, int cols, float eps,
@@ -121,8 +136,10 @@ int ptk_gemm_timer_enable(int on);   /* 0 off, 1 every class, (1 << 8) | class m
 int ptk_gemm_force_small_tiles(int mode);
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
 /* Dispatch census (tests): counts[path * 8 + act] = GEMM launches since the last reset per kernel family
- * (0 128x128, 1 256x256 8-wave, 2 staggered 256x256 8-wave, 3 persistent 4-wave, 4 and 5 retired (the
- * ping-pong and stream-K kernels, removed), 6 persistent 8-wave, 7 token-major weight grad) and epilogue class (PTK_ACT_*); counts may be
+ * (0 128x128, 1 256x256 8-wave, 2 staggered 256x256 8-wave, 3 persistent 4-wave, 4 128x128 batched (split-K
+ * slices, batch > 1), 5 persistent 8-wave with a stream-K tail round, 6 persistent 8-wave, 7 token-major weight
+ * grad) and epilogue
+ * class (PTK_ACT_*); counts may be
  * NULL; reset != 0 zeroes them afterwards.  Host-side counters, no GPU work. */
 int ptk_gemm_path_counts(int64_t* counts, int reset);
 
@@ -207,6 +224,8 @@ typedef struct {
   const void* w1;   const float* b1;    /* bf16 [I, Dv], f32 [I] */
   const void* w2;   const float* b2;    /* bf16 [Dl, I], f32 [Dl] */
   const void* w2t;                      /* bf16 [I, Dl] (backward) */
+  void* tail_ws;                        /* optional stream-K tail scratch of the projector's GEMMs (see
+                                           ptk_gemm_desc.tail_ws; zeroed by every projector call; NULL = off) */
 } ptk_projector;
 
 /* x bf16 [rows, Dv] -> a (pre-activation, bf16 [rows, I]), h (bf16 [rows, I]),

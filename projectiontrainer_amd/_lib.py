@@ -33,7 +33,8 @@ class GemmDesc(C.Structure):
                 ("ld_rowadd", c_int64), ("resid", c_void_p), ("ld_resid", c_int64),
                 ("aux", c_void_p), ("aux2", c_void_p), ("ld_aux", c_int64),
                 ("aux_in", c_void_p), ("aux_in2", c_void_p), ("ld_aux_in", c_int64),
-                ("amap", RowMap), ("cmap", RowMap)]
+                ("amap", RowMap), ("cmap", RowMap), ("resid16", c_void_p), ("ld_resid16", c_int64),
+                ("bf16_linear", c_int), ("tail_ws", c_void_p)]
 
 
 class FlashDesc(C.Structure):
@@ -75,7 +76,8 @@ class SiglipWeightsC(C.Structure):
 
 class ProjectorC(C.Structure):
     _fields_ = [("vision_dim", c_int), ("inter_dim", c_int), ("llm_dim", c_int),
-                ("w1", c_void_p), ("b1", c_void_p), ("w2", c_void_p), ("b2", c_void_p), ("w2t", c_void_p)]
+                ("w1", c_void_p), ("b1", c_void_p), ("w2", c_void_p), ("b2", c_void_p), ("w2t", c_void_p),
+                ("tail_ws", c_void_p)]
 
 
 class Gemma3ConfigC(C.Structure):
@@ -120,13 +122,15 @@ class ImageDesc(C.Structure):
                 ("coef_off", c_int64), ("tmp_off", c_int64)]
 
 
-ABI_VERSION = 3      # include/ptk.h PTK_ABI_VERSION
+ABI_VERSION = 4      # include/ptk.h PTK_ABI_VERSION
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
     "ptk_abi_version": (c_int, []),
     "ptk_last_error": (C.c_char_p, []),
     "ptk_gemm": (c_int, [C.POINTER(GemmDesc), c_void_p]),
+    "ptk_gemm_tail_scratch_bytes": (c_size_t, []),
+    "ptk_gemm_tail_split": (c_int, [C.POINTER(GemmDesc)]),
     "ptk_layernorm": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
     "ptk_rmsnorm": (c_int, [c_void_p, c_void_p, c_void_p, c_void_p, c_int, c_int, c_float, c_void_p]),
     "ptk_rmsnorm_bwd": (c_int, [c_void_p] * 6 + [c_int, c_int, c_void_p]),
@@ -219,7 +223,8 @@ def ptr(t) -> int | None:
     return None if t is None else t.data_ptr()
 
 
-GEMM_PATHS = ("nt128", "big", "big2", "w4", "pingpong", "streamk", "p8", "tn")
+# nt128b: batched / split-K slices of the 128x128 kernel; p8sk: the persistent 8-wave kernel with a stream-K tail
+GEMM_PATHS = ("nt128", "big", "big2", "w4", "nt128b", "p8sk", "p8", "tn")
 
 
 def gemm_path_counts(reset=False):

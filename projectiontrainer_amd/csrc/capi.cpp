@@ -33,6 +33,8 @@ GemmArgs to_args(const ptk_gemm_desc* d) {
   a.aux = (bf16_t*)d->aux; a.aux2 = (bf16_t*)d->aux2; a.ld_aux = d->ld_aux;
   a.aux_in = (const bf16_t*)d->aux_in; a.aux_in2 = (const bf16_t*)d->aux_in2; a.ld_aux_in = d->ld_aux_in;
   a.amap = to_map(d->amap); a.cmap = to_map(d->cmap);
+  a.resid16 = (const bf16_t*)d->resid16; a.ld_resid16 = d->ld_resid16; a.bf16_linear = d->bf16_linear;
+  a.tail_ws = d->tail_ws;
   return a;
 }
 
@@ -50,6 +52,12 @@ int ptk_gemm(const ptk_gemm_desc* d, void* stream) {
   if (!d) return set_error("ptk_gemm: null desc");
   if (d->act == PTK_ACT_GEGLU && (d->N % 32)) return set_error("ptk_gemm: GEGLU needs N %% 32 == 0");
   return launch_gemm(to_args(d), d->act, d->out, d->batch > 0 ? d->batch : 1, ST);
+}
+
+size_t ptk_gemm_tail_scratch_bytes(void) { return p8_tail_scratch_bytes(); }
+int ptk_gemm_tail_split(const ptk_gemm_desc* d) {
+  if (!d) return set_error("ptk_gemm_tail_split: null desc");
+  return p8_tail_split(to_args(d), d->act, d->out);
 }
 
 int ptk_layernorm(const float* x, const float* w, const float* b, void* y, int rows, int cols, float eps,
@@ -163,6 +171,8 @@ int ptk_flash_attn_bwd(const ptk_flash_bwd_desc* d, void* stream) {
 int ptk_projector_fwd(const ptk_projector* p, int rows, const void* x, void* a, void* h, float* out,
                       ptk_rowmap out_map, int64_t ld_out, int round_bf16, void* stream) {
   const int Dv = p->vision_dim, I = p->inter_dim, Dl = p->llm_dim;
+  TailScratchScope tail(p->tail_ws, ST);
+  if (tail.status) return -1;
   GemmArgs g1;
   g1.A = (const bf16_t*)x; g1.B = (const bf16_t*)p->w1; g1.C = h;
   g1.M = rows; g1.N = I; g1.K = Dv; g1.lda = Dv; g1.ldb = Dv; g1.ldc = I;
@@ -236,6 +246,8 @@ extern "C" {
 
 int ptk_projector_bwd(const ptk_projector* p, int rows, const void* x, const void* a, const void* h, const void* dy,
                       float* dw1, float* db1, float* dw2, float* db2, void* ws, size_t ws_bytes, void* stream) {
+  TailScratchScope tail(p->tail_ws, ST);
+  if (tail.status) return -1;
   if (projector_bwd_stage(p, rows, x, a, h, dy, dw1, db1, dw2, db2, ws, ws_bytes, 0, ST)) return -1;
   return projector_bwd_stage(p, rows, x, a, h, dy, dw1, db1, dw2, db2, ws, ws_bytes, 1, ST);
 }

@@ -141,7 +141,13 @@ int ptk_projector_bwd_allreduce(const ptk_projector* p, int rows, const void* x,
                                 const void* dy, float* flat_grad, void* ws, size_t ws_bytes, ptk_comm* comm,
                                 void* comm_stream, void* stream) {
   if (!comm) return set_error("ptk_projector_bwd_allreduce: null communicator");
+  int dev = -1;
+  if (hipGetDevice(&dev) != hipSuccess || dev != comm->device)
+    return set_error("ptk_projector_bwd_allreduce: current device %d is not the communicator's device %d", dev,
+                     comm->device);
   hipStream_t st = (hipStream_t)stream, cs = (hipStream_t)comm_stream;
+  TailScratchScope tail(p->tail_ws, st);
+  if (tail.status) return -1;
   const long Dv = p->vision_dim, I = p->inter_dim, Dl = p->llm_dim;
   float* dw1 = flat_grad;
   float* db1 = dw1 + I * Dv;

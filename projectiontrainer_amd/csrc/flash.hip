@@ -41,7 +41,9 @@ typedef __attribute__((address_space(3))) void* fa_lptr_t;
 // kept out of the compiler's view.
 PTK_DEV void fa_glds16(const void* src, void* lds) {
   const uint32_t m0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)(fa_lptr_t)lds);
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "s"(m0) : "memory");
+  // M0 is passed through the {m0} constraint: hipcc writes it and knows the asm reads it (never an
+  // undeclared M0 write inside the asm; the s_nop keeps the M0 -> LDS-DMA wait state)
+  asm volatile("s_nop 0\n\tglobal_load_lds_dwordx4 %0, off" ::"v"(src), "{m0}"(m0) : "memory");
 }
 
 // 16-B chunk swizzles (chunk index within a row of D/8 chunks)
@@ -361,8 +363,8 @@ __device__ unsigned long long g_fa_stamps[3][1 << 13][8];   // [kernel: fwd, dQ,
 #endif
 
 #define FA_DMA(VOFF, SOFF, RSRC, LDS)                                                                      \
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen lds"                   \
-               :: "v"(VOFF), "s"(LDS), "s"(RSRC), "s"(SOFF) : "memory")
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen lds"                                     \
+               :: "v"(VOFF), "{m0}"(LDS), "s"(RSRC), "s"(SOFF) : "memory")
 typedef __attribute__((ext_vector_type(4))) unsigned int fa_u32x4_t;
 PTK_DEV fa_u32x4_t fa_rsrc(const void* base, uint32_t bytes) {
   const uint64_t p = (uint64_t)base;

@@ -767,7 +767,7 @@ int timer_read(int cls, double* total_ms, int* count) {
     hipEvent_t e0 = nullptr, e1 = nullptr;                                                     \
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }                              \
     if (e0) (void)hipEventRecord(e0, st);                                                          \
-    count_path(GEMM_PATH_NT, act);                                                             \
+    count_path(batch > 1 ? GEMM_PATH_NTB : GEMM_PATH_NT, act);                                 \
     hipLaunchKernelGGL((gemm_nt_kernel<ACT_, OUT_>), grid, dim3(256), 0, st, a);              \
     if (e1) (void)hipEventRecord(e1, st);                                                          \
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm launch failed");             \
@@ -822,11 +822,17 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
                         ((act == ACT_GELU_ERF || act == ACT_GELU_ERF_BWD) && out == OUT_BF16 && a.K <= 2048 &&
                          w4_round_fill(a.M, a.N) >= 0.8) ||
                         (act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32) && a.K >= 12288 && a.N <= 2048));
-  if (batch == 1 && (g_force_tiles == 32 || p8_auto) && p8_supported(a, act, out)) {
+  // the stream-K tail (gemm_w4.hip P8Tail): a plain GEMM whose last tile round fills the CUs badly, with tail
+  // scratch lent by the model-level call (or in the descriptor), runs on the persistent 8-wave kernel with that
+  // round's K-tiles spread over the CUs (r04: the N = 1024 / 1152 / 1536 projections, the long-K d(gate|up) dX
+  // and down projection, the projector's fc2 and weight grads)
+  const int sk = (g_force_tiles == 0 || g_force_tiles == 32) && batch == 1 && act == ACT_NONE && a.M >= 1024 &&
+                 a.N >= 256 && a.N <= 16384 && p8_supported(a, act, out) ? p8_tail_split(a, act, out) : 0;
+  if (batch == 1 && (g_force_tiles == 32 || p8_auto || sk) && p8_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);
-    count_path(GEMM_PATH_P8, act);
+    count_path(sk ? GEMM_PATH_P8SK : GEMM_PATH_P8, act);
     const int rc = launch_gemm_p8(a, act, out, st);
     if (e1) (void)hipEventRecord(e1, st);
     return rc;

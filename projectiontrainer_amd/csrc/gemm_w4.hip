@@ -80,6 +80,7 @@ struct W4Row {
   long ro_rowadd;   // (rl % rowadd_period) * ld_rowadd
   long ro_c;        // cr * ldc
   long ro_resid;    // cr * ld_resid
+  long ro_resid16;  // cr * ld_resid16
 };
 PTK_DEV W4Row w4_row(const GemmArgs& p, long r) {
   W4Row w;
@@ -93,6 +94,7 @@ PTK_DEV W4Row w4_row(const GemmArgs& p, long r) {
   w.ro_rowadd = p.rowadd ? (long)((unsigned)rl % (unsigned)p.rowadd_period) * p.ld_rowadd : 0;
   w.ro_c = crl * p.ldc;
   w.ro_resid = crl * p.ld_resid;
+  w.ro_resid16 = crl * p.ld_resid16;
   return w;
 }
 
@@ -104,6 +106,14 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
   const bool rv = w.rv && cin, sv = w.cv && cin;
   const long c = cin ? c_ : 0;
   if (p.bias) add8(v, p.bias + c);
+  if (p.bf16_linear) {   // bf16(alpha acc + bias) before the row-add / bf16 residual (a bf16 nn.Linear)
+#pragma unroll
+    for (int e = 0; e < 8; e += 2) {
+      const f32x2_t y = bfround2(f32x2_t{v[e], v[e + 1]});
+      v[e] = y.x;
+      v[e + 1] = y.y;
+    }
+  }
   if (p.rowadd) add8(v, p.rowadd + w.ro_rowadd + c);
   if constexpr (ACT == ACT_GELU_TANH) {
 #pragma unroll
@@ -125,6 +135,12 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
     for (int e = 0; e < 8; ++e) v[e] = bfround(v[e]) * gelu_erf_grad(a[e]);
   }
   if (p.resid) add8(v, p.resid + w.ro_resid + c);
+  if (p.resid16) {   // bf16 residual (may alias C: each lane reads its own 8 columns before storing them)
+    float r[8];
+    ldbf8(sv ? p.resid16 + w.ro_resid16 + c : reinterpret_cast<const bf16_t*>(sink), r);
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] += r[e];
+  }
   if constexpr (OUT == OUT_BF16) {
     stbf8(sv ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + c : reinterpret_cast<bf16_t*>(sink), v);
   } else {
@@ -140,11 +156,15 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
 
 // row block I of the wave's tile: lane holds C[row0 + 16I + (lane&15)][col0 + 16j + 4(lane>>4) + e]
 // (one function per row block so every accumulator index is a compile-time constant)
-template <int ACT, int OUT, int I, int NJ = 8>
+template <int ACT, int OUT, int I, int NJ = 8, bool AGPR = true>
 PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, int lane, char* sink) {
-  // pin the accumulator reads to this row block (otherwise hipcc reads all 256 up front and spills)
+  // pin the accumulator reads to this row block (otherwise hipcc reads all 256 up front and spills); values
+  // summed in VGPRs (the stream-K reducer) are pinned there instead
 #pragma unroll
-  for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
+  for (int j = 0; j < NJ; ++j) {
+    if constexpr (AGPR) asm volatile("" : "+a"(a[j]) :: "memory");
+    else asm volatile("" : "+v"(a[j]) :: "memory");
+  }
   const int q = lane >> 4;
   const int cb = 16 * (q & 1) + 8 * (q >> 1);
   const long r = row0 + 16 * I + (lane & 15);
@@ -277,6 +297,21 @@ PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, lo
   w4_rows<ACT, OUT, 7, NJ>(p, acc[7], row0, col0, lane, sink);
 }
 
+// the kernel's own GemmArgs argument (offset 0 of the kernarg segment) behind a pointer the compiler cannot
+// see through: the epilogue reloads its fields (s_load) instead of keeping some 30 SGPRs of arguments live
+// across the K loop (which spilled SGPRs)
+PTK_DEV const GemmArgs& kernarg_args() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  // a generic pointer: the fields come in by vector loads in the epilogue (s_loads would put them all in
+  // SGPRs at once and spill)
+  const GemmArgs* pk = reinterpret_cast<const GemmArgs*>(__builtin_amdgcn_kernarg_segment_ptr());
+  asm volatile("" : "+s"(pk));
+  return *pk;
+#else
+  __builtin_unreachable();   // host pass: device code only
+#endif
+}
+
 PTK_DEV void w4_tile_coords(int t, int nbm, int nbn, int& bm, int& bn) {
   const int per_group = 8 * nbn;
   const int first_m = (t / per_group) * 8;
@@ -295,8 +330,9 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 #define W4_MFMA(ACC, FB, FA) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(ACC) : "v"(FB), "v"(FA))
 #define W4_MFMA0(ACC, FB, FA) asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, 0" : "=a"(ACC) : "v"(FB), "v"(FA))
 #define W4_DSREAD(DST, ADDR, OFF) asm volatile("ds_read_b128 %0, %1 offset:%2" : "=v"(DST) : "v"(ADDR), "i"(OFF))
-// one 1-KiB LDS-DMA piece: M0 = wave-uniform LDS destination.  hipcc emits no M0 use of its own in
-// these kernels (no LDS-DMA builtins, gfx950 ds_* do not read M0), so M0 is not saved / restored.
+// one 1-KiB LDS-DMA piece: M0 = wave-uniform LDS destination, passed through the {m0} constraint so that
+// hipcc writes M0 itself and knows the asm reads it (an M0 write hidden inside the asm would break any
+// M0 value hipcc keeps live, e.g. for an indexed register move or a spill sequence).
 // PTK_W4_DMA_POL (diagnostic builds, make w4pol): cache-policy bits on the pieces (1 sc1, 2 sc0, 3 nt);
 // measured (tools/gemm_ab.sh, r03): sc1 / sc0 within +-1 % of none on every step shape, nt 2x slower
 #if PTK_W4_DMA_POL == 1
@@ -309,8 +345,8 @@ typedef __attribute__((ext_vector_type(4))) unsigned int u32x4_t;
 #define W4_POL ""
 #endif
 #define W4_DMA(RSRC, VOFF, SOFF, LDS)                                                                      \
-  asm volatile("s_mov_b32 m0, %1\n\ts_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen" W4_POL " lds"        \
-               :: "v"(VOFF), "s"(LDS), "s"(RSRC), "s"(SOFF) : "memory")
+  asm volatile("s_nop 0\n\tbuffer_load_dwordx4 %0, %2, %3 offen" W4_POL " lds"                            \
+               :: "v"(VOFF), "{m0}"(LDS), "s"(RSRC), "s"(SOFF) : "memory")
 
 PTK_DEV u32x4_t w4_rsrc(const void* base, uint32_t bytes) {
   const uint64_t a = (uint64_t)base;
@@ -522,7 +558,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
       asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");   // MFMA D -> accumulator read wait states
       int bm, bn;
       w4_tile_coords(t, nbm, nbn, bm, bn);
-      w4_epilogue<ACT, OUT>(p, acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128, lane);
+      w4_epilogue<ACT, OUT>(kernarg_args(), acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128, lane);
       t += G;
       kt = 0;
     } else {
@@ -540,11 +576,11 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 bool w4_supported(const GemmArgs& a, int act, int out) {
   if (a.N % 8 || a.K % W4_KT) return false;
   if (a.row_stats) return false;   // the softmax-statistics epilogue lives in gemm.hip's epilogue only
-  if (a.resid16 || a.bf16_linear) return false;
+  if (a.resid16 && (out != OUT_BF16 || a.ld_resid16 % 8)) return false;
   if ((a.ldc % 8) || (a.resid && a.ld_resid % 4) || (a.rowadd && a.ld_rowadd % 4)) return false;
   if ((a.aux || a.aux2) && a.ld_aux % 8) return false;
   if ((a.aux_in || a.aux_in2) && a.ld_aux_in % 8) return false;
-  if (((uintptr_t)a.C | (uintptr_t)a.bias | (uintptr_t)a.resid | (uintptr_t)a.rowadd | (uintptr_t)a.aux |
+  if (((uintptr_t)a.C | (uintptr_t)a.bias | (uintptr_t)a.resid | (uintptr_t)a.resid16 | (uintptr_t)a.rowadd | (uintptr_t)a.aux |
        (uintptr_t)a.aux2 | (uintptr_t)a.aux_in | (uintptr_t)a.aux_in2) & 15)
     return false;
   if (act == ACT_GEGLU && (a.N % 32)) return false;
@@ -617,8 +653,73 @@ namespace {
 constexpr int P8_PIECES = 4;   // LDS-DMA pieces per wave per k-step
 }
 
+// ---- stream-K tail (P8Tail; SK kernels only).  A tile grid whose last round fills the persistent grid badly
+// (Gemma3's N = 1152 projections: 440 tiles = 1.72 rounds of 256 CUs; SigLIP's N = 1024 ones: 288 = 1.13) runs
+// its first R whole rounds data-parallel (tiles loc, loc + G, ..: the lock-step L2 sharing of the plain kernel)
+// and spreads the K-tiles of the remaining tail tiles evenly over the first Gs workgroups (Gs <= G, chosen on
+// the host: more workgroups shorten the tail round but cut each tile into more pieces, and every extra piece
+// costs its reducer one more 256-KiB partial read): workgroup g < Gs takes the K-tile units
+// [g U / Gs, (g + 1) U / Gs) of the tail's U = tail tiles x K-tiles, i.e. the end of one tail tile and / or the
+// start of the next.  A tile covered by one workgroup runs the normal epilogue.  A tile split
+// over workgroups g0 .. g1 (its pieces, in K order) is finished by the wave that arrives last: every wave of a
+// piece writes its 128x64 fp32 partial (32 KiB, write-through `sc1` stores) to its workgroup's slot (slot 0
+// for the workgroup's first piece, 1 for its last), drains it (vmcnt(0)) and adds 1 to the (tile, wave)
+// arrival counter (agent scope); the wave whose add returns pieces - 1 loads the other pieces' partials
+// (`sc1` loads: MI355X_MICROARCH.md's hand-off row "one lane per storing wave, agent atomic add, sc1 stores
+// and loads"), sums all pieces in K order (deterministic: the same sum whichever piece arrives last), resets
+// the counter (every launch leaves the counters zero) and runs the fused epilogue.  No wave ever waits for
+// another workgroup, so the grid needs no co-residency.
+struct P8Tail {
+  int dp_tiles = 0;           // tiles [0, dp_tiles) run whole (R rounds of G)
+  int units = 0;              // U = tail tiles x K-tile pairs (0: no tail split)
+  int gsplit = 0;             // Gs: workgroups sharing the tail
+  float* slab = nullptr;      // [G][2 slots][8 waves][128 x 64] fp32 partials
+  uint32_t* cnt = nullptr;    // [tail tiles][8 waves] arrival counters
+};
+constexpr size_t P8_WAVE_FLOATS = 128 * 64;
+
+// the tail tile's pieces are summed in K order: piece jj of tile tt belongs to workgroup g0 + jj, whose partial
+// sits in its slot 0 if the piece is that workgroup's first (its unit range starts inside the tile), else slot 1
+PTK_DEV int p8_owner(long x, int G, int U) { return (int)(((x + 1) * G - 1) / U); }   // workgroup of unit x
+PTK_DEV int p8_start(int g, int G, int U) { return (int)(((long)g * U) / G); }
+
+// row block I of the reducer: the tile's partials summed in K order (the reducer's own piece too, read back
+// from its slab: the accumulators are dead by then), then the fused epilogue of the row block
+template <int ACT, int OUT, int I>
+PTK_DEV void p8_tail_rows(const GemmArgs& p, const float* slab, int tt, int nt, int g0, int np, int G, int U,
+                          int wave, long row0, long col0, int lane, char* sink) {
+  f32x4_t sum[4];
+  for (int jj = 0; jj < np; ++jj) {
+    const int gj = g0 + jj;
+    const int slot = p8_start(gj, G, U) >= tt * nt ? 0 : 1;
+    const float* src = slab + (((size_t)gj * 2 + slot) * 8 + wave) * P8_WAVE_FLOATS + lane * 4;
+    f32x4_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[j]) : "v"(src + (4 * I + j) * 256) : "memory");
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sum[j] = jj == 0 ? v[j] : sum[j] + v[j];
+  }
+  w4_rows<ACT, OUT, I, 4, false>(p, sum, row0, col0, lane, sink);
+}
+
 template <int ACT, int OUT>
-__global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
+PTK_DEV void p8_tail_epilogue(const GemmArgs& p, const float* slab, int tt, int nt, int g0, int np, int G, int U,
+                              int wave, long row0, long col0, int lane) {
+  char* sink = g_w4_sink + lane * 64;
+  p8_tail_rows<ACT, OUT, 0>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 1>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 2>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 3>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 4>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 5>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 6>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 7>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
+}
+
+template <int ACT, int OUT, bool SK>
+__global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes, P8Tail tl) {
   __shared__ __attribute__((aligned(16))) char smem[W4_NSLOT * W4_SLOT];   // 160 KiB: the k-step ring
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -631,10 +732,28 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     const int b = blockIdx.x, q = G >> 3, rr = G & 7, x = b & 7;
     loc = (x < rr ? x * (q + 1) : rr * (q + 1) + (x - rr) * q) + (b >> 3);
   }
-  if (loc >= ntile) return;
   const int nt = p.K / W4_KT;                              // 64-deep K-tiles per output tile
-  const int nks = 2 * nt;                                  // 32-deep k-steps per output tile
-  const int total_ks = ((ntile - loc + G - 1) / G) * nks;
+  // this workgroup's segments: whole tiles loc, loc + G, .. below dp_tiles, then (SK) its tail pieces
+  const int dp_tiles = SK ? tl.dp_tiles : ntile;
+  const int n_dp = loc < dp_tiles ? (dp_tiles - loc + G - 1) / G : 0;
+  // tail units are pairs of K-tiles (nt is even for an SK launch), so every piece spans >= 2 K-tiles
+  const int U = SK ? tl.units : 0, Gs = SK ? tl.gsplit : 1, nu = nt >> 1;
+  const int u0 = SK && loc < Gs ? p8_start(loc, Gs, U) : 0, u1 = SK && loc < Gs ? p8_start(loc + 1, Gs, U) : 0;
+  const int n_tail = u1 > u0 ? (u1 - 1) / nu - u0 / nu + 1 : 0;
+  const int nseg = n_dp + n_tail;
+  if (nseg == 0) return;
+  const int total_ks = 2 * n_dp * nt + 4 * (u1 - u0);     // 32-deep k-steps of the workgroup's whole stream
+  // segment s -> output tile t, K-tiles [k0, k1) (tt: tail tile index, -1 for a whole data-parallel tile)
+  auto segment = [&](int s, int& t, int& k0, int& k1, int& tt) __attribute__((always_inline)) {
+    if (!SK || s < n_dp) {
+      t = loc + s * G; k0 = 0; k1 = nt; tt = -1;
+    } else {
+      tt = u0 / nu + (s - n_dp);
+      k0 = 2 * (max(u0, tt * nu) - tt * nu);
+      k1 = 2 * (min(u1, (tt + 1) * nu) - tt * nu);
+      t = dp_tiles + tt;
+    }
+  };
   const u32x4_t rsa = w4_rsrc(p.A, a_bytes), rsb = w4_rsrc(p.B, b_bytes);
 
   // global -> LDS: wave w fills rows 32w..32w+31 of both operands (2 + 2 pieces of 16 rows x 64 B), lane i of
@@ -649,20 +768,25 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
   }
   const uint32_t lds_base = __builtin_amdgcn_readfirstlane(lds_addr(smem));
   const uint32_t lds_dma = lds_base + wave * 32 * 64;
-  int dt = loc, dks = 0, dcount = 0;
+  // DMA cursor: segment dseg, k-step dks of its dlen (past the last k-step it stays put and re-loads that k-step
+  // into a free slot, never read, so every k-step issues the same instructions)
+  int dseg = 0, dks = 0, dlen = 0, dcount = 0;
   uint32_t dsa = 0, dsb = 0;
-  auto dma_tile = [&](int t) {
+  auto dma_seg = [&](int s) {
+    int t, k0, k1, tt;
+    segment(s, t, k0, k1, tt);
     int bm, bn;
     w4_tile_coords(t, nbm, nbn, bm, bn);
-    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * W4 + (int)p.amap.off) * (uint32_t)p.lda * 2u);
-    dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * W4) * (uint32_t)p.ldb * 2u);
+    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * W4 + (int)p.amap.off) * (uint32_t)p.lda * 2u +
+                                         (uint32_t)k0 * (W4_KT * 2));
+    dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * W4) * (uint32_t)p.ldb * 2u + (uint32_t)k0 * (W4_KT * 2));
+    dlen = 2 * (k1 - k0);
   };
   auto dma_advance = [&]() {
     if (++dcount < total_ks) {
-      if (++dks == nks) {
+      if (++dks == dlen) {
         dks = 0;
-        dt += G;
-        dma_tile(dt);
+        dma_seg(++dseg);
       }
     }
   };
@@ -724,9 +848,28 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     if (rd) W4_DSREAD(fa[7], ba, 7 * 1024);
   };
 
+  // stream-K hand-off of one wave's 128x64 partial (P8Tail): returns true when this wave arrived last and must
+  // sum the pieces and run the epilogue
+  auto tail_arrive = [&](int tt, int np) __attribute__((always_inline)) -> bool {
+    const int slot = u0 >= tt * nu ? 0 : 1;
+    float* mine = tl.slab + (((size_t)loc * 2 + slot) * 8 + wave) * P8_WAVE_FLOATS + lane * 4;
+#pragma unroll
+    for (int q = 0; q < 8; ++q)
+#pragma unroll
+      for (int jj = 0; jj < 4; ++jj)
+        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(mine + (4 * q + jj) * 256), "a"(acc[q][jj])
+                     : "memory");   // straight from the AGPRs (a VGPR copy invites hipcc to re-home acc)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    uint32_t old = 0;
+    if (lane == 0)
+      old = __hip_atomic_fetch_add(tl.cnt + tt * 8 + wave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    old = __builtin_amdgcn_readfirstlane(old);
+    return (int)old == np - 1;
+  };
+
   auto run = [&](auto half_c) __attribute__((always_inline)) {
     // prologue: k-steps 0..3 into slots 0..3; 0..2 landed and published; fragments of k-step 0 read
-    dma_tile(dt);
+    dma_seg(0);
 #pragma unroll
     for (int b = 0; b < 4; ++b) {
       const uint32_t da = lds_dma + b * W4_SLOT, db = da + W4_SOPB;
@@ -746,9 +889,9 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     // flight, i+4 issued into the slot of i-1); vmcnt(4) before each pair's barrier leaves only the youngest
     // k-step's 4 pieces in flight
     uint32_t rs = W4_SLOT, ws = 4 * W4_SLOT;
-    // one pair of k-steps, then the wait + barrier; the tile's first k-step initialises the accumulators
-    // (MFMA with C = 0) and its last reads no fragments.  Peeled per tile (no branch between MFMA forms),
-    // so the 128 accumulators keep their registers across the K loop.
+    // one pair of k-steps (one 64-deep K-tile), then the wait + barrier; the segment's first K-tile
+    // initialises the accumulators (MFMA with C = 0) and its last reads no fragments.  Peeled per segment (no
+    // branch between MFMA forms), so the 128 accumulators keep their registers across the K loop.
     auto pair = [&](auto first_c, auto last_c) __attribute__((always_inline)) {
       constexpr bool lst = decltype(last_c)::value;
       kstep(first_c, std::true_type{}, half_c, fb0, fb1, rs, ws);
@@ -757,20 +900,31 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       ws = slot_next(ws);
       kstep(std::false_type{}, std::integral_constant<bool, !lst>{}, half_c, fb1, fb0, rs, ws);
       dma_advance();
-      if (!lst) rs = slot_next(rs);   // last pair: rs stays on the next tile's first k-step (read after the epilogue)
+      if (!lst) rs = slot_next(rs);   // last pair: rs stays on the next segment's first k-step
       ws = slot_next(ws);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
       __builtin_amdgcn_s_barrier();
     };
-    for (int t = loc; t < ntile; t += G) {
-      pair(std::true_type{}, std::false_type{});
-      for (int kt = 1; kt < nt - 1; ++kt) pair(std::false_type{}, std::false_type{});
+    for (int s = 0; s < nseg; ++s) {
+      int t, k0, k1, tt;
+      segment(s, t, k0, k1, tt);
+      pair(std::true_type{}, std::false_type{});   // (every segment spans >= 2 K-tiles: tail units are pairs)
+      for (int kt = k0 + 1; kt < k1 - 1; ++kt) pair(std::false_type{}, std::false_type{});
       pair(std::false_type{}, std::true_type{});
       asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");   // MFMA D -> accumulator read wait states
       int bm, bn;
       w4_tile_coords(t, nbm, nbn, bm, bn);
-      w4_epilogue<ACT, OUT, 4>(p, acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128 + hf * 64, lane);
-      // the next tile's first k-step (published by the barrier; harmless after the last).  Its slot is the
+      const long row0 = (long)bm * W4 + wr * 128, col0 = (long)bn * W4 + wc * 128 + hf * 64;
+      if (!SK || tt < 0 || (k0 == 0 && k1 == nt)) {
+        w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane);
+      } else if constexpr (SK) {
+        const int g0 = p8_owner((long)tt * nu, Gs, U), np = p8_owner((long)(tt + 1) * nu - 1, Gs, U) - g0 + 1;
+        if (tail_arrive(tt, np)) {
+          p8_tail_epilogue<ACT, OUT>(kernarg_args(), tl.slab, tt, nu, g0, np, Gs, U, wave, row0, col0, lane);
+          if (lane == 0) __hip_atomic_store(tl.cnt + tt * 8 + wave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+      }
+      // the next segment's first k-step (published by the barrier; harmless after the last).  Its slot is the
       // one the NEXT pair's second k-step restages (k-step i+6 lands in the slot of i+1), so a barrier keeps
       // a wave that finished its epilogue early from overwriting it before every wave has read it
       read_frags(rs);
@@ -786,17 +940,81 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
 // the p8 path takes what the w4 path takes, at K >= 128 (a tile's first and last k-step pairs are peeled)
 bool p8_supported(const GemmArgs& a, int act, int out) { return a.K >= 128 && w4_supported(a, act, out); }
 
+// stream-K tail scratch (P8Tail): the arrival counters first (zeroed by p8_tail_scratch_zero at the start of
+// every model-level call that uses it; each launch leaves them zero), then the partial slabs
+constexpr size_t P8_CNT_BYTES = 16384;
+size_t p8_tail_scratch_bytes() {
+  num_cu();
+  return P8_CNT_BYTES + (size_t)g_num_cu * 2 * 8 * P8_WAVE_FLOATS * sizeof(float);
+}
+
+// the stream-K plan of a launch.  Cost model of the tail round, in K-tiles of one workgroup (a 256x256x64 step,
+// ~1.7 us): unsplit, nt; split over Gs workgroups, ceil(U / Gs) plus, where a tile is cut, one partial write
+// and (pieces - 1) partial reads by its reducer, each ~HANDOFF K-tiles (a 256-KiB slab at the ~70 GB/s one
+// workgroup moves across XCDs: ~3.7 us).  The cheapest Gs is taken when it saves >= 10 % of the round.
+constexpr double P8_HANDOFF_KTILES = 2.4;
+static P8Tail p8_tail_plan(const GemmArgs& a, long ntile, long G, int act, int out) {
+  P8Tail tl;
+  void* ws = a.tail_ws ? a.tail_ws : tail_scope();
+  if (!ws || act != ACT_NONE || (out != OUT_BF16 && out != OUT_F32 && out != OUT_F32_BFR)) return tl;
+  const long R = ntile / G, T = ntile - R * G, nt = a.K / W4_KT;
+  if (T == 0 || T * 8 * 4 > (long)P8_CNT_BYTES || (nt & 1)) return tl;
+  const long U = T * (nt / 2);                                // tail units: pairs of K-tiles
+  double best = (double)nt * 0.9;
+  long bestG = 0;
+  for (long gs = T + 1; gs <= G; ++gs) {
+    const long per = (U + gs - 1) / gs;                       // units of the busiest workgroup
+    const long lo = U / gs;                                   // units of the least busy (>= 1 needed)
+    if (lo < 1) break;
+    const long pieces = (nt / 2 + lo - 1) / lo + 1;           // most pieces one tile can be cut into
+    const double cost = 2.0 * (double)per + P8_HANDOFF_KTILES * (double)pieces;
+    if (cost < best - 1e-9) { best = cost; bestG = gs; }
+  }
+  if (!bestG) return tl;
+  tl.dp_tiles = (int)(R * G);
+  tl.units = (int)U;
+  tl.gsplit = (int)bestG;
+  tl.cnt = (uint32_t*)ws;
+  tl.slab = (float*)((char*)ws + P8_CNT_BYTES);
+  return tl;
+}
+
+static thread_local void* g_tail_scope = nullptr;
+void* tail_scope() { return g_tail_scope; }
+TailScratchScope::TailScratchScope(void* ws, hipStream_t st) : prev(g_tail_scope) {
+  g_tail_scope = ws;
+  if (ws) status = launch_zero(ws, P8_CNT_BYTES, st);
+}
+TailScratchScope::~TailScratchScope() { g_tail_scope = prev; }
+
+int p8_tail_split(const GemmArgs& a, int act, int out) {
+  num_cu();
+  const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
+  return p8_tail_plan(a, ntile, g_num_cu, act, out).gsplit;
+}
+
 int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st) {
   num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
-  const long grid = std::min<long>(ntile, g_num_cu);
+  const P8Tail tl = p8_tail_plan(a, ntile, g_num_cu, act, out);
+  const long grid = tl.units ? g_num_cu : std::min<long>(ntile, g_num_cu);
   const long arows = a.M + a.amap.off;
   const uint32_t ab = (uint32_t)std::min<double>((double)arows * a.lda * 2, 2147483000.0);
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
-#define PTK_P8_CASE(ACT_, OUT_)                                                                   \
-  if (act == ACT_ && out == OUT_) {                                                               \
-    hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb); \
-    return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");              \
+#define PTK_P8_CASE(ACT_, OUT_)                                                                       \
+  if (act == ACT_ && out == OUT_) {                                                                   \
+    hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_, false>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb, tl); \
+    return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");                  \
+  }
+#define PTK_P8SK_CASE(ACT_, OUT_)                                                                     \
+  if (act == ACT_ && out == OUT_) {                                                                   \
+    hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_, true>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb, tl); \
+    return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");                  \
+  }
+  if (tl.units) {
+    PTK_P8SK_CASE(ACT_NONE, OUT_BF16)
+    PTK_P8SK_CASE(ACT_NONE, OUT_F32)
+    PTK_P8SK_CASE(ACT_NONE, OUT_F32_BFR)
   }
   PTK_P8_CASE(ACT_NONE, OUT_BF16)
   PTK_P8_CASE(ACT_NONE, OUT_F32)
@@ -807,6 +1025,7 @@ int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st) {
   PTK_P8_CASE(ACT_GELU_ERF_BWD, OUT_BF16)
   PTK_P8_CASE(ACT_GEGLU_BWD, OUT_BF16)
 #undef PTK_P8_CASE
+#undef PTK_P8SK_CASE
   return set_error("gemm_p8: unsupported (act=%d, out=%d)", act, out);
 }
 

@@ -2,6 +2,8 @@
 // transpose, im2col, LLM input assembly, fused cross-entropy fwd/bwd,
 // projector-grad gather, column sums, grad-norm + clip + AdamW, synthetic init.
 #include "common.h"
+
+#include <algorithm>
 #include "ptk_internal.h"
 
 namespace ptk {
@@ -224,7 +226,7 @@ __global__ void __launch_bounds__(256) ce_stats_kernel(bf16_t* __restrict__ logi
   float m = -INFINITY, s = 0.f;
   for (int k = threadIdx.x; k < nch; k += 256) {
     const float2 ms = *reinterpret_cast<const float2*>(st + 2 * k);
-    const float mn = fmaxf(m, ms.x);
+    const float mn = fmaxe(m, ms.x);   // NaN-propagating: a NaN chunk max makes the row NaN (fmaxf would drop it)
     s = (m == -INFINITY ? 0.f : s * __expf(m - mn)) + (ms.x == -INFINITY ? 0.f : ms.y * __expf(ms.x - mn));
     m = mn;
   }
@@ -250,6 +252,20 @@ int launch_ce_fwd_bwd(bf16_t* logits, long ld, int R, int V, const int64_t* targ
   if (R <= 0) return 0;
   hipLaunchKernelGGL(ce_kernel, dim3(R), dim3(256), 0, st, logits, ld, V, targets, row_loss, gscale);
   RET_OK("ce");
+}
+
+// zero-fill of a 16-B aligned buffer (bytes % 16 == 0) by 16-B stores.  Used instead of hipMemsetAsync so
+// that a captured step is kernel nodes only (graph_step); grid-stride over at most 4 blocks per CU.
+__global__ void __launch_bounds__(256) zero16_kernel(uint4* __restrict__ p, long n16) {
+  for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) p[i] = uint4{0, 0, 0, 0};
+}
+int launch_zero(void* p, size_t bytes, hipStream_t st) {
+  if (((uintptr_t)p | bytes) & 15) return set_error("zero: pointer / size not 16-B aligned");
+  const long n16 = (long)(bytes / 16);
+  if (n16 == 0) return 0;
+  const long blocks = std::min<long>((n16 + 255) / 256, 1024);
+  hipLaunchKernelGGL(zero16_kernel, dim3((unsigned)blocks), dim3(256), 0, st, (uint4*)p, n16);
+  RET_OK("zero");
 }
 
 __global__ void __launch_bounds__(256) count_valid_kernel(const int64_t* __restrict__ labels, int n, float loss_scale,

@@ -90,6 +90,7 @@ GemmArgs gemm(const void* A, long lda, const void* B, long ldb, void* C, long ld
 // ------------------------------------------------------------------ SigLIP
 struct SiglipWs {
   bf16_t *patches, *h, *a, *qkv, *o, *mlp;
+  void* tail;   // stream-K tail scratch of the tower's GEMMs
 };
 
 SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
@@ -102,6 +103,7 @@ SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
   w.qkv = bp.take<bf16_t>(M * 3 * D);
   w.o = bp.take<bf16_t>(M * D);
   w.mlp = bp.take<bf16_t>(M * I);
+  w.tail = bp.take<char>(p8_tail_scratch_bytes());
   return w;
 }
 
@@ -129,6 +131,7 @@ struct GemmaWs {
   float* wpart = nullptr;
   float* skpart = nullptr;     // split-K partials (gemm_split)
   long sk_floats = 0;
+  void* tail = nullptr;        // stream-K tail scratch of the model's GEMMs
 };
 
 GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp, bool train = false) {
@@ -220,6 +223,7 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
   w.sk_floats = std::max(std::max(2 * M * H, 2 * 2 * I * H), 4 * std::max(Dqkv, H) * H);
   if (train) w.sk_floats = std::max(w.sk_floats, V * H);   // the tied embedding's fp32 dW before its accumulate
   w.skpart = bp.take<float>(w.sk_floats);
+  w.tail = bp.take<char>(p8_tail_scratch_bytes());
   return w;
 }
 
@@ -300,6 +304,8 @@ int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int
   if (Kp % 64 || hd % 64) return set_error("siglip_fwd: patch dim %d and head dim %d must be multiples of 64", Kp, hd);
   Bump bp(ws);
   SiglipWs w = siglip_layout(bp, c, B);
+  TailScratchScope tail(w.tail, st);
+  CK(tail.status);
 
   // K1 patch embed: im2col + GEMM; bf16(conv + bias) + pos -> bf16 residual stream (modeling_siglip.py:175-186)
   CK(launch_im2col((const bf16_t*)pixels, w.patches, B, c->channels, c->image_size, c->image_size, P, st));
@@ -388,6 +394,8 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
   const float eps = c->eps, scale = 1.0f / sqrtf(c->query_pre_attn_scalar);
   Bump bp(ws);
   GemmaWs w = gemma_layout(bp, c, B, T, Sp, train);
+  TailScratchScope tail(w.tail, st);
+  CK(tail.status);
   AttnShape ash{B, Sp, Hq, Hkv, D};
   const RowMap ident{0, 0, 0, 0};
   const int Rp = (R + 63) / 64 * 64;
@@ -447,7 +455,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
       g.amap = lossmap;
       g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
       CK(launch_gemm(g, ACT_GEGLU, OUT_BF16, 1, st));
-      CKH(hipMemsetAsync(sv.dn, 0, (size_t)M * H * sizeof(bf16_t), st));
+      CK(launch_zero(sv.dn, (size_t)M * H * sizeof(bf16_t), st));
       GemmArgs g2 = gemm(hh, I, L.wd, I, sv.dn, H, R, H, I);
       g2.cmap = lossmap;
       CK(launch_gemm(g2, ACT_NONE, OUT_BF16, 1, st));
@@ -495,7 +503,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
     CK(launch_sum_partials(w.dxf_part, LM_SPLITK + (rem ? 1 : 0), (long)R * H, w.dxf, st));
   }
   float* dR = bt->dx;
-  CKH(hipMemsetAsync(dR, 0, (size_t)M * H * 4, st));
+  CK(launch_zero(dR, (size_t)M * H * 4, st));
   CK(launch_rmsnorm_bwd_scatter(w.x[nl], lossmap, wt->final_norm, w.rstd_f, w.dxf, dR, R, H, st));
   if (train)
     CK(launch_rms_wgrad(w.x[nl], H, lossmap, w.rstd_f, w.dxf, H, 1, R, H, (bf16_t*)gr->final_norm, w.wpart, st));
@@ -543,7 +551,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
       CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, R, I, st));
       if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, lossmap, H, R, w.TA, w.TB, GL->wgu, w.skpart, w.sk_floats, st));
-      CKH(hipMemsetAsync(w.dtmp, 0, (size_t)M * H * sizeof(bf16_t), st));
+      CK(launch_zero(w.dtmp, (size_t)M * H * sizeof(bf16_t), st));
       GemmArgs g2 = gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, R, H, 2 * I);
       g2.cmap = lossmap;
       CK(launch_gemm(g2, ACT_NONE, OUT_BF16, 1, st));

@@ -47,12 +47,15 @@ struct GemmArgs {
   // (the lm_head's softmax statistics: the cross-entropy pass then reads the logits once)
   float* row_stats = nullptr;
   long ld_stats = 0;
+  // stream-K tail scratch of the persistent 8-wave kernel (gemm_w4.hip P8Tail, p8_tail_scratch_bytes); nullptr:
+  // the calling thread's TailScratchScope, if any
+  void* tail_ws = nullptr;
 };
 
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
 // kernel families launch_gemm dispatches to (census: path_counts, ptk_gemm_path_counts)
-enum GemmPath { GEMM_PATH_NT = 0, GEMM_PATH_BIG = 1, GEMM_PATH_BIG2 = 2, GEMM_PATH_W4 = 3, GEMM_PATH_PP = 4,
-                GEMM_PATH_SK = 5, GEMM_PATH_P8 = 6, GEMM_PATH_TN = 7, GEMM_NPATH = 8 };
+enum GemmPath { GEMM_PATH_NT = 0, GEMM_PATH_BIG = 1, GEMM_PATH_BIG2 = 2, GEMM_PATH_W4 = 3, GEMM_PATH_NTB = 4,
+                GEMM_PATH_P8SK = 5, GEMM_PATH_P8 = 6, GEMM_PATH_TN = 7, GEMM_NPATH = 8 };
 int path_counts(int64_t* out, int reset);   // out [GEMM_NPATH][8] launches per (path, act class)
 // persistent 256x256 4-wave GEMM (gemm_w4.hip): batch 1 only; w4_supported says whether a shape qualifies
 bool w4_supported(const GemmArgs& a, int act, int out);
@@ -63,6 +66,18 @@ int device_cus();   // compute units of the current device (cached)
 // persistent 8-wave variant (gemm_w4.hip): the w4 tiles and ring with two waves per SIMD
 bool p8_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st);
+// stream-K tail of the persistent 8-wave kernel: scratch bytes (arrival counters, then partial slabs), the
+// workgroups its plan spreads a GEMM's tail over (0: no split), and the thread-local scratch a model-level
+// call lends to every GEMM it launches (the counters are zeroed when the scope opens)
+size_t p8_tail_scratch_bytes();
+int p8_tail_split(const GemmArgs& a, int act, int out);
+void* tail_scope();
+struct TailScratchScope {
+  void* prev;
+  int status = 0;   // launch status of the counter zero-fill
+  TailScratchScope(void* ws, hipStream_t st);
+  ~TailScratchScope();
+};
 // live GEMM timing per activation class (events recorded around each launch when enabled)
 void timer_enable(int on);
 void force_small_tiles(int mode);
@@ -240,6 +255,8 @@ int launch_clip_adamw(float* p, const float* g, float* m, float* v, long n, cons
                       int nparts, float grad_scale, float max_norm, float lr, float b1, float b2,
                       float eps, float wd, int step, float* norm_out, hipStream_t st);
 int launch_sum_partials(const float* part, int nsplit, long n, float* out, hipStream_t st);
+// zero-fill (16-B aligned pointer and size) by a kernel, not hipMemsetAsync
+int launch_zero(void* p, size_t bytes, hipStream_t st);
 int launch_geglu_bwd(const bf16_t* dh, const bf16_t* g, const bf16_t* u, bf16_t* dgu, long M, int I, hipStream_t st);
 int launch_fill_normal_bf16(bf16_t* out, long n, uint64_t seed, float std, float mean, hipStream_t st);
 

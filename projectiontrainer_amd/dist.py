@@ -157,10 +157,11 @@ def allreduce_grads_chunked_(flat_grad, chunks, world: int, group=None):
 
 class RcclComm:
     """libptk's RCCL communicator (ptk_comm_*) over the ranks of an initialised torch process group: rank 0
-    creates the unique id, the group broadcasts it, every rank joins on its current device."""
+    creates the unique id, the group broadcasts it, every rank joins on `device` (default: the current one)."""
 
-    def __init__(self, group=None):
+    def __init__(self, group=None, device=None):
         import ctypes
+
         from . import _lib as L
         self._L = L
         lib = L.lib()
@@ -173,7 +174,9 @@ class RcclComm:
         dist.broadcast_object_list(obj, src=dist.get_global_rank(group, 0) if group is not None else 0, group=group)
         uid = (ctypes.c_char * nb).from_buffer_copy(obj[0])
         self.handle = ctypes.c_void_p()
-        L.check(lib.ptk_comm_init(ctypes.byref(self.handle), uid, world, rank), "ptk_comm_init")
+        # ptk_comm_init joins RCCL on the current HIP device: make that the engine's device
+        with torch.cuda.device(device if device is not None else torch.cuda.current_device()):
+            L.check(lib.ptk_comm_init(ctypes.byref(self.handle), uid, world, rank), "ptk_comm_init")
         self.world, self.rank = world, rank
 
     def allreduce_sum_(self, t, stream):

@@ -53,6 +53,14 @@ def geglu_step_flops(cfg: Stage1Config) -> float:
     return per_row * cfg.batch_size * (cfg.seq_len * (t.num_hidden_layers - 1) + cfg.text_len)
 
 
+def geglu_algo_bytes(cfg: Stage1Config) -> float:
+    """Algorithmic HBM bytes of one full-size gate|up launch: read the normed input xn [B*S, H] and the
+    interleaved weight [2I, H] once, write h, g, u [B*S, I] (bf16)."""
+    t = cfg.text
+    rows = cfg.batch_size * cfg.seq_len
+    return 2.0 * (rows * t.hidden_size + 2 * t.intermediate_size * t.hidden_size + 3 * rows * t.intermediate_size)
+
+
 def stage2_flops_per_image(cfg: Stage1Config) -> dict:
     """Algorithmic FLOPs of one Stage-2 (unfrozen LLM) micro-batch per image: frozen SigLIP and projector
     forward; Gemma3 forward with the lm_head on the answer rows (the question rows carry no target,

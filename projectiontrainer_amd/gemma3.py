@@ -187,20 +187,20 @@ class Gemma3CausalLM:
     def loss_and_input_grad(self, x, dx, token_ids, labels, num_vision, loss_scale, loss, pad_token_id=None):
         """x: f32 [B*Spad, H] LLM input rows (vision rows filled by the caller),
         token_ids/labels int64 [B, T].  Writes loss [1] (mean CE) and dx (grad of
-        loss*loss_scale w.r.t. x).  pad_token_id: id whose text positions are
+        loss*loss_scale w.r.t. x; dx None = forward and loss only, ptk_gemma3_loss_fwd).  pad_token_id: id whose text positions are
         masked as keys (the trainer passes the tokenizer's, projector_trainer.py:207;
         -1 masks none); None = the model config's."""
         B, T = token_ids.shape
         Sp = x.shape[0] // B
         ws = self.workspace(B, T, Sp)
         bt = L.Gemma3BatchC(B, T, num_vision, Sp, token_ids.data_ptr(), labels.data_ptr(), x.data_ptr(),
-                            dx.data_ptr(), loss_scale, loss.data_ptr())
+                            0 if dx is None else dx.data_ptr(), loss_scale, loss.data_ptr())
         cfg = self.c_cfg
         if pad_token_id is not None and pad_token_id != cfg.pad_token_id:
             cfg = L.Gemma3ConfigC.from_buffer_copy(cfg)
             cfg.pad_token_id = int(pad_token_id)
-        L.check(L.lib().ptk_gemma3_loss_fwd_bwd(cfg, self.c_w, bt, ws.data_ptr(), ws.numel(),
-                                                L.stream_ptr(self.device)), "ptk_gemma3_loss_fwd_bwd")
+        fn = "ptk_gemma3_loss_fwd" if dx is None else "ptk_gemma3_loss_fwd_bwd"
+        L.check(getattr(L.lib(), fn)(cfg, self.c_w, bt, ws.data_ptr(), ws.numel(), L.stream_ptr(self.device)), fn)
 
     def get_input_embeddings(self):
         return self.embed

@@ -23,8 +23,9 @@ def _bits(t):
 def gemm(A, B, *, C=None, out_dtype=torch.bfloat16, act=L.ACT_NONE, alpha=1.0, bias=None, rowadd=None,
          resid=None, aux=None, aux2=None, aux_in=None, aux_in2=None, M=None, N=None, K=None,
          lda=None, ldb=None, ldc=None, batch=1, batch_inner=1, strides=(0, 0, 0, 0, 0, 0),
-         amap=(0, 0, 0, 0), cmap=(0, 0, 0, 0), out_mode=None):
-    """C = epi(alpha * A . B^T) with A [M,K], B [N,K] bf16 (K-contiguous)."""
+         amap=(0, 0, 0, 0), cmap=(0, 0, 0, 0), out_mode=None, resid16=None, bf16_linear=False, tail_ws=None):
+    """C = epi(alpha * A . B^T) with A [M,K], B [N,K] bf16 (K-contiguous).  tail_ws: stream-K tail scratch
+    (uint8 [ptk_gemm_tail_scratch_bytes], its counters zero)."""
     _require_cuda(A, B)
     M = A.shape[-2] if M is None else M
     K = A.shape[-1] if K is None else K
@@ -56,6 +57,10 @@ def gemm(A, B, *, C=None, out_dtype=torch.bfloat16, act=L.ACT_NONE, alpha=1.0, b
     d.aux_in2 = ptr(aux_in2)
     d.amap = L.RowMap(*amap)
     d.cmap = L.RowMap(*cmap)
+    if resid16 is not None:
+        d.resid16, d.ld_resid16 = ptr(resid16), resid16.stride(-2)
+    d.bf16_linear = int(bool(bf16_linear))
+    d.tail_ws = ptr(tail_ws)
     check(L.lib().ptk_gemm(d, L.stream_ptr(A.device)), "ptk_gemm")
     return C
 

@@ -167,10 +167,10 @@ class ProjectionTrainerStage1:
         self.save_projection(epoch=self.num_epochs)
 
     def validation_loss(self):
-        """Mean LM loss over the validation set (no optimizer step; grads are discarded)."""
+        """Mean LM loss over the validation set: forward + CE only (no backward, no grad exchange)."""
         tot, n = torch.zeros(1, device=self.device), 0
         for batch in self._batches(self.val_dataset, 0, shuffle=False):
-            tot += self.engine.forward_backward(batch["pixel_values"], batch["token_ids"], batch["labels"])
+            tot += self.engine.forward_loss(batch["pixel_values"], batch["token_ids"], batch["labels"])
             n += 1
         cnt = torch.tensor([float(n)], device=self.device)
         self.accelerator.all_reduce_sum_(tot)

@@ -87,11 +87,14 @@ class MLPProjector(nn.Module):
             self._w1b = torch.empty(self.w1.shape, dtype=torch.bfloat16, device=self.flat.device)
             self._w2b = torch.empty(self.w2.shape, dtype=torch.bfloat16, device=self.flat.device)
             self._w2t = torch.empty((self.inter_dim, self.llm_dim), dtype=torch.bfloat16, device=self.flat.device)
+            # stream-K tail scratch of the projector's GEMMs (ptk_projector.tail_ws)
+            self._tail = torch.zeros(L.lib().ptk_gemm_tail_scratch_bytes(), dtype=torch.uint8, device=self.flat.device)
         K.cast_bf16(self.w1.detach(), self._w1b)
         K.cast_bf16(self.w2.detach(), self._w2b)
         K.transpose(self._w2b, out=self._w2t)     # in place: no allocation per optimizer step
         self.c = L.ProjectorC(self.vision_dim, self.inter_dim, self.llm_dim, self._w1b.data_ptr(),
-                              self.b1.data_ptr(), self._w2b.data_ptr(), self.b2.data_ptr(), self._w2t.data_ptr())
+                              self.b1.data_ptr(), self._w2b.data_ptr(), self.b2.data_ptr(), self._w2t.data_ptr(),
+                              self._tail.data_ptr())
         self._shadow_dirty = False
 
     def desc(self):

@@ -29,6 +29,8 @@ from __future__ import annotations
 
 import math
 
+import os
+
 import torch
 
 from . import _lib as L
@@ -78,15 +80,18 @@ class Stage1Engine:
         self._graph_key = None
         self._graph_in = None
         self._retired_graphs = []
-        # DDP exchange of the projector grads.  RCCL process group: libptk's communicator, the all-reduce
-        # overlapped with the projector backward (ptk_projector_bwd_allreduce).  Otherwise (gloo): the
-        # collective library, piece by piece in the same order, after the backward.  comm=True forces the
-        # RCCL path (e.g. at world 1, to exercise it on one GPU); False disables it.
+        # DDP exchange of the projector grads.  Default: the process group's collective (RCCL under the nccl
+        # backend, gloo on CPU), piece by piece in a fixed order after the backward (allreduce_grads_chunked_,
+        # checked bit for bit at world 2 / 3).  comm=True (or comm="auto" with PTK_RCCL_OVERLAP=1 on an nccl
+        # group): libptk's own RCCL communicator with the dW2 | db2 all-reduce overlapped with the dA / dW1
+        # GEMMs (ptk_projector_bwd_allreduce).  The overlapped path has run on hardware at world 1 only (one
+        # GPU per box here), so it is opt-in until a world >= 2 run has compared it with the collective path.
         self.comm, self._comm_stream, self._exchanged = None, None, False
-        use = comm is True or (comm == "auto" and world_size > 1 and torch.distributed.is_initialized()
+        use = comm is True or (comm == "auto" and os.environ.get("PTK_RCCL_OVERLAP") == "1" and world_size > 1
+                               and torch.distributed.is_initialized()
                                and torch.distributed.get_backend(process_group) == "nccl")
         if use:
-            self.comm = RcclComm(process_group)
+            self.comm = RcclComm(process_group, device=self.device)
             self._comm_stream = torch.cuda.Stream(self.device)
 
     def _buffers(self, B, T):
@@ -198,6 +203,21 @@ class Stage1Engine:
             rel = torch.cuda.Event()
             rel.record(main)
             self._released[i] = rel
+        return self.loss
+
+    def forward_loss(self, pixel_values, token_ids, labels):
+        """Loss only (the validation pass, projector_trainer.py:292-340 under no_grad): SigLIP, projector
+        forward and the Gemma3 forward + CE (ptk_gemma3_loss_fwd); no backward, no exchange, grads untouched."""
+        B, T = token_ids.shape
+        self._buffers(B, T)
+        if self._prefetched is not None:
+            raise RuntimeError("Stage1Engine.forward_loss: a vision prefetch is pending")
+        i = self._cur
+        self._vision(pixel_values, i)
+        self.px, self.vis = self.px_bufs[i], self.vis_bufs[i]
+        self.proj.fwd_into(self.vis, self.a, self.h, self.x, out_map=(self.N, 1, self.Sp, -1), round_bf16=True)
+        self.llm.loss_and_input_grad(self.x, None, token_ids, labels, self.N - 1, 1.0, self.loss,
+                                     pad_token_id=self.pad_token_id)
         return self.loss
 
     def encode_vision(self, pixel_values, token_ids):

@@ -169,6 +169,10 @@ class Stage2Engine:
         # zero1: reduce-scatter / sharded AdamW / all-gather through the process group (default: world > 1;
         # True at world 1 runs the same collectives on a one-rank group, which tests the RCCL path on one GPU)
         self.zero1 = world_size > 1 if zero1 is None else bool(zero1)
+        if world_size > 1 and not self.zero1:
+            # the optimizer step exchanges grads only through the reduce-scatter / all-gather of ZeRO-1; without
+            # it every rank would update from its own grads and the replicas would drift apart
+            raise ValueError("Stage2Engine: zero1=False is not supported with world_size > 1")
         self.state = Gemma3TrainState(llm, world_size)
         o, n = self.state.shard(rank)
         self.shard_lo, self.shard_n = o, n

@@ -120,19 +120,139 @@ def hazards(body):
     return found
 
 
-@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip"])
-def test_inline_asm_mfma_hazards(src, tmp_path):
+# every HIP source of libptk.so (capi / models / comm are host code)
+PRODUCT_SOURCES = ["flash.hip", "gemm_w4.hip", "gemm.hip", "norm.hip", "attn.hip", "misc.hip", "image.hip",
+                   "train.hip"]
+_ASM_CACHE = {}
+
+
+def product_asm(src, tmp_dir):
+    """gfx950 assembly of one product source; the first call compiles every product source in parallel."""
     if not os.path.exists(HIPCC):
         pytest.skip("hipcc not available")
-    out = tmp_path / (src + ".s")
-    subprocess.check_call([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only", "-S",
-                           "-I", CSRC, os.path.join(CSRC, src), "-o", str(out)],
-                          stderr=subprocess.DEVNULL)
-    asm = out.read_text()
+    if not _ASM_CACHE:
+        from concurrent.futures import ThreadPoolExecutor
+
+        def build(f):
+            out = os.path.join(str(tmp_dir), f + ".s")
+            subprocess.check_call([HIPCC, "-O3", "-std=c++17", "--offload-arch=gfx950", "--cuda-device-only",
+                                   "-S", "-I", CSRC, os.path.join(CSRC, f), "-o", out], stderr=subprocess.DEVNULL)
+            return f, open(out).read()
+        with ThreadPoolExecutor(max_workers=min(8, os.cpu_count() or 1)) as ex:
+            _ASM_CACHE.update(ex.map(build, PRODUCT_SOURCES))
+    return _ASM_CACHE[src]
+
+
+@pytest.fixture(scope="module")
+def asm_dir(tmp_path_factory):
+    return tmp_path_factory.mktemp("asm")
+
+
+@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip"])
+def test_inline_asm_mfma_hazards(src, asm_dir):
+    asm = product_asm(src, asm_dir)
     bad = []
     for name, body in kernels(asm):
         for j, i, what in hazards(body):
             bad.append(f"{name}: {what}: [{j}] {body[j].strip()} -> [{i}] {body[i].strip()}")
+    assert not bad, "\n".join(bad[:20])
+
+
+# ---- register spills.  The round-3 split-tail GEMM (commit 982c7a5, reverted in 44564ce) pushed
+# gemm_p8_kernel to 81 SGPR spills; under that pressure hipcc moved the 128 MFMA accumulators of
+# gemm_p8_kernel<ACT_GELU_ERF_BWD> between AGPRs and VGPRs right after the inline-asm MFMAs that wrote them
+# (v_accvgpr_read 0 wait states after the MFMA: 372 hazards by the scanner above, which did not exist yet),
+# so the projector backward summed garbage whether or not the split ran.  Spill counts are therefore pinned
+# per kernel: SGPR spills go to VGPR lanes (v_writelane / v_readlane, no memory traffic), the only VGPR spills
+# (scratch) are the d-256 dK/dV kernels' epilogue stores of 16 accumulators; a kernel whose counts grow, a new
+# kernel that spills, or a scratch access inside a loop fails.
+SPILL_BUDGET = {   # kernel symbol substring -> (sgpr_spill_count, vgpr_spill_count, private_segment bytes)
+    "attn_bwd_dkv256b_kernel": (27, 16, 68),
+    "attn_dkv_reduce_kernel": (19, 0, 0),
+    "attn_bwd_dkv256_kernelILi32E": (15, 13, 56),
+    # the persistent kernels' epilogues read their arguments through a laundered kernarg pointer
+    # (gemm_w4.hip kernarg_args): 0 spills, except the stream-K tail variants' segment bookkeeping
+    "gemm_p8_kernelILi0ELi0ELb1E": (18, 0, 0),
+    "gemm_p8_kernelILi0ELi1ELb1E": (18, 0, 0),
+    "gemm_p8_kernelILi0ELi2ELb1E": (18, 0, 0),
+    "gemm_big2_kernelILi0ELi0E": (27, 0, 0),
+    "gemm_big2_kernelILi1ELi0E": (11, 0, 0),
+    "gemm_big2_kernelILi2ELi0E": (25, 0, 0),
+    "gemm_big2_kernelILi4ELi0E": (11, 0, 0),
+    "gemm_big_kernelILi0ELi0E": (27, 0, 0),
+    "gemm_big_kernelILi1ELi0E": (11, 0, 0),
+    "gemm_big_kernelILi2ELi0E": (25, 0, 0),
+    "gemm_big_kernelILi4ELi0E": (11, 0, 0),
+    "gemm_nt_kernelILi2ELi0E": (5, 0, 0),
+    "gemm_nt_kernelILi4ELi0E": (1, 0, 0),
+    "qknorm_rope_bwd_kernelILi4E": (28, 0, 0),
+}
+
+
+def kernel_resources(asm):
+    """{kernel symbol: (sgpr_spill_count, vgpr_spill_count, private_segment_fixed_size)} from the amdhsa
+    metadata of one assembly file."""
+    md = asm[asm.find("amdhsa.kernels:"):]
+    out = {}
+    for ent in re.split(r"\n  - ", md)[1:]:
+        m = re.search(r"\.name:\s+(\S+)", ent)
+        if not m:
+            continue
+
+        def g(k):
+            v = re.search(r"\.%s:\s+(\d+)" % k, ent)
+            return int(v.group(1)) if v else 0
+        out[m.group(1)] = (g("sgpr_spill_count"), g("vgpr_spill_count"), g("private_segment_fixed_size"))
+    return out
+
+
+def loop_scratch(body):
+    """Scratch spill / reload instructions inside a loop (hipcc tags loop blocks `; in Loop:` / `Loop Header`)."""
+    bad, in_loop = [], False
+    for line in body:
+        t = line.strip()
+        if re.match(r"^\.LBB\S*:", t):
+            in_loop = "Loop" in t
+            continue
+        if in_loop and re.match(r"^(scratch_|buffer_(store|load)\S*\s.*\boff(set)?\b.*s\[0:3\])", t):
+            bad.append(t)
+    return bad
+
+
+@pytest.mark.parametrize("src", PRODUCT_SOURCES)
+def test_kernel_spills_within_budget(src, asm_dir):
+    asm = product_asm(src, asm_dir)
+    res = kernel_resources(asm)
+    assert res, "no kernel metadata parsed"
+    bad = []
+    for name, got in res.items():
+        budget = next((b for k, b in SPILL_BUDGET.items() if k in name), (0, 0, 0))
+        if any(x > y for x, y in zip(got, budget)):
+            bad.append(f"{name}: (sgpr spills, vgpr spills, private bytes) = {got} > budget {budget}")
+    for name, body in kernels(asm):
+        for t in loop_scratch(body):
+            bad.append(f"{name}: scratch access inside a loop: {t}")
+    assert not bad, "\n".join(bad[:20])
+
+
+@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip"])
+def test_asm_never_writes_m0(src, asm_dir):
+    """LDS-DMA asm takes its LDS address through the {m0} constraint (hipcc writes M0 and knows the asm reads
+    it); an M0 write hidden inside an asm statement would break any M0 value hipcc keeps live."""
+    asm = product_asm(src, asm_dir)
+    bad = []
+    for name, body in kernels(asm):
+        in_asm = False
+        for line in body:
+            t = line.strip()
+            if t.startswith(";;#ASMSTART"):
+                in_asm = True
+            elif t.startswith(";;#ASMEND"):
+                in_asm = False
+            elif in_asm:
+                p = parse(line)
+                if p and p[0].startswith("s_") and re.match(r"^\S+\s+m0\b", t):
+                    bad.append(f"{name}: {t}")
     assert not bad, "\n".join(bad[:20])
 
 
@@ -152,3 +272,10 @@ def test_hazard_scanner_catches_known_patterns():
               A, "s_nop 2", "v_mfma_f32_32x32x16_bf16 v[0:15], v[16:19], v[40:43], v[0:15]", E,
               A, "v_mfma_f32_32x32x16_bf16 v[0:15], v[16:19], v[20:23], v[0:15]", E]
     assert not hazards(padded)
+    # the spill checks
+    loop_body = [".LBB3_9:                                ; =>This Inner Loop Header: Depth=1",
+                 "scratch_store_dwordx4 off, a[0:3], off  ; 16-byte Folded Spill", ".LBB3_41:",
+                 "scratch_load_dwordx4 v[12:15], off, off offset:48 ; 16-byte Folded Reload"]
+    assert loop_scratch(loop_body) == ["scratch_store_dwordx4 off, a[0:3], off  ; 16-byte Folded Spill"]
+    md = "amdhsa.kernels:\n  - .name: k\n    .sgpr_spill_count: 3\n    .vgpr_spill_count: 0\n"
+    assert kernel_resources(md) == {"k": (3, 0, 0)}

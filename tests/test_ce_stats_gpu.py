@@ -31,3 +31,59 @@ def test_ce_from_gemm_statistics_matches_two_pass(tmp_path):
     assert rel(a["dx"], b["dx"]) <= 1e-2, rel(a["dx"], b["dx"])
     for ga, gb in zip(a["grads"], b["grads"]):
         assert rel(ga, gb) <= 1e-2, rel(ga, gb)
+
+
+def _small_engine(nan_column=None):
+    """tests/dkv_fused_worker.py's engine (Gemma3-1B dims, 1 SigLIP + 2 Gemma layers, bs 2), optionally with
+    one tied-embedding row set to NaN (a token id absent from the inputs: only its logit column is NaN)."""
+    import numpy as np
+
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.gemma3 import Gemma3CausalLM
+    from projectiontrainer_amd.projectors import MLPProjector
+    from projectiontrainer_amd.siglip import SiglipVisionTower
+    from projectiontrainer_amd.stage1 import Stage1Engine
+    gpu = torch.device("cuda:0")
+    cfg = PRESETS["cfg2"]
+    cfg = cfg.replace(vision=cfg.vision.__class__(**{**cfg.vision.__dict__, "num_hidden_layers": 1}),
+                      text=cfg.text.__class__(**{**cfg.text.__dict__, "num_hidden_layers": 2,
+                                                          "sliding_window_pattern": 2}),
+                      batch_size=2, text_len=128)
+    vp = W.siglip_vision_params(cfg.vision, seed=3)
+    lp = W.gemma3_params(cfg.text, seed=4)
+    pp = W.projector_params(cfg.vision.hidden_size, cfg.text.hidden_size, seed=5)
+    px, ids, labels = W.synthetic_batch(cfg, seed=7, max_pad=40)
+    if nan_column is not None:
+        assert not np.any(ids == nan_column)
+        lp["model.embed_tokens.weight"][nan_column] = np.nan
+    proj = MLPProjector(cfg.vision.hidden_size, cfg.text.hidden_size)
+    proj.load_state_dict({k: torch.from_numpy(v) for k, v in pp.items()})
+    proj.to(gpu)
+    eng = Stage1Engine(SiglipVisionTower(cfg.vision, vp, gpu),
+                       Gemma3CausalLM(cfg.text, lp, gpu, max_pos=Gemma3CausalLM.seq_pad(cfg.seq_len)), proj,
+                       gradient_accumulation_steps=1)
+    return eng, [torch.from_numpy(a).to(gpu) for a in (px, ids, labels)]
+
+
+@pytest.mark.gpu
+def test_ce_statistics_keep_a_nan_logit():
+    """A NaN logit in one vocab column (the first 256 chunks, where a NaN chunk max once met m = -inf and was
+    dropped: ADVICE r03) makes every row's loss NaN, as torch's CE does."""
+    eng, (px, ids, labels) = _small_engine(nan_column=100)
+    loss = eng.forward_backward(px, ids, labels)
+    torch.cuda.synchronize()
+    assert torch.isnan(loss).all(), float(loss)
+
+
+@pytest.mark.gpu
+def test_forward_loss_matches_forward_backward_loss():
+    """Stage1Engine.forward_loss (validation: ptk_gemma3_loss_fwd, no backward) gives the training pass's loss and
+    leaves the projector grads untouched."""
+    eng, (px, ids, labels) = _small_engine()
+    l_train = float(eng.forward_backward(px, ids, labels))
+    g0 = eng.proj.flat_grad.clone()
+    l_val = float(eng.forward_loss(px, ids, labels))
+    torch.cuda.synchronize()
+    assert l_val == l_train, (l_val, l_train)
+    assert torch.equal(eng.proj.flat_grad, g0)

@@ -535,3 +535,61 @@ def test_projector_module_autograd(gpu):
     torch.testing.assert_close(x.grad, xr.grad, rtol=5e-2, atol=5e-2 * xr.grad.abs().max().item())
     for g, p in zip(proj.grads(), [ref[0].weight, ref[0].bias, ref[2].weight, ref[2].bias]):
         assert F.cosine_similarity(g.flatten(), p.grad.flatten(), dim=0) > 0.999
+
+
+# the stream-K tail of the persistent 8-wave GEMM (gemm_w4.hip P8Tail): (M, N, K, epilogue) at the shapes the
+# step sends to it -- Gemma3's N = 1152 projections (440 tiles: 184 in the last round; dqkv-like K 1536 and the
+# long-K d(gate|up) dX cut to K 4608), SigLIP's N = 1024 fc2 with bias + bf16 residual (288 tiles), the
+# projector's weight grad (M = 1152, N = 10240: 200 tiles, fewer than the CUs: the whole grid is "tail") and
+# its fc2 (fp32 out, bf16-rounded, row-scattered)
+SK_CASES = [(22528, 1152, 1536, "plain"), (22528, 1152, 4608, "plain"), (18432, 1024, 4096, "siglip"),
+            (1152, 10240, 18432, "f32"), (18432, 1152, 10240, "proj_fc2")]
+
+
+@pytest.mark.parametrize("M,N,K,kind", SK_CASES)
+def test_gemm_stream_k_tail_vs_fp32(gpu, M, N, K, kind):
+    """The stream-K tail against torch fp32 of the same GEMM and epilogue, against the same GEMM without the
+    tail split (every output element the sum of the same products; only the K-split summation order differs),
+    and bit for bit against itself (a second launch: the K-order sum of the pieces is deterministic whichever
+    piece arrives last); the census shows the p8sk path ran, the arrival counters are left zero."""
+    Kn, L = _k()
+    tail = torch.zeros(L.lib().ptk_gemm_tail_scratch_bytes(), dtype=torch.uint8, device=gpu)
+    A, B = rnd(M, K, dev=gpu, seed=91), rnd(N, K, dev=gpu, seed=92, scale=0.03)
+    kw, ref = {}, A.float() @ B.float().T
+    out_dtype = torch.bfloat16
+    if kind == "siglip":   # h = bf16(h + bf16(fc2 + bias))
+        bias = torch.randn(N, device=gpu) * 0.1
+        res = rnd(M, N, dev=gpu, seed=93)
+        kw = dict(bias=bias, resid16=res, bf16_linear=True)
+        ref = (ref + bias).to(torch.bfloat16).float() + res.float()
+    elif kind == "f32":
+        out_dtype = torch.float32
+    elif kind == "proj_fc2":   # fp32 out rounded to bf16, rows (b, i >= 1) scattered as in the projector's fc2
+        out_dtype = torch.float32
+        bias = torch.randn(N, device=gpu) * 0.1
+        kw = dict(bias=bias, out_mode=L.OUT_F32_BFR, cmap=(576, 1, 704, -1))
+        ref = (ref + bias).to(torch.bfloat16).float()
+    rows_out = M if kind != "proj_fc2" else (M // 576) * 704
+    mk = lambda: torch.zeros(rows_out, N, dtype=out_dtype, device=gpu)
+    C1, C2, C0 = mk(), mk(), mk()
+    d = L.GemmDesc()
+    d.M, d.N, d.K, d.act, d.out = M, N, K, L.ACT_NONE, kw.get("out_mode", L.OUT_BF16 if out_dtype == torch.bfloat16 else L.OUT_F32)
+    d.tail_ws = tail.data_ptr()
+    assert L.lib().ptk_gemm_tail_split(d) > 0, "the plan does not split this shape"
+    L.gemm_path_counts(reset=True)
+    Kn.gemm(A, B, C=C1, tail_ws=tail, **{k: (v.clone() if k == "resid16" else v) for k, v in kw.items()})
+    paths = L.gemm_path_counts(reset=True)
+    kw2 = {k: (v.clone() if k == "resid16" else v) for k, v in kw.items()}
+    Kn.gemm(A, B, C=C2, tail_ws=tail, **kw2)
+    Kn.gemm(A, B, C=C0, **{k: (v.clone() if k == "resid16" else v) for k, v in kw.items()})   # no tail split
+    torch.cuda.synchronize()
+    assert ("p8sk", L.ACT_NONE) in paths, paths
+    assert not tail[:16384].any(), "arrival counters not left zero"
+    assert torch.equal(C1, C2)
+    got = C1 if kind != "proj_fc2" else C1.view(M // 576, 704, N)[:, :575].reshape(-1, N)
+    if kind == "proj_fc2":
+        ref = ref.view(M // 576, 576, N)[:, 1:].reshape(-1, N)
+    torch.testing.assert_close(got.float(), ref, rtol=2e-2, atol=2e-2 if out_dtype == torch.bfloat16 else 1e-2)
+    # against the unsplit kernel: equal up to the fp32 summation order of the K pieces (and one bf16 rounding)
+    d0 = (C1.float() - C0.float()).abs().max().item()
+    assert d0 <= 2e-2 * max(1.0, C0.float().abs().max().item()), d0
