@@ -171,6 +171,7 @@ PTK_DEV void epilogue(const GemmArgs& p, char* smem, int wave, int lane, f32x4_t
       const float ms = b3 ? m2[1] : m2[0];
       const long rs = row0 + (4 * b1 + 2 * b2 + b3) * 8 + rr;
       if (rs < p.M) *reinterpret_cast<float2*>(p.row_stats + rs * p.ld_stats + 2 * (col0 >> 6)) = make_float2(ms, ss);
+      if (p.stats_only) return;   // diagnostic: what the lm_head costs without writing its logits
     }
 #pragma unroll
     for (int it = 0; it < 8; ++it) {

@@ -26,6 +26,7 @@
 #include "gemm_epi.h"
 
 #include <algorithm>
+#include <cstdlib>
 #include <type_traits>
 
 #ifndef PTK_W4_RDS
@@ -300,13 +301,15 @@ PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, lo
 // the kernel's own GemmArgs argument (offset 0 of the kernarg segment) behind a pointer the compiler cannot
 // see through: the epilogue reloads its fields (s_load) instead of keeping some 30 SGPRs of arguments live
 // across the K loop (which spilled SGPRs)
+typedef const GemmArgs __attribute__((address_space(4)))* kargs_ptr_t;
 PTK_DEV const GemmArgs& kernarg_args() {
 #if defined(__HIP_DEVICE_COMPILE__)
-  // a generic pointer: the fields come in by vector loads in the epilogue (s_loads would put them all in
-  // SGPRs at once and spill)
-  const GemmArgs* pk = reinterpret_cast<const GemmArgs*>(__builtin_amdgcn_kernarg_segment_ptr());
+  // laundered in the constant address space, so the fields come in by scalar loads (lgkmcnt): a vector load of
+  // an argument would make hipcc wait vmcnt(0) before its use, i.e. for every LDS-DMA piece of the next tile
+  // the stream already has in flight (r04: -15 % on the gate|up GEMM)
+  kargs_ptr_t pk = (kargs_ptr_t)__builtin_amdgcn_kernarg_segment_ptr();
   asm volatile("" : "+s"(pk));
-  return *pk;
+  return *(const GemmArgs*)pk;
 #else
   __builtin_unreachable();   // host pass: device code only
 #endif
@@ -684,38 +687,40 @@ PTK_DEV int p8_owner(long x, int G, int U) { return (int)(((x + 1) * G - 1) / U)
 PTK_DEV int p8_start(int g, int G, int U) { return (int)(((long)g * U) / G); }
 
 // row block I of the reducer: the tile's partials summed in K order (the reducer's own piece too, read back
-// from its slab: the accumulators are dead by then), then the fused epilogue of the row block
+// from its slab: the accumulators are dead by then), then the fused epilogue of the row block.  Piece jj of the
+// tile belongs to workgroup g0 + jj; its partial sits in that workgroup's slot 0, except piece 0's when the
+// workgroup's range started in an earlier tile (s0 = 1: its slot 1)
 template <int ACT, int OUT, int I>
-PTK_DEV void p8_tail_rows(const GemmArgs& p, const float* slab, int tt, int nt, int g0, int np, int G, int U,
-                          int wave, long row0, long col0, int lane, char* sink) {
+PTK_DEV void p8_tail_rows(const GemmArgs& p, const float* slab, int g0, int np, int s0, int wave, long row0,
+                          long col0, int lane, char* sink) {
+  // sc1 buffer loads through the builtin (hipcc sees them and waits for their data itself: an asm load whose
+  // result register hipcc copies before an asm wait reads garbage -- the first version of this reducer did)
+  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)slab, 0, 0x7fffffff, 0x00020000);
   f32x4_t sum[4];
   for (int jj = 0; jj < np; ++jj) {
-    const int gj = g0 + jj;
-    const int slot = p8_start(gj, G, U) >= tt * nt ? 0 : 1;
-    const float* src = slab + (((size_t)gj * 2 + slot) * 8 + wave) * P8_WAVE_FLOATS + lane * 4;
-    f32x4_t v[4];
+    const uint32_t off = (uint32_t)(((((g0 + jj) * 2 + (jj == 0 ? s0 : 0)) * 8 + wave) * (int)P8_WAVE_FLOATS +
+                                     lane * 4 + 4 * I * 256) * 4);
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v[j]) : "v"(src + (4 * I + j) * 256) : "memory");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < 4; ++j) sum[j] = jj == 0 ? v[j] : sum[j] + v[j];
+    for (int j = 0; j < 4; ++j) {   // K order: piece 0, 1, ..
+      const f32x4_t v = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off + j * 1024, 0, 16));
+      sum[j] = jj == 0 ? v : sum[j] + v;
+    }
   }
   w4_rows<ACT, OUT, I, 4, false>(p, sum, row0, col0, lane, sink);
 }
 
 template <int ACT, int OUT>
-PTK_DEV void p8_tail_epilogue(const GemmArgs& p, const float* slab, int tt, int nt, int g0, int np, int G, int U,
-                              int wave, long row0, long col0, int lane) {
+PTK_DEV void p8_tail_epilogue(const GemmArgs& p, const float* slab, int g0, int np, int s0, int wave, long row0,
+                              long col0, int lane) {
   char* sink = g_w4_sink + lane * 64;
-  p8_tail_rows<ACT, OUT, 0>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 1>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 2>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 3>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 4>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 5>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 6>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 7>(p, slab, tt, nt, g0, np, G, U, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 0>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 1>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 2>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 3>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 4>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 5>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 6>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
+  p8_tail_rows<ACT, OUT, 7>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
 }
 
 template <int ACT, int OUT, bool SK>
@@ -743,15 +748,42 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
   const int nseg = n_dp + n_tail;
   if (nseg == 0) return;
   const int total_ks = 2 * n_dp * nt + 4 * (u1 - u0);     // 32-deep k-steps of the workgroup's whole stream
-  // segment s -> output tile t, K-tiles [k0, k1) (tt: tail tile index, -1 for a whole data-parallel tile)
-  auto segment = [&](int s, int& t, int& k0, int& k1, int& tt) __attribute__((always_inline)) {
-    if (!SK || s < n_dp) {
-      t = loc + s * G; k0 = 0; k1 = nt; tt = -1;
+  // segment table (SK): lane i holds segment i (the host keeps nseg <= 64) -- tile t, tail tile tt (-1 for a
+  // whole data-parallel tile), K-tiles [k0, k1) and for a cut tail tile its pieces' first workgroup g0, their
+  // count np, piece 0's slot s0 and this workgroup's slot -- read back by v_readlane at segment boundaries, so
+  // the bookkeeping costs 3 VGPRs instead of a dozen SGPRs live across the K loop
+  uint32_t segA = 0, segB = 0, segC = 0;
+  if constexpr (SK) {
+    const int i = lane;
+    int t, k0, k1, tt;
+    if (i < n_dp) {
+      t = loc + i * G; k0 = 0; k1 = nt; tt = -1;
     } else {
-      tt = u0 / nu + (s - n_dp);
+      tt = u0 / nu + (i - n_dp);
       k0 = 2 * (max(u0, tt * nu) - tt * nu);
       k1 = 2 * (min(u1, (tt + 1) * nu) - tt * nu);
       t = dp_tiles + tt;
+    }
+    int g0 = 0, np = 1, s0 = 0, myslot = 0;
+    if (tt >= 0 && i < nseg) {
+      g0 = p8_owner((long)tt * nu, Gs, U);
+      np = p8_owner((long)(tt + 1) * nu - 1, Gs, U) - g0 + 1;
+      s0 = p8_start(g0, Gs, U) < tt * nu ? 1 : 0;
+      myslot = u0 < tt * nu ? 1 : 0;
+      if (np == 1) tt = -1;   // the whole tile in one piece: plain epilogue
+    }
+    segA = (uint32_t)t | ((uint32_t)(tt + 1) << 16);
+    segB = (uint32_t)k0 | ((uint32_t)k1 << 16);
+    segC = (uint32_t)g0 | ((uint32_t)np << 10) | ((uint32_t)s0 << 20) | ((uint32_t)myslot << 21);
+  }
+  // segment s -> output tile t, K-tiles [k0, k1) (tt: tail tile index, -1 for a whole tile)
+  auto segment = [&](int s, int& t, int& k0, int& k1, int& tt) __attribute__((always_inline)) {
+    if constexpr (!SK) {
+      t = loc + s * G; k0 = 0; k1 = nt; tt = -1;
+    } else {
+      const uint32_t a = __builtin_amdgcn_readlane(segA, s), b = __builtin_amdgcn_readlane(segB, s);
+      t = (int)(a & 0xffffu); tt = (int)(a >> 16) - 1;
+      k0 = (int)(b & 0xffffu); k1 = (int)(b >> 16);
     }
   };
   const u32x4_t rsa = w4_rsrc(p.A, a_bytes), rsb = w4_rsrc(p.B, b_bytes);
@@ -850,8 +882,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
 
   // stream-K hand-off of one wave's 128x64 partial (P8Tail): returns true when this wave arrived last and must
   // sum the pieces and run the epilogue
-  auto tail_arrive = [&](int tt, int np) __attribute__((always_inline)) -> bool {
-    const int slot = u0 >= tt * nu ? 0 : 1;
+  auto tail_arrive = [&](int tt, int np, int slot) __attribute__((always_inline)) -> bool {
     float* mine = tl.slab + (((size_t)loc * 2 + slot) * 8 + wave) * P8_WAVE_FLOATS + lane * 4;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
@@ -915,12 +946,18 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       int bm, bn;
       w4_tile_coords(t, nbm, nbn, bm, bn);
       const long row0 = (long)bm * W4 + wr * 128, col0 = (long)bn * W4 + wc * 128 + hf * 64;
-      if (!SK || tt < 0 || (k0 == 0 && k1 == nt)) {
+      if (!SK || tt < 0) {
         w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane);
       } else if constexpr (SK) {
-        const int g0 = p8_owner((long)tt * nu, Gs, U), np = p8_owner((long)(tt + 1) * nu - 1, Gs, U) - g0 + 1;
-        if (tail_arrive(tt, np)) {
-          p8_tail_epilogue<ACT, OUT>(kernarg_args(), tl.slab, tt, nu, g0, np, Gs, U, wave, row0, col0, lane);
+        const uint32_t c = __builtin_amdgcn_readlane(segC, s);
+        const int g0 = (int)(c & 1023u), np = (int)((c >> 10) & 1023u), s0 = (int)((c >> 20) & 1u);
+        if (tail_arrive(tt, np, (int)((c >> 21) & 1u))) {
+          // agent-scope acquire before reading the other pieces (the hand-off is per wave with the counter's
+          // returned value as the signal, not one of MI355X_MICROARCH.md's measured sc1-only rows; the
+          // invalidate also drops any line of the slab an earlier launch left in this XCD's caches)
+          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+          p8_tail_epilogue<ACT, OUT>(kernarg_args(), tl.slab, g0, np, s0, wave, row0, col0, lane);
           if (lane == 0) __hip_atomic_store(tl.cnt + tt * 8 + wave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
@@ -959,6 +996,13 @@ static P8Tail p8_tail_plan(const GemmArgs& a, long ntile, long G, int act, int o
   if (!ws || act != ACT_NONE || (out != OUT_BF16 && out != OUT_F32 && out != OUT_F32_BFR)) return tl;
   const long R = ntile / G, T = ntile - R * G, nt = a.K / W4_KT;
   if (T == 0 || T * 8 * 4 > (long)P8_CNT_BYTES || (nt & 1)) return tl;
+  // where it measured faster (tools/sk_ab.py, profiles/r04_sk_ab.txt): few tail tiles -- a grid of at most 64
+  // tiles, or one full round plus at most 24 -- as the Stage-2 weight grads and the M = 14 336 projections
+  // are (0.43-0.80 of the unsplit time).  With more tail tiles the pieces of a tile stream different K ranges
+  // at the same time, the L2 sharing of a lock-step round is lost, and every Stage-1 shape measured slower
+  // (1.1-1.4x); PTK_NO_STREAMK=1 turns the tail off everywhere (A/B)
+  static const bool off = [] { const char* e = getenv("PTK_NO_STREAMK"); return e && e[0] == '1'; }();
+  if (off || !((R == 0 && T <= 64) || (R == 1 && T <= 24))) return tl;
   const long U = T * (nt / 2);                                // tail units: pairs of K-tiles
   double best = (double)nt * 0.9;
   long bestG = 0;
@@ -970,7 +1014,7 @@ static P8Tail p8_tail_plan(const GemmArgs& a, long ntile, long G, int act, int o
     const double cost = 2.0 * (double)per + P8_HANDOFF_KTILES * (double)pieces;
     if (cost < best - 1e-9) { best = cost; bestG = gs; }
   }
-  if (!bestG) return tl;
+  if (!bestG || R + 3 > 64 || G > 1023 || ntile > 65535) return tl;   // the kernel's per-lane segment table
   tl.dp_tiles = (int)(R * G);
   tl.units = (int)U;
   tl.gsplit = (int)bestG;

@@ -74,6 +74,14 @@ static bool dkv_reduce_split() {
 
 // PTK_CE_TWO_PASS=1: the cross-entropy pass computes its own row statistics (two reads of the logits) instead
 // of taking them from the lm_head GEMM's epilogue (A/B; tests/test_stage1_gpu.py checks both agree)
+// PTK_LM_STATS_ONLY=1 (diagnostic, wrong results by construction): the lm_head GEMM computes its softmax
+// statistics but skips the logits store -- the forward half of a fused lm_head + online-LSE CE, timed against
+// the shipped chain
+static bool lm_stats_only() {
+  static const int v = [] { const char* e = getenv("PTK_LM_STATS_ONLY"); return e && e[0] == '1' ? 1 : 0; }();
+  return v != 0;
+}
+
 static bool ce_two_pass() {
   static const int v = [] { const char* e = getenv("PTK_CE_TWO_PASS"); return e && e[0] == '1' ? 1 : 0; }();
   return v != 0;
@@ -234,6 +242,10 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
 // optional bf16 accumulate (bf16_linear + resid16, the weight-grad epilogue).  The slices go to the batched
 // 128x128 kernel as fp32 partials [S][M][N]; one pass sums them in slice order (deterministic).
 int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStream_t st) {
+  // the persistent kernel's stream-K tail takes the shapes it measured faster on (gemm_w4.hip p8_tail_plan:
+  // Stage 2's weight grads and M = 14 336 projections) before any host-side split
+  if (a.M >= 1024 && a.N >= 256 && a.N <= 16384 && p8_supported(a, ACT_NONE, out) && p8_tail_split(a, ACT_NONE, out))
+    return launch_gemm(a, ACT_NONE, out, 1, st);
   const long nbig = (long)((a.M + 255) / 256) * ((a.N + 255) / 256);
   int S = 1, kmin = 1024;
   if (a.K >= 4096 && nbig <= 64) S = 4;
@@ -476,6 +488,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
     if (w.ce_stats && !ce_two_pass()) {
       g.row_stats = w.ce_stats;
       g.ld_stats = (V / 64) * 2;
+      g.stats_only = lm_stats_only() ? 1 : 0;
     }
     CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
     CK(launch_count_valid(bt->labels, R, bt->loss_scale, w.gscale, w.count, st));

@@ -47,6 +47,7 @@ struct GemmArgs {
   // (the lm_head's softmax statistics: the cross-entropy pass then reads the logits once)
   float* row_stats = nullptr;
   long ld_stats = 0;
+  int stats_only = 0;   // diagnostic (PTK_LM_STATS_ONLY=1): the row statistics without the logits store
   // stream-K tail scratch of the persistent 8-wave kernel (gemm_w4.hip P8Tail, p8_tail_scratch_bytes); nullptr:
   // the calling thread's TailScratchScope, if any
   void* tail_ws = nullptr;

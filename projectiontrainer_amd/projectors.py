@@ -92,6 +92,8 @@ class MLPProjector(nn.Module):
         K.cast_bf16(self.w1.detach(), self._w1b)
         K.cast_bf16(self.w2.detach(), self._w2b)
         K.transpose(self._w2b, out=self._w2t)     # in place: no allocation per optimizer step
+        if getattr(self, "_w1t", None) is not None:   # W1^T of the autograd input grad, once built
+            K.transpose(self._w1b, out=self._w1t)
         self.c = L.ProjectorC(self.vision_dim, self.inter_dim, self.llm_dim, self._w1b.data_ptr(),
                               self.b1.data_ptr(), self._w2b.data_ptr(), self.b2.data_ptr(), self._w2t.data_ptr(),
                               self._tail.data_ptr())
@@ -153,15 +155,24 @@ class _ProjectorFn(torch.autograd.Function):
         xb, a, h = ctx.saved_tensors
         mod = ctx.mod
         dy = gout.reshape(-1, mod.llm_dim).to(torch.bfloat16).contiguous()
-        ws = torch.empty(mod.workspace_bytes(xb.shape[0]), dtype=torch.uint8, device=xb.device)
-        prev = mod.flat_grad.clone()
-        mod.bwd_into(xb, a, h, dy, ws)
-        mod.flat_grad.add_(prev)           # accumulate like autograd would
+        # workspace and grad scratch kept on the module across calls (grown when a larger batch comes)
+        nb = mod.workspace_bytes(xb.shape[0])
+        if getattr(mod, "_bwd_ws", None) is None or mod._bwd_ws.numel() < nb:
+            mod._bwd_ws = torch.empty(nb, dtype=torch.uint8, device=xb.device)
+        if getattr(mod, "_grad_tmp", None) is None:
+            mod._grad_tmp = torch.empty_like(mod.flat_grad)
+        g = [mod._grad_tmp[o:o + k] for o, k, _ in mod._views]
+        L.check(L.lib().ptk_projector_bwd(mod.desc(), xb.shape[0], xb.data_ptr(), a.data_ptr(), h.data_ptr(),
+                                          dy.data_ptr(), g[0].data_ptr(), g[1].data_ptr(), g[2].data_ptr(),
+                                          g[3].data_ptr(), mod._bwd_ws.data_ptr(), mod._bwd_ws.numel(),
+                                          L.stream_ptr(xb.device)), "ptk_projector_bwd")
+        mod.flat_grad.add_(mod._grad_tmp)   # accumulate like autograd would
         dx = None
         if ctx.needs_input_grad[0]:
             # dA = (dY . W2) * gelu'(a) (bf16, the fused GELU-backward epilogue), then dX = dA . W1
             da = K.gemm(dy, mod._w2t, act=L.ACT_GELU_ERF_BWD, aux_in=a)
-            w1t = K.transpose(mod._w1b)   # [Dv, I]: W1 as the K-contiguous B operand
-            dx = K.gemm(da, w1t, out_dtype=torch.float32)
+            if getattr(mod, "_w1t", None) is None:   # [Dv, I]: W1 as the K-contiguous B operand (cached)
+                mod._w1t = K.transpose(mod._w1b)
+            dx = K.gemm(da, mod._w1t, out_dtype=torch.float32)
             dx = dx.view(*ctx.x_shape).to(ctx.x_dtype)
         return dx, None, None

@@ -79,7 +79,6 @@ class Stage1Engine:
         self._graph = None         # graph_step: captured forward_backward, its input key and static inputs
         self._graph_key = None
         self._graph_in = None
-        self._retired_graphs = []
         # DDP exchange of the projector grads.  Default: the process group's collective (RCCL under the nccl
         # backend, gloo on CPU), piece by piece in a fixed order after the backward (allreduce_grads_chunked_,
         # checked bit for bit at world 2 / 3).  comm=True (or comm="auto" with PTK_RCCL_OVERLAP=1 on an nccl
@@ -266,7 +265,7 @@ class Stage1Engine:
         """step() with forward_backward replayed from a HIP graph.  The ~900 kernel launches of the SigLIP,
         projector and Gemma3 passes are captured once per input shape and then replayed as one launch: at a
         small batch (cfg1: bs 2) the step is bound by launch latency, not by the kernels.  Capture needs every
-        lazy initialisation (hipBLASLt plans and workspace, step buffers) done, so at least one eager step()
+        lazy initialisation (step buffers, workspaces, the projector's bf16 shadows) done, so at least one eager step()
         at this shape must precede the first call.  Inputs are copied into static buffers that the graph reads.
         The optimizer step stays eager: its learning rate and step count are kernel arguments that change every
         step (and the DDP all-reduce runs there).  Same kernels in the same order: bit-identical to step()."""
@@ -281,13 +280,14 @@ class Stage1Engine:
         key = (tuple(pixel_values.shape), pixel_values.dtype, tuple(token_ids.shape), tuple(labels.shape),
                self._buffer_fingerprint())
         if self._graph is None or self._graph_key != key:
-            # a replaced graph is kept, not destroyed: on this ROCm (7.2 / torch 2.10) destroying a captured
-            # graph and capturing another made the NEW graph's second and later replays compute garbage
-            # (tools/graph_debug.py: NaN grads; kept alive, every replay is bit-identical to eager).  Only a
-            # shape or buffer change retires one, so the list stays short.
-            if self._graph is not None:
-                self._retired_graphs.append((self._graph, self._graph_in))
+            # a replaced graph is destroyed.  (Until round 4 it was kept alive: destroying one and capturing
+            # another made the new graph's second and later replays compute NaN grads.  Root cause: the step's
+            # three hipMemsetAsync calls became memset nodes of the captured graph; with them replaced by a
+            # zero-fill kernel (csrc/misc.hip launch_zero) every destroy / re-capture sequence of
+            # tools/graph_debug.py is bit-identical to eager, and with PTK_HIP_MEMSET=1 (memset nodes back)
+            # the NaNs return -- profiles/r04_graph_memset_ab.txt.)
             self._graph = None
+            self._graph_in = None
             static = (pixel_values.clone(), token_ids.clone(), labels.clone())
             g = torch.cuda.CUDAGraph()
             with torch.cuda.graph(g):      # capture only: nothing runs until replay

@@ -171,10 +171,14 @@ SPILL_BUDGET = {   # kernel symbol substring -> (sgpr_spill_count, vgpr_spill_co
     "attn_dkv_reduce_kernel": (19, 0, 0),
     "attn_bwd_dkv256_kernelILi32E": (15, 13, 56),
     # the persistent kernels' epilogues read their arguments through a laundered kernarg pointer
-    # (gemm_w4.hip kernarg_args): 0 spills, except the stream-K tail variants' segment bookkeeping
-    "gemm_p8_kernelILi0ELi0ELb1E": (18, 0, 0),
-    "gemm_p8_kernelILi0ELi1ELb1E": (18, 0, 0),
-    "gemm_p8_kernelILi0ELi2ELb1E": (18, 0, 0),
+    # (gemm_w4.hip kernarg_args, scalar loads): 0 spills, except the GELU-erf epilogues (the projector's) and
+    # the stream-K tail variants' bookkeeping
+    "gemm_p8_kernelILi0ELi0ELb1E": (16, 0, 0),
+    "gemm_p8_kernelILi0ELi1ELb1E": (16, 0, 0),
+    "gemm_p8_kernelILi0ELi2ELb1E": (16, 0, 0),
+    "gemm_p8_kernelILi1ELi0ELb0E": (4, 0, 0),
+    "gemm_p8_kernelILi2ELi0ELb0E": (28, 0, 0),
+    "gemm_p8_kernelILi4ELi0ELb0E": (20, 0, 0),
     "gemm_big2_kernelILi0ELi0E": (27, 0, 0),
     "gemm_big2_kernelILi1ELi0E": (11, 0, 0),
     "gemm_big2_kernelILi2ELi0E": (25, 0, 0),

@@ -64,3 +64,24 @@ def test_graph_step_recaptures_after_reallocation(gpu):
         keys.append(graphed._graph_key)
     assert keys[1] is not None and keys[3] != keys[1], "bs-4 reallocation did not force a recapture"
     assert keys[4] == keys[3]
+
+
+def test_graph_step_recapture_after_destroy_stays_bit_identical(gpu):
+    """A forced re-capture destroys the replaced graph (graph_step keeps no retired graphs); the new graph's
+    later replays must stay bit-identical to eager.  This is the sequence that gave NaN grads while the captured
+    step held hipMemsetAsync nodes (tools/graph_debug.py V1/V7, profiles/r04_graph_memset_ab.txt)."""
+    import gc
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    cfg = PRESETS["tiny"].replace(batch_size=2)
+    b = [tuple(torch.from_numpy(a).to(gpu) for a in W.synthetic_batch(cfg, seed=60 + s)) for s in range(5)]
+    eager, graphed = _engine(cfg, gpu), _engine(cfg, gpu)
+    for k, (mode, x) in enumerate([("e", b[0]), ("g", b[1]), ("new", b[2]), ("g", b[3]), ("g", b[4])]):
+        if mode == "new":              # force a re-capture: the old graph is dropped and destroyed
+            graphed._graph_key = None
+            gc.collect()
+        le = float(eager.step(*x))
+        lg = float(graphed.step(*x) if mode == "e" else graphed.graph_step(*x))
+        torch.cuda.synchronize()
+        assert le == lg, (k, le, lg)
+        assert torch.equal(eager.proj.flat_grad, graphed.proj.flat_grad), k

@@ -166,11 +166,16 @@ def _census(run):
     return set(L.gemm_path_counts(reset=True))
 
 
-def _bench_census(gpu):
-    """The dispatch of the benchmarked step (cfg2 at bs 32, bench.py's workload), HIP only."""
+def _bench_census(gpu, preset="cfg2"):
+    """The dispatch of the benchmarked step (bench.py's workload: cfg2 at bs 32; cfg5 at bs 16), HIP only.  cfg5
+    runs at 2 SigLIP + 6 Gemma layers: every layer of a tower has the same shapes, so depth does not change the
+    dispatch (tools/census_probe2.py)."""
     from projectiontrainer_amd.config import PRESETS
     from projectiontrainer_amd.stage1 import Stage1Engine
-    cfg = PRESETS["cfg2"]
+    cfg = PRESETS[preset]
+    if preset != "cfg2":
+        cfg = cfg.replace(vision=cfg.vision.__class__(**{**cfg.vision.__dict__, "num_hidden_layers": 2}),
+                          text=cfg.text.__class__(**{**cfg.text.__dict__, "num_hidden_layers": 6}))
     eng = Stage1Engine.synthetic(cfg, gpu, seed=0)
     from projectiontrainer_amd import weights as W
     px, ids, labels = W.synthetic_batch(cfg, seed=7, max_pad=40)
@@ -182,9 +187,14 @@ def _bench_census(gpu):
     return got
 
 
+# (preset, batch) whose compared step must run every kernel family of the benchmarked step (census asserted)
+CENSUS_CASES = {("cfg2", 30), ("cfg5", 8)}
+
+
 @pytest.mark.slow
 @pytest.mark.parametrize("preset,bs,T,vl,tl", [("cfg2", 2, 128, None, None), ("cfg2", 1, 512, None, None),
-                                               ("cfg2", 30, 128, 2, 6), ("cfg5", 1, 256, 2, 6)])
+                                               ("cfg2", 30, 128, 2, 6), ("cfg5", 1, 256, 2, 6),
+                                               ("cfg5", 8, 256, 2, 6)])
 def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
     """Full architecture vs the fp32 CPU oracle (the oracle is pinned to the reference by the fixtures).
     cfg2: SigLIP-L/16-384 (24 layers) + Gemma3-1B (26 layers) at bs 2, T 128 (S = 703 > window 512,
@@ -199,7 +209,9 @@ def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
     launches also ran in this compared step.
     cfg5: Gemma3-4B dims (hidden 2560, GQA 8:4, window 1024, linear RoPE x8 on the full layer, vocab
     262 208 = 4 097 x 64, which leaves a remainder slice in the split-K lm_head backward) at 2 SigLIP and
-    6 Gemma layers, bs 1, T 256.
+    6 Gemma layers, bs 1, T 256, and at bs 8: the smallest batch whose dispatch census equals cfg5's
+    benchmarked bs-16 step's (tools/census_probe2.py cfg5: bs 1-6 and 10-14 each differ by a family;
+    train_projection_stage1.py:204-210 loads the 4B LLM the same way as the 1B).
     The HIP path runs the reference's bf16 flow (pure-bf16 SigLIP, bf16 GEMM operands) and the
     oracle fp32, so these tolerances bound the bf16-vs-fp32 difference of the whole step."""
     from oracle import stage1_ref as R
@@ -238,12 +250,12 @@ def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
     loss = float(loss)
     del eng, lm, vt
     torch.cuda.empty_cache()
-    if bs == 30:
-        bench = _bench_census(gpu)
+    if (preset, bs) in CENSUS_CASES:
+        bench = _bench_census(gpu, preset)
         record(f"arch[{preset}-bs{bs}-T{T}]", "paths", n_bench=len(bench), n_here=len(paths),
                missing=len(bench - paths))
-        assert bench <= paths, ("kernel families of the bs-32 step not exercised", sorted(bench - paths))
-        assert ("w4", 3) in paths and ("w4", 5) in paths, sorted(paths)   # gate|up GEGLU, dh + GEGLU bwd
+        assert bench <= paths, ("kernel families of the benchmarked step not exercised", sorted(bench - paths))
+        assert ("w4", 5) in paths, sorted(paths)   # dh + GEGLU bwd
     torch.set_num_threads(min(16, torch.get_num_threads()))
     st = R.init_state(pp)
     out = R.stage1_step(vp, cfg.vision, lp, cfg.text, st, (px, ids, labels), R.StepConfig(gradient_accumulation_steps=1),

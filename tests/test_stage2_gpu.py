@@ -322,8 +322,31 @@ def test_stage2_zero1_rccl_world1(gpu):
     assert r[0] == 1 and r[1] == 1 and r[2] == 1, r
 
 
+def _stage2_bench_census(gpu):
+    """The GEMM dispatch of one benchmarked Stage-2 micro-batch (cfg4, bs 16: forward, backward, every weight
+    grad) at 2 SigLIP + 6 Gemma layers (depth does not change the dispatch, tools/census_probe2.py)."""
+    from projectiontrainer_amd import _lib as L
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.stage2 import synthetic_engine
+    cfg = PRESETS["cfg4"]
+    cfg = cfg.replace(vision=cfg.vision.__class__(**{**cfg.vision.__dict__, "num_hidden_layers": 2}),
+                      text=cfg.text.__class__(**{**cfg.text.__dict__, "num_hidden_layers": 6}))
+    eng = synthetic_engine(cfg, gpu, seed=0, total_steps=10)
+    args = [torch.from_numpy(t).to(gpu) for t in W.synthetic_vqa_batch(cfg, seed=17, padding_side="left")]
+    eng.forward_backward(*args)
+    L.gemm_path_counts(reset=True)
+    eng.forward_backward(*args)
+    torch.cuda.synchronize()
+    got = set(L.gemm_path_counts(reset=True))
+    del eng
+    torch.cuda.empty_cache()
+    return got
+
+
 @pytest.mark.slow
-def test_stage2_architecture_scale_vs_oracle(gpu):
+@pytest.mark.parametrize("bs", [2, 8])
+def test_stage2_architecture_scale_vs_oracle(gpu, bs):
     """Stage 2 at cfg4's architecture (SigLIP-L/16-384 + Gemma3-1B widths, full vocab 262 144, question 64
     + answer 256 tokens, S = 895 > the 512-token window) at reduced depth (2 SigLIP, 6 Gemma layers: five
     sliding and one global) and bs 2, one micro-batch and one optimizer step, vs oracle/stage2_ref.py (pinned
@@ -331,7 +354,11 @@ def test_stage2_architecture_scale_vs_oracle(gpu):
     bf16-valued weights (the reference's bf16-loaded LLM, train_vqa_stage2.py:141-147); no twin fixture
     exists at these sizes, so the bars are SURVEY.md:297's with rel-L2 on the weight grads widened to 6e-2
     (the bf16-vs-fp32 distance the s2_tiny twins show, tests/golden/s2_tiny*.npz: up to 0.05); params
-    after AdamW within 2.5 lr + 1 bf16 ulp (Adam moves each weight by ~lr; bf16 parameters)."""
+    after AdamW within 2.5 lr + 1 bf16 ulp (Adam moves each weight by ~lr; bf16 parameters).
+    bs 8 (M = 7 168 token rows) is the smallest batch whose GEMM dispatch census equals the benchmarked bs-16
+    micro-batch's (tools/census_probe2.py stage2: bs 2-6 and 10-14 each differ by a family): the weight grads
+    over K = 7 168 tokens run the benchmarked paths (transposes, the stream-K / split-K GEMMs and their
+    reductions), asserted through ptk_gemm_path_counts."""
     from oracle import stage2_ref as S
     from projectiontrainer_amd import weights as W
     from projectiontrainer_amd.config import PRESETS
@@ -341,7 +368,7 @@ def test_stage2_architecture_scale_vs_oracle(gpu):
     from projectiontrainer_amd.stage2 import Stage2Engine
     cfg = PRESETS["cfg4"]
     cfg = cfg.replace(vision=cfg.vision.__class__(**{**cfg.vision.__dict__, "num_hidden_layers": 2}),
-                      text=cfg.text.__class__(**{**cfg.text.__dict__, "num_hidden_layers": 6}), batch_size=2)
+                      text=cfg.text.__class__(**{**cfg.text.__dict__, "num_hidden_layers": 6}), batch_size=bs)
     vp = {k: G.bf16_round(v) for k, v in W.siglip_vision_params(cfg.vision, seed=3).items()}
     lp = {k: G.bf16_round(v) for k, v in W.gemma3_params(cfg.text, seed=4).items()}
     pp = {k: G.bf16_round(v) for k, v in W.projector_params(cfg.vision.hidden_size, cfg.text.hidden_size,
@@ -355,14 +382,22 @@ def test_stage2_architecture_scale_vs_oracle(gpu):
                        Gemma3CausalLM(cfg.text, lp, gpu, max_pos=Gemma3CausalLM.seq_pad(cfg.seq_len)), proj,
                        learning_rate=lr, weight_decay=0.01, max_grad_norm=1.0, warmup_steps=0, total_steps=10,
                        pad_token_id=cfg.text.pad_token_id)
+    from projectiontrainer_amd import _lib as L
+    L.gemm_path_counts(reset=True)
     loss = float(eng.forward_backward(*(torch.from_numpy(t).to(gpu) for t in (px, q, a))))
     torch.cuda.synchronize()
+    paths = set(L.gemm_path_counts(reset=True))
     grads = {k: v.float().cpu() for k, v in eng.state.state_dict_hf(grads=True).items()}
     eng.optimizer_step()
     torch.cuda.synchronize()
     params = {k: v.float().cpu() for k, v in eng.state.state_dict_hf().items()}
     del eng
     torch.cuda.empty_cache()
+    t = f"stage2_arch[cfg4-L6-bs{bs}]"
+    if bs == 8:
+        bench = _stage2_bench_census(gpu)
+        record(t, "paths", n_bench=len(bench), n_here=len(paths), missing=len(bench - paths))
+        assert bench <= paths, ("kernel families of the bs-16 micro-batch not exercised", sorted(bench - paths))
     torch.set_num_threads(min(16, torch.get_num_threads()))
     st = S.Stage2State(lp)
     ref_loss = S.stage2_loss({k: torch.from_numpy(v) for k, v in vp.items()}, cfg.vision, st.params, cfg.text,
@@ -371,7 +406,6 @@ def test_stage2_architecture_scale_vs_oracle(gpu):
                              torch.from_numpy(q), torch.from_numpy(a), cfg.text.pad_token_id)
     ref_loss.backward()
     rec = S.optimizer_step(st, lr, 0, 10)
-    t = "stage2_arch[cfg4-L6-bs2]"
     record(t, "loss", abs=abs(loss - float(ref_loss)))
     assert abs(loss - float(ref_loss)) <= 2e-2, (loss, float(ref_loss))
     worst = 0.0
