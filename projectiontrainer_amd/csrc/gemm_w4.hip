@@ -35,6 +35,9 @@
 #ifndef PTK_W4_DMS
 #define PTK_W4_DMS 0      // diagnostic builds: DMA placement (1 = groups 8..15, 2 = groups 0..7, 3 = odd groups)
 #endif
+#ifndef PTK_P8_PRIO
+#define PTK_P8_PRIO 0     // diagnostic builds: static s_setprio of the p8 kernel's younger half (waves 4-7)
+#endif
 #ifndef PTK_W4_ABLATE
 #define PTK_W4_ABLATE 0   // diagnostic builds only: 1 = no DMA in the K loop, 2 = no fragment reads,
                           // 3 = the DMA re-reads one L2-resident K-tile, 4 = no K-loop barrier,
@@ -899,6 +902,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
   };
 
   auto run = [&](auto half_c) __attribute__((always_inline)) {
+    if (PTK_P8_PRIO && decltype(half_c)::value) __builtin_amdgcn_s_setprio(PTK_P8_PRIO);
     // prologue: k-steps 0..3 into slots 0..3; 0..2 landed and published; fragments of k-step 0 read
     dma_seg(0);
 #pragma unroll
@@ -992,17 +996,16 @@ size_t p8_tail_scratch_bytes() {
 constexpr double P8_HANDOFF_KTILES = 2.4;
 static P8Tail p8_tail_plan(const GemmArgs& a, long ntile, long G, int act, int out) {
   P8Tail tl;
-  void* ws = a.tail_ws ? a.tail_ws : tail_scope();
+  void* ws = a.tail_ws ? a.tail_ws : tail_scope();   // (the scope is lent only under PTK_STREAMK=1)
   if (!ws || act != ACT_NONE || (out != OUT_BF16 && out != OUT_F32 && out != OUT_F32_BFR)) return tl;
   const long R = ntile / G, T = ntile - R * G, nt = a.K / W4_KT;
   if (T == 0 || T * 8 * 4 > (long)P8_CNT_BYTES || (nt & 1)) return tl;
-  // where it measured faster (tools/sk_ab.py, profiles/r04_sk_ab.txt): few tail tiles -- a grid of at most 64
-  // tiles, or one full round plus at most 24 -- as the Stage-2 weight grads and the M = 14 336 projections
-  // are (0.43-0.80 of the unsplit time).  With more tail tiles the pieces of a tile stream different K ranges
-  // at the same time, the L2 sharing of a lock-step round is lost, and every Stage-1 shape measured slower
-  // (1.1-1.4x); PTK_NO_STREAMK=1 turns the tail off everywhere (A/B)
-  static const bool off = [] { const char* e = getenv("PTK_NO_STREAMK"); return e && e[0] == '1'; }();
-  if (off || !((R == 0 && T <= 64) || (R == 1 && T <= 24))) return tl;
+  // only few tail tiles -- a grid of at most 64 tiles, or one full round plus at most 24: where the tail split
+  // measured faster than the same launch unsplit (tools/sk_ab.py, profiles/r04_sk_ab.txt: Stage 2's weight grads
+  // and M = 14 336 projections at 0.43-0.80 of the time).  With more tail tiles the pieces of a tile stream
+  // different K ranges at the same time, the L2 sharing of a lock-step round is lost, and every Stage-1 shape
+  // measured slower (1.1-1.4x)
+  if (!((R == 0 && T <= 64) || (R == 1 && T <= 24))) return tl;
   const long U = T * (nt / 2);                                // tail units: pairs of K-tiles
   double best = (double)nt * 0.9;
   long bestG = 0;
@@ -1023,9 +1026,18 @@ static P8Tail p8_tail_plan(const GemmArgs& a, long ntile, long G, int act, int o
   return tl;
 }
 
+// The model-level calls lend their tail scratch only under PTK_STREAMK=1: on the whole step the stream-K tail
+// measured slower than the dispatch without it (r04, same box: Stage-2 cfg4 130.7 vs 137.0 img/s against its
+// split-K 128x128 weight grads; no Stage-1 shape qualifies), so it stays an opt-in of the model path and a
+// per-call option of ptk_gemm (ptk_gemm_desc.tail_ws)
+static bool streamk_models() {
+  static const bool v = [] { const char* e = getenv("PTK_STREAMK"); return e && e[0] == '1'; }();
+  return v;
+}
 static thread_local void* g_tail_scope = nullptr;
 void* tail_scope() { return g_tail_scope; }
 TailScratchScope::TailScratchScope(void* ws, hipStream_t st) : prev(g_tail_scope) {
+  if (!streamk_models()) ws = nullptr;
   g_tail_scope = ws;
   if (ws) status = launch_zero(ws, P8_CNT_BYTES, st);
 }
