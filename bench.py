@@ -51,6 +51,9 @@ def _args(argv=None):
                     help="replay each step's SigLIP/projector/Gemma3 launches from a HIP graph (Stage 1); auto = on "
                          "for per-GPU batches <= 4.  Off by default: measured equal at cfg1 (bs 2: 146 vs 147 img/s, "
                          "the kernels themselves, not their launches, set the step time) and at cfg2")
+    ap.add_argument("--stage-timers", action="store_true",
+                    help="after the timed window, run --steps more steps with the per-stage HIP event timers on "
+                         "(libptk stages.cpp) and add their per-step times to the line as stages_ms_per_step")
     ap.add_argument("--launch-check", action="store_true",
                     help="launcher plumbing only: every rank joins a gloo group, rank 0 prints the world; no GPU")
     return ap.parse_args(argv)
@@ -353,6 +356,17 @@ def main(argv=None):
         "flop_per_image": fpi, "loss": round(float(loss), 5), "host_wall_s_timed": round(t_wall, 3),
         "hip_graph": graph,
     }
+    if args.stage_timers and not graph:
+        # outside the timed window: the event records add host work per stage
+        L.stage_timers_enable(True)
+        L.stage_timers_read(reset=True)
+        for _ in range(args.steps):
+            step()
+        eng.join_prefetch()
+        torch.cuda.synchronize()
+        L.stage_timers_enable(False)
+        line["stages_ms_per_step"] = {k: round(ms / args.steps, 4)
+                                      for k, (ms, n) in L.stage_timers_read(reset=True).items()}
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         line["cpu_baseline"] = cpu_baseline(args.config)
         cb1 = cpu_baseline("cfg1", seconds_budget=20.0)

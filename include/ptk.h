@@ -143,6 +143,18 @@ int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
  * NULL; reset != 0 zeroes them afterwards.  Host-side counters, no GPU work. */
 int ptk_gemm_path_counts(int64_t* counts, int reset);
 
+/* Per-stage device timers (SURVEY §5 tracing; the reference has none).  Off unless PTK_STAGE_TIMERS=1 or
+ * ptk_stage_timers_enable(1).  The model entry points mark their pieces (siglip.fwd.*, gemma.fwd.*,
+ * gemma.lm_head_ce, gemma.bwd.*, projector.*); host code brackets its own with ptk_stage_begin / ptk_stage_end
+ * on a stream (spans nest per thread; a span begun while its stream is captured into a graph records
+ * nothing).  ptk_stage_timers_read waits for the recorded spans and writes "name\tms\tcount\n" per stage in
+ * first-seen order into buf (NUL-terminated, truncated to cap - 1); it returns the full report's length, or -1
+ * with ptk_last_error set; reset != 0 clears the totals afterwards. */
+int ptk_stage_timers_enable(int on);
+int ptk_stage_begin(const char* name, void* stream);
+int ptk_stage_end(void* stream);
+int64_t ptk_stage_timers_read(char* buf, size_t cap, int reset);
+
 /* Flash attention forward: O = softmax(scale * Q K^T + mask) V per z, bf16 in/out,
  * LSE (natural log) per query row.  z -> (z0, z1) = (z / batch_inner, z % batch_inner);
  * Q row r of z at Q + z0*sQ0 + z1*sQ1 + qmap(r)*ldq; keys/values at K/V + ... + k*ldk;

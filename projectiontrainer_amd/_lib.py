@@ -147,6 +147,10 @@ SIGNATURES = {
     "ptk_gemm_force_small_tiles": (c_int, [c_int]),
     "ptk_gemm_timer_read": (c_int, [c_int, C.POINTER(C.c_double), C.POINTER(c_int)]),
     "ptk_gemm_path_counts": (c_int, [c_void_p, c_int]),
+    "ptk_stage_timers_enable": (c_int, [c_int]),
+    "ptk_stage_begin": (c_int, [C.c_char_p, c_void_p]),
+    "ptk_stage_end": (c_int, [c_void_p]),
+    "ptk_stage_timers_read": (c_int64, [C.c_char_p, c_size_t, c_int]),
     "ptk_flash_attn_fwd": (c_int, [C.POINTER(FlashDesc), c_void_p]),
     "ptk_flash_attn_bwd": (c_int, [C.POINTER(FlashBwdDesc), c_void_p]),
     "ptk_flash_bwd_workspace_bytes": (c_size_t, [C.POINTER(FlashBwdDesc)]),
@@ -232,6 +236,52 @@ def gemm_path_counts(reset=False):
     buf = (C.c_int64 * (8 * len(GEMM_PATHS)))()
     check(lib().ptk_gemm_path_counts(buf, int(reset)), "gemm_path_counts")
     return {(GEMM_PATHS[i // 8], i % 8): int(v) for i, v in enumerate(buf) if v}
+
+
+_stages_on = os.environ.get("PTK_STAGE_TIMERS", "0") not in ("", "0")
+
+
+def stage_timers_enable(on=True):
+    """Per-stage device timers (stages.cpp; SURVEY §5 tracing) on or off for this process."""
+    global _stages_on
+    _stages_on = bool(on)
+    check(lib().ptk_stage_timers_enable(int(bool(on))), "stage_timers_enable")
+
+
+class stage:
+    """`with stage("projector.bwd", device):` brackets the enclosed launches on the current stream as one
+    stage (nothing is recorded unless the timers are on)."""
+
+    def __init__(self, name, device=None):
+        self.name, self.device, self.on = name, device, False
+
+    def __enter__(self):
+        self.on = _stages_on
+        if self.on:
+            self.st = stream_ptr(self.device)
+            check(lib().ptk_stage_begin(self.name.encode(), self.st), "stage_begin")
+        return self
+
+    def __exit__(self, *exc):
+        if self.on:
+            check(lib().ptk_stage_end(self.st), "stage_end")
+        return False
+
+
+def stage_timers_read(reset=False):
+    """{stage name: (total ms, spans)} recorded since the last reset (waits for the recorded spans)."""
+    n = lib().ptk_stage_timers_read(None, 0, 0)
+    if n < 0:
+        check(-1, "stage_timers_read")
+    buf = C.create_string_buffer(int(n) + 64)
+    n = lib().ptk_stage_timers_read(buf, len(buf), int(reset))
+    if n < 0:
+        check(-1, "stage_timers_read")
+    out = {}
+    for line in buf.value.decode().splitlines():
+        name, ms, cnt = line.split("\t")
+        out[name] = (float(ms), int(cnt))
+    return out
 
 
 def stream_ptr(device=None) -> int:

@@ -173,6 +173,7 @@ int ptk_projector_fwd(const ptk_projector* p, int rows, const void* x, void* a, 
   const int Dv = p->vision_dim, I = p->inter_dim, Dl = p->llm_dim;
   TailScratchScope tail(p->tail_ws, ST);
   if (tail.status) return -1;
+  StageScope stage("projector.fwd", ST);
   GemmArgs g1;
   g1.A = (const bf16_t*)x; g1.B = (const bf16_t*)p->w1; g1.C = h;
   g1.M = rows; g1.N = I; g1.K = Dv; g1.lda = Dv; g1.ldb = Dv; g1.ldc = I;
@@ -248,6 +249,7 @@ int ptk_projector_bwd(const ptk_projector* p, int rows, const void* x, const voi
                       float* dw1, float* db1, float* dw2, float* db2, void* ws, size_t ws_bytes, void* stream) {
   TailScratchScope tail(p->tail_ws, ST);
   if (tail.status) return -1;
+  StageScope stage("projector.bwd", ST);
   if (projector_bwd_stage(p, rows, x, a, h, dy, dw1, db1, dw2, db2, ws, ws_bytes, 0, ST)) return -1;
   return projector_bwd_stage(p, rows, x, a, h, dy, dw1, db1, dw2, db2, ws, ws_bytes, 1, ST);
 }

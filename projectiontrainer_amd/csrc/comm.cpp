@@ -148,6 +148,7 @@ int ptk_projector_bwd_allreduce(const ptk_projector* p, int rows, const void* x,
   hipStream_t st = (hipStream_t)stream, cs = (hipStream_t)comm_stream;
   TailScratchScope tail(p->tail_ws, st);
   if (tail.status) return -1;
+  StageScope stage("projector.bwd_allreduce", st);
   const long Dv = p->vision_dim, I = p->inter_dim, Dl = p->llm_dim;
   float* dw1 = flat_grad;
   float* db1 = dw1 + I * Dv;

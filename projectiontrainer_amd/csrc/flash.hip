@@ -346,7 +346,7 @@ constexpr int FA_MAXT = 128;   // key tiles (of 32) the mask table holds: nkeys 
 // diagnostic build (make fastamps): s_memtime stamps of the 32-row d-256 kernels' phases per workgroup, kept in
 // registers and written by lane 0 of wave 0 at the end (no extra memory op inside the counted-vmcnt pipeline)
 #ifdef PTK_FA_STAMPS
-__device__ unsigned long long g_fa_stamps[3][1 << 13][8];   // [kernel: fwd, dQ, dK/dV][workgroup][stamp]
+__device__ unsigned long long g_fa_stamps[4][1 << 13][8];   // [kernel: fwd, dQ, dK/dV, fwd64][workgroup][stamp]
 #define FA_STAMP(i) st_[i] = __builtin_amdgcn_s_memtime()
 #define FA_STAMPS_DECL unsigned long long st_[8] = {}; st_[5] = __builtin_amdgcn_s_memrealtime(); FA_STAMP(0)
 #define FA_STAMPS_WRITE(kid, ntiles)                                                               \
@@ -959,6 +959,7 @@ __global__ void __launch_bounds__(512, 2) attn_fwd64_kernel(FlashArgs a) {
   char* const kring = smem;
   char* const vring = smem + NB * TILE;
   uint32_t* const kmask_s = reinterpret_cast<uint32_t*>(smem + 2 * NB * TILE);   // 2 words per 64-key tile
+  FA_STAMPS_DECL;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1001,6 +1002,7 @@ __global__ void __launch_bounds__(512, 2) attn_fwd64_kernel(FlashArgs a) {
 #pragma unroll
   for (int ks = 0; ks < KS; ++ks) fa_pin(qf[ks]);
   __syncthreads();
+  FA_STAMP(1);
 
   const int causal = a.causal != 0, nowin = a.window <= 0;
   const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
@@ -1160,6 +1162,7 @@ __global__ void __launch_bounds__(512, 2) attn_fwd64_kernel(FlashArgs a) {
   };
   if (t_lo < t_hi) stage(0, t_lo);
   if (t_lo + 1 < t_hi) stage(1, t_lo + 1);
+  FA_STAMP(2);
   if (wave < 4) {
     for (int t = t_lo; t < t_hi;) {
       early(fa_ic<0>{}, t);
@@ -1183,6 +1186,7 @@ __global__ void __launch_bounds__(512, 2) attn_fwd64_kernel(FlashArgs a) {
       ++t;
     }
   }
+  FA_STAMP(3);
   if (qrow >= a.rows) return;
   const float inv = l_run > 0.f ? 1.f / l_run : 0.f;
   bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow) * a.ldo + 4 * g;
@@ -1195,6 +1199,7 @@ __global__ void __launch_bounds__(512, 2) attn_fwd64_kernel(FlashArgs a) {
   }
   if (a.lse && g == 0)
     a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_run)) * 0.6931471805599453f;
+  FA_STAMPS_WRITE(3, t_hi - t_lo);
 }
 
 // ---------------------------------------------------------------- dQ, head_dim 256, 32 rows per wave

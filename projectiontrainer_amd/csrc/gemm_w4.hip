@@ -36,7 +36,13 @@
 #define PTK_W4_DMS 0      // diagnostic builds: DMA placement (1 = groups 8..15, 2 = groups 0..7, 3 = odd groups)
 #endif
 #ifndef PTK_P8_PRIO
-#define PTK_P8_PRIO 0     // diagnostic builds: static s_setprio of the p8 kernel's younger half (waves 4-7)
+#define PTK_P8_PRIO 1     // static s_setprio of the p8 kernel's younger half (waves 4-7): the two waves of a SIMD
+                          // stop trading issue slots evenly and one runs ahead, so their LDS reads and MFMA
+                          // bursts interleave (A/B r04: 298.5 vs 296.4 img/s, 3 rounds; 0 = diagnostic off)
+#endif
+#ifndef PTK_P8_MPRIO
+#define PTK_P8_MPRIO 0    // diagnostic builds: s_setprio 1 around each p8 MFMA group (the issue arbitration
+                          // between the two waves of a SIMD favours the one issuing MFMAs)
 #endif
 #ifndef PTK_W4_ABLATE
 #define PTK_W4_ABLATE 0   // diagnostic builds only: 1 = no DMA in the K loop, 2 = no fragment reads,
@@ -873,11 +879,13 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
         if (pc & 1) W4_DMA(rsb, offb[pc >> 1], sb, db + (pc >> 1) * 1024);
         else W4_DMA(rsa, offa[pc >> 1], sa, da + (pc >> 1) * 1024);
       }
+      if (PTK_P8_MPRIO) asm volatile("s_setprio 1" ::: "memory");
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj) {
         if (first) W4_MFMA0(acc[q][jj], FB[jj], fa[q]);
         else W4_MFMA(acc[q][jj], FB[jj], fa[q]);
       }
+      if (PTK_P8_MPRIO) asm volatile("s_setprio 0" ::: "memory");
       if (rd && q >= 1) W4_DSREAD(fa[q - 1], ba, (q - 1) * 1024);   // one group after its last reader
     }
     if (rd) W4_DSREAD(fa[7], ba, 7 * 1024);

@@ -318,6 +318,9 @@ int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int
   SiglipWs w = siglip_layout(bp, c, B);
   TailScratchScope tail(w.tail, st);
   CK(tail.status);
+  StageScope stage_all("siglip.fwd", st);
+  StageSeq sq(st);
+  sq.next("siglip.embed");
 
   // K1 patch embed: im2col + GEMM; bf16(conv + bias) + pos -> bf16 residual stream (modeling_siglip.py:175-186)
   CK(launch_im2col((const bf16_t*)pixels, w.patches, B, c->channels, c->image_size, c->image_size, P, st));
@@ -330,6 +333,7 @@ int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int
   }
   for (int l = 0; l < c->layers; ++l) {
     const ptk_siglip_layer& L = wt->layers[l];
+    sq.next("siglip.attn");
     CK(launch_layernorm_bf16(w.h, L.ln1_w, L.ln1_b, w.a, M, D, c->eps, st));
     {  // fused q|k|v projection
       GemmArgs g = gemm(w.a, D, L.wqkv, D, w.qkv, 3 * D, M, 3 * D, D);
@@ -345,6 +349,7 @@ int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int
       fa.sQ0 = fa.sK0 = (long)Nn * 3 * D; fa.sQ1 = fa.sK1 = hd;
       fa.sO0 = (long)Nn * D; fa.sO1 = hd;
       fa.scale = 1.0f / sqrtf((float)hd);
+      StageScope sf("siglip.flash", st);
       CK(launch_attn_fwd(fa, B * Hh, st));
     }
     {  // h = bf16(h + bf16(out_proj + bias))   (modeling_siglip.py:343-346, bf16 module)
@@ -352,6 +357,7 @@ int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int
       g.bias = L.bo; g.bf16_linear = 1; g.resid16 = w.h; g.ld_resid16 = D;
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
     }
+    sq.next("siglip.mlp");
     CK(launch_layernorm_bf16(w.h, L.ln2_w, L.ln2_b, w.a, M, D, c->eps, st));
     {
       GemmArgs g = gemm(w.a, D, L.w1, D, w.mlp, I, M, I, D);
@@ -364,6 +370,7 @@ int ptk_siglip_fwd(const ptk_siglip_config* c, const ptk_siglip_weights* wt, int
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
     }
   }
+  sq.next("siglip.post_norm");
   CK(launch_layernorm_bf16(w.h, wt->post_w, wt->post_b, (bf16_t*)out, M, D, c->eps, st));
   return 0;
 }
@@ -411,6 +418,8 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
   AttnShape ash{B, Sp, Hq, Hkv, D};
   const RowMap ident{0, 0, 0, 0};
   const int Rp = (R + 63) / 64 * 64;
+  StageSeq sq(st);
+  sq.next("gemma.embed");
 
   // K11/K12: text embeddings (x bf16(sqrt H)), padded rows, key-valid mask; vision rows already in x
   const float escale = bfround_host(sqrtf((float)H));
@@ -434,6 +443,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
     bf16_t* xin = train ? sv.xn_in : w.xn;
     bf16_t* xff = train ? sv.xn_ff : w.xn;
     bf16_t* hh = train ? sv.h : w.h;
+    sq.next("gemma.fwd.attn");
     CK(gemm_split(gemm(xin, H, L.wqkv, H, sv.qkv, Dqkv, M, Dqkv, H), OUT_BF16, w.skpart, w.sk_floats, st));
     CK(launch_qknorm_rope_fwd(sv.qkv, L.q_norm, L.k_norm, cs, sn, ash, eps, sv.Q, sv.K, sv.V, sv.rstd_q, sv.rstd_k,
                               st));
@@ -450,11 +460,13 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
       fa.qdiv = G; fa.causal = 1; fa.window = sliding ? c->sliding_window : 0;
       fa.key_valid = w.key_valid;
       fa.scale = scale;
+      StageScope sf("gemma.fwd.flash", st);
       CK(launch_attn_fwd(fa, Z, st));
     }
     CK(gemm_split(gemm(sv.O, Dq, L.wo, Dq, sv.ao, H, M, H, Dq), OUT_BF16, w.skpart, w.sk_floats, st));
     CK(launch_residual_norm_fwd(sv.ao, w.x[l], L.ln_post_attn, L.ln_pre_ff, sv.x2, xff, sv.rstd_ao, sv.rstd_pre, M,
                                 H, eps, st));
+    sq.next("gemma.fwd.mlp");
     if (l + 1 < nl) {
       GemmArgs g = gemm(xff, H, L.wgu, H, hh, I, M, 2 * I, H);
       g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
@@ -480,6 +492,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
   }
 
   // ---------------- loss (text-predicting rows only)
+  sq.next("gemma.lm_head_ce");
   CK(launch_rmsnorm_fwd(w.x[nl], H, lossmap, wt->final_norm, w.xf, w.rstd_f, R, H, eps, st));
   {
     // lm_head: logits (bf16) plus, from the GEMM epilogue, each row's softmax statistics per 64 columns, so
@@ -499,6 +512,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
   }
   CK(launch_loss_reduce(w.row_loss, R, w.count, bt->loss, st));
   if (fwd_only) return 0;   // validation loss (no_grad): the CE pass's d(logits) is left unused
+  sq.next("gemma.lm_head_bwd");
   // tied lm_head weight grad: dE += dlogits^T . xf (the logits rows outside the loss rows have zero grad)
   if (train) CK(weight_grad(w.logits, V, ident, V, w.xf, H, ident, H, R, w.TL, w.TX, gr->embed, w.skpart, w.sk_floats, st));
   {  // d(xf) = dlogits . E, K = vocab: split-K over LM_SPLITK equal slices (fp32 partials, ordered sum);
@@ -530,6 +544,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
     const float* cs = sliding ? wt->rope_cos_local : wt->rope_cos_global;
     const float* sn = sliding ? wt->rope_sin_local : wt->rope_sin_global;
     const bool last = l == nl - 1;
+    sq.next("gemma.bwd.mlp");
     // MLP half
     // post-ff norm backward: for layers below the last it ran fused into the previous iteration's
     // input-norm backward (one pass over dR instead of two)
@@ -570,6 +585,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
       CK(launch_gemm(g2, ACT_NONE, OUT_BF16, 1, st));
     }
     if (train) CK(launch_rms_wgrad_bdy(sv.x2, H, ident, sv.rstd_pre, w.dtmp, H, M, H, (bf16_t*)GL->ln_pre_ff, w.wpart, st));
+    sq.next("gemma.bwd.attn");
     CK(launch_residual_norm_bwd_bdn(sv.x2, L.ln_pre_ff, sv.rstd_pre, w.dtmp, dR, sv.ao, L.ln_post_attn, sv.rstd_ao, w.dao,
                                 M, H, st));
     if (train) {
@@ -596,6 +612,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
       fb.key_valid = w.key_valid;
       fb.scale = scale;
       fb.dkv_part = w.dkv_part; fb.dkv_part_bytes = w.dkv_part_bytes;
+      StageScope sf("gemma.bwd.flash", st);
       // the k_norm weight grad reads the complete dK: the unfrozen path reduces split slabs in attn_bwd
       CK(launch_attn_bwd(fb, Z, st, (dkv_reduce_split() || train) ? nullptr : &dkv_plan));
     }
@@ -622,6 +639,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
     }
   }
   // input-embedding grads of every text token (tied with the lm_head grad above)
+  sq.next("gemma.embed_grad");
   if (train) CK(launch_embed_grad(bt->token_ids, B, T, Nv, Sp, H, escale, dR, (bf16_t*)gr->embed, st));
   return 0;
 }

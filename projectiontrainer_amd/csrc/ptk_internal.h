@@ -79,6 +79,29 @@ struct TailScratchScope {
   TailScratchScope(void* ws, hipStream_t st);
   ~TailScratchScope();
 };
+// per-stage device timers (stages.cpp; PTK_STAGE_TIMERS=1): spans of one stream, nested per thread
+bool stage_timers_on();
+void stage_begin(const char* name, hipStream_t st);
+int stage_end(hipStream_t st);
+struct StageScope {
+  hipStream_t st;
+  bool on;
+  StageScope(const char* name, hipStream_t s) : st(s), on(stage_timers_on()) { if (on) stage_begin(name, s); }
+  ~StageScope() { if (on) (void)stage_end(st); }
+};
+// consecutive stages of one stream: next(name) ends the previous one and begins `name`
+struct StageSeq {
+  hipStream_t st;
+  bool on, open = false;
+  explicit StageSeq(hipStream_t s) : st(s), on(stage_timers_on()) {}
+  void next(const char* name) {
+    if (!on) return;
+    if (open) (void)stage_end(st);
+    stage_begin(name, st);
+    open = true;
+  }
+  ~StageSeq() { if (on && open) (void)stage_end(st); }
+};
 // live GEMM timing per activation class (events recorded around each launch when enabled)
 void timer_enable(int on);
 void force_small_tiles(int mode);

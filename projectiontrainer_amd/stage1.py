@@ -143,11 +143,12 @@ class Stage1Engine:
                              f"input {tuple(px.shape)}")
         if pixel_values.device != px.device:
             raise ValueError(f"pixel_values on {pixel_values.device}, the vision tower runs on {px.device}")
-        if pixel_values.dtype == torch.bfloat16:
-            px.copy_(pixel_values)
-        else:
-            K.cast_bf16(pixel_values.contiguous(), px)
-        self.vision.forward_into(px, self.vis_bufs[i])
+        with L.stage("vision", self.device):
+            if pixel_values.dtype == torch.bfloat16:
+                px.copy_(pixel_values)
+            else:
+                K.cast_bf16(pixel_values.contiguous(), px)
+            self.vision.forward_into(px, self.vis_bufs[i])
 
     def forward_backward(self, pixel_values, token_ids, labels, next_pixel_values=None):
         """Everything up to (and including) the projector grads; returns loss (device [1]).
@@ -183,8 +184,9 @@ class Stage1Engine:
                 ready.record(self.vstream)
             self._prefetched = ready
             self._cur = j
-        self.llm.loss_and_input_grad(self.x, self.dx, token_ids, labels, self.N - 1,
-                                     1.0 / float(self.gas * self.gas), self.loss, pad_token_id=self.pad_token_id)
+        with L.stage("llm", self.device):
+            self.llm.loss_and_input_grad(self.x, self.dx, token_ids, labels, self.N - 1,
+                                         1.0 / float(self.gas * self.gas), self.loss, pad_token_id=self.pad_token_id)
         L.check(L.lib().ptk_gather_vision_grad(self.dx.data_ptr(), B, self.N, self.Sp, self.llm.cfg.hidden_size,
                                                self.dy.data_ptr(), L.stream_ptr(self.device)), "gather_vision_grad")
         if self.comm is not None:
@@ -240,18 +242,20 @@ class Stage1Engine:
         if self._exchanged:      # summed over the ranks inside the backward (RCCL, overlapped)
             grad_scale = 1.0 / self.world
         else:
-            grad_scale = allreduce_grads_chunked_(self.proj.flat_grad, grad_exchange_chunks(self.proj), self.world,
-                                                  self.pg)
+            with L.stage("grad_exchange", self.device):
+                grad_scale = allreduce_grads_chunked_(self.proj.flat_grad, grad_exchange_chunks(self.proj),
+                                                      self.world, self.pg)
         self._exchanged = False
         lr = self.lr0 * cosine_lambda(self.sched_step, self.warmup, self.total)
         self.opt_step += 1
         b1, b2 = self.betas
-        L.check(L.lib().ptk_clip_adamw(self.proj.flat.data_ptr(), self.proj.flat_grad.data_ptr(),
-                                       self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(), self.proj.flat.numel(),
-                                       grad_scale, self.max_norm, lr, b1, b2, self.eps, self.wd, self.opt_step,
-                                       self._partial.data_ptr(), self.grad_norm.data_ptr(),
-                                       L.stream_ptr(self.device)), "clip_adamw")
-        self.proj.refresh_shadows()
+        with L.stage("optimizer", self.device):
+            L.check(L.lib().ptk_clip_adamw(self.proj.flat.data_ptr(), self.proj.flat_grad.data_ptr(),
+                                           self.exp_avg.data_ptr(), self.exp_avg_sq.data_ptr(),
+                                           self.proj.flat.numel(), grad_scale, self.max_norm, lr, b1, b2, self.eps,
+                                           self.wd, self.opt_step, self._partial.data_ptr(),
+                                           self.grad_norm.data_ptr(), L.stream_ptr(self.device)), "clip_adamw")
+            self.proj.refresh_shadows()
         self.sched_step += self.world
         self.last_lr = lr
         return lr

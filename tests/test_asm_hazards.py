@@ -173,23 +173,23 @@ SPILL_BUDGET = {   # kernel symbol substring -> (sgpr_spill_count, vgpr_spill_co
     # the persistent kernels' epilogues read their arguments through a laundered kernarg pointer
     # (gemm_w4.hip kernarg_args, scalar loads): 0 spills, except the GELU-erf epilogues (the projector's) and
     # the stream-K tail variants' bookkeeping
-    "gemm_p8_kernelILi0ELi0ELb1E": (16, 0, 0),
-    "gemm_p8_kernelILi0ELi1ELb1E": (16, 0, 0),
-    "gemm_p8_kernelILi0ELi2ELb1E": (16, 0, 0),
+    "gemm_p8_kernelILi0ELi0ELb1E": (24, 0, 0),
+    "gemm_p8_kernelILi0ELi1ELb1E": (24, 0, 0),
+    "gemm_p8_kernelILi0ELi2ELb1E": (24, 0, 0),
     "gemm_p8_kernelILi1ELi0ELb0E": (4, 0, 0),
     "gemm_p8_kernelILi2ELi0ELb0E": (28, 0, 0),
     "gemm_p8_kernelILi4ELi0ELb0E": (20, 0, 0),
-    "gemm_big2_kernelILi0ELi0E": (27, 0, 0),
+    "gemm_big2_kernelILi0ELi0E": (28, 0, 0),   # + the stats_only early-out of the row-statistics epilogue
     "gemm_big2_kernelILi1ELi0E": (11, 0, 0),
     "gemm_big2_kernelILi2ELi0E": (25, 0, 0),
     "gemm_big2_kernelILi4ELi0E": (11, 0, 0),
-    "gemm_big_kernelILi0ELi0E": (27, 0, 0),
+    "gemm_big_kernelILi0ELi0E": (28, 0, 0),
     "gemm_big_kernelILi1ELi0E": (11, 0, 0),
     "gemm_big_kernelILi2ELi0E": (25, 0, 0),
     "gemm_big_kernelILi4ELi0E": (11, 0, 0),
     "gemm_nt_kernelILi2ELi0E": (5, 0, 0),
     "gemm_nt_kernelILi4ELi0E": (1, 0, 0),
-    "qknorm_rope_bwd_kernelILi4E": (28, 0, 0),
+    "qknorm_rope_bwd_kernelILi4E": (30, 0, 0),   # + the unrolled dK/dV piece loads
 }
 
 

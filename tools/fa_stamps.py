@@ -2,7 +2,8 @@
 (build/libptk_fastamps.so, `make -C projectiontrainer_amd/csrc fastamps`), at the cfg2 step's shape.
 Forward / dQ phases: 0 entry, 1 Q (dO, O) fragments + key masks, 2 first three K/V tiles landed + the first
 tile's MFMAs, 3 main loop done, 4 epilogue stores issued.  dK/dV: 1 = 2 K/V fragments loaded, 3 chunk loop
-done, 4 outputs stored.  usage: fa_stamps.py [window] [fwd|bwd].  Never used by tests or the bench."""
+done, 4 outputs stored.  usage: fa_stamps.py [window] [fwd|bwd|fwd64] (fwd64: SigLIP's
+d-64 forward, stamps 1 Q + masks, 2 first two tiles staged, 3 loop done).  Never used by tests or the bench."""
 import ctypes
 import json
 import os
@@ -15,13 +16,15 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from projectiontrainer_amd import _lib as L  # noqa: E402
 
-L.LIB_PATH = os.path.join(ROOT, "build", "libptk_fastamps.so")
+L.LIB_PATH = os.path.join(ROOT, "ablibs", "libptk_fastamps.so")   # make ablib AB_NAME=fastamps AB_SRC=flash.hip AB_DEFS=-DPTK_FA_STAMPS
 from projectiontrainer_amd import kernels as Kn  # noqa: E402
 
 lib = L.lib()
 lib.ptk_debug_fa_stamps_read.argtypes = [ctypes.c_void_p, ctypes.c_size_t]
 dev = torch.device("cuda:0")
 B, S, G, D = 32, 704, 4, 256
+if len(sys.argv) > 2 and sys.argv[2] == "fwd64":   # SigLIP: 32 images x 16 heads, 576 patches, d 64, no mask
+    B, S, G, D = 512, 576, 1, 64
 window = int(sys.argv[1]) if len(sys.argv) > 1 else 512
 what = sys.argv[2] if len(sys.argv) > 2 else "fwd"
 g = torch.Generator(device=dev).manual_seed(0)
@@ -32,8 +35,9 @@ kv[:, S - 1] = 0
 O = torch.zeros(B, S * G, D, dtype=torch.bfloat16, device=dev)
 lse = torch.zeros(B, S * G, dtype=torch.float32, device=dev)
 f = lambda: Kn.flash_attn(Q, Kt, Vt, O, lse=lse, ldq=D, ldk=D, ldo=D, strides=(S * G * D, 0, S * D, 0, S * G * D, 0),
-                          rows=S * G, nkeys=S, head_dim=D, batch=B, batch_inner=1, zdiv=1, qdiv=G, causal=True,
-                          window=window, key_valid=kv, scale=D ** -0.5)
+                          rows=S * G, nkeys=S, head_dim=D, batch=B, batch_inner=1, zdiv=1, qdiv=G,
+                          causal=what != "fwd64", window=window if what != "fwd64" else 0,
+                          key_valid=kv if what != "fwd64" else None, scale=D ** -0.5)
 f()
 if what == "bwd":
     dO = rnd(B, S * G, D)
@@ -44,7 +48,7 @@ if what == "bwd":
 for _ in range(100):
     f()
 torch.cuda.synchronize()
-buf = np.zeros((3, 1 << 13, 8), dtype=np.uint64)
+buf = np.zeros((4, 1 << 13, 8), dtype=np.uint64)
 assert lib.ptk_debug_fa_stamps_read(buf.ctypes.data, buf.nbytes) == 0
 
 
@@ -69,5 +73,5 @@ for _ in range(20):
 e1.record()
 torch.cuda.synchronize()
 print(json.dumps({"what": what, "window": window, "us": round(e0.elapsed_time(e1) / 20 * 1e3, 1)}))
-for kid, name in ((0, "fwd"),) if what == "fwd" else ((1, "dq"), (2, "dkv")):
+for kid, name in {"fwd": ((0, "fwd"),), "fwd64": ((3, "fwd64"),)}.get(what, ((1, "dq"), (2, "dkv"))):
     print(json.dumps(summary(buf[kid], name)))
