@@ -155,29 +155,9 @@ __global__ void __launch_bounds__(256) qknorm_rope_bwd_kernel(
         float acc[EPL];
 #pragma unroll
         for (int e = 0; e < EPL; ++e) acc[e] = 0.f;
-        int pc = 0;
-        for (; pc + 4 <= dkv_np; pc += 4) {   // four pieces' loads in flight, summed in piece order
-          float t[4][EPL];
+        for (int pc = 0; pc < dkv_np; ++pc) {
 #pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int e = 0; e < EPL; ++e) t[u][e] = src[(pc + u) * pstride + e];
-#pragma unroll
-          for (int u = 0; u < 4; ++u)
-#pragma unroll
-            for (int e = 0; e < EPL; ++e) acc[e] += t[u][e];
-        }
-        if (pc < dkv_np) {                    // the last 1..3 pieces, likewise
-          float t[3][EPL];
-#pragma unroll
-          for (int u = 0; u < 3; ++u)
-#pragma unroll
-            for (int e = 0; e < EPL; ++e) t[u][e] = pc + u < dkv_np ? src[(pc + u) * pstride + e] : 0.f;
-#pragma unroll
-          for (int u = 0; u < 3; ++u)
-            if (pc + u < dkv_np)
-#pragma unroll
-              for (int e = 0; e < EPL; ++e) acc[e] += t[u][e];
+          for (int e = 0; e < EPL; ++e) acc[e] += src[pc * pstride + e];
         }
         const float mul = which == 0 ? fb.scale : 1.f;
 #pragma unroll

@@ -35,6 +35,12 @@
 #ifndef PTK_W4_DMS
 #define PTK_W4_DMS 0      // diagnostic builds: DMA placement (1 = groups 8..15, 2 = groups 0..7, 3 = odd groups)
 #endif
+#ifndef PTK_W4_STAGE
+#define PTK_W4_STAGE 1    // bf16 epilogue stores staged through LDS, written line-wise (0: register layout, A/B)
+#endif
+#ifndef PTK_GBWD_SETS
+#define PTK_GBWD_SETS 3   // row blocks of g, u in flight in the GEGLU-backward epilogue (2: one block ahead, A/B)
+#endif
 #ifndef PTK_P8_PRIO
 #define PTK_P8_PRIO 1     // static s_setprio of the p8 kernel's younger half (waves 4-7): the two waves of a SIMD
                           // stop trading issue slots evenly and one runs ahead, so their LDS reads and MFMA
@@ -78,6 +84,23 @@ PTK_DEV void add8(float* v, const float* s) {
   v[0] += a.x; v[1] += a.y; v[2] += a.z; v[3] += a.w; v[4] += b.x; v[5] += b.y; v[6] += b.z; v[7] += b.w;
 }
 
+// diagnostic build (make ablib AB_NAME=p8stamps AB_SRC=gemm_w4.hip AB_DEFS=-DPTK_P8_STAMPS; tools/p8_stamps.py):
+// s_memtime stamps of wave 0 of the persistent GEMMs (w4 and p8) per segment -- 0 segment start, 1 first K-tile done (its end wait passed), 2 K loop
+// done, 3 epilogue issued -- kept in VGPR lanes (lane = segment) so no memory op enters the counted vmcnt
+// pipeline, written at the end; g_p8_epi_mode 1 skips the epilogue (wrong results: K-loop-only timing)
+#ifdef PTK_P8_STAMPS
+__device__ unsigned int g_p8_stamps[1024][4][64];
+__device__ int g_p8_epi_mode;
+#define P8_STAMP(K, S)                                                                   \
+  do {                                                                                   \
+    unsigned long long t_;                                                               \
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)); \
+    stv_[K] = lane == ((S) & 63) ? (unsigned int)t_ : stv_[K];                           \
+  } while (0)
+#else
+#define P8_STAMP(K, S) (void)0
+#endif
+
 // per-lane row state of one row block, computed once for its four 8-column groups: the row's
 // validity, its clamped index and the element offsets of its rows in C (after the row map), the
 // residual and the side inputs / outputs (the 64-bit products and the row-map division stay out of
@@ -110,7 +133,7 @@ PTK_DEV W4Row w4_row(const GemmArgs& p, long r) {
 
 // 8 consecutive columns [c, c+8) of one row (c % 8 == 0); rows r >= M, unmapped rows and columns
 // c >= N store into the sink
-template <int ACT, int OUT>
+template <int ACT, int OUT, bool STORE = true>
 PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char* sink) {
   const bool cin = c_ < p.N;                // N % 8 == 0: c < N covers all 8 columns
   const bool rv = w.rv && cin, sv = w.cv && cin;
@@ -151,7 +174,9 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
 #pragma unroll
     for (int e = 0; e < 8; ++e) v[e] += r[e];
   }
-  if constexpr (OUT == OUT_BF16) {
+  if constexpr (!STORE) {
+    return;   // the caller stores v (the staged bf16 epilogue)
+  } else if constexpr (OUT == OUT_BF16) {
     stbf8(sv ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + c : reinterpret_cast<bf16_t*>(sink), v);
   } else {
     if constexpr (OUT == OUT_F32_BFR) {
@@ -164,10 +189,49 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
   }
 }
 
+// Staged bf16 stores.  In the register layout a lane holds 8 consecutive columns of one row, so a store instruction
+// writes 16 rows x 64 B (p8) or 16 rows x 64 B in 4 column groups (w4); the write path pays per row touched, and
+// the epilogue of a 256x256 tile took ~11 k cycles (tools/p8_stamps.py, profiles/r04_gemm_epilogue_stamps.jsonl;
+// 8 rows x 128 B per instruction measured ~45 % less).  With a staging area the row block's values go to LDS
+// row-wise and come back line-wise: store s of the row block writes rows s*RPS.. of it, lane l the 16-B chunk
+// l % CPR of row l / CPR, i.e. whole rows of the wave's 16 NJ columns.  The staging area is the wave's own rows of
+// the ring slot nobody reads during the epilogue (the tile's last k-step in p8, the next tile's first in w4,
+// already in registers); even row blocks use its A part, odd ones its B part.
+constexpr uint32_t W4_NO_STAGE = 0xffffffffu;
+template <int CPR>   // 16-B chunks per staged row
+PTK_DEV uint32_t w4_stg_off(int rr, int ch) {   // 16-B chunk ch of staged row rr, XOR-swizzled: conflict-free
+  const int sw = CPR == 16 ? (rr & 15) : CPR == 8 ? ((rr >> 1) & 7) : ((rr >> 2) & 3);   // both for the row-wise
+  return (uint32_t)(rr * (CPR * 16) + ((ch ^ sw) << 4));                                // writes and line-wise reads
+}
+typedef __attribute__((ext_vector_type(4))) unsigned int w4_v4u;
+typedef __attribute__((address_space(3))) w4_v4u w4_lds_u4;
+PTK_DEV void w4_stg_put(uint32_t a, uint4 v) {
+  *reinterpret_cast<w4_lds_u4*>((uintptr_t)a) = w4_v4u{v.x, v.y, v.z, v.w};
+}
+// the staged 16 x 8 CPR block at sb to rows row0.. (through cmap when CMAP, else raw rows < M), columns
+// col0 + 8 ch (< ncol) of base / ld: store s writes rows s RPS .. s RPS + RPS - 1, lane l row l / CPR, chunk l % CPR
+template <int CPR, bool CMAP>
+PTK_DEV void w4_stg_flush(const GemmArgs& p, uint32_t sb, bf16_t* base, long ld, long row0, long col0, long ncol,
+                          int lane, char* sink) {
+  constexpr int RPS = 64 / CPR;
+  const int ch = lane % CPR;
+  const long c = col0 + 8 * ch;
+#pragma unroll
+  for (int st = 0; st < 16 / RPS; ++st) {
+    const int rr = st * RPS + lane / CPR;
+    const w4_v4u dv = *reinterpret_cast<const w4_lds_u4*>((uintptr_t)(sb + w4_stg_off<CPR>(rr, ch)));
+    const uint4 d = uint4{dv.x, dv.y, dv.z, dv.w};
+    const long gr = row0 + rr;
+    const long dr = gr < p.M && c < ncol ? (CMAP ? map_row32(p.cmap, (int)gr) : gr) : -1;
+    *reinterpret_cast<uint4*>(dr >= 0 ? reinterpret_cast<char*>(base + dr * ld + c) : sink) = d;
+  }
+}
+
 // row block I of the wave's tile: lane holds C[row0 + 16I + (lane&15)][col0 + 16j + 4(lane>>4) + e]
 // (one function per row block so every accumulator index is a compile-time constant)
 template <int ACT, int OUT, int I, int NJ = 8, bool AGPR = true>
-PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, int lane, char* sink) {
+PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, int lane, char* sink,
+                     uint32_t stg = W4_NO_STAGE) {
   // pin the accumulator reads to this row block (otherwise hipcc reads all 256 up front and spills); values
   // summed in VGPRs (the stream-K reducer) are pinned there instead
 #pragma unroll
@@ -180,6 +244,38 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
   const long r = row0 + 16 * I + (lane & 15);
   if constexpr (ACT == ACT_GEGLU) {
     const W4Row w = w4_row(p, r);
+    constexpr int CPR = NJ;   // a staged row: the wave's 8 NJ h columns
+    if constexpr (PTK_W4_STAGE && CPR >= 8) {
+      if (stg != W4_NO_STAGE) {   // g, u in the A part, h in the B part (16 x 16 NJ bytes each)
+        const uint32_t sg = stg, su = stg + 16 * CPR * 16, sh = stg + (uint32_t)W4_SOPB;
+#pragma unroll
+        for (int pp = 0; pp < NJ / 4; ++pp) {
+          f32x4_t g0 = a[4 * pp] * p.alpha, g1 = a[4 * pp + 2] * p.alpha;
+          f32x4_t u0 = a[4 * pp + 1] * p.alpha, u1 = a[4 * pp + 3] * p.alpha;
+          swap16(g0, g1);
+          swap16(u0, u1);
+          const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+          const float u[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+          uint32_t gp[4], up[4], hp[4];
+#pragma unroll
+          for (int e = 0; e < 8; e += 2) {
+            gp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{g[e], g[e + 1]}, bf16x2_t));
+            up[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{u[e], u[e + 1]}, bf16x2_t));
+            const f32x2_t hh = bfround2(gelu_tanh2(bf2x2(gp[e / 2]))) * bf2x2(up[e / 2]);
+            hp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(hh, bf16x2_t));
+          }
+          const uint32_t o = w4_stg_off<CPR>(lane & 15, 4 * pp + (cb >> 3));
+          if (p.aux) w4_stg_put(sg + o, uint4{gp[0], gp[1], gp[2], gp[3]});
+          if (p.aux2) w4_stg_put(su + o, uint4{up[0], up[1], up[2], up[3]});
+          w4_stg_put(sh + o, uint4{hp[0], hp[1], hp[2], hp[3]});
+        }
+        const long hr0 = row0 + 16 * I, hc0 = col0 / 2, hn = p.N / 2;
+        if (p.aux) w4_stg_flush<CPR, false>(p, sg, p.aux, p.ld_aux, hr0, hc0, hn, lane, sink);
+        if (p.aux2) w4_stg_flush<CPR, false>(p, su, p.aux2, p.ld_aux, hr0, hc0, hn, lane, sink);
+        w4_stg_flush<CPR, true>(p, sh, reinterpret_cast<bf16_t*>(p.C), p.ldc, hr0, hc0, hn, lane, sink);
+        return;
+      }
+    }
     // GEMM columns: 16-wide gate / up groups alternate (interleaved weights); tiles 4pp, 4pp+2 are
     // gate and 4pp+1, 4pp+3 up for h columns [col0/2 + 32pp, +32)
 #pragma unroll
@@ -209,6 +305,24 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
     }
   } else {
     const W4Row w = w4_row(p, r);
+    if constexpr (OUT == OUT_BF16 && PTK_W4_STAGE) {
+      if (stg != W4_NO_STAGE) {
+        const uint32_t sb = stg + ((I & 1) ? (uint32_t)W4_SOPB : 0u);
+#pragma unroll
+        for (int pp = 0; pp < NJ / 2; ++pp) {
+          f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
+          swap16(x, y);
+          float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+          w4_epi8<ACT, OUT, false>(p, w, col0 + 32 * pp + cb, v, sink);
+          u16x8_t u;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
+          w4_stg_put(sb + w4_stg_off<2 * NJ>(lane & 15, 4 * pp + (cb >> 3)), __builtin_bit_cast(uint4, u));
+        }
+        w4_stg_flush<2 * NJ, true>(p, sb, reinterpret_cast<bf16_t*>(p.C), p.ldc, row0 + 16 * I, col0, p.N, lane, sink);
+        return;
+      }
+    }
 #pragma unroll
     for (int pp = 0; pp < NJ / 2; ++pp) {
       f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
@@ -274,10 +388,32 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[2 * NP], long row0, lo
 
 // the wave's 128 x 16NJ accumulator tile (8 row blocks of NJ 16x16 MFMA tiles)
 template <int ACT, int OUT, int NJ = 8>
-PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, long col0, int lane) {
+PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, long col0, int lane,
+                         uint32_t stg = W4_NO_STAGE) {
   char* sink = g_w4_sink + lane * 64;
   if constexpr (ACT == ACT_GEGLU_BWD) {
     constexpr int NP = NJ / 2;
+    if constexpr (PTK_GBWD_SETS >= 3) {
+      // three row blocks' g, u in flight: block I+2's loads go out before block I's math
+      u16x8_t G0[NP], U0[NP], G1[NP], U1[NP], G2[NP], U2[NP];
+      w4_gbwd_load<0, NP>(p, row0, col0, lane, G0, U0);
+      w4_gbwd_load<1, NP>(p, row0, col0, lane, G1, U1);
+      w4_gbwd_load<2, NP>(p, row0, col0, lane, G2, U2);
+      w4_gbwd_rows<0, NP>(p, acc[0], row0, col0, lane, sink, G0, U0);
+      w4_gbwd_load<3, NP>(p, row0, col0, lane, G0, U0);
+      w4_gbwd_rows<1, NP>(p, acc[1], row0, col0, lane, sink, G1, U1);
+      w4_gbwd_load<4, NP>(p, row0, col0, lane, G1, U1);
+      w4_gbwd_rows<2, NP>(p, acc[2], row0, col0, lane, sink, G2, U2);
+      w4_gbwd_load<5, NP>(p, row0, col0, lane, G2, U2);
+      w4_gbwd_rows<3, NP>(p, acc[3], row0, col0, lane, sink, G0, U0);
+      w4_gbwd_load<6, NP>(p, row0, col0, lane, G0, U0);
+      w4_gbwd_rows<4, NP>(p, acc[4], row0, col0, lane, sink, G1, U1);
+      w4_gbwd_load<7, NP>(p, row0, col0, lane, G1, U1);
+      w4_gbwd_rows<5, NP>(p, acc[5], row0, col0, lane, sink, G2, U2);
+      w4_gbwd_rows<6, NP>(p, acc[6], row0, col0, lane, sink, G0, U0);
+      w4_gbwd_rows<7, NP>(p, acc[7], row0, col0, lane, sink, G1, U1);
+      return;
+    }
     u16x8_t G0[NP], U0[NP], G1[NP], U1[NP];
     w4_gbwd_load<0, NP>(p, row0, col0, lane, G0, U0);
     w4_gbwd_load<1, NP>(p, row0, col0, lane, G1, U1);
@@ -297,14 +433,14 @@ PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, lo
     w4_gbwd_rows<7, NP>(p, acc[7], row0, col0, lane, sink, G1, U1);
     return;
   }
-  w4_rows<ACT, OUT, 0, NJ>(p, acc[0], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 1, NJ>(p, acc[1], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 2, NJ>(p, acc[2], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 3, NJ>(p, acc[3], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 4, NJ>(p, acc[4], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 5, NJ>(p, acc[5], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 6, NJ>(p, acc[6], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 7, NJ>(p, acc[7], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 0, NJ>(p, acc[0], row0, col0, lane, sink, stg);
+  w4_rows<ACT, OUT, 1, NJ>(p, acc[1], row0, col0, lane, sink, stg);
+  w4_rows<ACT, OUT, 2, NJ>(p, acc[2], row0, col0, lane, sink, stg);
+  w4_rows<ACT, OUT, 3, NJ>(p, acc[3], row0, col0, lane, sink, stg);
+  w4_rows<ACT, OUT, 4, NJ>(p, acc[4], row0, col0, lane, sink, stg);
+  w4_rows<ACT, OUT, 5, NJ>(p, acc[5], row0, col0, lane, sink, stg);
+  w4_rows<ACT, OUT, 6, NJ>(p, acc[6], row0, col0, lane, sink, stg);
+  w4_rows<ACT, OUT, 7, NJ>(p, acc[7], row0, col0, lane, sink, stg);
 }
 
 // the kernel's own GemmArgs argument (offset 0 of the kernarg segment) behind a pointer the compiler cannot
@@ -370,6 +506,7 @@ PTK_DEV u32x4_t w4_rsrc(const void* base, uint32_t bytes) {
   return r;
 }
 PTK_DEV uint32_t lds_addr(const void* p) { return (uint32_t)(uintptr_t)(lds_ptr_t)p; }
+
 
 template <int ACT, int OUT>
 __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
@@ -548,7 +685,12 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
   // (two k-steps later) drains them too.
   uint32_t rs = W4_SLOT, ws = 4 * W4_SLOT;
   int t = loc, kt = 0;
+#ifdef PTK_P8_STAMPS
+  unsigned int stv_[4] = {0u, 0u, 0u, 0u};
+  const int em_ = g_p8_epi_mode;
+#endif
   for (int g = 0; g < total_ks; g += 2) {
+    if (kt == 0) P8_STAMP(0, (t - loc) / G);
     if (kt == 0) kstep(std::true_type{}, fa0, fb0, fa1, fb1, rs, ws);
     else kstep(std::false_type{}, fa0, fb0, fa1, fb1, rs, ws);
     W4_PIN(fa1, fb1);
@@ -563,14 +705,24 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 #if PTK_W4_ABLATE != 5
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 #endif
+    // tile end: every wave's reads of the next tile's first k-step (the epilogue's staging slot) are done before
+    // the barrier lets any wave write its staging rows there
+    if (kt == nt - 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #if PTK_W4_ABLATE != 4
     __builtin_amdgcn_s_barrier();
 #endif
+    if (kt == 0) P8_STAMP(1, (t - loc) / G);
     if (kt == nt - 1) {
+      P8_STAMP(2, (t - loc) / G);
       asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");   // MFMA D -> accumulator read wait states
       int bm, bn;
       w4_tile_coords(t, nbm, nbn, bm, bn);
-      w4_epilogue<ACT, OUT>(kernarg_args(), acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128, lane);
+#ifdef PTK_P8_STAMPS
+      if (em_ != 1)
+#endif
+      w4_epilogue<ACT, OUT>(kernarg_args(), acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128, lane,
+                            lds_dma + (rs + (W4_NSLOT - 1) * W4_SLOT) % (W4_NSLOT * W4_SLOT));
+      P8_STAMP(3, (t - loc) / G);
       t += G;
       kt = 0;
     } else {
@@ -578,6 +730,11 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
     }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup exits
+#ifdef PTK_P8_STAMPS
+  if (wave == 0 && blockIdx.x < 1024)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g_p8_stamps[blockIdx.x][k][lane] = stv_[k];
+#endif
 #undef W4_GROUP
 #undef W4_READ
 #undef W4_PIN
@@ -628,6 +785,9 @@ int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_
   num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   long grid = std::min<long>(ntile, max_grid > 0 ? max_grid : g_num_cu);
+#ifdef PTK_P8_STAMPS
+  if (const char* e = getenv("PTK_GEMM_GRID")) grid = std::min<long>(grid, atol(e));   // diagnostic: fewer CUs
+#endif
   const long arows = a.M + a.amap.off;
   const uint32_t ab = (uint32_t)std::min<double>((double)arows * a.lda * 2, 2147483000.0);
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
@@ -663,6 +823,7 @@ int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_
 // The ring, the DMA cursor and the one wait + barrier per pair of k-steps are w4's; the waits are vmcnt(4).
 namespace {
 constexpr int P8_PIECES = 4;   // LDS-DMA pieces per wave per k-step
+
 }
 
 // ---- stream-K tail (P8Tail; SK kernels only).  A tile grid whose last round fills the persistent grid badly
@@ -909,6 +1070,10 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     return (int)old == np - 1;
   };
 
+#ifdef PTK_P8_STAMPS
+  unsigned int stv_[4] = {0u, 0u, 0u, 0u};
+  const int em_ = g_p8_epi_mode;
+#endif
   auto run = [&](auto half_c) __attribute__((always_inline)) {
     if (PTK_P8_PRIO && decltype(half_c)::value) __builtin_amdgcn_s_setprio(PTK_P8_PRIO);
     // prologue: k-steps 0..3 into slots 0..3; 0..2 landed and published; fragments of k-step 0 read
@@ -951,15 +1116,22 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     for (int s = 0; s < nseg; ++s) {
       int t, k0, k1, tt;
       segment(s, t, k0, k1, tt);
+      P8_STAMP(0, s);
       pair(std::true_type{}, std::false_type{});   // (every segment spans >= 2 K-tiles: tail units are pairs)
+      P8_STAMP(1, s);
       for (int kt = k0 + 1; kt < k1 - 1; ++kt) pair(std::false_type{}, std::false_type{});
       pair(std::false_type{}, std::true_type{});
+      P8_STAMP(2, s);
       asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");   // MFMA D -> accumulator read wait states
       int bm, bn;
       w4_tile_coords(t, nbm, nbn, bm, bn);
       const long row0 = (long)bm * W4 + wr * 128, col0 = (long)bn * W4 + wc * 128 + hf * 64;
       if (!SK || tt < 0) {
-        w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane);
+#ifdef PTK_P8_STAMPS
+        if (em_ != 1)
+#endif
+        w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane,
+                                 lds_dma + (rs + (W4_NSLOT - 1) * W4_SLOT) % (W4_NSLOT * W4_SLOT));
       } else if constexpr (SK) {
         const uint32_t c = __builtin_amdgcn_readlane(segC, s);
         const int g0 = (int)(c & 1023u), np = (int)((c >> 10) & 1023u), s0 = (int)((c >> 20) & 1u);
@@ -973,6 +1145,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
           if (lane == 0) __hip_atomic_store(tl.cnt + tt * 8 + wave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
       }
+      P8_STAMP(3, s);
       // the next segment's first k-step (published by the barrier; harmless after the last).  Its slot is the
       // one the NEXT pair's second k-step restages (k-step i+6 lands in the slot of i+1), so a barrier keeps
       // a wave that finished its epilogue early from overwriting it before every wave has read it
@@ -984,8 +1157,23 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
   if (hf) run(std::integral_constant<int, 1>{});
   else run(std::integral_constant<int, 0>{});
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup exits
+#ifdef PTK_P8_STAMPS
+  if (wave == 0 && blockIdx.x < 1024)
+#pragma unroll
+    for (int k = 0; k < 4; ++k) g_p8_stamps[blockIdx.x][k][lane] = stv_[k];
+#endif
 }
 
+#ifdef PTK_P8_STAMPS
+}  // namespace ptk
+extern "C" int ptk_debug_p8_stamps_read(void* host, size_t bytes) {
+  return hipMemcpyFromSymbol(host, HIP_SYMBOL(ptk::g_p8_stamps), bytes, 0, hipMemcpyDeviceToHost) == hipSuccess ? 0 : -1;
+}
+extern "C" int ptk_debug_p8_epi_mode(int m) {
+  return hipMemcpyToSymbol(HIP_SYMBOL(ptk::g_p8_epi_mode), &m, sizeof(int), 0, hipMemcpyHostToDevice) == hipSuccess ? 0 : -1;
+}
+namespace ptk {
+#endif
 // the p8 path takes what the w4 path takes, at K >= 128 (a tile's first and last k-step pairs are peeled)
 bool p8_supported(const GemmArgs& a, int act, int out) { return a.K >= 128 && w4_supported(a, act, out); }
 
@@ -1061,7 +1249,10 @@ int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st) {
   num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   const P8Tail tl = p8_tail_plan(a, ntile, g_num_cu, act, out);
-  const long grid = tl.units ? g_num_cu : std::min<long>(ntile, g_num_cu);
+  long grid = tl.units ? g_num_cu : std::min<long>(ntile, g_num_cu);
+#ifdef PTK_P8_STAMPS
+  if (const char* e = getenv("PTK_GEMM_GRID")) grid = std::min<long>(grid, atol(e));   // diagnostic: fewer CUs
+#endif
   const long arows = a.M + a.amap.off;
   const uint32_t ab = (uint32_t)std::min<double>((double)arows * a.lda * 2, 2147483000.0);
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);

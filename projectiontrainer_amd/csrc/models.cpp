@@ -639,7 +639,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
     }
   }
   // input-embedding grads of every text token (tied with the lm_head grad above)
-  sq.next("gemma.embed_grad");
+  if (train) sq.next("gemma.embed_grad");
   if (train) CK(launch_embed_grad(bt->token_ids, B, T, Nv, Sp, H, escale, dR, (bf16_t*)gr->embed, st));
   return 0;
 }

@@ -98,19 +98,17 @@ __global__ void __launch_bounds__(256) residual_norm_fwd_kernel(
     const float* __restrict__ w_next, float* __restrict__ xo, bf16_t* __restrict__ n,
     float* __restrict__ rstd_t, float* __restrict__ rstd_x, long rows, int cols, float eps) {
   ROW_SETUP
-  float4 r[NV], xr[NV];   // t and the residual row xi both loaded up front (one memory round trip per row)
+  float4 r[NV];
   float q = 0.f;
 #pragma unroll
-  FOR_V { r[v] = ld4bf(t + row * cols + COL); xr[v] = ld4(xi + row * cols + COL); }
-#pragma unroll
-  FOR_V { q += dot4(r[v], r[v]); }
+  FOR_V { r[v] = ld4bf(t + row * cols + COL); q += dot4(r[v], r[v]); }
   const float rs = rsqrtf(warp_sum(q) / cols + eps);
   if (lane == 0) rstd_t[row] = rs;
   float q2 = 0.f;
 #pragma unroll
   FOR_V {
     float4 yv = bfr4(mul4(scl4(r[v], rs), onep(ld4(w_post + COL))));   // post-norm output is bf16
-    float4 xv = add4(xr[v], yv);                                        // fp32 residual stream
+    float4 xv = add4(ld4(xi + row * cols + COL), yv);                   // fp32 residual stream
     st4(xo + row * cols + COL, xv);
     r[v] = xv;
     q2 += dot4(xv, xv);
@@ -195,29 +193,25 @@ PTK_DEV void residual_norm_bwd_body(
     const float* __restrict__ w_post, const float* __restrict__ rstd_t, bf16_t* __restrict__ dt, long rows,
     int cols) {
   ROW_SETUP
-  // every input of the row (x2, dn, dR, t: 12 KiB at H 1152) is loaded up front, so the row costs one memory
-  // round trip instead of three (the dR and t loads used to wait behind the reductions)
-  float4 xv[NV], dv[NV], nd[NV], tv[NV];   // nd: the updated dR row, kept in registers for the post-norm pass
-#pragma unroll
-  FOR_V {
-    xv[v] = ld4(x2 + row * cols + COL);
-    dv[v] = ldx4(dn + row * cols + COL);
-    nd[v] = ld4(dR + row * cols + COL);
-    tv[v] = ld4bf(t + row * cols + COL);
-  }
-  const float rs_pre = rstd_pre[row], rs_t = rstd_t[row];
+  float4 nd[NV];   // the updated dR row stays in registers for the post-norm pass
   {
     const float* w = w_pre;
-    RMS_BWD_BODY(xv, dv, rs_pre, {
-      nd[v] = add4(nd[v], dxv);
+    float4 xv[NV], dv[NV];
+#pragma unroll
+    FOR_V { xv[v] = ld4(x2 + row * cols + COL); dv[v] = ldx4(dn + row * cols + COL); }
+    const float rs = rstd_pre[row];
+    RMS_BWD_BODY(xv, dv, rs, {
+      nd[v] = add4(ld4(dR + row * cols + COL), dxv);
       st4(dR + row * cols + COL, nd[v]);
     })
   }
   {
     const float* w = w_post;
+    const float rs = rstd_t[row];
+    float4 xv[NV], dv[NV];
 #pragma unroll
-    FOR_V { dv[v] = bfr4(nd[v]); }
-    RMS_BWD_BODY(tv, dv, rs_t, { st4bf(dt + row * cols + COL, dxv); })
+    FOR_V { xv[v] = ld4bf(t + row * cols + COL); dv[v] = bfr4(nd[v]); }
+    RMS_BWD_BODY(xv, dv, rs, { st4bf(dt + row * cols + COL, dxv); })
   }
 }
 template <int NV>

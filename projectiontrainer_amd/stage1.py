@@ -27,8 +27,8 @@ backward that reads it has run.
 """
 from __future__ import annotations
 
+import contextlib
 import math
-
 import os
 
 import torch
@@ -242,7 +242,7 @@ class Stage1Engine:
         if self._exchanged:      # summed over the ranks inside the backward (RCCL, overlapped)
             grad_scale = 1.0 / self.world
         else:
-            with L.stage("grad_exchange", self.device):
+            with L.stage("grad_exchange", self.device) if self.world > 1 else contextlib.nullcontext():
                 grad_scale = allreduce_grads_chunked_(self.proj.flat_grad, grad_exchange_chunks(self.proj),
                                                       self.world, self.pg)
         self._exchanged = False

@@ -189,7 +189,7 @@ SPILL_BUDGET = {   # kernel symbol substring -> (sgpr_spill_count, vgpr_spill_co
     "gemm_big_kernelILi4ELi0E": (11, 0, 0),
     "gemm_nt_kernelILi2ELi0E": (5, 0, 0),
     "gemm_nt_kernelILi4ELi0E": (1, 0, 0),
-    "qknorm_rope_bwd_kernelILi4E": (30, 0, 0),   # + the unrolled dK/dV piece loads
+    "qknorm_rope_bwd_kernelILi4E": (28, 0, 0),
 }
 
 
