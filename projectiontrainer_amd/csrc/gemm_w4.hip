@@ -35,11 +35,9 @@
 #ifndef PTK_W4_DMS
 #define PTK_W4_DMS 0      // diagnostic builds: DMA placement (1 = groups 8..15, 2 = groups 0..7, 3 = odd groups)
 #endif
-#ifndef PTK_W4_STAGE
-#define PTK_W4_STAGE 1    // bf16 epilogue stores staged through LDS, written line-wise (0: register layout, A/B)
-#endif
-#ifndef PTK_GBWD_SETS
-#define PTK_GBWD_SETS 3   // row blocks of g, u in flight in the GEGLU-backward epilogue (2: one block ahead, A/B)
+#ifndef PTK_W4_LINES
+#define PTK_W4_LINES 1    // bf16 epilogue stores as whole 128-B lines (row pairs exchanged by DPP): plain / GELU and
+                          // GEGLU-backward epilogues; 2 also gate|up; 0 the register layout (A/B)
 #endif
 #ifndef PTK_P8_PRIO
 #define PTK_P8_PRIO 1     // static s_setprio of the p8 kernel's younger half (waves 4-7): the two waves of a SIMD
@@ -175,7 +173,7 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
     for (int e = 0; e < 8; ++e) v[e] += r[e];
   }
   if constexpr (!STORE) {
-    return;   // the caller stores v (the staged bf16 epilogue)
+    return;   // the caller stores v (the whole-line bf16 stores)
   } else if constexpr (OUT == OUT_BF16) {
     stbf8(sv ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + c : reinterpret_cast<bf16_t*>(sink), v);
   } else {
@@ -189,49 +187,42 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
   }
 }
 
-// Staged bf16 stores.  In the register layout a lane holds 8 consecutive columns of one row, so a store instruction
-// writes 16 rows x 64 B (p8) or 16 rows x 64 B in 4 column groups (w4); the write path pays per row touched, and
-// the epilogue of a 256x256 tile took ~11 k cycles (tools/p8_stamps.py, profiles/r04_gemm_epilogue_stamps.jsonl;
-// 8 rows x 128 B per instruction measured ~45 % less).  With a staging area the row block's values go to LDS
-// row-wise and come back line-wise: store s of the row block writes rows s*RPS.. of it, lane l the 16-B chunk
-// l % CPR of row l / CPR, i.e. whole rows of the wave's 16 NJ columns.  The staging area is the wave's own rows of
-// the ring slot nobody reads during the epilogue (the tile's last k-step in p8, the next tile's first in w4,
-// already in registers); even row blocks use its A part, odd ones its B part.
-constexpr uint32_t W4_NO_STAGE = 0xffffffffu;
-template <int CPR>   // 16-B chunks per staged row
-PTK_DEV uint32_t w4_stg_off(int rr, int ch) {   // 16-B chunk ch of staged row rr, XOR-swizzled: conflict-free
-  const int sw = CPR == 16 ? (rr & 15) : CPR == 8 ? ((rr >> 1) & 7) : ((rr >> 2) & 3);   // both for the row-wise
-  return (uint32_t)(rr * (CPR * 16) + ((ch ^ sw) << 4));                                // writes and line-wise reads
+// Whole-line stores.  In the register layout lane (r = lane & 15, q = lane >> 4) holds 8 consecutive columns of row
+// r, so a store instruction writes 16 rows x 64 B: half of each 128-B line, the other half by the next instruction.
+// The persistent GEMMs' epilogues took 11-56 k cycles per tile (tools/p8_stamps.py,
+// profiles/r04_gemm_epilogue_stamps.jsonl) and the same stores written as whole lines measured ~40 % shorter.  For
+// two chunks X (row r, line chunk cx(q)) and Y (row r, line chunk cy(q)) that together cover a line of every row,
+// one DPP exchange with lane r ^ 8 (row_ror:8) lets store 1 write rows 0-7 and store 2 rows 8-15 whole: lanes
+// r < 8 store X at row r and the partner's X at row r + 8, lanes r >= 8 the partner's Y at row r - 8 and Y at row
+// r, both at chunk (r < 8 ? cx : cy).  The row offsets travel the same way.
+PTK_DEV uint32_t w4_x8(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false); }
+PTK_DEV long w4_x8(long v) {
+  const uint64_t u = (uint64_t)v;
+  return (long)(((uint64_t)w4_x8((uint32_t)(u >> 32)) << 32) | w4_x8((uint32_t)u));
 }
-typedef __attribute__((ext_vector_type(4))) unsigned int w4_v4u;
-typedef __attribute__((address_space(3))) w4_v4u w4_lds_u4;
-PTK_DEV void w4_stg_put(uint32_t a, uint4 v) {
-  *reinterpret_cast<w4_lds_u4*>((uintptr_t)a) = w4_v4u{v.x, v.y, v.z, v.w};
+PTK_DEV void w4_line_pair(const uint4& X, const uint4& Y, bool lo, uint4& d1, uint4& d2) {
+  const uint4 sel = lo ? Y : X;
+  const uint4 rcv = uint4{w4_x8(sel.x), w4_x8(sel.y), w4_x8(sel.z), w4_x8(sel.w)};
+  d1 = lo ? X : rcv;
+  d2 = lo ? rcv : Y;
 }
-// the staged 16 x 8 CPR block at sb to rows row0.. (through cmap when CMAP, else raw rows < M), columns
-// col0 + 8 ch (< ncol) of base / ld: store s writes rows s RPS .. s RPS + RPS - 1, lane l row l / CPR, chunk l % CPR
-template <int CPR, bool CMAP>
-PTK_DEV void w4_stg_flush(const GemmArgs& p, uint32_t sb, bf16_t* base, long ld, long row0, long col0, long ncol,
-                          int lane, char* sink) {
-  constexpr int RPS = 64 / CPR;
-  const int ch = lane % CPR;
-  const long c = col0 + 8 * ch;
+PTK_DEV uint4 w4_pack8(const float* v) {
+  u16x8_t u;
 #pragma unroll
-  for (int st = 0; st < 16 / RPS; ++st) {
-    const int rr = st * RPS + lane / CPR;
-    const w4_v4u dv = *reinterpret_cast<const w4_lds_u4*>((uintptr_t)(sb + w4_stg_off<CPR>(rr, ch)));
-    const uint4 d = uint4{dv.x, dv.y, dv.z, dv.w};
-    const long gr = row0 + rr;
-    const long dr = gr < p.M && c < ncol ? (CMAP ? map_row32(p.cmap, (int)gr) : gr) : -1;
-    *reinterpret_cast<uint4*>(dr >= 0 ? reinterpret_cast<char*>(base + dr * ld + c) : sink) = d;
-  }
+  for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
+  return __builtin_bit_cast(uint4, u);
+}
+// row offsets (elements) of the two stores of a row pair, -1 = sink: own is this lane's row (valid flag ok)
+PTK_DEV void w4_pair_rows(long own, bool ok, bool lo, long& o1, long& o2) {
+  const long mine = ok ? own : -1, part = w4_x8(mine);
+  o1 = lo ? mine : part;
+  o2 = lo ? part : mine;
 }
 
 // row block I of the wave's tile: lane holds C[row0 + 16I + (lane&15)][col0 + 16j + 4(lane>>4) + e]
 // (one function per row block so every accumulator index is a compile-time constant)
 template <int ACT, int OUT, int I, int NJ = 8, bool AGPR = true>
-PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, int lane, char* sink,
-                     uint32_t stg = W4_NO_STAGE) {
+PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, int lane, char* sink) {
   // pin the accumulator reads to this row block (otherwise hipcc reads all 256 up front and spills); values
   // summed in VGPRs (the stream-K reducer) are pinned there instead
 #pragma unroll
@@ -244,37 +235,53 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
   const long r = row0 + 16 * I + (lane & 15);
   if constexpr (ACT == ACT_GEGLU) {
     const W4Row w = w4_row(p, r);
-    constexpr int CPR = NJ;   // a staged row: the wave's 8 NJ h columns
-    if constexpr (PTK_W4_STAGE && CPR >= 8) {
-      if (stg != W4_NO_STAGE) {   // g, u in the A part, h in the B part (16 x 16 NJ bytes each)
-        const uint32_t sg = stg, su = stg + 16 * CPR * 16, sh = stg + (uint32_t)W4_SOPB;
+    if constexpr (PTK_W4_LINES >= 2 && NJ == 8) {
+      // (PTK_W4_LINES=2 only: measured slower on gate|up, 710 vs 696 us -- its three outputs' exchanges add VALU
+      // to an epilogue that is VALU-heavy already, profiles/r04_gemm_lines_ab.txt)
+      // the wave's 64 h columns are one line of every row: X = column pair 0 (line chunk cb / 8), Y = pair 1
+      const bool lo = (lane & 8) == 0;
+      long a1, a2, c1, c2;
+      w4_pair_rows(w.ro_aux, w.rv, lo, a1, a2);
+      w4_pair_rows(w.ro_c, w.cv, lo, c1, c2);
+      uint4 G[2], U[2], H[2];
 #pragma unroll
-        for (int pp = 0; pp < NJ / 4; ++pp) {
-          f32x4_t g0 = a[4 * pp] * p.alpha, g1 = a[4 * pp + 2] * p.alpha;
-          f32x4_t u0 = a[4 * pp + 1] * p.alpha, u1 = a[4 * pp + 3] * p.alpha;
-          swap16(g0, g1);
-          swap16(u0, u1);
-          const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
-          const float u[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-          uint32_t gp[4], up[4], hp[4];
+      for (int pp = 0; pp < 2; ++pp) {
+        f32x4_t g0 = a[4 * pp] * p.alpha, g1 = a[4 * pp + 2] * p.alpha;
+        f32x4_t u0 = a[4 * pp + 1] * p.alpha, u1 = a[4 * pp + 3] * p.alpha;
+        swap16(g0, g1);
+        swap16(u0, u1);
+        const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
+        const float u[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
+        uint32_t gp[4], up[4], hp[4];
 #pragma unroll
-          for (int e = 0; e < 8; e += 2) {
-            gp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{g[e], g[e + 1]}, bf16x2_t));
-            up[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{u[e], u[e + 1]}, bf16x2_t));
-            const f32x2_t hh = bfround2(gelu_tanh2(bf2x2(gp[e / 2]))) * bf2x2(up[e / 2]);
-            hp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(hh, bf16x2_t));
-          }
-          const uint32_t o = w4_stg_off<CPR>(lane & 15, 4 * pp + (cb >> 3));
-          if (p.aux) w4_stg_put(sg + o, uint4{gp[0], gp[1], gp[2], gp[3]});
-          if (p.aux2) w4_stg_put(su + o, uint4{up[0], up[1], up[2], up[3]});
-          w4_stg_put(sh + o, uint4{hp[0], hp[1], hp[2], hp[3]});
+        for (int e = 0; e < 8; e += 2) {
+          gp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{g[e], g[e + 1]}, bf16x2_t));
+          up[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{u[e], u[e + 1]}, bf16x2_t));
+          const f32x2_t hh = bfround2(gelu_tanh2(bf2x2(gp[e / 2]))) * bf2x2(up[e / 2]);
+          hp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(hh, bf16x2_t));
         }
-        const long hr0 = row0 + 16 * I, hc0 = col0 / 2, hn = p.N / 2;
-        if (p.aux) w4_stg_flush<CPR, false>(p, sg, p.aux, p.ld_aux, hr0, hc0, hn, lane, sink);
-        if (p.aux2) w4_stg_flush<CPR, false>(p, su, p.aux2, p.ld_aux, hr0, hc0, hn, lane, sink);
-        w4_stg_flush<CPR, true>(p, sh, reinterpret_cast<bf16_t*>(p.C), p.ldc, hr0, hc0, hn, lane, sink);
-        return;
+        G[pp] = uint4{gp[0], gp[1], gp[2], gp[3]};
+        U[pp] = uint4{up[0], up[1], up[2], up[3]};
+        H[pp] = uint4{hp[0], hp[1], hp[2], hp[3]};
       }
+      const long hc = col0 / 2 + (lo ? cb : 32 + cb);
+      const bool cin = 2 * hc < p.N;
+      uint4 d1, d2;
+      if (p.aux) {
+        w4_line_pair(G[0], G[1], lo, d1, d2);
+        *reinterpret_cast<uint4*>(a1 >= 0 && cin ? reinterpret_cast<char*>(p.aux + a1 + hc) : sink) = d1;
+        *reinterpret_cast<uint4*>(a2 >= 0 && cin ? reinterpret_cast<char*>(p.aux + a2 + hc) : sink) = d2;
+      }
+      if (p.aux2) {
+        w4_line_pair(U[0], U[1], lo, d1, d2);
+        *reinterpret_cast<uint4*>(a1 >= 0 && cin ? reinterpret_cast<char*>(p.aux2 + a1 + hc) : sink) = d1;
+        *reinterpret_cast<uint4*>(a2 >= 0 && cin ? reinterpret_cast<char*>(p.aux2 + a2 + hc) : sink) = d2;
+      }
+      w4_line_pair(H[0], H[1], lo, d1, d2);
+      bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+      *reinterpret_cast<uint4*>(c1 >= 0 && cin ? reinterpret_cast<char*>(C + c1 + hc) : sink) = d1;
+      *reinterpret_cast<uint4*>(c2 >= 0 && cin ? reinterpret_cast<char*>(C + c2 + hc) : sink) = d2;
+      return;
     }
     // GEMM columns: 16-wide gate / up groups alternate (interleaved weights); tiles 4pp, 4pp+2 are
     // gate and 4pp+1, 4pp+3 up for h columns [col0/2 + 32pp, +32)
@@ -305,23 +312,31 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
     }
   } else {
     const W4Row w = w4_row(p, r);
-    if constexpr (OUT == OUT_BF16 && PTK_W4_STAGE) {
-      if (stg != W4_NO_STAGE) {
-        const uint32_t sb = stg + ((I & 1) ? (uint32_t)W4_SOPB : 0u);
+    if constexpr (OUT == OUT_BF16 && PTK_W4_LINES) {
+      // column pairs (2m, 2m + 1) = the 64-column line m of every row: X = pair 2m (line chunk cb / 8), Y = 2m + 1
+      const bool lo = (lane & 8) == 0;
+      long o1, o2;
+      w4_pair_rows(w.ro_c, w.cv, lo, o1, o2);
 #pragma unroll
-        for (int pp = 0; pp < NJ / 2; ++pp) {
+      for (int m = 0; m < NJ / 4; ++m) {
+        uint4 X, Y;
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int pp = 2 * m + h;
           f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
           swap16(x, y);
           float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
           w4_epi8<ACT, OUT, false>(p, w, col0 + 32 * pp + cb, v, sink);
-          u16x8_t u;
-#pragma unroll
-          for (int e = 0; e < 8; ++e) u[e] = f2bf(v[e]);
-          w4_stg_put(sb + w4_stg_off<2 * NJ>(lane & 15, 4 * pp + (cb >> 3)), __builtin_bit_cast(uint4, u));
+          (h ? Y : X) = w4_pack8(v);
         }
-        w4_stg_flush<2 * NJ, true>(p, sb, reinterpret_cast<bf16_t*>(p.C), p.ldc, row0 + 16 * I, col0, p.N, lane, sink);
-        return;
+        uint4 d1, d2;
+        w4_line_pair(X, Y, lo, d1, d2);
+        const long c = col0 + 64 * m + (lo ? cb : 32 + cb);
+        bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+        *reinterpret_cast<uint4*>(o1 >= 0 && c < p.N ? reinterpret_cast<char*>(C + o1 + c) : sink) = d1;
+        *reinterpret_cast<uint4*>(o2 >= 0 && c < p.N ? reinterpret_cast<char*>(C + o2 + c) : sink) = d2;
       }
+      return;
     }
 #pragma unroll
     for (int pp = 0; pp < NJ / 2; ++pp) {
@@ -379,6 +394,20 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[2 * NP], long row0, lo
       du[e + 1] = b.y;
     }
     const long c = col0 + 32 * pp + cb;
+    if constexpr (PTK_W4_LINES) {
+      // column pair pp = output line pp of every row (64 dg | du columns): X = dg (line chunk 4 (cb >> 4) +
+      // ((cb >> 3) & 1)), Y = du (two chunks on)
+      const bool lo = (lane & 8) == 0;
+      long o1, o2;
+      w4_pair_rows(w.ro_c, w.cv, lo, o1, o2);
+      uint4 d1, d2;
+      w4_line_pair(w4_pack8(dg), w4_pack8(du), lo, d1, d2);
+      const long oc = 2 * col0 + 64 * pp + 8 * (4 * (cb >> 4) + ((cb >> 3) & 1) + (lo ? 0 : 2));
+      bf16_t* C = reinterpret_cast<bf16_t*>(p.C);
+      *reinterpret_cast<uint4*>(o1 >= 0 && c < p.N ? reinterpret_cast<char*>(C + o1 + oc) : sink) = d1;
+      *reinterpret_cast<uint4*>(o2 >= 0 && c < p.N ? reinterpret_cast<char*>(C + o2 + oc) : sink) = d2;
+      continue;
+    }
     bf16_t* o = w.cv && c < p.N ? reinterpret_cast<bf16_t*>(p.C) + w.ro_c + (c >> 4) * 32 + (c & 15)
                                 : reinterpret_cast<bf16_t*>(sink);
     stbf8(o, dg);
@@ -388,32 +417,10 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[2 * NP], long row0, lo
 
 // the wave's 128 x 16NJ accumulator tile (8 row blocks of NJ 16x16 MFMA tiles)
 template <int ACT, int OUT, int NJ = 8>
-PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, long col0, int lane,
-                         uint32_t stg = W4_NO_STAGE) {
+PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, long col0, int lane) {
   char* sink = g_w4_sink + lane * 64;
   if constexpr (ACT == ACT_GEGLU_BWD) {
     constexpr int NP = NJ / 2;
-    if constexpr (PTK_GBWD_SETS >= 3) {
-      // three row blocks' g, u in flight: block I+2's loads go out before block I's math
-      u16x8_t G0[NP], U0[NP], G1[NP], U1[NP], G2[NP], U2[NP];
-      w4_gbwd_load<0, NP>(p, row0, col0, lane, G0, U0);
-      w4_gbwd_load<1, NP>(p, row0, col0, lane, G1, U1);
-      w4_gbwd_load<2, NP>(p, row0, col0, lane, G2, U2);
-      w4_gbwd_rows<0, NP>(p, acc[0], row0, col0, lane, sink, G0, U0);
-      w4_gbwd_load<3, NP>(p, row0, col0, lane, G0, U0);
-      w4_gbwd_rows<1, NP>(p, acc[1], row0, col0, lane, sink, G1, U1);
-      w4_gbwd_load<4, NP>(p, row0, col0, lane, G1, U1);
-      w4_gbwd_rows<2, NP>(p, acc[2], row0, col0, lane, sink, G2, U2);
-      w4_gbwd_load<5, NP>(p, row0, col0, lane, G2, U2);
-      w4_gbwd_rows<3, NP>(p, acc[3], row0, col0, lane, sink, G0, U0);
-      w4_gbwd_load<6, NP>(p, row0, col0, lane, G0, U0);
-      w4_gbwd_rows<4, NP>(p, acc[4], row0, col0, lane, sink, G1, U1);
-      w4_gbwd_load<7, NP>(p, row0, col0, lane, G1, U1);
-      w4_gbwd_rows<5, NP>(p, acc[5], row0, col0, lane, sink, G2, U2);
-      w4_gbwd_rows<6, NP>(p, acc[6], row0, col0, lane, sink, G0, U0);
-      w4_gbwd_rows<7, NP>(p, acc[7], row0, col0, lane, sink, G1, U1);
-      return;
-    }
     u16x8_t G0[NP], U0[NP], G1[NP], U1[NP];
     w4_gbwd_load<0, NP>(p, row0, col0, lane, G0, U0);
     w4_gbwd_load<1, NP>(p, row0, col0, lane, G1, U1);
@@ -433,14 +440,14 @@ PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, lo
     w4_gbwd_rows<7, NP>(p, acc[7], row0, col0, lane, sink, G1, U1);
     return;
   }
-  w4_rows<ACT, OUT, 0, NJ>(p, acc[0], row0, col0, lane, sink, stg);
-  w4_rows<ACT, OUT, 1, NJ>(p, acc[1], row0, col0, lane, sink, stg);
-  w4_rows<ACT, OUT, 2, NJ>(p, acc[2], row0, col0, lane, sink, stg);
-  w4_rows<ACT, OUT, 3, NJ>(p, acc[3], row0, col0, lane, sink, stg);
-  w4_rows<ACT, OUT, 4, NJ>(p, acc[4], row0, col0, lane, sink, stg);
-  w4_rows<ACT, OUT, 5, NJ>(p, acc[5], row0, col0, lane, sink, stg);
-  w4_rows<ACT, OUT, 6, NJ>(p, acc[6], row0, col0, lane, sink, stg);
-  w4_rows<ACT, OUT, 7, NJ>(p, acc[7], row0, col0, lane, sink, stg);
+  w4_rows<ACT, OUT, 0, NJ>(p, acc[0], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 1, NJ>(p, acc[1], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 2, NJ>(p, acc[2], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 3, NJ>(p, acc[3], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 4, NJ>(p, acc[4], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 5, NJ>(p, acc[5], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 6, NJ>(p, acc[6], row0, col0, lane, sink);
+  w4_rows<ACT, OUT, 7, NJ>(p, acc[7], row0, col0, lane, sink);
 }
 
 // the kernel's own GemmArgs argument (offset 0 of the kernarg segment) behind a pointer the compiler cannot
@@ -705,9 +712,6 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 #if PTK_W4_ABLATE != 5
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
 #endif
-    // tile end: every wave's reads of the next tile's first k-step (the epilogue's staging slot) are done before
-    // the barrier lets any wave write its staging rows there
-    if (kt == nt - 1) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #if PTK_W4_ABLATE != 4
     __builtin_amdgcn_s_barrier();
 #endif
@@ -720,8 +724,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 #ifdef PTK_P8_STAMPS
       if (em_ != 1)
 #endif
-      w4_epilogue<ACT, OUT>(kernarg_args(), acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128, lane,
-                            lds_dma + (rs + (W4_NSLOT - 1) * W4_SLOT) % (W4_NSLOT * W4_SLOT));
+      w4_epilogue<ACT, OUT>(kernarg_args(), acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128, lane);
       P8_STAMP(3, (t - loc) / G);
       t += G;
       kt = 0;
@@ -1130,8 +1133,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
 #ifdef PTK_P8_STAMPS
         if (em_ != 1)
 #endif
-        w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane,
-                                 lds_dma + (rs + (W4_NSLOT - 1) * W4_SLOT) % (W4_NSLOT * W4_SLOT));
+        w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane);
       } else if constexpr (SK) {
         const uint32_t c = __builtin_amdgcn_readlane(segC, s);
         const int g0 = (int)(c & 1023u), np = (int)((c >> 10) & 1023u), s0 = (int)((c >> 20) & 1u);

@@ -179,6 +179,10 @@ SPILL_BUDGET = {   # kernel symbol substring -> (sgpr_spill_count, vgpr_spill_co
     "gemm_p8_kernelILi1ELi0ELb0E": (4, 0, 0),
     "gemm_p8_kernelILi2ELi0ELb0E": (28, 0, 0),
     "gemm_p8_kernelILi4ELi0ELb0E": (20, 0, 0),
+    # the 4-wave kernel's GELU-erf epilogues (not dispatched: the projector's GELU-erf shapes run on p8), with the
+    # whole-line stores' row-pair exchange
+    "gemm_w4_kernelILi2ELi0E": (18, 0, 0),
+    "gemm_w4_kernelILi4ELi0E": (14, 0, 0),
     "gemm_big2_kernelILi0ELi0E": (28, 0, 0),   # + the stats_only early-out of the row-statistics epilogue
     "gemm_big2_kernelILi1ELi0E": (11, 0, 0),
     "gemm_big2_kernelILi2ELi0E": (25, 0, 0),
