@@ -36,8 +36,10 @@
 #define PTK_W4_DMS 0      // diagnostic builds: DMA placement (1 = groups 8..15, 2 = groups 0..7, 3 = odd groups)
 #endif
 #ifndef PTK_W4_LINES
-#define PTK_W4_LINES 1    // bf16 epilogue stores as whole 128-B lines (row pairs exchanged by DPP): plain / GELU and
-                          // GEGLU-backward epilogues; 2 also gate|up; 0 the register layout (A/B)
+#define PTK_W4_LINES 1    // whole 128-B lines in the epilogues (row pairs exchanged by DPP), bit flags: 1 the bf16
+                          // stores of the plain / GELU and GEGLU-backward epilogues, 4 the gate|up stores (measured
+                          // slower, off); 0 the register layout everywhere (A/B).  (The GEGLU-backward g, u loads as
+                          // whole lines measured equal, 500.8 vs 494.1 us, and were removed.)
 #endif
 #ifndef PTK_P8_PRIO
 #define PTK_P8_PRIO 1     // static s_setprio of the p8 kernel's younger half (waves 4-7): the two waves of a SIMD
@@ -235,8 +237,8 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
   const long r = row0 + 16 * I + (lane & 15);
   if constexpr (ACT == ACT_GEGLU) {
     const W4Row w = w4_row(p, r);
-    if constexpr (PTK_W4_LINES >= 2 && NJ == 8) {
-      // (PTK_W4_LINES=2 only: measured slower on gate|up, 710 vs 696 us -- its three outputs' exchanges add VALU
+    if constexpr ((PTK_W4_LINES & 4) && NJ == 8) {
+      // (bit 4 only: measured slower on gate|up, 710 vs 696 us -- its three outputs' exchanges add VALU
       // to an epilogue that is VALU-heavy already, profiles/r04_gemm_lines_ab.txt)
       // the wave's 64 h columns are one line of every row: X = column pair 0 (line chunk cb / 8), Y = pair 1
       const bool lo = (lane & 8) == 0;
@@ -312,7 +314,7 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
     }
   } else {
     const W4Row w = w4_row(p, r);
-    if constexpr (OUT == OUT_BF16 && PTK_W4_LINES) {
+    if constexpr (OUT == OUT_BF16 && (PTK_W4_LINES & 1)) {
       // column pairs (2m, 2m + 1) = the 64-column line m of every row: X = pair 2m (line chunk cb / 8), Y = 2m + 1
       const bool lo = (lane & 8) == 0;
       long o1, o2;
@@ -394,7 +396,7 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[2 * NP], long row0, lo
       du[e + 1] = b.y;
     }
     const long c = col0 + 32 * pp + cb;
-    if constexpr (PTK_W4_LINES) {
+    if constexpr (PTK_W4_LINES & 1) {
       // column pair pp = output line pp of every row (64 dg | du columns): X = dg (line chunk 4 (cb >> 4) +
       // ((cb >> 3) & 1)), Y = du (two chunks on)
       const bool lo = (lane & 8) == 0;

@@ -72,3 +72,4 @@ def test_geglu_bwd_output_columns(pp):
         ch = 4 * (cb_of(q) >> 4) + ((cb_of(q) >> 3) & 1)
         assert 64 * pp + 8 * ch == (c >> 4) * 32 + (c & 15)
         assert 64 * pp + 8 * (ch + 2) == (c >> 4) * 32 + (c & 15) + 16
+

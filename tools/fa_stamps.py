@@ -16,7 +16,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 from projectiontrainer_amd import _lib as L  # noqa: E402
 
-L.LIB_PATH = os.path.join(ROOT, "ablibs", "libptk_fastamps.so")   # make ablib AB_NAME=fastamps AB_SRC=flash.hip AB_DEFS=-DPTK_FA_STAMPS
+L.LIB_PATH = os.environ.get("FA_STAMPS_LIB", os.path.join(ROOT, "ablibs", "libptk_fastamps.so"))   # make ablib AB_NAME=fastamps AB_SRC=flash.hip AB_DEFS=-DPTK_FA_STAMPS
 from projectiontrainer_amd import kernels as Kn  # noqa: E402
 
 lib = L.lib()
