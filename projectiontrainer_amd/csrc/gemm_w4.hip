@@ -197,16 +197,21 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
 // one DPP exchange with lane r ^ 8 (row_ror:8) lets store 1 write rows 0-7 and store 2 rows 8-15 whole: lanes
 // r < 8 store X at row r and the partner's X at row r + 8, lanes r >= 8 the partner's Y at row r - 8 and Y at row
 // r, both at chunk (r < 8 ? cx : cy).  The row offsets travel the same way.
-PTK_DEV uint32_t w4_x8(uint32_t v) { return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x128, 0xf, 0xf, false); }
-PTK_DEV long w4_x8(long v) {
-  const uint64_t u = (uint64_t)v;
-  return (long)(((uint64_t)w4_x8((uint32_t)(u >> 32)) << 32) | w4_x8((uint32_t)u));
+// keep `old` in lanes r < 8 (HI = false) or r >= 8 (HI = true) of each 16-lane row, take lane r ^ 8's `src` in
+// the others: one DPP move (row_ror:8, bank mask = the 4-lane banks written), no select
+template <bool HI>
+PTK_DEV uint32_t w4_x8(uint32_t old, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)old, (int)src, 0x128, 0xf, HI ? 0x3 : 0xc, false);
 }
-PTK_DEV void w4_line_pair(const uint4& X, const uint4& Y, bool lo, uint4& d1, uint4& d2) {
-  const uint4 sel = lo ? Y : X;
-  const uint4 rcv = uint4{w4_x8(sel.x), w4_x8(sel.y), w4_x8(sel.z), w4_x8(sel.w)};
-  d1 = lo ? X : rcv;
-  d2 = lo ? rcv : Y;
+template <bool HI>
+PTK_DEV uint4 w4_x8(const uint4& old, const uint4& src) {
+  return uint4{w4_x8<HI>(old.x, src.x), w4_x8<HI>(old.y, src.y), w4_x8<HI>(old.z, src.z), w4_x8<HI>(old.w, src.w)};
+}
+// store 1 (rows 0-7): X in lanes r < 8, the partner's Y in lanes r >= 8; store 2 (rows 8-15): the partner's X in
+// lanes r < 8, Y in lanes r >= 8
+PTK_DEV void w4_line_pair(const uint4& X, const uint4& Y, bool, uint4& d1, uint4& d2) {
+  d1 = w4_x8<false>(X, Y);
+  d2 = w4_x8<true>(Y, X);
 }
 PTK_DEV uint4 w4_pack8(const float* v) {
   u16x8_t u;
@@ -215,10 +220,11 @@ PTK_DEV uint4 w4_pack8(const float* v) {
   return __builtin_bit_cast(uint4, u);
 }
 // row offsets (elements) of the two stores of a row pair, -1 = sink: own is this lane's row (valid flag ok)
-PTK_DEV void w4_pair_rows(long own, bool ok, bool lo, long& o1, long& o2) {
-  const long mine = ok ? own : -1, part = w4_x8(mine);
-  o1 = lo ? mine : part;
-  o2 = lo ? part : mine;
+PTK_DEV void w4_pair_rows(long own, bool ok, bool, long& o1, long& o2) {
+  const uint64_t m = (uint64_t)(ok ? own : -1);
+  const uint32_t lo32 = (uint32_t)m, hi32 = (uint32_t)(m >> 32);
+  o1 = (long)(((uint64_t)w4_x8<false>(hi32, hi32) << 32) | w4_x8<false>(lo32, lo32));
+  o2 = (long)(((uint64_t)w4_x8<true>(hi32, hi32) << 32) | w4_x8<true>(lo32, lo32));
 }
 
 // row block I of the wave's tile: lane holds C[row0 + 16I + (lane&15)][col0 + 16j + 4(lane>>4) + e]
