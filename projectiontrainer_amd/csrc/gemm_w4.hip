@@ -2,7 +2,7 @@
 // tile per wave (256 accumulator registers: the kernel runs at one wave per SIMD with the full
 // 512-register file).
 //
-//   C[M,N] = epi( alpha * A[M,K] . B[N,K]^T )        (same contract as gemm_nt_kernel, batch 1)
+//   C[M,N] = epi( A[M,K] . B[N,K]^T )   (gemm_nt_kernel's contract at batch 1 and alpha = 1; other alphas go there)
 //
 // Why this shape: the Stage-1 step's projections are K = 1024..1536 deep, so a
 // 256x256 tile runs only 16..24 K-tiles and the per-tile prologue (first DMA round trip) and
@@ -139,7 +139,7 @@ PTK_DEV void w4_epi8(const GemmArgs& p, const W4Row& w, long c_, float* v, char*
   const bool rv = w.rv && cin, sv = w.cv && cin;
   const long c = cin ? c_ : 0;
   if (p.bias) add8(v, p.bias + c);
-  if (p.bf16_linear) {   // bf16(alpha acc + bias) before the row-add / bf16 residual (a bf16 nn.Linear)
+  if (p.bf16_linear) {   // bf16(acc + bias) before the row-add / bf16 residual (a bf16 nn.Linear)
 #pragma unroll
     for (int e = 0; e < 8; e += 2) {
       const f32x2_t y = bfround2(f32x2_t{v[e], v[e + 1]});
@@ -254,8 +254,8 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
       uint4 G[2], U[2], H[2];
 #pragma unroll
       for (int pp = 0; pp < 2; ++pp) {
-        f32x4_t g0 = a[4 * pp] * p.alpha, g1 = a[4 * pp + 2] * p.alpha;
-        f32x4_t u0 = a[4 * pp + 1] * p.alpha, u1 = a[4 * pp + 3] * p.alpha;
+        f32x4_t g0 = a[4 * pp], g1 = a[4 * pp + 2];
+        f32x4_t u0 = a[4 * pp + 1], u1 = a[4 * pp + 3];
         swap16(g0, g1);
         swap16(u0, u1);
         const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
@@ -295,8 +295,8 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
     // gate and 4pp+1, 4pp+3 up for h columns [col0/2 + 32pp, +32)
 #pragma unroll
     for (int pp = 0; pp < NJ / 4; ++pp) {
-      f32x4_t g0 = a[4 * pp] * p.alpha, g1 = a[4 * pp + 2] * p.alpha;
-      f32x4_t u0 = a[4 * pp + 1] * p.alpha, u1 = a[4 * pp + 3] * p.alpha;
+      f32x4_t g0 = a[4 * pp], g1 = a[4 * pp + 2];
+      f32x4_t u0 = a[4 * pp + 1], u1 = a[4 * pp + 3];
       swap16(g0, g1);
       swap16(u0, u1);
       const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
@@ -331,7 +331,7 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
 #pragma unroll
         for (int h = 0; h < 2; ++h) {
           const int pp = 2 * m + h;
-          f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
+          f32x4_t x = a[2 * pp], y = a[2 * pp + 1];
           swap16(x, y);
           float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
           w4_epi8<ACT, OUT, false>(p, w, col0 + 32 * pp + cb, v, sink);
@@ -348,7 +348,7 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
     }
 #pragma unroll
     for (int pp = 0; pp < NJ / 2; ++pp) {
-      f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
+      f32x4_t x = a[2 * pp], y = a[2 * pp + 1];
       swap16(x, y);
       float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
       w4_epi8<ACT, OUT>(p, w, col0 + 32 * pp + cb, v, sink);
@@ -384,7 +384,7 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[2 * NP], long row0, lo
   const W4Row w = w4_row(p, r);
 #pragma unroll
   for (int pp = 0; pp < NP; ++pp) {
-    f32x4_t x = a[2 * pp] * p.alpha, y = a[2 * pp + 1] * p.alpha;
+    f32x4_t x = a[2 * pp], y = a[2 * pp + 1];
     swap16(x, y);
     const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
     const uint4 gw = __builtin_bit_cast(uint4, G[pp]), uw = __builtin_bit_cast(uint4, U[pp]);
@@ -755,6 +755,7 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 // N % 8 == 0, byte extents of A and B below 2^31 (32-bit buffer offsets)
 bool w4_supported(const GemmArgs& a, int act, int out) {
   if (a.N % 8 || a.K % W4_KT) return false;
+  if (a.alpha != 1.f) return false;   // the persistent epilogues take the accumulators as they are (no scale)
   if (a.row_stats) return false;   // the softmax-statistics epilogue lives in gemm.hip's epilogue only
   if (a.resid16 && (out != OUT_BF16 || a.ld_resid16 % 8)) return false;
   if ((a.ldc % 8) || (a.resid && a.ld_resid % 4) || (a.rowadd && a.ld_rowadd % 4)) return false;
