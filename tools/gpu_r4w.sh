@@ -1,6 +1,6 @@
 #!/bin/bash
-# round-4: the 128x128 GEMM's K loop as a 4-slot ring of 32-deep k-steps (k-step s+3 in flight) instead of the
-# double-buffered 64-deep form: GEMM + golden tests, step-shape GEMM timings new / previous, step A/B
+# round-4: the 128x128 GEMM with the MFMA operands swapped (transposed accumulator layout) so the epilogue stages its
+# accumulators by 16-B LDS stores instead of 4-B ones: GEMM + golden tests, step-shape GEMM timings new / previous, step A/B
 set -o pipefail
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
