@@ -123,6 +123,11 @@ int ptk_cross_entropy(void* logits, int64_t ld, int rows, int vocab, const int64
                       const float* gscale, void* stream);
 int ptk_transpose_bf16(const void* in, int64_t ld_in, void* out, int64_t ld_out, int nz, int64_t s_in,
                        int64_t s_out, int rows, int cols, int rows_pad, void* stream);
+/* Stage-2 weight-grad operand transpose with a row gather: out[c][r] = in[map(r)][c] for r < rows, 0 for
+ * rows <= r < rows_pad; map(r) = (r / g) * gs + (r % g) + off (g = 0: r + off).  The token-major dY / X of
+ * dW = dY^T X (Stage2/trainer.py:400-441 autograd) become K-contiguous operands of the library's GEMMs. */
+int ptk_transpose_rows_bf16(const void* in, int64_t ld_in, int map_g, int64_t map_gs, int64_t map_off, int rows,
+                            int cols, void* out, int64_t ld_out, int rows_pad, void* stream);
 int ptk_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream);
 int ptk_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float std, float mean, void* stream);
 /* Live GEMM timing: when enabled, HIP events are recorded on the launch stream

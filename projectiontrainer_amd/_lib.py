@@ -141,6 +141,8 @@ SIGNATURES = {
     "ptk_cross_entropy": (c_int, [c_void_p, c_int64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ptk_transpose_bf16": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_int, c_int64, c_int64, c_int,
                                    c_int, c_int, c_void_p]),
+    "ptk_transpose_rows_bf16": (c_int, [c_void_p, c_int64, c_int, c_int64, c_int64, c_int, c_int, c_void_p, c_int64,
+                                        c_int, c_void_p]),
     "ptk_cast_f32_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "ptk_fill_normal_bf16": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_void_p]),
     "ptk_gemm_timer_enable": (c_int, [c_int]),

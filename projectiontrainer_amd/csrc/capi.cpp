@@ -107,6 +107,12 @@ int ptk_transpose_bf16(const void* in, int64_t ld_in, void* out, int64_t ld_out,
                           rows_pad, ST);
 }
 
+int ptk_transpose_rows_bf16(const void* in, int64_t ld_in, int map_g, int64_t map_gs, int64_t map_off, int rows,
+                            int cols, void* out, int64_t ld_out, int rows_pad, void* stream) {
+  const RowMap m{map_g, 0, map_gs, map_off};
+  return launch_transpose_rows((const bf16_t*)in, ld_in, m, rows, cols, (bf16_t*)out, ld_out, rows_pad, ST);
+}
+
 int ptk_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream) {
   return launch_cast_f32_bf16(in, (bf16_t*)out, n, ST);
 }

@@ -133,6 +133,19 @@ def cross_entropy_(logits, targets, gscale):
     return row_loss
 
 
+def transpose_rows(x, rows, rows_pad, map_g=0, map_gs=0, map_off=0, ld_out=None):
+    """Stage-2 weight-grad operand transpose (ptk_transpose_rows_bf16): out[c][r] = x[map(r)][c] for r < rows,
+    0 up to rows_pad; map(r) = (r // g) * gs + r % g + off (g = 0: r + off).  x: 2-D bf16, row stride x.stride(0)."""
+    if x.dtype != torch.bfloat16 or x.dim() != 2 or x.stride(1) != 1:
+        raise L.PtkError("transpose_rows: x must be a 2-D bf16 tensor with unit column stride")
+    cols = x.shape[1]
+    ld = rows_pad if ld_out is None else ld_out
+    out = torch.empty((cols, ld), dtype=torch.bfloat16, device=x.device)
+    check(L.lib().ptk_transpose_rows_bf16(ptr(x), x.stride(0), map_g, map_gs, map_off, rows, cols, ptr(out), ld,
+                                          rows_pad, L.stream_ptr(x.device)), "transpose_rows")
+    return out
+
+
 def transpose(x, rows_pad=None, out=None):
     """[Z, rows, cols] or [rows, cols] bf16 -> [.., cols, rows_pad] (zero-padded); out: preallocated result."""
     squeeze = x.dim() == 2

@@ -217,6 +217,24 @@ def test_transpose(gpu):
     assert t[..., 100:].abs().sum() == 0
 
 
+@pytest.mark.parametrize("rows,cols,rows_pad,map_g,map_gs,map_off,ld_extra", [
+    (14336, 1152, 14336, 0, 0, 0, 8),        # Stage-2 weight-grad operand (16-B path), padded input rows
+    (1000, 200, 1024, 0, 0, 24, 0),          # rows not a tile multiple, zero padding, row offset
+    (700, 64, 768, 175, 224, 0, 0),          # gathered rows (per-sample groups)
+    (130, 36, 192, 0, 0, 0, 0),              # cols % 8 != 0: the 8-B fallback kernel
+])
+def test_transpose_rows_gathered(gpu, rows, cols, rows_pad, map_g, map_gs, map_off, ld_extra):
+    """Bit-exact: out[c][r] = x[map(r)][c] for r < rows, zeros to rows_pad (train.hip transpose_rows)."""
+    Kn, L = _k()
+    n_src = (rows // map_g) * map_gs + map_g if map_g else rows + map_off
+    x = rnd(n_src, cols + ld_extra, dev=gpu, seed=23)[:, :cols]
+    t = Kn.transpose_rows(x, rows, rows_pad, map_g, map_gs, map_off)
+    r = torch.arange(rows, device=gpu)
+    src = (r // map_g) * map_gs + r % map_g if map_g else r + map_off
+    assert torch.equal(t[:, :rows], x[src].t())
+    assert t[:, rows:].abs().sum() == 0
+
+
 def test_cross_entropy(gpu):
     Kn, L = _k()
     R, V = 33, 4096
