@@ -328,21 +328,8 @@ __device__ int g_epi_mode;   // 0 normal, 1 no global stores, 2 no epilogue
 #define PTK_STAMP(i)
 #endif
 
-// diagnostic ablations of the 256x256 kernel's K loop (timing only, wrong results): 1 = no LDS-DMA,
-// 4 = no barriers
-#ifndef PTK_BIG_ABLATE
-#define PTK_BIG_ABLATE 0
-#endif
-#if PTK_BIG_ABLATE == 4
-#define PTK_BIG_BAR() ((void)0)
-#else
 #define PTK_BIG_BAR() __builtin_amdgcn_s_barrier()
-#endif
-#if PTK_BIG_ABLATE == 1
-#define PTK_BIG_STAGE(h, t) ((void)0)
-#else
 #define PTK_BIG_STAGE(h, t) stage(h, t)
-#endif
 
 template <int ACT, int OUT>
 __global__ void __launch_bounds__(512, 1) gemm_big_kernel(GemmArgs p) {
@@ -834,7 +821,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);
     count_path(sk ? GEMM_PATH_P8SK : GEMM_PATH_P8, act);
-    const int rc = launch_gemm_p8(a, act, out, st);
+    const int rc = launch_gemm_p8(a, act, out, st, sk != 0);
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
   }

@@ -50,11 +50,6 @@
 #define PTK_P8_MPRIO 0    // diagnostic builds: s_setprio 1 around each p8 MFMA group (the issue arbitration
                           // between the two waves of a SIMD favours the one issuing MFMAs)
 #endif
-#ifndef PTK_W4_ABLATE
-#define PTK_W4_ABLATE 0   // diagnostic builds only: 1 = no DMA in the K loop, 2 = no fragment reads,
-                          // 3 = the DMA re-reads one L2-resident K-tile, 4 = no K-loop barrier,
-                          // 5 = no K-loop vmcnt wait
-#endif
 
 namespace ptk {
 
@@ -626,14 +621,9 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
     constexpr bool first = decltype(first_c)::value;
     const uint32_t ba = frag_a + rs, bb = frag_b + rs;
     const uint32_t da = lds_dma + ws, db = da + W4_SOPB;
-#if PTK_W4_ABLATE == 3
-    const uint32_t sa = dsa, sb = dsb;   // always k-step 0 of the tile: L2-resident (timing only)
-#else
     const uint32_t sa = dsa + dks * (W4_KS * 2), sb = dsb + dks * (W4_KS * 2);
-#endif
 #pragma unroll
     for (int q = 0; q < 16; ++q) {
-#if PTK_W4_ABLATE != 2
 #if PTK_W4_RDS == 1
       if (q < 8) {
         W4_READ(NA, NB, ba, bb, 2 * q);
@@ -647,8 +637,6 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
         W4_READ(NA, NB, ba, bb, 9 + 2 * (q - 8));
       }
 #endif
-#endif
-#if PTK_W4_ABLATE != 1
 #if PTK_W4_DMS == 1
       if (q >= 8) {
         const int pc = q - 8;
@@ -665,7 +653,6 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
         if (pc & 1) W4_DMA(rsb, offb[pc >> 1], sb, db + (pc >> 1) * 1024);
         else W4_DMA(rsa, offa[pc >> 1], sa, da + (pc >> 1) * 1024);
       }
-#endif
       W4_GROUP(FA, FB, q, first);
     }
   };
@@ -717,12 +704,8 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
     dma_advance();
     rs = slot_next(rs);
     ws = slot_next(ws);
-#if PTK_W4_ABLATE != 5
     asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-#endif
-#if PTK_W4_ABLATE != 4
     __builtin_amdgcn_s_barrier();
-#endif
     if (kt == 0) P8_STAMP(1, (t - loc) / G);
     if (kt == nt - 1) {
       P8_STAMP(2, (t - loc) / G);
@@ -1250,16 +1233,20 @@ TailScratchScope::TailScratchScope(void* ws, hipStream_t st) : prev(g_tail_scope
 }
 TailScratchScope::~TailScratchScope() { g_tail_scope = prev; }
 
+// the model-level workspaces reserve tail scratch only when it will be lent (PTK_STREAMK=1)
+size_t p8_tail_scratch_bytes_models() { return streamk_models() ? p8_tail_scratch_bytes() : 0; }
+
 int p8_tail_split(const GemmArgs& a, int act, int out) {
   num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   return p8_tail_plan(a, ntile, g_num_cu, act, out).gsplit;
 }
 
-int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st) {
+int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk) {
   num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
-  const P8Tail tl = p8_tail_plan(a, ntile, g_num_cu, act, out);
+  // the stream-K plan only where launch_gemm's gates chose the tail split (its census counts it as p8sk)
+  const P8Tail tl = sk ? p8_tail_plan(a, ntile, g_num_cu, act, out) : P8Tail{};
   long grid = tl.units ? g_num_cu : std::min<long>(ntile, g_num_cu);
 #ifdef PTK_P8_STAMPS
   if (const char* e = getenv("PTK_GEMM_GRID")) grid = std::min<long>(grid, atol(e));   // diagnostic: fewer CUs

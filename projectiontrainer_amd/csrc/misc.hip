@@ -260,11 +260,16 @@ int launch_ce_fwd_bwd(bf16_t* logits, long ld, int R, int V, const int64_t* targ
 __global__ void __launch_bounds__(256) zero16_kernel(uint4* __restrict__ p, long n16) {
   for (long i = (long)blockIdx.x * 256 + threadIdx.x; i < n16; i += (long)gridDim.x * 256) p[i] = uint4{0, 0, 0, 0};
 }
-// PTK_HIP_MEMSET=1 (A/B, read once): hipMemsetAsync instead, the form graph_step's retired-graph corruption was
-// traced to (tools/graph_debug.py DESTROY=1: NaN grads with memset nodes in the captured step, none without)
+// PTK_HIP_MEMSET=1 (diagnostic builds only, -DPTK_DIAG): hipMemsetAsync instead, the form graph_step's
+// retired-graph corruption was traced to (tools/graph_debug.py DESTROY=1: NaN grads with memset nodes in the
+// captured step, none without).  The product library always zero-fills by kernel.
 static bool hip_memset_ab() {
+#ifdef PTK_DIAG
   static const bool v = [] { const char* e = getenv("PTK_HIP_MEMSET"); return e && e[0] == '1'; }();
   return v;
+#else
+  return false;
+#endif
 }
 int launch_zero(void* p, size_t bytes, hipStream_t st) {
   if (((uintptr_t)p | bytes) & 15) return set_error("zero: pointer / size not 16-B aligned");

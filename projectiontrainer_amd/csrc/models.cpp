@@ -74,12 +74,16 @@ static bool dkv_reduce_split() {
 
 // PTK_CE_TWO_PASS=1: the cross-entropy pass computes its own row statistics (two reads of the logits) instead
 // of taking them from the lm_head GEMM's epilogue (A/B; tests/test_stage1_gpu.py checks both agree)
-// PTK_LM_STATS_ONLY=1 (diagnostic, wrong results by construction): the lm_head GEMM computes its softmax
-// statistics but skips the logits store -- the forward half of a fused lm_head + online-LSE CE, timed against
-// the shipped chain
+// PTK_LM_STATS_ONLY=1 (diagnostic builds only, -DPTK_DIAG: wrong results by construction): the lm_head GEMM
+// computes its softmax statistics but skips the logits store -- the forward half of a fused lm_head + online-LSE
+// CE, timed against the shipped chain.  The product library has no such switch.
 static bool lm_stats_only() {
+#ifdef PTK_DIAG
   static const int v = [] { const char* e = getenv("PTK_LM_STATS_ONLY"); return e && e[0] == '1' ? 1 : 0; }();
   return v != 0;
+#else
+  return false;
+#endif
 }
 
 static bool ce_two_pass() {
@@ -111,7 +115,7 @@ SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
   w.qkv = bp.take<bf16_t>(M * 3 * D);
   w.o = bp.take<bf16_t>(M * D);
   w.mlp = bp.take<bf16_t>(M * I);
-  w.tail = bp.take<char>(p8_tail_scratch_bytes());
+  w.tail = bp.take<char>(p8_tail_scratch_bytes_models());
   return w;
 }
 
@@ -231,7 +235,7 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
   w.sk_floats = std::max(std::max(2 * M * H, 2 * 2 * I * H), 4 * std::max(Dqkv, H) * H);
   if (train) w.sk_floats = std::max(w.sk_floats, V * H);   // the tied embedding's fp32 dW before its accumulate
   w.skpart = bp.take<float>(w.sk_floats);
-  w.tail = bp.take<char>(p8_tail_scratch_bytes());
+  w.tail = bp.take<char>(p8_tail_scratch_bytes_models());
   return w;
 }
 

@@ -66,11 +66,12 @@ double w4_round_fill(long M, long N);
 int device_cus();   // compute units of the current device (cached)
 // persistent 8-wave variant (gemm_w4.hip): the w4 tiles and ring with two waves per SIMD
 bool p8_supported(const GemmArgs& a, int act, int out);
-int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st);
+int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk);
 // stream-K tail of the persistent 8-wave kernel: scratch bytes (arrival counters, then partial slabs), the
 // workgroups its plan spreads a GEMM's tail over (0: no split), and the thread-local scratch a model-level
 // call lends to every GEMM it launches (the counters are zeroed when the scope opens)
 size_t p8_tail_scratch_bytes();
+size_t p8_tail_scratch_bytes_models();   // 0 unless PTK_STREAMK=1 (the model workspaces lend it only then)
 int p8_tail_split(const GemmArgs& a, int act, int out);
 void* tail_scope();
 struct TailScratchScope {

@@ -8,6 +8,7 @@
 // events back to a pool.  Spans begun while the stream is being captured into a HIP graph record nothing.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -32,10 +33,10 @@ struct Total {
 };
 
 std::mutex g_mu;
-bool g_on = [] {
+std::atomic<bool> g_on{[] {
   const char* e = getenv("PTK_STAGE_TIMERS");
   return e && *e && strcmp(e, "0") != 0;
-}();
+}()};   // read and written from any thread
 std::vector<hipEvent_t> g_pool;   // events ready for reuse
 std::vector<Span> g_closed;        // recorded, not yet read
 std::vector<Total> g_totals;       // first-seen order
@@ -58,7 +59,7 @@ bool capturing(hipStream_t st) {
 
 }  // namespace
 
-bool stage_timers_on() { return g_on; }
+bool stage_timers_on() { return g_on.load(std::memory_order_relaxed); }
 
 void stage_begin(const char* name, hipStream_t st) {
   Span s;
@@ -94,12 +95,12 @@ using namespace ptk;
 extern "C" {
 
 int ptk_stage_timers_enable(int on) {
-  g_on = on != 0;
+  g_on.store(on != 0, std::memory_order_relaxed);
   return 0;
 }
 
 int ptk_stage_begin(const char* name, void* stream) {
-  if (g_on) stage_begin(name, (hipStream_t)stream);
+  if (stage_timers_on()) stage_begin(name, (hipStream_t)stream);
   else g_open.push_back(Span{});   // keeps begin / end paired across an enable in between
   return 0;
 }
@@ -121,8 +122,13 @@ int64_t ptk_stage_timers_read(char* buf, size_t cap, int reset) {
     const Span& s = g_closed[k];
     float ms = 0;
     if (hipEventSynchronize(s.e1) != hipSuccess || hipEventElapsedTime(&ms, s.e0, s.e1) != hipSuccess) {
-      g_closed.erase(g_closed.begin(), g_closed.begin() + k);   // the spans already added are not added again
-      return set_error("stage timers: the events of %s failed", s.name.c_str()), -1;
+      // the spans already added and the failing one are dropped (its events destroyed, not pooled), so the next
+      // read starts after it instead of failing on it again
+      const std::string nm = s.name;
+      (void)hipEventDestroy(s.e0);
+      (void)hipEventDestroy(s.e1);
+      g_closed.erase(g_closed.begin(), g_closed.begin() + k + 1);
+      return set_error("stage timers: the events of %s failed", nm.c_str()), -1;
     }
     size_t i = 0;
     while (i < g_totals.size() && g_totals[i].name != s.name) ++i;

@@ -11,6 +11,8 @@ torch.autograd.Function; there is no CPU path.
 """
 from __future__ import annotations
 
+import os
+
 import torch
 import torch.nn as nn
 
@@ -46,7 +48,13 @@ class MLPProjector(nn.Module):
             self._views.append((o, k, tuple(p.shape)))
             o += k
         self.flat, self.flat_grad = flat, grad
-        self._w1b = None          # bf16 shadows are (re)allocated on the new device by refresh_shadows
+        # every device-resident cache is dropped: the bf16 shadows, W1^T, the stream-K tail scratch and the
+        # autograd backward's workspace / grad scratch are (re)allocated on the new device when next used
+        self._w1b = None
+        self._w1t = None
+        self._tail = None
+        self._bwd_ws = None
+        self._grad_tmp = None
         self._shadow_dirty = True
 
     def _apply(self, fn, *args, **kw):      # keep the flat layout across .to()/.cuda()
@@ -87,8 +95,10 @@ class MLPProjector(nn.Module):
             self._w1b = torch.empty(self.w1.shape, dtype=torch.bfloat16, device=self.flat.device)
             self._w2b = torch.empty(self.w2.shape, dtype=torch.bfloat16, device=self.flat.device)
             self._w2t = torch.empty((self.inter_dim, self.llm_dim), dtype=torch.bfloat16, device=self.flat.device)
-            # stream-K tail scratch of the projector's GEMMs (ptk_projector.tail_ws)
-            self._tail = torch.zeros(L.lib().ptk_gemm_tail_scratch_bytes(), dtype=torch.uint8, device=self.flat.device)
+            # stream-K tail scratch of the projector's GEMMs (ptk_projector.tail_ws): the library lends it only
+            # under PTK_STREAMK=1 (off by default), so it is allocated only then
+            self._tail = (torch.zeros(L.lib().ptk_gemm_tail_scratch_bytes(), dtype=torch.uint8,
+                                      device=self.flat.device) if os.environ.get("PTK_STREAMK") == "1" else None)
         K.cast_bf16(self.w1.detach(), self._w1b)
         K.cast_bf16(self.w2.detach(), self._w2b)
         K.transpose(self._w2b, out=self._w2t)     # in place: no allocation per optimizer step
@@ -96,7 +106,7 @@ class MLPProjector(nn.Module):
             K.transpose(self._w1b, out=self._w1t)
         self.c = L.ProjectorC(self.vision_dim, self.inter_dim, self.llm_dim, self._w1b.data_ptr(),
                               self.b1.data_ptr(), self._w2b.data_ptr(), self.b2.data_ptr(), self._w2t.data_ptr(),
-                              self._tail.data_ptr())
+                              self._tail.data_ptr() if self._tail is not None else None)
         self._shadow_dirty = False
 
     def desc(self):

@@ -190,12 +190,15 @@ class Stage1Engine:
         L.check(L.lib().ptk_gather_vision_grad(self.dx.data_ptr(), B, self.N, self.Sp, self.llm.cfg.hidden_size,
                                                self.dy.data_ptr(), L.stream_ptr(self.device)), "gather_vision_grad")
         if self.comm is not None:
-            L.check(L.lib().ptk_projector_bwd_allreduce(self.proj.desc(), self.vis.shape[0], self.vis.data_ptr(),
-                                                        self.a.data_ptr(), self.h.data_ptr(), self.dy.data_ptr(),
-                                                        self.proj.flat_grad.data_ptr(), self.proj_ws.data_ptr(),
-                                                        self.proj_ws.numel(), self.comm.handle,
-                                                        self._comm_stream.cuda_stream, L.stream_ptr(self.device)),
-                    "ptk_projector_bwd_allreduce")
+            # the communicator's device must be the current HIP device (comm.cpp checks it), whichever device
+            # the caller left current
+            with torch.cuda.device(self.device):
+                L.check(L.lib().ptk_projector_bwd_allreduce(self.proj.desc(), self.vis.shape[0], self.vis.data_ptr(),
+                                                            self.a.data_ptr(), self.h.data_ptr(), self.dy.data_ptr(),
+                                                            self.proj.flat_grad.data_ptr(), self.proj_ws.data_ptr(),
+                                                            self.proj_ws.numel(), self.comm.handle,
+                                                            self._comm_stream.cuda_stream, L.stream_ptr(self.device)),
+                        "ptk_projector_bwd_allreduce")
             self._exchanged = True
         else:
             self.proj.bwd_into(self.vis, self.a, self.h, self.dy, self.proj_ws)

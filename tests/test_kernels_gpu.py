@@ -555,6 +555,27 @@ def test_projector_module_autograd(gpu):
         assert F.cosine_similarity(g.flatten(), p.grad.flatten(), dim=0) > 0.999
 
 
+def test_projector_module_device_move(gpu):
+    """Moving the module drops every device-resident cache (bf16 shadows, W1^T, backward workspace, grad scratch,
+    tail scratch): autograd backward, a move to the CPU and back, and the same backward again give the same grads
+    (a one-GPU box cannot move between GPUs; the CPU round trip re-homes the caches the same way)."""
+    from projectiontrainer_amd.projectors import MLPProjector
+    torch.manual_seed(0)
+    proj = MLPProjector(64, 128, expansion_factor=4).to(gpu)
+    x = rnd(2, 40, 64, dev=gpu, dtype=torch.float32, seed=93).requires_grad_(True)
+    w = rnd(2, 40, 128, dev=gpu, dtype=torch.float32, seed=94)
+    (proj(x) * w).sum().backward()
+    g1, dx1 = proj.flat_grad.clone(), x.grad.clone()
+    proj.cpu()
+    for name in ("_w1b", "_w1t", "_tail", "_bwd_ws", "_grad_tmp"):
+        assert getattr(proj, name) is None, name
+    proj.to(gpu)
+    x.grad = None
+    (proj(x) * w).sum().backward()
+    assert proj.flat_grad.device == x.device
+    assert torch.equal(proj.flat_grad, g1) and torch.equal(x.grad, dx1)
+
+
 # the stream-K tail of the persistent 8-wave GEMM (gemm_w4.hip P8Tail): (M, N, K, epilogue) at shapes its plan
 # splits (a grid of <= 64 tiles, or one full round + <= 24: where it measured faster, profiles/r04_sk_ab.txt) --
 # Stage 2's M = 14 336 down projection and d(gate|up) dX (cut to K 4608), its q|k|v weight grad with the bf16
