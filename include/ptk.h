@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTK_ABI_VERSION 4
+#define PTK_ABI_VERSION 5
 
 int ptk_abi_version(void);
 const char* ptk_last_error(void);
@@ -137,15 +137,16 @@ int ptk_gemm_timer_enable(int on);   /* 0 off, 1 every class, (1 << 8) | class m
 /* Tile-path test hook: 0 = shape heuristic, 1 = every GEMM on the 128x128 kernel,
    2 / 4 = every single-batch GEMM on the 256x256 / barrier-staggered 256x256 kernel,
    8 / 32 = every single-batch GEMM the persistent 4-wave / 8-wave (two waves per SIMD) 256x256 kernel
-   supports on it. */
+   supports on it, 64 = the same on the persistent two-group 256x128 kernel (gemm_dual.hip). */
 int ptk_gemm_force_small_tiles(int mode);
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
 /* Dispatch census (tests): counts[path * 8 + act] = GEMM launches since the last reset per kernel family
  * (0 128x128, 1 256x256 8-wave, 2 staggered 256x256 8-wave, 3 persistent 4-wave, 4 128x128 batched (split-K
  * slices, batch > 1), 5 persistent 8-wave with a stream-K tail round, 6 persistent 8-wave, 7 token-major weight
- * grad) and epilogue
+ * grad, 8 persistent two-group 256x128) and epilogue class (PTK_ACT_*): PTK_GEMM_NPATHS * 8 counts (ABI 5: 9 paths)
  * class (PTK_ACT_*); counts may be
  * NULL; reset != 0 zeroes them afterwards.  Host-side counters, no GPU work. */
+#define PTK_GEMM_NPATHS 9
 int ptk_gemm_path_counts(int64_t* counts, int reset);
 
 /* Per-stage device timers (SURVEY §5 tracing; the reference has none).  Off unless PTK_STAGE_TIMERS=1 or

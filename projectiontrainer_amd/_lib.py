@@ -122,7 +122,7 @@ class ImageDesc(C.Structure):
                 ("coef_off", c_int64), ("tmp_off", c_int64)]
 
 
-ABI_VERSION = 4      # include/ptk.h PTK_ABI_VERSION
+ABI_VERSION = 5      # include/ptk.h PTK_ABI_VERSION
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -230,7 +230,7 @@ def ptr(t) -> int | None:
 
 
 # nt128b: batched / split-K slices of the 128x128 kernel; p8sk: the persistent 8-wave kernel with a stream-K tail
-GEMM_PATHS = ("nt128", "big", "big2", "w4", "nt128b", "p8sk", "p8", "tn")
+GEMM_PATHS = ("nt128", "big", "big2", "w4", "nt128b", "p8sk", "p8", "tn", "dual")
 
 
 def gemm_path_counts(reset=False):

@@ -715,7 +715,8 @@ static int num_cus() {
 static bool g_timing = false;
 static int g_timing_mask = 0;   // activation classes whose launches are timed
 static int g_force_tiles = 0;   // tests: 1 = every GEMM on 128x128, 2 / 4 = single-batch GEMMs on 256x256 / staggered 256x256,
-                                // 8 = persistent 4-wave kernel, 32 = persistent 8-wave kernel wherever they are supported
+                                // 8 = persistent 4-wave kernel, 32 = persistent 8-wave kernel, 64 = persistent two-group kernel
+                                // wherever they are supported
 void force_small_tiles(int mode) { g_force_tiles = mode; }
 static std::vector<hipEvent_t> g_ev[8];
 static size_t g_ev_used[8];
@@ -816,6 +817,18 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // and down projection, the projector's fc2 and weight grads)
   const int sk = (g_force_tiles == 0 || g_force_tiles == 32) && batch == 1 && act == ACT_NONE && a.M >= 1024 &&
                  a.N >= 256 && a.N <= 16384 && p8_supported(a, act, out) ? p8_tail_split(a, act, out) : 0;
+  // two-group persistent kernel (gemm_dual.hip): PTK_DUAL=1 puts every persistent (w4 / p8) shape on it (A/B)
+  static const bool dual_env = [] { const char* e = getenv("PTK_DUAL"); return e && e[0] == '1'; }();
+  const bool dual_auto = g_force_tiles == 0 && !sk && dual_env && (p8_auto || w4_auto);
+  if (batch == 1 && (g_force_tiles == 64 || dual_auto) && dual_supported(a, act, out)) {
+    hipEvent_t e0 = nullptr, e1 = nullptr;
+    if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
+    if (e0) (void)hipEventRecord(e0, st);
+    count_path(GEMM_PATH_DUAL, act);
+    const int rc = launch_gemm_dual(a, act, out, st);
+    if (e1) (void)hipEventRecord(e1, st);
+    return rc;
+  }
   if (batch == 1 && (g_force_tiles == 32 || p8_auto || sk) && p8_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }

@@ -56,7 +56,7 @@ struct GemmArgs {
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
 // kernel families launch_gemm dispatches to (census: path_counts, ptk_gemm_path_counts)
 enum GemmPath { GEMM_PATH_NT = 0, GEMM_PATH_BIG = 1, GEMM_PATH_BIG2 = 2, GEMM_PATH_W4 = 3, GEMM_PATH_NTB = 4,
-                GEMM_PATH_P8SK = 5, GEMM_PATH_P8 = 6, GEMM_PATH_TN = 7, GEMM_NPATH = 8 };
+                GEMM_PATH_P8SK = 5, GEMM_PATH_P8 = 6, GEMM_PATH_TN = 7, GEMM_PATH_DUAL = 8, GEMM_NPATH = 9 };
 int path_counts(int64_t* out, int reset);   // out [GEMM_NPATH][8] launches per (path, act class)
 // persistent 256x256 4-wave GEMM (gemm_w4.hip): batch 1 only; w4_supported says whether a shape qualifies
 bool w4_supported(const GemmArgs& a, int act, int out);
@@ -67,6 +67,9 @@ int device_cus();   // compute units of the current device (cached)
 // persistent 8-wave variant (gemm_w4.hip): the w4 tiles and ring with two waves per SIMD
 bool p8_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk);
+// persistent two-group kernel (gemm_dual.hip): 256x128 tiles, one group's epilogue beside the other's K loop
+bool dual_supported(const GemmArgs& a, int act, int out);
+int launch_gemm_dual(const GemmArgs& a, int act, int out, hipStream_t st);
 // stream-K tail of the persistent 8-wave kernel: scratch bytes (arrival counters, then partial slabs), the
 // workgroups its plan spreads a GEMM's tail over (0: no split), and the thread-local scratch a model-level
 // call lends to every GEMM it launches (the counters are zeroed when the scope opens)

@@ -88,7 +88,7 @@ int main(int argc, char** argv) {
                                      nullptr) != 0);
 
   // dispatch census and stage timers (timers off: begin / end pair up without recording)
-  std::vector<int64_t> counts(8 * 8, -1);
+  std::vector<int64_t> counts(PTK_GEMM_NPATHS * 8, -1);
   EXPECT(ptk_gemm_path_counts(counts.data(), 1) == 0);
   for (int64_t v : counts) EXPECT(v == 0);
   EXPECT(ptk_stage_begin("outer", nullptr) == 0);

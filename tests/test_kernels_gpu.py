@@ -481,20 +481,23 @@ def test_qknorm_rope_fwd_bwd(gpu, Hq, Hkv, D):
 
 
 @pytest.mark.parametrize("M,N,K", [(1000, 1024, 1152), (4096, 2304, 640), (2304, 3072, 1024), (513, 896, 1280),
-                                   (22528, 1152, 1152), (300, 256, 128), (4608, 13824, 1152)])
+                                   (22528, 1152, 1152), (300, 256, 128), (4608, 13824, 1152), (256, 128, 128),
+                                   (18432, 1024, 4096)])
 def test_gemm_p8_matches_w4(gpu, M, N, K):
     """Persistent 8-wave kernel (forced mode 32: two waves per SIMD, 128x64 per wave, several tiles per
-    workgroup, ragged M/N) against the persistent 4-wave kernel (mode 8): the same k-step order per output
-    element, so every epilogue -- plain bf16 / fp32 / fp32-rounded, bias + residual, GELU-tanh, GELU-erf
-    with its pre-activation, GELU-erf backward, GEGLU with g, u side outputs, GEGLU backward into the
-    interleaved dg|du layout -- is bit-identical; plain fp32 also against torch fp32."""
+    workgroup, ragged M/N) and the persistent two-group kernel (mode 64: 256x128 tiles, one group's epilogue beside
+    the other's K loop; one-tile grids leave the second group idle) against the persistent 4-wave kernel (mode 8):
+    the same k-step order per output element, so every epilogue -- plain bf16 / fp32 / fp32-rounded, bias +
+    residual, GELU-tanh, GELU-erf with its pre-activation, GELU-erf backward, GEGLU with g, u side outputs, GEGLU
+    backward into the interleaved dg|du layout -- is bit-identical; plain fp32 also against torch fp32."""
     Kn, L = _k()
     A, B = rnd(M, K, dev=gpu, seed=11), rnd(N, K, dev=gpu, seed=12, scale=0.05)
     gin, uin = rnd(M, N, dev=gpu, seed=13), rnd(M, N, dev=gpu, seed=14)
     bias = rnd(N, dev=gpu, dtype=torch.float32, seed=15)
     res = rnd(M, N, dev=gpu, dtype=torch.float32, seed=16)
     outs = []
-    for md in (8, 32):
+    modes = {8: "w4", 32: "p8", 64: "dual"}
+    for md in modes:
         L.lib().ptk_gemm_force_small_tiles(md)
         L.gemm_path_counts(reset=True)
         try:
@@ -516,14 +519,15 @@ def test_gemm_p8_matches_w4(gpu, M, N, K):
             o["dgdu"] = Kn.gemm(A, B, act=L.ACT_GEGLU_BWD, aux_in=gin, aux_in2=uin)
             torch.cuda.synchronize()
             paths = {p for p, _ in L.gemm_path_counts(reset=True)}
-            assert paths == {"w4" if md == 8 else "p8"}, paths
+            assert paths == {modes[md]}, paths
             outs.append(o)
         finally:
             L.lib().ptk_gemm_force_small_tiles(0)
-    for k in outs[0]:
-        assert torch.equal(outs[0][k], outs[1][k]), (k, (outs[0][k].float() - outs[1][k].float()).abs().max())
+    for other in outs[1:]:
+        for k in outs[0]:
+            assert torch.equal(outs[0][k], other[k]), (k, (outs[0][k].float() - other[k].float()).abs().max())
     ref = A.float() @ B.float().T
-    torch.testing.assert_close(outs[1]["f32"], ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
+    torch.testing.assert_close(outs[2]["f32"], ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
 
 
 def test_projector_module_autograd(gpu):

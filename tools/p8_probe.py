@@ -1,4 +1,4 @@
-"""Persistent 4-wave (mode 8) vs persistent 8-wave (mode 32) vs the automatic dispatch (mode 0) on the GEMM
+"""Persistent 4-wave (mode 8) vs persistent 8-wave (mode 32) vs two-group (mode 64) vs the automatic dispatch (mode 0) on the GEMM
 shapes of the cfg2 / cfg4 steps: HIP-event time per launch, TFLOP/s, rounds interleaved (one process)."""
 import json
 import os
@@ -61,7 +61,8 @@ def timed(A, B, kw, act, odt, C, reps):
 
 
 only = set(a for a in sys.argv[1:] if not a.startswith("-"))
-modes = (8, 32, 0)
+TAGS = {8: "w4", 32: "p8", 64: "dual", 0: "auto"}
+modes = tuple(int(x) for x in os.environ.get("MODES", "8,32,64,0").split(","))
 for name, m, n, k, act, odt in SHAPES:
     if only and name not in only:
         continue
@@ -77,7 +78,8 @@ for name, m, n, k, act, odt in SHAPES:
     L.lib().ptk_gemm_force_small_tiles(0)
     fl = 2.0 * m * n * k
     out = {"name": name, "M": m, "N": n, "K": k}
-    for md, tag in zip(modes, ("w4", "p8", "auto")):
+    for md in modes:
+        tag = TAGS[md]
         ms = min(res[md])
         out[tag + "_us"] = round(ms * 1e3, 1)
         out[tag + "_TF"] = round(fl / ms / 1e9, 1)
