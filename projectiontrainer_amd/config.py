@@ -132,6 +132,11 @@ PRESETS = {
     "cfg5": Stage1Config(vision=SIGLIP_L16_384, text=GEMMA3_4B, batch_size=16, text_len=256),
     # BASELINE.json configs[3]: Stage 2 VQA fine-tune, Gemma3-1B unfrozen, 576 vis + 64 Q + 256 A tokens
     "cfg4": Stage1Config(vision=SIGLIP_L16_384, text=GEMMA3_1B, batch_size=16, text_len=64 + 256, question_len=64),
+    # cfg2 WIDTHS at reduced depth for reference-generated fixtures (tests/golden/make_golden.py: the reference's own
+    # train() at SigLIP-L/16-384 + Gemma3-1B widths, 2 + 6 layers with one global Gemma layer, bs 2, T 128 -- S 703
+    # > the 512-key sliding window, the step's per-layer shapes at bs 2)
+    "cfg2w": Stage1Config(vision=SiglipVisionConfig(num_hidden_layers=2),
+                          text=Gemma3TextConfig(num_hidden_layers=6), batch_size=2, text_len=128),
     "tiny": Stage1Config(vision=SIGLIP_TINY, text=GEMMA3_TINY, batch_size=3, text_len=16),
     "tiny_gqa": Stage1Config(vision=SIGLIP_TINY, text=GEMMA3_TINY_GQA, batch_size=3, text_len=16),
 }

@@ -19,6 +19,8 @@
 
 namespace ptk {
 
+typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v_t;
+
 namespace {
 constexpr int W4 = 256;                  // output tile edge
 constexpr int W4_KT = 64;                // K granularity of the path (a pair of k-steps per barrier)
@@ -382,6 +384,121 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[2 * NP], long row0, lo
     stbf8(o, dg);
     stbf8(o + 16, du);
   }
+}
+
+// Lean bf16 epilogue (chosen on the host by lean_epilogue_ok: ACT_NONE or ACT_GELU_TANH, OUT_BF16, an optional
+// bias / bf16-linear rounding / bf16 residual (SigLIP's linears), no row-add or fp32 residual, a C row map that
+// is an offset (cmap.g == 0, or a group map that is the identity), N % 64 == 0).  The values are w4_epi8's, in
+// its order (bias, bf16(linear), GELU-tanh, + bf16 residual), and the whole-line row-pair exchange is
+// w4_rows' (bit-identical); what goes is the per-store address work -- row validity, row-map offsets, sink
+// selects and 64-bit addresses per row block.  Stores (and residual loads) go through buffer resources whose
+// num_records end at row M (rows past M fall outside them: stores dropped, loads zero), with one per-lane
+// 32-bit offset computed once per tile plus a uniform row-block offset (kept in the VGPR offset: the range check
+// does not include soffset).  The bias of the wave's columns is loaded once per tile.  A wave whose 16NJ columns
+// start at or past N stores nothing (N % 64 == 0: a wave's columns are all inside N or all outside).
+struct LeanEpi {
+  __amdgpu_buffer_rsrc_t rc, rr;   // C, resid16
+  uint32_t voff, ldc_bytes;        // store 1 of row block 0 / line 0 (row lane & 7, chunk lo ? cb : 32 + cb)
+  uint32_t roff, ldr_bytes;        // resid16 of row block 0 (row lane & 15, columns col0 + cb)
+  bool hb, lin, hr;
+};
+template <int ACT, int I, int NJ>
+PTK_DEV void w4_rows_lean(f32x4_t (&a)[NJ], const LeanEpi& e, const float (&bias)[NJ / 2][8]) {
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
+  u16x8_t res[NJ / 2];
+  if (e.hr) {
+#pragma unroll
+    for (int pp = 0; pp < NJ / 2; ++pp)
+      res[pp] = __builtin_bit_cast(u16x8_t, __builtin_amdgcn_raw_buffer_load_b128(
+                                                e.rr, e.roff + (uint32_t)(16 * I) * e.ldr_bytes + 64u * pp, 0, 0));
+  }
+#pragma unroll
+  for (int m = 0; m < NJ / 4; ++m) {
+    uint4 X, Y;
+#pragma unroll
+    for (int h = 0; h < 2; ++h) {
+      const int pp = 2 * m + h;
+      f32x4_t x = a[2 * pp], y = a[2 * pp + 1];
+      swap16(x, y);
+      float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+      if (e.hb) {
+#pragma unroll
+        for (int k = 0; k < 8; ++k) v[k] += bias[pp][k];
+      }
+      if (e.lin) {
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          const f32x2_t r = bfround2(f32x2_t{v[k], v[k + 1]});
+          v[k] = r.x;
+          v[k + 1] = r.y;
+        }
+      }
+      if constexpr (ACT == ACT_GELU_TANH) {
+#pragma unroll
+        for (int k = 0; k < 8; k += 2) {
+          const f32x2_t r = gelu_tanh2(bfround2(f32x2_t{v[k], v[k + 1]}));
+          v[k] = r.x;
+          v[k + 1] = r.y;
+        }
+      }
+      if (e.hr) {
+        const uint4 rw = __builtin_bit_cast(uint4, res[pp]);
+        const uint32_t rv[4] = {rw.x, rw.y, rw.z, rw.w};
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const f32x2_t r = bf2x2(rv[k]);
+          v[2 * k] += r.x;
+          v[2 * k + 1] += r.y;
+        }
+      }
+      (h ? Y : X) = w4_pack8(v);
+    }
+    uint4 d1, d2;
+    w4_line_pair(X, Y, false, d1, d2);
+    const uint32_t v1 = e.voff + (uint32_t)(16 * I) * e.ldc_bytes + 128u * m;   // rows 16I + (lane & 7), line m
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v_t, d1), e.rc, v1, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v_t, d2), e.rc, v1 + 8u * e.ldc_bytes, 0, 0);
+  }
+}
+template <int ACT, int NJ>
+PTK_DEV void w4_epilogue_lean(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, long col0, int lane,
+                              uint32_t c_bytes) {
+  if (col0 >= p.N) return;
+  LeanEpi e;
+  const int q = lane >> 4;
+  const int cb = 16 * (q & 1) + 8 * (q >> 1);
+  const bool lo = (lane & 8) == 0;
+  const uint32_t crow0 = (uint32_t)(row0 + p.cmap.off);
+  e.rc = __builtin_amdgcn_make_buffer_rsrc(p.C, 0, (int)c_bytes, 0x00020000);
+  e.ldc_bytes = __builtin_amdgcn_readfirstlane((uint32_t)p.ldc * 2u);
+  // store 1 of a row pair writes row (lane & 7) of the row block, store 2 row 8 + (lane & 7), both at line chunk
+  // lo ? cb : 32 + cb (w4_line_pair)
+  e.voff = (crow0 + (lane & 7)) * e.ldc_bytes + (uint32_t)(col0 + (lo ? cb : 32 + cb)) * 2u;
+  e.hb = p.bias != nullptr;
+  e.lin = p.bf16_linear != 0;
+  e.hr = p.resid16 != nullptr;
+  e.ldr_bytes = __builtin_amdgcn_readfirstlane((uint32_t)p.ld_resid16 * 2u);
+  e.rr = __builtin_amdgcn_make_buffer_rsrc((void*)p.resid16, 0, (int)(c_bytes / e.ldc_bytes * e.ldr_bytes), 0x00020000);
+  e.roff = (crow0 + (lane & 15)) * e.ldr_bytes + (uint32_t)(col0 + cb) * 2u;
+  float bias[NJ / 2][8];
+  if (e.hb) {
+#pragma unroll
+    for (int pp = 0; pp < NJ / 2; ++pp) {
+      const float4 b0 = *reinterpret_cast<const float4*>(p.bias + col0 + 32 * pp + cb);
+      const float4 b1 = *reinterpret_cast<const float4*>(p.bias + col0 + 32 * pp + cb + 4);
+      bias[pp][0] = b0.x; bias[pp][1] = b0.y; bias[pp][2] = b0.z; bias[pp][3] = b0.w;
+      bias[pp][4] = b1.x; bias[pp][5] = b1.y; bias[pp][6] = b1.z; bias[pp][7] = b1.w;
+    }
+  }
+  w4_rows_lean<ACT, 0, NJ>(acc[0], e, bias);
+  w4_rows_lean<ACT, 1, NJ>(acc[1], e, bias);
+  w4_rows_lean<ACT, 2, NJ>(acc[2], e, bias);
+  w4_rows_lean<ACT, 3, NJ>(acc[3], e, bias);
+  w4_rows_lean<ACT, 4, NJ>(acc[4], e, bias);
+  w4_rows_lean<ACT, 5, NJ>(acc[5], e, bias);
+  w4_rows_lean<ACT, 6, NJ>(acc[6], e, bias);
+  w4_rows_lean<ACT, 7, NJ>(acc[7], e, bias);
 }
 
 // the wave's 128 x 16NJ accumulator tile (8 row blocks of NJ 16x16 MFMA tiles)

@@ -48,8 +48,9 @@
 
 namespace ptk {
 
-template <int ACT, int OUT>
-__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
+template <int ACT, int OUT, bool LEAN = false>
+__global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes,
+                                                         uint32_t c_bytes) {
   __shared__ __attribute__((aligned(16))) char smem[W4_NSLOT * W4_SLOT];   // 160 KiB: the k-step ring
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -245,7 +246,11 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 #ifdef PTK_P8_STAMPS
       if (em_ != 1)
 #endif
-      w4_epilogue<ACT, OUT>(kernarg_args(), acc, (long)bm * W4 + wr * 128, (long)bn * W4 + wc * 128, lane);
+      {
+        const long row0 = (long)bm * W4 + wr * 128, col0 = (long)bn * W4 + wc * 128;
+        if constexpr (LEAN) w4_epilogue_lean<ACT, 8>(kernarg_args(), acc, row0, col0, lane, c_bytes);
+        else w4_epilogue<ACT, OUT>(kernarg_args(), acc, row0, col0, lane);
+      }
       P8_STAMP(3, (t - loc) / G);
       t += G;
       kt = 0;
@@ -306,6 +311,27 @@ double w4_round_fill(long M, long N) {
   return (double)ntile / (double)(((ntile + cu - 1) / cu) * cu);
 }
 
+// the lean bf16 epilogue (gemm_persist.h w4_epilogue_lean) applies: ACT_NONE / ACT_GELU_TANH into bf16 with at most
+// a bias, the bf16-linear rounding and a bf16 residual (row-aligned with C, 16-B rows); a C row map that is an
+// offset (cmap.g == 0, or a group map without skipped rows whose group stride equals its size: the identity
+// plus cmap.off); whole 64-column wave ranges; C's extent (rows cmap.off .. M + cmap.off) below 2^31 bytes.
+// c_bytes = that extent (num_records of the store resource: rows past M are dropped).  PTK_LEAN_EPI=0 keeps the
+// general epilogue (A/B; bit-identical either way)
+bool lean_epilogue_ok(const GemmArgs& a, int act, int out, uint32_t& c_bytes) {
+  static const bool on = [] { const char* e = getenv("PTK_LEAN_EPI"); return !(e && e[0] == '0'); }();
+  if (!on || (act != ACT_NONE && act != ACT_GELU_TANH) || out != OUT_BF16) return false;
+  if (a.rowadd || a.resid || a.aux || a.aux2 || a.aux_in || a.aux_in2 || a.row_stats || a.alpha != 1.f) return false;
+  const bool affine = a.cmap.g == 0 || (a.cmap.skip == 0 && a.cmap.gs == a.cmap.g);
+  if (!affine || a.cmap.off < 0 || a.N % 64 || a.ldc % 8 || a.ldc < a.N || ((uintptr_t)a.C & 15)) return false;
+  if (a.bias && ((uintptr_t)a.bias & 15)) return false;
+  if (a.resid16 && (a.ld_resid16 % 8 || ((uintptr_t)a.resid16 & 15))) return false;
+  const double rows = (double)a.M + (double)a.cmap.off;
+  const double bytes = rows * (double)a.ldc * 2.0, rbytes = a.resid16 ? rows * (double)a.ld_resid16 * 2.0 : 0.0;
+  if (bytes >= 2147483000.0 || rbytes >= 2147483000.0) return false;
+  c_bytes = (uint32_t)bytes;
+  return true;
+}
+
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid) {
   num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
@@ -316,9 +342,17 @@ int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_
   const long arows = a.M + a.amap.off;
   const uint32_t ab = (uint32_t)std::min<double>((double)arows * a.lda * 2, 2147483000.0);
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
+  uint32_t cb = 0;
+  if (lean_epilogue_ok(a, act, out, cb)) {
+    if (act == ACT_GELU_TANH)
+      hipLaunchKernelGGL((gemm_w4_kernel<ACT_GELU_TANH, OUT_BF16, true>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb, cb);
+    else
+      hipLaunchKernelGGL((gemm_w4_kernel<ACT_NONE, OUT_BF16, true>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb, cb);
+    return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_w4 launch failed");
+  }
 #define PTK_W4_CASE(ACT_, OUT_)                                                                   \
   if (act == ACT_ && out == OUT_) {                                                               \
-    hipLaunchKernelGGL((gemm_w4_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb); \
+    hipLaunchKernelGGL((gemm_w4_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb, 0u); \
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_w4 launch failed");              \
   }
   PTK_W4_CASE(ACT_NONE, OUT_BF16)
@@ -418,8 +452,9 @@ PTK_DEV void p8_tail_epilogue(const GemmArgs& p, const float* slab, int g0, int 
   p8_tail_rows<ACT, OUT, 7>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
 }
 
-template <int ACT, int OUT, bool SK>
-__global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes, P8Tail tl) {
+template <int ACT, int OUT, bool SK, bool LEAN = false>
+__global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes, P8Tail tl,
+                                                         uint32_t c_bytes) {
   __shared__ __attribute__((aligned(16))) char smem[W4_NSLOT * W4_SLOT];   // 160 KiB: the k-step ring
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
@@ -655,7 +690,10 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
 #ifdef PTK_P8_STAMPS
         if (em_ != 1)
 #endif
-        w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane);
+        {
+          if constexpr (LEAN) w4_epilogue_lean<ACT, 4>(kernarg_args(), acc, row0, col0, lane, c_bytes);
+          else w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane);
+        }
       } else if constexpr (SK) {
         const uint32_t c = __builtin_amdgcn_readlane(segC, s);
         const int g0 = (int)(c & 1023u), np = (int)((c >> 10) & 1023u), s0 = (int)((c >> 20) & 1u);
@@ -784,14 +822,24 @@ int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk)
   const long arows = a.M + a.amap.off;
   const uint32_t ab = (uint32_t)std::min<double>((double)arows * a.lda * 2, 2147483000.0);
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
+  uint32_t cb = 0;
+  if (!tl.units && lean_epilogue_ok(a, act, out, cb)) {
+    if (act == ACT_GELU_TANH)
+      hipLaunchKernelGGL((gemm_p8_kernel<ACT_GELU_TANH, OUT_BF16, false, true>), dim3((unsigned)grid), dim3(512), 0, st,
+                         a, ab, bb, tl, cb);
+    else
+      hipLaunchKernelGGL((gemm_p8_kernel<ACT_NONE, OUT_BF16, false, true>), dim3((unsigned)grid), dim3(512), 0, st, a,
+                         ab, bb, tl, cb);
+    return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");
+  }
 #define PTK_P8_CASE(ACT_, OUT_)                                                                       \
   if (act == ACT_ && out == OUT_) {                                                                   \
-    hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_, false>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb, tl); \
+    hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_, false>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb, tl, 0u); \
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");                  \
   }
 #define PTK_P8SK_CASE(ACT_, OUT_)                                                                     \
   if (act == ACT_ && out == OUT_) {                                                                   \
-    hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_, true>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb, tl); \
+    hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_, true>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb, tl, 0u); \
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");                  \
   }
   if (tl.units) {

@@ -22,6 +22,8 @@ Fixtures:
                       under autocast -- the precision flow of SURVEY F8
   cfg1, cfg1_bf16     BASELINE cfg1 shapes: SigLIP-B/16-224 + Gemma3-1B (26 layers,
                       vocab 262144), bs 2, T 64, fp32 / bf16 as above
+  cfg2w, cfg2w_bf16   BASELINE cfg2 WIDTHS (SigLIP-L/16-384 + Gemma3-1B, vocab 262144) at 2 + 6 layers
+                      (one global Gemma layer), bs 2, T 128 (S 703 > the sliding window), fp32 / bf16
 
 Large tensors are stored as a strided sub-sample `<key>@sub<sr>x<sc>` (every
 sr-th row, every sc-th column of the [rows, last-dim] view) plus the exact
@@ -195,6 +197,10 @@ FIXTURES = {   # name: (gas, batch seed, precision)
     "tiny_gqa_bf16": (1, 12, "bf16"),
     "cfg1": (2, 14, "no"),
     "cfg1_bf16": (2, 14, "bf16"),     # same batch as "cfg1"
+    # cfg2 widths (SigLIP-L/16-384 + Gemma3-1B) at 2 + 6 layers, bs 2, T 128: pins the cfg2 per-layer shapes to the
+    # reference itself, and its bf16 twin measures the reference's own mixed-precision noise at those widths
+    "cfg2w": (2, 15, "no"),
+    "cfg2w_bf16": (2, 15, "bf16"),   # same batch as "cfg2w"
 }
 
 

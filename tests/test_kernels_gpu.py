@@ -295,6 +295,12 @@ def test_gemm_big_vs_small_all_epilogues(gpu, mode):
             Kn.gemm(A, B, C=C, bias=bias, resid=C)
             o["resid"] = C
             o["gelu_tanh"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_TANH)
+            # SigLIP's linear: bf16(acc + bias) + bf16 residual, in place (the lean epilogue's residual path)
+            C16 = res.to(torch.bfloat16)
+            Kn.gemm(A, B, C=C16, bias=bias, resid16=C16, bf16_linear=True)
+            o["resid16"] = C16
+            # a group row map that is the identity (the Gemma dO GEMM's at one kv head): the lean path's affine case
+            o["gmap"] = Kn.gemm(A, B, C=torch.zeros(M, N, dtype=torch.bfloat16, device=gpu), cmap=(128, 0, 128, 0))
             aux = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
             o["gelu_erf"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_ERF, aux=aux)
             o["aux"] = aux
@@ -488,8 +494,10 @@ def test_gemm_p8_matches_w4(gpu, M, N, K):
     workgroup, ragged M/N) and the persistent two-group kernel (mode 64: 256x128 tiles, one group's epilogue beside
     the other's K loop; one-tile grids leave the second group idle) against the persistent 4-wave kernel (mode 8):
     the same k-step order per output element, so every epilogue -- plain bf16 / fp32 / fp32-rounded, bias +
-    residual, GELU-tanh, GELU-erf with its pre-activation, GELU-erf backward, GEGLU with g, u side outputs, GEGLU
-    backward into the interleaved dg|du layout -- is bit-identical; plain fp32 also against torch fp32."""
+    residual, bias + bf16(linear) + bf16 residual in place, an identity group row map, GELU-tanh, GELU-erf with its
+    pre-activation, GELU-erf backward, GEGLU with g, u side outputs, GEGLU backward into the interleaved dg|du
+    layout -- is bit-identical (w4 / p8 take the lean bf16 epilogue where it applies, the two-group kernel the
+    general one); plain fp32 also against torch fp32."""
     Kn, L = _k()
     A, B = rnd(M, K, dev=gpu, seed=11), rnd(N, K, dev=gpu, seed=12, scale=0.05)
     gin, uin = rnd(M, N, dev=gpu, seed=13), rnd(M, N, dev=gpu, seed=14)
@@ -507,6 +515,12 @@ def test_gemm_p8_matches_w4(gpu, M, N, K):
             Kn.gemm(A, B, C=C, bias=bias, resid=C)
             o["resid"] = C
             o["gelu_tanh"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_TANH)
+            # SigLIP's linear: bf16(acc + bias) + bf16 residual, in place (the lean epilogue's residual path)
+            C16 = res.to(torch.bfloat16)
+            Kn.gemm(A, B, C=C16, bias=bias, resid16=C16, bf16_linear=True)
+            o["resid16"] = C16
+            # a group row map that is the identity (the Gemma dO GEMM's at one kv head): the lean path's affine case
+            o["gmap"] = Kn.gemm(A, B, C=torch.zeros(M, N, dtype=torch.bfloat16, device=gpu), cmap=(128, 0, 128, 0))
             aux = torch.empty(M, N, dtype=torch.bfloat16, device=gpu)
             o["gelu_erf"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_ERF, aux=aux)
             o["aux"] = aux

@@ -24,6 +24,11 @@ SHAPES = [  # name, M, N, K, act, out dtype
     ("sig_qkv", MS, 3072, 1024, L.ACT_NONE, torch.bfloat16),
     ("sig_fc1", MS, 4096, 1024, L.ACT_GELU_TANH, torch.bfloat16),
     ("sig_fc2", MS, 1024, 4096, L.ACT_NONE, torch.bfloat16),
+    # the SigLIP calls as the model makes them (models.cpp: bias; out / fc2 with bf16(linear) + bf16 residual)
+    ("sig_qkv_b", MS, 3072, 1024, L.ACT_NONE, torch.bfloat16, "bias"),
+    ("sig_o_br", MS, 1024, 1024, L.ACT_NONE, torch.bfloat16, "bias_res"),
+    ("sig_fc1_b", MS, 4096, 1024, L.ACT_GELU_TANH, torch.bfloat16, "bias"),
+    ("sig_fc2_br", MS, 1024, 4096, L.ACT_NONE, torch.bfloat16, "bias_res"),
     ("proj_fc1", MS, 11520, 1024, L.ACT_GELU_ERF, torch.bfloat16),
     ("proj_fc2", MS, 1152, 11520, L.ACT_NONE, torch.float32),
     ("proj_dW2", 1152, 11520, 18432, L.ACT_NONE, torch.float32),
@@ -33,10 +38,15 @@ SHAPES = [  # name, M, N, K, act, out dtype
 ]
 
 
-def setup(m, n, k, act, odt):
+def setup(m, n, k, act, odt, extra=None):
     A = torch.randn(m, k, device=dev).to(torch.bfloat16)
     B = (torch.randn(n, k, device=dev) * 0.05).to(torch.bfloat16)
     kw = {}
+    if extra in ("bias", "bias_res"):
+        kw["bias"] = torch.randn(n, device=dev)
+    if extra == "bias_res":
+        kw["resid16"] = torch.randn(m, n, device=dev).to(torch.bfloat16)
+        kw["bf16_linear"] = True
     if act == L.ACT_GEGLU:
         kw = dict(aux=torch.empty(m, n // 2, dtype=torch.bfloat16, device=dev),
                   aux2=torch.empty(m, n // 2, dtype=torch.bfloat16, device=dev))
@@ -63,10 +73,10 @@ def timed(A, B, kw, act, odt, C, reps):
 only = set(a for a in sys.argv[1:] if not a.startswith("-"))
 TAGS = {8: "w4", 32: "p8", 64: "dual", 0: "auto"}
 modes = tuple(int(x) for x in os.environ.get("MODES", "8,32,64,0").split(","))
-for name, m, n, k, act, odt in SHAPES:
+for name, m, n, k, act, odt, *extra in SHAPES:
     if only and name not in only:
         continue
-    A, B, kw = setup(m, n, k, act, odt)
+    A, B, kw = setup(m, n, k, act, odt, *extra)
     C = K.gemm(A, B, out_dtype=odt, act=act, **kw)
     reps = max(3, min(50, int(2e12 / (2.0 * m * n * k))))
     res = {m_: [] for m_ in modes}
