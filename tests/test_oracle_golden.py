@@ -11,8 +11,10 @@ import torch
 from oracle import stage1_ref as R
 from tests import golden_util as G
 
-CASES = ["tiny", "tiny_gqa", "cfg1"]          # fp32 reference runs (cfg1: SigLIP-B/16-224 + Gemma3-1B)
-ALL = CASES + ["tiny_bf16", "cfg1_bf16"]      # + the --mixed_precision bf16 runs
+# fp32 reference runs (cfg1: SigLIP-B/16-224 + Gemma3-1B; cfg2w: cfg2 widths, SigLIP-L/16-384 + Gemma3-1B at
+# 2 + 6 layers, bs 2, T 128)
+CASES = ["tiny", "tiny_gqa", "cfg1", "cfg2w"]
+ALL = CASES + ["tiny_bf16", "cfg1_bf16", "cfg2w_bf16"]      # + the --mixed_precision bf16 runs
 
 
 def rms(t):

@@ -5,7 +5,9 @@
    fwd, projector, Gemma3 fwd/loss/bwd, clip, AdamW, schedule) at
    * tiny dims, fp32 (tiny, tiny_gqa) and under `--mixed_precision bf16` (tiny_bf16);
    * BASELINE cfg1 dims (SigLIP-B/16-224 + the full 26-layer Gemma3-1B, vocab
-     262144, bs 2, T 64), fp32 (cfg1) and bf16 (cfg1_bf16).
+     262144, bs 2, T 64), fp32 (cfg1) and bf16 (cfg1_bf16);
+   * BASELINE cfg2 WIDTHS (SigLIP-L/16-384 + Gemma3-1B, vocab 262144) at 2 + 6 layers
+     (one global Gemma layer, S 703 > the sliding window), bs 2, T 128: cfg2w / cfg2w_bf16.
 2. Against the CPU oracle at architecture-true sizes (SigLIP-L/16-384 and
    Gemma3-1B dims at full depth, S = 703 > sliding window 512, and T = 512).
 
@@ -125,7 +127,8 @@ def build_engine(name, gpu, gas, lr, total):
     return cfg, eng
 
 
-@pytest.mark.parametrize("name", ["tiny", "tiny_gqa", "tiny_bf16", "tiny_gqa_bf16", "cfg1", "cfg1_bf16"])
+@pytest.mark.parametrize("name", ["tiny", "tiny_gqa", "tiny_bf16", "tiny_gqa_bf16", "cfg1", "cfg1_bf16", "cfg2w",
+                                  "cfg2w_bf16"])
 def test_two_steps_vs_reference_golden(gpu, name):
     d, meta = G.load(name)
     cfg, eng = build_engine(name, gpu, meta["gas"], meta["lr"], meta["max_train_steps"])
@@ -261,13 +264,15 @@ def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
     out = R.stage1_step(vp, cfg.vision, lp, cfg.text, st, (px, ids, labels), R.StepConfig(gradient_accumulation_steps=1),
                         embed_dtype=torch.bfloat16)
     t = f"arch[{preset}-bs{bs}-T{T}]"
-    # no reference twin at these sizes: the bar is SURVEY.md:297's, with rel-L2 on the backward quantities
-    # widened to the reference's own bf16-vs-fp32 noise measured at cfg1 (0.04 on d(projector output))
+    # the bar is SURVEY.md:297's, widened on the backward quantities to twice the reference's own bf16-vs-fp32
+    # noise at cfg2 WIDTHS (the cfg2w / cfg2w_bf16 fixtures: SigLIP-L/16-384 + Gemma3-1B at 2 + 6 layers, bs 2,
+    # T 128, the reference's train() run both ways; 0.075 on d(projector output), 0.02-0.03 on the grads)
     record(t, "loss", abs=abs(loss - float(out["loss"])))
     assert abs(loss - float(out["loss"])) <= LOSS_TOL, (loss, float(out["loss"]))
+    bar = lambda key: max(RL2, 2.0 * twin_noise("cfg2w", "s0_" + key)[0])
     for key, got, ref, rtol in (("patch", vis, out["patch"], RL2), ("proj", xv, out["proj"], RL2),
-                                ("d_proj", dxv, out["d_proj"], 4e-2)) + tuple(
-            ("grad." + k, gc, out["grads"][k], 4e-2)
+                                ("d_proj", dxv, out["d_proj"], bar("d_proj"))) + tuple(
+            ("grad." + k, gc, out["grads"][k], bar("grad." + k))
             for k, gc in zip(["model.0.weight", "model.0.bias", "model.2.weight", "model.2.bias"], grads)):
         r, c = rel_l2(got, ref), cosine(got, ref)
         record(t, key, rel_l2=r, cos=c, tol_rel_l2=rtol, tol_cos=COS)
