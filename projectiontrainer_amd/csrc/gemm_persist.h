@@ -501,6 +501,98 @@ PTK_DEV void w4_epilogue_lean(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row
   w4_rows_lean<ACT, 7, NJ>(acc[7], e, bias);
 }
 
+// Lean GEGLU-backward epilogue (lean_glu_ok): w4_gbwd_rows' values and whole-line dg | du stores, the saved g, u
+// loaded by buffer loads one row block ahead (rows past M read as zero and their stores are dropped)
+struct LeanGbwd {
+  __amdgpu_buffer_rsrc_t rgi, rui, rc;
+  uint32_t vin, ldin_bytes, vout, ldc_bytes;
+};
+template <int I, int NP>
+PTK_DEV void w4_gbwd_load_lean(const LeanGbwd& e, u16x8_t (&G)[NP], u16x8_t (&U)[NP]) {
+#pragma unroll
+  for (int pp = 0; pp < NP; ++pp) {
+    const uint32_t o = e.vin + (uint32_t)(16 * I) * e.ldin_bytes + 64u * pp;
+    G[pp] = __builtin_bit_cast(u16x8_t, __builtin_amdgcn_raw_buffer_load_b128(e.rgi, o, 0, 0));
+    U[pp] = __builtin_bit_cast(u16x8_t, __builtin_amdgcn_raw_buffer_load_b128(e.rui, o, 0, 0));
+  }
+}
+template <int I, int NP>
+PTK_DEV void w4_gbwd_rows_lean(f32x4_t (&a)[2 * NP], const LeanGbwd& e, const u16x8_t (&G)[NP],
+                               const u16x8_t (&U)[NP]) {
+#pragma unroll
+  for (int j = 0; j < 2 * NP; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
+#pragma unroll
+  for (int pp = 0; pp < NP; ++pp) {
+    f32x4_t x = a[2 * pp], y = a[2 * pp + 1];
+    swap16(x, y);
+    const float v[8] = {x[0], x[1], x[2], x[3], y[0], y[1], y[2], y[3]};
+    const uint4 gw = __builtin_bit_cast(uint4, G[pp]), uw = __builtin_bit_cast(uint4, U[pp]);
+    const uint32_t gv[4] = {gw.x, gw.y, gw.z, gw.w}, uv[4] = {uw.x, uw.y, uw.z, uw.w};
+    float dg[8], du[8];
+#pragma unroll
+    for (int k = 0; k < 8; k += 2) {   // w4_gbwd_rows' math
+      const f32x2_t d = bfround2(f32x2_t{v[k], v[k + 1]}), g = bf2x2(gv[k / 2]), u = bf2x2(uv[k / 2]);
+      f32x2_t f, df;
+      gelu_tanh_fg2(g, f, df);
+      const f32x2_t aa = bfround2(d * u) * df, bb = d * bfround2(f);
+      dg[k] = aa.x;
+      dg[k + 1] = aa.y;
+      du[k] = bb.x;
+      du[k + 1] = bb.y;
+    }
+    uint4 d1, d2;
+    w4_line_pair(w4_pack8(dg), w4_pack8(du), false, d1, d2);
+    const uint32_t o1 = e.vout + (uint32_t)(16 * I) * e.ldc_bytes + 128u * pp;
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v_t, d1), e.rc, o1, 0, 0);
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v_t, d2), e.rc, o1 + 8u * e.ldc_bytes, 0, 0);
+  }
+}
+// (a lean gate|up GEGLU epilogue -- the same buffer-resource addressing for its g, u, h register-layout stores --
+// measured 1 % slower than w4_rows' on the 4-wave kernel, 762.7 vs 755.7 us, profiles/r05_lean_epilogue_ab.txt, and
+// is not kept)
+template <int ACT, int NJ>
+PTK_DEV void w4_epilogue_lean_glu(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, long col0, int lane,
+                                  uint32_t c_bytes) {
+  static_assert(ACT == ACT_GEGLU_BWD, "lean GEGLU backward only");
+  if (col0 >= p.N) return;
+  const int q = lane >> 4;
+  const int cb = 16 * (q & 1) + 8 * (q >> 1);
+  const uint32_t rows = (uint32_t)p.M;
+  const uint32_t ldc_bytes = __builtin_amdgcn_readfirstlane((uint32_t)p.ldc * 2u);
+  const uint32_t crow0 = (uint32_t)(row0 + p.cmap.off);
+  {
+    constexpr int NP = NJ / 2;
+    LeanGbwd e;
+    e.ldin_bytes = __builtin_amdgcn_readfirstlane((uint32_t)p.ld_aux_in * 2u);
+    e.ldc_bytes = ldc_bytes;
+    e.rgi = __builtin_amdgcn_make_buffer_rsrc((void*)p.aux_in, 0, (int)(rows * e.ldin_bytes), 0x00020000);
+    e.rui = __builtin_amdgcn_make_buffer_rsrc((void*)p.aux_in2, 0, (int)(rows * e.ldin_bytes), 0x00020000);
+    e.rc = __builtin_amdgcn_make_buffer_rsrc(p.C, 0, (int)c_bytes, 0x00020000);
+    e.vin = ((uint32_t)row0 + (lane & 15)) * e.ldin_bytes + (uint32_t)(col0 + cb) * 2u;
+    // dg | du line pp of rows (lane & 7) / 8 + (lane & 7): w4_gbwd_rows' output column map
+    const bool lo = (lane & 8) == 0;
+    e.vout = (crow0 + (lane & 7)) * ldc_bytes +
+             (uint32_t)(2 * col0 + 8 * (4 * (cb >> 4) + ((cb >> 3) & 1) + (lo ? 0 : 2))) * 2u;
+    u16x8_t G0[NP], U0[NP], G1[NP], U1[NP];
+    w4_gbwd_load_lean<0, NP>(e, G0, U0);
+    w4_gbwd_load_lean<1, NP>(e, G1, U1);
+    w4_gbwd_rows_lean<0, NP>(acc[0], e, G0, U0);
+    w4_gbwd_load_lean<2, NP>(e, G0, U0);
+    w4_gbwd_rows_lean<1, NP>(acc[1], e, G1, U1);
+    w4_gbwd_load_lean<3, NP>(e, G1, U1);
+    w4_gbwd_rows_lean<2, NP>(acc[2], e, G0, U0);
+    w4_gbwd_load_lean<4, NP>(e, G0, U0);
+    w4_gbwd_rows_lean<3, NP>(acc[3], e, G1, U1);
+    w4_gbwd_load_lean<5, NP>(e, G1, U1);
+    w4_gbwd_rows_lean<4, NP>(acc[4], e, G0, U0);
+    w4_gbwd_load_lean<6, NP>(e, G0, U0);
+    w4_gbwd_rows_lean<5, NP>(acc[5], e, G1, U1);
+    w4_gbwd_load_lean<7, NP>(e, G1, U1);
+    w4_gbwd_rows_lean<6, NP>(acc[6], e, G0, U0);
+    w4_gbwd_rows_lean<7, NP>(acc[7], e, G1, U1);
+  }
+}
+
 // the wave's 128 x 16NJ accumulator tile (8 row blocks of NJ 16x16 MFMA tiles)
 template <int ACT, int OUT, int NJ = 8>
 PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, long col0, int lane) {

@@ -248,7 +248,9 @@ __global__ void __launch_bounds__(256, 1) gemm_w4_kernel(GemmArgs p, uint32_t a_
 #endif
       {
         const long row0 = (long)bm * W4 + wr * 128, col0 = (long)bn * W4 + wc * 128;
-        if constexpr (LEAN) w4_epilogue_lean<ACT, 8>(kernarg_args(), acc, row0, col0, lane, c_bytes);
+        if constexpr (LEAN && ACT == ACT_GEGLU_BWD)
+          w4_epilogue_lean_glu<ACT, 8>(kernarg_args(), acc, row0, col0, lane, c_bytes);
+        else if constexpr (LEAN) w4_epilogue_lean<ACT, 8>(kernarg_args(), acc, row0, col0, lane, c_bytes);
         else w4_epilogue<ACT, OUT>(kernarg_args(), acc, row0, col0, lane);
       }
       P8_STAMP(3, (t - loc) / G);
@@ -317,9 +319,29 @@ double w4_round_fill(long M, long N) {
 // plus cmap.off); whole 64-column wave ranges; C's extent (rows cmap.off .. M + cmap.off) below 2^31 bytes.
 // c_bytes = that extent (num_records of the store resource: rows past M are dropped).  PTK_LEAN_EPI=0 keeps the
 // general epilogue (A/B; bit-identical either way)
-bool lean_epilogue_ok(const GemmArgs& a, int act, int out, uint32_t& c_bytes) {
+static bool lean_on() {
   static const bool on = [] { const char* e = getenv("PTK_LEAN_EPI"); return !(e && e[0] == '0'); }();
-  if (!on || (act != ACT_NONE && act != ACT_GELU_TANH) || out != OUT_BF16) return false;
+  return on;
+}
+// the lean GEGLU-backward epilogue (w4_epilogue_lean_glu): the saved g, u inputs with 16-B rows, no other epilogue
+// input, an offset C row map, whole 128-column wave ranges, extents below 2^31 bytes
+static bool lean_glu_ok(const GemmArgs& a, int act, int out, uint32_t& c_bytes) {
+  if (!lean_on() || act != ACT_GEGLU_BWD || out != OUT_BF16) return false;
+  if (a.bias || a.rowadd || a.resid || a.resid16 || a.bf16_linear || a.row_stats || a.alpha != 1.f) return false;
+  const bool affine = a.cmap.g == 0 || (a.cmap.skip == 0 && a.cmap.gs == a.cmap.g);
+  if (!affine || a.cmap.off < 0 || a.amap.g != 0 || a.N % 128 || a.ldc % 8 || ((uintptr_t)a.C & 15)) return false;
+  if (!a.aux_in || !a.aux_in2 || a.ld_aux_in % 8 || a.ld_aux_in < a.N) return false;
+  if (((uintptr_t)a.aux_in | (uintptr_t)a.aux_in2) & 15) return false;
+  if (a.ldc < 2 * a.N) return false;
+  const double side = (double)a.M * (double)a.ld_aux_in * 2.0;
+  const double bytes = ((double)a.M + (double)a.cmap.off) * (double)a.ldc * 2.0;
+  if (bytes >= 2147483000.0 || side >= 2147483000.0) return false;
+  c_bytes = (uint32_t)bytes;
+  return true;
+}
+bool lean_epilogue_ok(const GemmArgs& a, int act, int out, uint32_t& c_bytes) {
+  if (act == ACT_GEGLU_BWD) return lean_glu_ok(a, act, out, c_bytes);
+  if (!lean_on() || (act != ACT_NONE && act != ACT_GELU_TANH) || out != OUT_BF16) return false;
   if (a.rowadd || a.resid || a.aux || a.aux2 || a.aux_in || a.aux_in2 || a.row_stats || a.alpha != 1.f) return false;
   const bool affine = a.cmap.g == 0 || (a.cmap.skip == 0 && a.cmap.gs == a.cmap.g);
   if (!affine || a.cmap.off < 0 || a.N % 64 || a.ldc % 8 || a.ldc < a.N || ((uintptr_t)a.C & 15)) return false;
@@ -344,10 +366,13 @@ int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
   uint32_t cb = 0;
   if (lean_epilogue_ok(a, act, out, cb)) {
-    if (act == ACT_GELU_TANH)
-      hipLaunchKernelGGL((gemm_w4_kernel<ACT_GELU_TANH, OUT_BF16, true>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb, cb);
-    else
-      hipLaunchKernelGGL((gemm_w4_kernel<ACT_NONE, OUT_BF16, true>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb, cb);
+#define PTK_W4L_CASE(ACT_)                                                                                   \
+    if (act == ACT_)                                                                                         \
+      hipLaunchKernelGGL((gemm_w4_kernel<ACT_, OUT_BF16, true>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb, cb);
+    PTK_W4L_CASE(ACT_NONE)
+    PTK_W4L_CASE(ACT_GELU_TANH)
+    PTK_W4L_CASE(ACT_GEGLU_BWD)
+#undef PTK_W4L_CASE
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_w4 launch failed");
   }
 #define PTK_W4_CASE(ACT_, OUT_)                                                                   \
@@ -691,7 +716,9 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
         if (em_ != 1)
 #endif
         {
-          if constexpr (LEAN) w4_epilogue_lean<ACT, 4>(kernarg_args(), acc, row0, col0, lane, c_bytes);
+          if constexpr (LEAN && ACT == ACT_GEGLU_BWD)
+            w4_epilogue_lean_glu<ACT, 4>(kernarg_args(), acc, row0, col0, lane, c_bytes);
+          else if constexpr (LEAN) w4_epilogue_lean<ACT, 4>(kernarg_args(), acc, row0, col0, lane, c_bytes);
           else w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane);
         }
       } else if constexpr (SK) {
@@ -824,12 +851,14 @@ int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk)
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
   uint32_t cb = 0;
   if (!tl.units && lean_epilogue_ok(a, act, out, cb)) {
-    if (act == ACT_GELU_TANH)
-      hipLaunchKernelGGL((gemm_p8_kernel<ACT_GELU_TANH, OUT_BF16, false, true>), dim3((unsigned)grid), dim3(512), 0, st,
-                         a, ab, bb, tl, cb);
-    else
-      hipLaunchKernelGGL((gemm_p8_kernel<ACT_NONE, OUT_BF16, false, true>), dim3((unsigned)grid), dim3(512), 0, st, a,
-                         ab, bb, tl, cb);
+#define PTK_P8L_CASE(ACT_)                                                                                   \
+    if (act == ACT_)                                                                                         \
+      hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_BF16, false, true>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, \
+                         bb, tl, cb);
+    PTK_P8L_CASE(ACT_NONE)
+    PTK_P8L_CASE(ACT_GELU_TANH)
+    PTK_P8L_CASE(ACT_GEGLU_BWD)
+#undef PTK_P8L_CASE
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");
   }
 #define PTK_P8_CASE(ACT_, OUT_)                                                                       \
