@@ -820,12 +820,12 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // two-group persistent kernel (gemm_dual.hip): PTK_DUAL=1 puts every persistent (w4 / p8) shape on it (A/B)
   static const bool dual_env = [] { const char* e = getenv("PTK_DUAL"); return e && e[0] == '1'; }();
   const bool dual_auto = g_force_tiles == 0 && !sk && dual_env && (p8_auto || w4_auto);
-  if (batch == 1 && (g_force_tiles == 64 || dual_auto) && dual_supported(a, act, out)) {
+  if (batch == 1 && (g_force_tiles == 64 || g_force_tiles == 128 || dual_auto) && dual_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);
     count_path(GEMM_PATH_DUAL, act);
-    const int rc = launch_gemm_dual(a, act, out, st);
+    const int rc = launch_gemm_dual(a, act, out, st, g_force_tiles == 128);
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
   }

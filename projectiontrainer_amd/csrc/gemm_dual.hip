@@ -49,23 +49,26 @@ constexpr int DU_PIECES = 6;                        // LDS-DMA pieces per wave p
 static_assert(DU_LAG % 2 == 1 && DU_LAG >= DU_EPI && DU_EPI % 2 == 0, "phase offsets");
 }  // namespace
 
-template <int ACT, int OUT>
-__global__ void __launch_bounds__(512, 1) gemm_dual_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes) {
-  __shared__ __attribute__((aligned(16))) char smem[2 * DU_RING];   // 144 KiB: the two groups' rings
+// SOLO: one group per workgroup (256 threads, 72 KiB of LDS, two workgroups per CU): the same tiles, ring and
+// phases, the two groups of a CU independent (their own barriers) instead of LAG phases apart in one workgroup
+template <int ACT, int OUT, bool SOLO>
+__global__ void __launch_bounds__(SOLO ? 256 : 512, SOLO ? 2 : 1) gemm_dual_kernel(GemmArgs p, uint32_t a_bytes,
+                                                                                   uint32_t b_bytes) {
+  __shared__ __attribute__((aligned(16))) char smem[(SOLO ? 1 : 2) * DU_RING];   // the groups' rings
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int grp = wave >> 2, q = wave & 3, wr = q >> 1, wc = q & 1;
+  const int grp = SOLO ? 0 : wave >> 2, q = wave & 3, wr = q >> 1, wc = q & 1;
   const int nbm = (p.M + W4 - 1) / W4, nbn = (p.N + DU_BN - 1) / DU_BN;
   const int ntile = nbm * nbn;
-  const int G = gridDim.x, G2 = 2 * G;
+  const int G = gridDim.x, G2 = SOLO ? G : 2 * G;
   int loc;
   {
     const int b = blockIdx.x, qq = G >> 3, rr = G & 7, x = b & 7;
     loc = (x < rr ? x * (qq + 1) : rr * (qq + 1) + (x - rr) * qq) + (b >> 3);
   }
-  const int gid0 = 2 * loc, gid = gid0 + grp;
+  const int gid0 = SOLO ? loc : 2 * loc, gid = gid0 + grp;
   const int n0 = gid0 < ntile ? (ntile - gid0 + G2 - 1) / G2 : 0;
-  const int n1 = gid0 + 1 < ntile ? (ntile - gid0 - 1 + G2 - 1) / G2 : 0;
+  const int n1 = (!SOLO && gid0 + 1 < ntile) ? (ntile - gid0 - 1 + G2 - 1) / G2 : 0;
   const int nmine = grp ? n1 : n0;
   const int nks = p.K / W4_KS;                      // 32-deep k-steps per tile
   const int per_tile = 2 * nks + DU_EPI;            // phases per tile
@@ -240,16 +243,19 @@ __global__ void __launch_bounds__(512, 1) gemm_dual_kernel(GemmArgs p, uint32_t 
 // the dual path takes what the persistent kernels take (gemm_w4.hip w4_supported)
 bool dual_supported(const GemmArgs& a, int act, int out) { return w4_supported(a, act, out); }
 
-int launch_gemm_dual(const GemmArgs& a, int act, int out, hipStream_t st) {
+int launch_gemm_dual(const GemmArgs& a, int act, int out, hipStream_t st, bool solo) {
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + DU_BN - 1) / DU_BN);
-  const long grid = std::min<long>((ntile + 1) / 2, device_cus());
+  const long grid = solo ? std::min<long>(ntile, 2L * device_cus()) : std::min<long>((ntile + 1) / 2, device_cus());
   if (grid <= 0) return 0;
   const long arows = a.M + a.amap.off;
   const uint32_t ab = (uint32_t)std::min<double>((double)arows * a.lda * 2, 2147483000.0);
   const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
 #define PTK_DU_CASE(ACT_, OUT_)                                                                       \
   if (act == ACT_ && out == OUT_) {                                                                   \
-    hipLaunchKernelGGL((gemm_dual_kernel<ACT_, OUT_>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb); \
+    if (solo)                                                                                         \
+      hipLaunchKernelGGL((gemm_dual_kernel<ACT_, OUT_, true>), dim3((unsigned)grid), dim3(256), 0, st, a, ab, bb); \
+    else                                                                                              \
+      hipLaunchKernelGGL((gemm_dual_kernel<ACT_, OUT_, false>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb); \
     return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_dual launch failed");                \
   }
   PTK_DU_CASE(ACT_NONE, OUT_BF16)
