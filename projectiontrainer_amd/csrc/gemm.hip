@@ -810,7 +810,12 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
                        ((w4_auto && (p8_env || (act != ACT_GEGLU && act != ACT_GEGLU_BWD && a.K <= 2048))) ||
                         ((act == ACT_GELU_ERF || act == ACT_GELU_ERF_BWD) && out == OUT_BF16 && a.K <= 2048 &&
                          w4_round_fill(a.M, a.N) >= 0.8) ||
-                        (act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32) && a.K >= 12288 && a.N <= 2048));
+                        (act == ACT_NONE && (out == OUT_BF16 || out == OUT_F32) && a.K >= 12288 && a.N <= 2048) ||
+                        // r05: with the lean bf16 epilogue the 8-wave kernel also beats the 128x128 one on the N 1536
+                        // projection at 69 % round fill (Gemma q|k|v 90.7 vs 95.3 us, profiles/r05_dual_solo_probe.txt);
+                        // the N 1024 ones stay on 128x128 (dO 66.0 vs 63.2, SigLIP fc2 187 vs 171)
+                        (act == ACT_NONE && out == OUT_BF16 && a.N >= 1536 && a.K <= 2048 &&
+                         w4_round_fill(a.M, a.N) >= 0.65 && lean_epilogue_candidate(a)));
   // the stream-K tail (gemm_w4.hip P8Tail): a plain GEMM whose last tile round fills the CUs badly, with tail
   // scratch lent by the model-level call (or in the descriptor), runs on the persistent 8-wave kernel with that
   // round's K-tiles spread over the CUs (r04: the N = 1024 / 1152 / 1536 projections, the long-K d(gate|up) dX

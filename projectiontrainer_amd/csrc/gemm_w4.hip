@@ -354,6 +354,11 @@ bool lean_epilogue_ok(const GemmArgs& a, int act, int out, uint32_t& c_bytes) {
   return true;
 }
 
+bool lean_epilogue_candidate(const GemmArgs& a) {
+  uint32_t cb = 0;
+  return lean_epilogue_ok(a, ACT_NONE, OUT_BF16, cb);
+}
+
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid) {
   num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);

@@ -69,6 +69,8 @@ bool p8_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk);
 // persistent two-group kernel (gemm_dual.hip): 256x128 tiles, one group's epilogue beside the other's K loop
 bool dual_supported(const GemmArgs& a, int act, int out);
+// the persistent kernels would take their lean bf16 epilogue for this plain bf16 GEMM (gemm_w4.hip lean_epilogue_ok)
+bool lean_epilogue_candidate(const GemmArgs& a);
 int launch_gemm_dual(const GemmArgs& a, int act, int out, hipStream_t st, bool solo);   // solo: 256x128 tiles, 2 WGs/CU
 // stream-K tail of the persistent 8-wave kernel: scratch bytes (arrival counters, then partial slabs), the
 // workgroups its plan spreads a GEMM's tail over (0: no split), and the thread-local scratch a model-level

@@ -29,18 +29,20 @@ def roles(cfg):
                  t.num_attention_heads * B for i in range(L))
     # family -> list of (role, launches per step, FLOPs per launch)
     return {
-        "gemm_p8_kernel<0, 0": [
+        # r05: the plain bf16 projections run the lean epilogue (gemm_p8_kernel<0, 0, false, true>), Gemma q|k|v
+        # moved here from the 128x128 kernel
+        "gemm_p8_kernel<0, 0, false, true>": [
             ("SigLIP q|k|v", Lv, 2 * M_v * D * 3 * D),
+            ("Gemma q|k|v", L, 2 * M_g * H * (q + 2 * kv)),
             ("Gemma o", L, 2 * M_g * q * H),
             ("Gemma d(gate|up) dX", L - 1, 2 * M_g * 2 * I * H),
             ("Gemma d(q|k|v) dX", L, 2 * M_g * (q + 2 * kv) * H)],
-        "gemm_w4_kernel<3, 0>": [("Gemma gate|up + GEGLU", L - 1, 2 * M_g * 2 * I * H)],
-        "gemm_w4_kernel<5, 0>": [("Gemma dh + GEGLU backward", L - 1, 2 * M_g * I * H)],
-        "gemm_w4_kernel<0, 0>": [("Gemma down", L - 1, 2 * M_g * I * H)],
+        "gemm_w4_kernel<3, 0,": [("Gemma gate|up + GEGLU", L - 1, 2 * M_g * 2 * I * H)],
+        "gemm_w4_kernel<5, 0,": [("Gemma dh + GEGLU backward", L - 1, 2 * M_g * I * H)],
+        "gemm_w4_kernel<0, 0,": [("Gemma down", L - 1, 2 * M_g * I * H)],
         "gemm_nt_kernel<0, 0>": [
             ("SigLIP o", Lv, 2 * M_v * D * D),
             ("SigLIP fc2", Lv, 2 * M_v * Iv * D),
-            ("Gemma q|k|v", L, 2 * M_g * H * (q + 2 * kv)),
             ("Gemma dO", L, 2 * M_g * H * q)],
         "gemm_p8_kernel<1, 0": [("SigLIP fc1 + GELU-tanh", Lv, 2 * M_v * D * Iv)],
         "attn_fwd64_kernel": [("SigLIP attention", Lv, 2 * 2 * N * N * D * B)],
