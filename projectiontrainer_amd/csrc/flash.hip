@@ -376,6 +376,19 @@ PTK_DEV fa_u32x4_t fa_rsrc(const void* base, uint32_t bytes) {
   return r;
 }
 PTK_DEV uint32_t fa_lds_addr(const void* p) { return (uint32_t)(uintptr_t)(fa_lptr_t)p; }
+// the kernel's FlashArgs argument (offset 0 of the kernarg segment) behind a pointer the compiler cannot see
+// through: the persistent kernels read the per-item fields by scalar loads at item boundaries instead of keeping
+// some 50 SGPRs of arguments live across the K/V loop (which spilled)
+typedef const FlashArgs __attribute__((address_space(4)))* fa_kargs_ptr_t;
+PTK_DEV const FlashArgs& fa_kernarg() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  fa_kargs_ptr_t pk = (fa_kargs_ptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(pk));
+  return *(const FlashArgs*)pk;
+#else
+  __builtin_unreachable();
+#endif
+}
 template <int N> using fa_ic = std::integral_constant<int, N>;
 
 // per-tile 32-bit key masks (key valid and < nkeys) of tiles [t_lo, t_hi) into LDS, tile tt by wave tt % NW:
@@ -419,7 +432,7 @@ PTK_DEV void fa_key_masks(const int* kvl, int nkeys, int t_lo, int t_hi, int wav
 // LDS images (32 rows x 512 B, chunk c of row r at chunk c ^ swz(r)): K swz = r & 15 (the b128 row reads of
 // 16 distinct keys per lane group hit 16 distinct bank quads), V swz = 4 (r & 3) (each 32-lane half of a
 // transposed read takes 4 rows r..r+3 x 64 B: 4 distinct bank quads of 16).
-__global__ void __launch_bounds__(256, 1) attn_fwd256w_kernel(FlashArgs a) {
+__global__ void __launch_bounds__(256, 1) attn_fwd256w_kernel(FlashArgs a, int nz, int nitems) {
   constexpr int D = 256, KT = 32, NB = 4;
   constexpr int TILE = KT * D * 2;   // 16 KiB
   __shared__ __attribute__((aligned(16))) char smem[2 * NB * TILE + FA_MAXT * 4];
@@ -431,50 +444,57 @@ __global__ void __launch_bounds__(256, 1) attn_fwd256w_kernel(FlashArgs a) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, c32 = lane & 31;
-  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
-  const int z = blockIdx.x % nz, z0 = z / a.zin, z1 = z - z0 * a.zin;
-  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;   // heaviest (latest) row blocks first
-  const bf16_t* Q = a.Q + z0 * a.sQ0 + z1 * a.sQ1;
-  const bf16_t* K = a.K + z0 * a.sK0 + z1 * a.sK1;
-  const bf16_t* V = a.V + z0 * a.sK0 + z1 * a.sK1;
-  const long b = z / a.zdiv;
-  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
+  const int nqb = (a.rows + 127) / 128;
+  const int causal = a.causal != 0, nowin = a.window <= 0;
 
-  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
-  int k_hi = a.nkeys, k_lo = 0;
-  if (a.causal) {
-    k_hi = min(k_hi, pos_hi + 1);
-    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
-  }
-  const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
-
-  // ---- Q fragments: B operand of S^T = K Q^T for k-step ks, lane holds Q[row c32][16 ks + 8 h .. +7]; the
-  // loads are issued first and stay in flight while the key masks are built
-  const int wrow0 = r0 + wave * 32;
-  const int qrow = wrow0 + c32;
-  const int qrow_c = min(qrow, a.rows - 1);
-  const int qpos = qrow_c / a.qdiv;
+  // ---- work items (row block of 128 query rows, z), heaviest (latest) row blocks first: item i is row block
+  // nqb - 1 - i / nz of z = i % nz.  Workgroup b runs items b, 2G - 1 - b, 2G + b, .. (G = gridDim.x; a grid of
+  // one workgroup per item runs one each).  Per-item state, set by begin_item:
+  int z0 = 0, z1 = 0, t_lo = 0, t_hi = 0, wrow0 = 0, qrow = 0, qpos = 0, wpos_lo = 0, wpos_hi = 0;
+  long zi = 0;
+  fa_u32x4_t rsk, rsv;
   bf16x8_t qf[16];
-  {
-    const bf16_t* qp = Q + map_row(a.qmap, qrow_c) * a.ldq + 8 * h;
+  // begin_item part 1: the item's geometry and its key-mask table (kmask_s: every wave must have passed its last
+  // read of the previous item's table); part 2: the Q fragments (B operand of S^T = K Q^T for k-step ks: lane holds
+  // Q[row c32][16 ks + 8 h .. +7]), whose loads stay in flight until the K/V loop needs them
+  auto begin_item = [&](int item) __attribute__((always_inline)) {
+    const FlashArgs& a = fa_kernarg();
+    const int z = item % nz;
+    zi = z;
+    z0 = z / a.zin;
+    z1 = z - z0 * a.zin;
+    const int r0 = (nqb - 1 - item / nz) * 128;
+    const long b = z / a.zdiv;
+    const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
+    const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
+    int k_hi = a.nkeys, k_lo = 0;
+    if (a.causal) {
+      k_hi = min(k_hi, pos_hi + 1);
+      if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
+    }
+    t_lo = k_lo / KT;
+    t_hi = (k_hi + KT - 1) / KT;
+    wrow0 = r0 + wave * 32;
+    qrow = wrow0 + c32;
+    wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
+    wpos_hi = min(wrow0 + 31, a.rows - 1) / a.qdiv;
+    fa_key_masks<4>(kvl, a.nkeys, t_lo, t_hi, wave, lane, kmask_s);
+    const bf16_t* K = a.K + z0 * a.sK0 + z1 * a.sK1;
+    const bf16_t* V = a.V + z0 * a.sK0 + z1 * a.sK1;
+    rsk = fa_rsrc(K, (uint32_t)((long)a.nkeys * a.ldk * 2));
+    rsv = fa_rsrc(V, (uint32_t)((long)a.nkeys * a.ldk * 2));
+  };
+  auto load_q = [&]() __attribute__((always_inline)) {
+    const FlashArgs& a = fa_kernarg();
+    const int qrow_c = min(qrow, a.rows - 1);
+    qpos = qrow_c / a.qdiv;
+    const bf16_t* qp = a.Q + z0 * a.sQ0 + z1 * a.sQ1 + map_row(a.qmap, qrow_c) * a.ldq + 8 * h;
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) qf[ks] = *reinterpret_cast<const bf16x8_t*>(qp + 16 * ks);
-  }
-  fa_key_masks<4>(kvl, a.nkeys, t_lo, t_hi, wave, lane, kmask_s);
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) fa_pin(qf[ks]);
-  __syncthreads();   // key masks published (no LDS-DMA in flight yet)
-  FA_STAMP(1);
-
-  const int causal = a.causal != 0, nowin = a.window <= 0;
-  const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
-  const int wpos_hi = min(wrow0 + 31, a.rows - 1) / a.qdiv;
-  const bool idle = wrow0 >= a.rows;   // rows past the end: stage and keep the barriers only
+  };
 
   // ---- DMA: wave w stages rows 8w..8w+7 of each tile (4 pieces of 2 rows x 512 B per tensor); lane i of a
   // piece writes LDS row 8w + 2j + (i >> 5), chunk i & 31, fetched from logical chunk (i & 31) ^ swz(row)
-  const fa_u32x4_t rsk = fa_rsrc(K, (uint32_t)((long)a.nkeys * a.ldk * 2));
-  const fa_u32x4_t rsv = fa_rsrc(V, (uint32_t)((long)a.nkeys * a.ldk * 2));
   uint32_t dk[4], dv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -491,6 +511,13 @@ __global__ void __launch_bounds__(256, 1) attn_fwd256w_kernel(FlashArgs a) {
     for (int j = 0; j < 4; ++j) FA_DMA(dk[j], so, rsk, lds_k + bb * TILE + j * 1024);
 #pragma unroll
     for (int j = 0; j < 4; ++j) FA_DMA(dv[j], so, rsv, lds_v + bb * TILE + j * 1024);
+  };
+  // the first three tiles of the item into ring slots 0..2 (past the last tile: re-loads of it, never read)
+  auto stage_first = [&]() __attribute__((always_inline)) {
+    if (t_lo < t_hi) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) stage(i, min(t_lo + i, t_hi - 1));
+    }
   };
 
   // ---- LDS read addresses (lane part; the ring slot and the rest are immediates).
@@ -664,20 +691,21 @@ __global__ void __launch_bounds__(256, 1) attn_fwd256w_kernel(FlashArgs a) {
   // same 8 pieces and waits with the same count.  Fully masked tiles are computed like the others
   // (exp2(-inf) = 0).  The loop body is unrolled by two so the two score accumulators swap roles without a
   // copy.
-  if (t_lo < t_hi) {
+  // Persistent items: after an item's last P.V, a barrier (every wave is done with the ring and the key-mask
+  // table), then the next item's key masks, Q loads and first three K / V tiles are issued BEFORE this item's
+  // epilogue, so their latency runs under the epilogue's normalisation and stores.
+  int item = blockIdx.x, round_k = 0;
+  begin_item(item);
+  load_q();
 #pragma unroll
-    for (int i = 0; i < 3; ++i) stage(i, min(t_lo + i, t_hi - 1));
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
+  for (int ks = 0; ks < 16; ++ks) fa_pin(qf[ks]);
+  __syncthreads();   // key masks published (no LDS-DMA in flight yet)
+  FA_STAMP(1);
+  stage_first();
   using T_ = std::true_type;
   using F_ = std::false_type;
-  f32x16_t sa, sb = (f32x16_t){};
+  f32x16_t sa, sb;
   bf16x8_t pf[2];
-  phase_a(T_{}, F_{}, 0, sa, sb, pf);   // QK^T of tile t_lo (t_lo == t_hi: slot 0 holds nothing, unused)
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // its MFMA results -> the first VALU reads
-  FA_STAMP(2);
   auto slot = [&](int t) { return (uint32_t)((t - t_lo) & (NB - 1)) * (uint32_t)TILE; };
   auto iter = [&](int t, f32x16_t& s_cur, f32x16_t& s_next) __attribute__((always_inline)) {
     mask(t, s_cur);
@@ -688,51 +716,90 @@ __global__ void __launch_bounds__(256, 1) attn_fwd256w_kernel(FlashArgs a) {
     rescale();
     phase_b(T_{}, slot(t), pf, (t - t_lo + 3) & (NB - 1), min(t + 3, t_hi - 1));
   };
-  int t = t_lo;
-  for (; t + 2 < t_hi; t += 2) {
-    iter(t, sa, sb);
-    iter(t + 1, sb, sa);
-  }
-  if (t + 1 < t_hi) {
-    iter(t, sa, sb);
-    ++t;
-    sa = sb;
-  }
-  if (t < t_hi) {   // the last tile: softmax and P.V only
-    mask(t, sa);
-    phase_a(F_{}, T_{}, 0, sb, sa, pf);
-    rescale();
-    phase_b(F_{}, slot(t), pf, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup exits
-  FA_STAMP(3);
-
-  // ---- epilogue: O[q][d] = O^T[d][q] / l.  Lane half h holds d = 32db + 8i + 4h + (0..3) for query c32;
-  // one permlane32 swap per register pair (i = 2m, 2m + 1) gives the lower half d 32db + 16m + 0..7 and the
-  // upper half 32db + 16m + 8..15, stored 16 B per lane.
-  const float l_tot = l_run + xor32_get(l_run);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // the last P.V MFMAs -> VALU reads of O
-  if (qrow >= a.rows) return;
-  const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
-  bf16_t* op = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow) * a.ldo + 8 * h;
-#pragma unroll
-  for (int db = 0; db < 8; ++db) {
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      uint32_t w[4];   // packed bf16 pairs: registers (i = 2m: 0-1, i = 2m + 1: 2-3)
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int r = 8 * m + 2 * k;
-        w[k] = (uint32_t)f2bf(o[db][r] * inv) | ((uint32_t)f2bf(o[db][r + 1] * inv) << 16);
-      }
-      // lower half keeps registers of i = 2m and takes the upper half's i = 2m; the upper half keeps i = 2m+1
-      const auto s0 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
-      const auto s1 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
-      *reinterpret_cast<uint4*>(op + 32 * db + 16 * m) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+  for (;;) {
+    if (t_lo < t_hi) {
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // tile t_lo landed (tiles t_lo + 1, + 2 in flight)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
     }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) o[i] = (f32x16_t){};
+    m_run = -INFINITY;
+    l_run = 0.f;
+    sb = (f32x16_t){};
+    phase_a(T_{}, F_{}, 0, sa, sb, pf);   // QK^T of tile t_lo (t_lo == t_hi: slot 0 holds nothing, unused)
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // its MFMA results -> the first VALU reads
+    FA_STAMP(2);
+    int t = t_lo;
+    for (; t + 2 < t_hi; t += 2) {
+      iter(t, sa, sb);
+      iter(t + 1, sb, sa);
+    }
+    if (t + 1 < t_hi) {
+      iter(t, sa, sb);
+      ++t;
+      sa = sb;
+    }
+    if (t < t_hi) {   // the last tile: softmax and P.V only
+      mask(t, sa);
+      phase_a(F_{}, T_{}, 0, sb, sa, pf);
+      rescale();
+      phase_b(F_{}, slot(t), pf, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the item's stream is done; nothing else in flight)
+    FA_STAMP(3);
+
+    // ---- epilogue: O[q][d] = O^T[d][q] / l.  Lane half h holds d = 32db + 8i + 4h + (0..3) for query c32;
+    // one permlane32 swap per register pair (i = 2m, 2m + 1) gives the lower half d 32db + 16m + 0..7 and the
+    // upper half 32db + 16m + 8..15, stored 16 B per lane.  Its outputs' addresses are taken before the next
+    // item's state replaces this one's.
+    const float l_tot = l_run + xor32_get(l_run);
+    const FlashArgs& ka = fa_kernarg();
+    const bool row_ok = qrow < ka.rows;
+    bf16_t* op = ka.O + z0 * ka.sO0 + z1 * ka.sO1 + map_row(ka.omap, row_ok ? qrow : 0) * ka.ldo + 8 * h;
+    float* lsep = ka.lse ? ka.lse + zi * ka.rows + qrow : nullptr;
+    const float lse_v = (m_run * sl2 + log2f(l_tot)) * 0.6931471805599453f;
+    // snake order over rounds of G items (round k: workgroup b takes item kG + b for even k, kG + G - 1 - b for
+    // odd k): a heavy row block pairs with a light one (the causal tiles per item fall with the item index);
+    // round-robin measured slower than one workgroup per item, r05
+    ++round_k;
+    const int next = round_k * (int)gridDim.x +
+                     ((round_k & 1) ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x);
+    if (next < nitems) {
+      __builtin_amdgcn_s_barrier();   // every wave is past its last read of the ring and of the mask table
+      begin_item(next);
+      load_q();
+      stage_first();
+    }
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // the last P.V MFMAs -> VALU reads of O
+    if (row_ok) {
+      const float inv = l_tot > 0.f ? 1.f / l_tot : 0.f;
+#pragma unroll
+      for (int db = 0; db < 8; ++db) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          uint32_t w[4];   // packed bf16 pairs: registers (i = 2m: 0-1, i = 2m + 1: 2-3)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int r = 8 * m + 2 * k;
+            w[k] = (uint32_t)f2bf(o[db][r] * inv) | ((uint32_t)f2bf(o[db][r + 1] * inv) << 16);
+          }
+          // lower half keeps registers of i = 2m and takes the upper half's i = 2m; the upper half keeps i = 2m+1
+          const auto s0 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+          *reinterpret_cast<uint4*>(op + 32 * db + 16 * m) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        }
+      }
+      if (lsep && h == 0) *lsep = lse_v;
+    }
+    if (next >= nitems) break;
+    item = next;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) fa_pin(qf[ks]);
+    // the next item's key masks published; raw barrier: its LDS-DMA stays in flight (a __syncthreads would drain it)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
-  if (a.lse && h == 0)
-    a.lse[(long)z * a.rows + qrow] = (m_run * sl2 + log2f(l_tot)) * 0.6931471805599453f;
   FA_STAMPS_WRITE(0, t_hi - t_lo);
 }
 
@@ -2435,8 +2502,13 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
       // the generic kernel past the 4096-key mask table
       if ((a.nkeys + 31) / 32 > FA_MAXT || (long)a.nkeys * a.ldk * 2 > 0x7fffffffL)
         hipLaunchKernelGGL((attn_fwd_kernel<256, 1>), grid, dim3(512), 0, st, a);
-      else
-        hipLaunchKernelGGL(attn_fwd256w_kernel, grid, dim3(256), 0, st, a);
+      else {
+        // persistent grid (one workgroup per CU walking the row blocks heaviest first, the next item's prologue
+        // beside this one's epilogue); PTK_ATTN_PERSIST=0: one workgroup per item (A/B, bit-identical)
+        static const bool persist = [] { const char* e = getenv("PTK_ATTN_PERSIST"); return !(e && e[0] == '0'); }();
+        const long g = persist ? std::min<long>(nblk, num_cus()) : nblk;
+        hipLaunchKernelGGL(attn_fwd256w_kernel, dim3((unsigned)g), dim3(256), 0, st, a, nz, (int)nblk);
+      }
       break;
     }
     default: return set_error("attn_fwd: head_dim %d unsupported (64, 256)", a.D);
