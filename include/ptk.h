@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTK_ABI_VERSION 5
+#define PTK_ABI_VERSION 6
 
 int ptk_abi_version(void);
 const char* ptk_last_error(void);
@@ -128,6 +128,15 @@ int ptk_transpose_bf16(const void* in, int64_t ld_in, void* out, int64_t ld_out,
  * dW = dY^T X (Stage2/trainer.py:400-441 autograd) become K-contiguous operands of the library's GEMMs. */
 int ptk_transpose_rows_bf16(const void* in, int64_t ld_in, int map_g, int64_t map_gs, int64_t map_off, int rows,
                             int cols, void* out, int64_t ld_out, int rows_pad, void* stream);
+/* Stage-2 weight grad of one nn.Linear (the autograd accumulate of Stage2/trainer.py:420-423 into a bf16 .grad):
+ * grad [Ny, Nx] = bf16(grad + bf16(dY^T X)) over `rows` token rows, dY [.., Ny] / X [.., Nx] token-major with row
+ * maps as ptk_transpose_rows_bf16's.  Identity maps and rows % 64 == 0: the persistent TN GEMM reads both where
+ * they lie (K slices as fp32 partials in `part` [slices][Ny][Nx], summed in slice order; part may be NULL: one
+ * slice); otherwise both are transposed into ta [Ny][Kp] / tb [Nx][Kp] (Kp = rows rounded up to 64) for the NT
+ * GEMMs.  mode: 0 auto, 1 the transpose path, 2 the TN path only (error where it does not apply). */
+int ptk_weight_grad_bf16(const void* dy, int64_t lddy, int y_map_g, int64_t y_map_gs, int64_t y_map_off, int Ny,
+                         const void* x, int64_t ldx, int x_map_g, int64_t x_map_gs, int64_t x_map_off, int Nx, int rows,
+                         void* grad, void* ta, void* tb, float* part, int64_t part_floats, int mode, void* stream);
 int ptk_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream);
 int ptk_fill_normal_bf16(void* out, int64_t n, uint64_t seed, float std, float mean, void* stream);
 /* Live GEMM timing: when enabled, HIP events are recorded on the launch stream

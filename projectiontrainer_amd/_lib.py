@@ -122,7 +122,7 @@ class ImageDesc(C.Structure):
                 ("coef_off", c_int64), ("tmp_off", c_int64)]
 
 
-ABI_VERSION = 5      # include/ptk.h PTK_ABI_VERSION
+ABI_VERSION = 6      # include/ptk.h PTK_ABI_VERSION
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -143,6 +143,9 @@ SIGNATURES = {
                                    c_int, c_int, c_void_p]),
     "ptk_transpose_rows_bf16": (c_int, [c_void_p, c_int64, c_int, c_int64, c_int64, c_int, c_int, c_void_p, c_int64,
                                         c_int, c_void_p]),
+    "ptk_weight_grad_bf16": (c_int, [c_void_p, c_int64, c_int, c_int64, c_int64, c_int,
+                                     c_void_p, c_int64, c_int, c_int64, c_int64, c_int, c_int,
+                                     c_void_p, c_void_p, c_void_p, c_void_p, c_int64, c_int, c_void_p]),
     "ptk_cast_f32_bf16": (c_int, [c_void_p, c_void_p, c_int64, c_void_p]),
     "ptk_fill_normal_bf16": (c_int, [c_void_p, c_int64, c_uint64, c_float, c_float, c_void_p]),
     "ptk_gemm_timer_enable": (c_int, [c_int]),

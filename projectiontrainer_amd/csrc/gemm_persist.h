@@ -21,6 +21,22 @@ namespace ptk {
 
 typedef __attribute__((ext_vector_type(4))) unsigned int u32x4v_t;
 
+// stream-K tail of the persistent 8-wave kernels (gemm_w4.hip gemm_p8_kernel, gemm_tn.hip gemm_tn_kernel): the
+// plan (p8_tail_plan) and the fixup that sums the cut tiles' pieces (launch_p8_fixup), described in gemm_w4.hip
+struct P8Tail {
+  int dp_tiles = 0;           // tiles [0, dp_tiles) run whole (R rounds of G)
+  int units = 0;              // U = tail tiles x K-tile pairs (0: no tail split)
+  int gsplit = 0;             // Gs: workgroups sharing the tail
+  float* slab = nullptr;      // [G][2 slots][8 waves][128 x 64] fp32 partials
+};
+constexpr size_t P8_WAVE_FLOATS = 128 * 64;
+// the plan of a GEMM with ntile tiles on a grid of G over scratch ws (nullptr: no split); the tail is split only
+// for R == 0 with at most max_t0 tail tiles or R == 1 with at most max_t1
+P8Tail p8_tail_plan_ws(const GemmArgs& a, long ntile, long G, void* ws, long max_t0, long max_t1);
+size_t p8_slab_bytes(long G);
+// the cut tail tiles' pieces summed in K order + the tile epilogue (ACT_NONE; the general epilogue's forms)
+int launch_p8_fixup(const GemmArgs& a, int act, int out, const P8Tail& tl, hipStream_t st);
+
 namespace {
 constexpr int W4 = 256;                  // output tile edge
 constexpr int W4_KT = 64;                // K granularity of the path (a pair of k-steps per barrier)
@@ -644,6 +660,12 @@ PTK_DEV const GemmArgs& kernarg_args() {
   __builtin_unreachable();   // host pass: device code only
 #endif
 }
+
+// stream-K tail units: the tail tile's pieces are summed in K order: piece jj of tile tt belongs to workgroup
+// g0 + jj, whose partial sits in its slot 0 if the piece is that workgroup's first (its unit range starts inside
+// the tile), else slot 1
+PTK_DEV int p8_owner(long x, int G, int U) { return (int)(((x + 1) * G - 1) / U); }   // workgroup of unit x
+PTK_DEV int p8_start(int g, int G, int U) { return (int)(((long)g * U) / G); }
 
 PTK_DEV void w4_tile_coords(int t, int nbm, int nbn, int& bm, int& bn) {
   const int per_group = 8 * nbn;

@@ -420,67 +420,16 @@ constexpr int P8_PIECES = 4;   // LDS-DMA pieces per wave per k-step
 // its first R whole rounds data-parallel (tiles loc, loc + G, ..: the lock-step L2 sharing of the plain kernel)
 // and spreads the K-tiles of the remaining tail tiles evenly over the first Gs workgroups (Gs <= G, chosen on
 // the host: more workgroups shorten the tail round but cut each tile into more pieces, and every extra piece
-// costs its reducer one more 256-KiB partial read): workgroup g < Gs takes the K-tile units
+// costs the fixup one more 256-KiB partial read): workgroup g < Gs takes the K-tile units
 // [g U / Gs, (g + 1) U / Gs) of the tail's U = tail tiles x K-tiles, i.e. the end of one tail tile and / or the
-// start of the next.  A tile covered by one workgroup runs the normal epilogue.  A tile split
-// over workgroups g0 .. g1 (its pieces, in K order) is finished by the wave that arrives last: every wave of a
-// piece writes its 128x64 fp32 partial (32 KiB, write-through `sc1` stores) to its workgroup's slot (slot 0
-// for the workgroup's first piece, 1 for its last), drains it (vmcnt(0)) and adds 1 to the (tile, wave)
-// arrival counter (agent scope); the wave whose add returns pieces - 1 loads the other pieces' partials
-// (`sc1` loads: MI355X_MICROARCH.md's hand-off row "one lane per storing wave, agent atomic add, sc1 stores
-// and loads"), sums all pieces in K order (deterministic: the same sum whichever piece arrives last), resets
-// the counter (every launch leaves the counters zero) and runs the fused epilogue.  No wave ever waits for
-// another workgroup, so the grid needs no co-residency.
-struct P8Tail {
-  int dp_tiles = 0;           // tiles [0, dp_tiles) run whole (R rounds of G)
-  int units = 0;              // U = tail tiles x K-tile pairs (0: no tail split)
-  int gsplit = 0;             // Gs: workgroups sharing the tail
-  float* slab = nullptr;      // [G][2 slots][8 waves][128 x 64] fp32 partials
-  uint32_t* cnt = nullptr;    // [tail tiles][8 waves] arrival counters
-};
-constexpr size_t P8_WAVE_FLOATS = 128 * 64;
+// start of the next.  A tile covered by one workgroup runs the normal epilogue.  A tile split over workgroups
+// g0 .. g1 (its pieces, in K order): every wave of a piece writes its 128x64 fp32 partial (32 KiB) to its
+// workgroup's slot (slot 0 for the workgroup's first piece, 1 for its last), and p8_fixup_kernel, launched
+// after the GEMM, sums each cut tile's pieces in K order (deterministic) and runs the tile's epilogue.  r04 let
+// the wave arriving last at a per-(tile, wave) counter do that sum inside the GEMM: one wave loading a piece's
+// row block at a time was latency-bound (~150 us on the Stage-2 d(gate|up) dX, profiles/r04_sk_ab.txt), where
+// the fixup spreads the same loads over 8 waves x 8 row blocks per tile.  No wave waits for another workgroup.
 
-// the tail tile's pieces are summed in K order: piece jj of tile tt belongs to workgroup g0 + jj, whose partial
-// sits in its slot 0 if the piece is that workgroup's first (its unit range starts inside the tile), else slot 1
-PTK_DEV int p8_owner(long x, int G, int U) { return (int)(((x + 1) * G - 1) / U); }   // workgroup of unit x
-PTK_DEV int p8_start(int g, int G, int U) { return (int)(((long)g * U) / G); }
-
-// row block I of the reducer: the tile's partials summed in K order (the reducer's own piece too, read back
-// from its slab: the accumulators are dead by then), then the fused epilogue of the row block.  Piece jj of the
-// tile belongs to workgroup g0 + jj; its partial sits in that workgroup's slot 0, except piece 0's when the
-// workgroup's range started in an earlier tile (s0 = 1: its slot 1)
-template <int ACT, int OUT, int I>
-PTK_DEV void p8_tail_rows(const GemmArgs& p, const float* slab, int g0, int np, int s0, int wave, long row0,
-                          long col0, int lane, char* sink) {
-  // sc1 buffer loads through the builtin (hipcc sees them and waits for their data itself: an asm load whose
-  // result register hipcc copies before an asm wait reads garbage -- the first version of this reducer did)
-  const __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)slab, 0, 0x7fffffff, 0x00020000);
-  f32x4_t sum[4];
-  for (int jj = 0; jj < np; ++jj) {
-    const uint32_t off = (uint32_t)(((((g0 + jj) * 2 + (jj == 0 ? s0 : 0)) * 8 + wave) * (int)P8_WAVE_FLOATS +
-                                     lane * 4 + 4 * I * 256) * 4);
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {   // K order: piece 0, 1, ..
-      const f32x4_t v = __builtin_bit_cast(f32x4_t, __builtin_amdgcn_raw_buffer_load_b128(rs, off + j * 1024, 0, 16));
-      sum[j] = jj == 0 ? v : sum[j] + v;
-    }
-  }
-  w4_rows<ACT, OUT, I, 4, false>(p, sum, row0, col0, lane, sink);
-}
-
-template <int ACT, int OUT>
-PTK_DEV void p8_tail_epilogue(const GemmArgs& p, const float* slab, int g0, int np, int s0, int wave, long row0,
-                              long col0, int lane) {
-  char* sink = g_w4_sink + lane * 64;
-  p8_tail_rows<ACT, OUT, 0>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 1>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 2>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 3>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 4>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 5>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 6>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
-  p8_tail_rows<ACT, OUT, 7>(p, slab, g0, np, s0, wave, row0, col0, lane, sink);
-}
 
 template <int ACT, int OUT, bool SK, bool LEAN = false>
 __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes, P8Tail tl,
@@ -642,22 +591,16 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     if (rd) W4_DSREAD(fa[7], ba, 7 * 1024);
   };
 
-  // stream-K hand-off of one wave's 128x64 partial (P8Tail): returns true when this wave arrived last and must
-  // sum the pieces and run the epilogue
-  auto tail_arrive = [&](int tt, int np, int slot) __attribute__((always_inline)) -> bool {
+  // stream-K piece of a cut tail tile: the wave's 128x64 fp32 partial to its workgroup's slot (slot 0 for the
+  // workgroup's first piece, 1 for its last); p8_fixup_kernel sums the pieces after the launch
+  auto tail_store = [&](int slot) __attribute__((always_inline)) {
     float* mine = tl.slab + (((size_t)loc * 2 + slot) * 8 + wave) * P8_WAVE_FLOATS + lane * 4;
 #pragma unroll
     for (int q = 0; q < 8; ++q)
 #pragma unroll
       for (int jj = 0; jj < 4; ++jj)
-        asm volatile("global_store_dwordx4 %0, %1, off sc1" :: "v"(mine + (4 * q + jj) * 256), "a"(acc[q][jj])
+        asm volatile("global_store_dwordx4 %0, %1, off" :: "v"(mine + (4 * q + jj) * 256), "a"(acc[q][jj])
                      : "memory");   // straight from the AGPRs (a VGPR copy invites hipcc to re-home acc)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    uint32_t old = 0;
-    if (lane == 0)
-      old = __hip_atomic_fetch_add(tl.cnt + tt * 8 + wave, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    old = __builtin_amdgcn_readfirstlane(old);
-    return (int)old == np - 1;
   };
 
 #ifdef PTK_P8_STAMPS
@@ -727,17 +670,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
           else w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane);
         }
       } else if constexpr (SK) {
-        const uint32_t c = __builtin_amdgcn_readlane(segC, s);
-        const int g0 = (int)(c & 1023u), np = (int)((c >> 10) & 1023u), s0 = (int)((c >> 20) & 1u);
-        if (tail_arrive(tt, np, (int)((c >> 21) & 1u))) {
-          // agent-scope acquire before reading the other pieces (the hand-off is per wave with the counter's
-          // returned value as the signal, not one of MI355X_MICROARCH.md's measured sc1-only rows; the
-          // invalidate also drops any line of the slab an earlier launch left in this XCD's caches)
-          __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-          p8_tail_epilogue<ACT, OUT>(kernarg_args(), tl.slab, g0, np, s0, wave, row0, col0, lane);
-          if (lane == 0) __hip_atomic_store(tl.cnt + tt * 8 + wave, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        }
+        tail_store((int)((__builtin_amdgcn_readlane(segC, s) >> 21) & 1u));
       }
       P8_STAMP(3, s);
       // the next segment's first k-step (published by the barrier; harmless after the last).  Its slot is the
@@ -768,6 +701,75 @@ extern "C" int ptk_debug_p8_epi_mode(int m) {
 }
 namespace ptk {
 #endif
+// stream-K fixup (P8Tail): workgroup (tail tile tt, row block I); wave w sums row block I of its 128x64 partial
+// over the tile's pieces in K order (4 x 16 B per lane per piece, up to 4 pieces' loads in flight) and runs the
+// general epilogue of those 16 rows (w4_rows: bit-identical to the lean one).  Tiles that ran whole are skipped.
+template <int ACT, int OUT, int I>
+PTK_DEV void p8_fixup_rows(const GemmArgs& p, const float* slab, int g0, int np, int s0, int wave, long row0,
+                           long col0, int lane) {
+  f32x4_t sum[4];
+  auto piece = [&](int jj) __attribute__((always_inline)) {
+    return slab + ((((size_t)(g0 + jj) * 2 + (jj == 0 ? s0 : 0)) * 8 + wave) * P8_WAVE_FLOATS + lane * 4 + 4 * I * 256);
+  };
+  int jj = 0;
+  for (; jj + 4 <= np; jj += 4) {
+    f32x4_t v[4][4];
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[u][j] = *reinterpret_cast<const f32x4_t*>(piece(jj + u) + j * 256);
+#pragma unroll
+    for (int u = 0; u < 4; ++u)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) sum[j] = jj + u == 0 ? v[u][j] : sum[j] + v[u][j];
+  }
+  for (; jj < np; ++jj) {
+    f32x4_t v[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) v[j] = *reinterpret_cast<const f32x4_t*>(piece(jj) + j * 256);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) sum[j] = jj == 0 ? v[j] : sum[j] + v[j];
+  }
+  w4_rows<ACT, OUT, I, 4, false>(p, sum, row0, col0, lane, g_w4_sink + lane * 64);
+}
+
+template <int ACT, int OUT>
+__global__ void __launch_bounds__(512) p8_fixup_kernel(GemmArgs p, P8Tail tl, int nu) {
+  const int tt = blockIdx.x, I = blockIdx.y;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int hf = wave >> 2, wq = wave & 3, wr = wq >> 1, wc = wq & 1;
+  const int U = tl.units, Gs = tl.gsplit;
+  const int g0 = p8_owner((long)tt * nu, Gs, U);
+  const int np = p8_owner((long)(tt + 1) * nu - 1, Gs, U) - g0 + 1;
+  if (np == 1) return;   // the tile ran whole in one workgroup (epilogue done there)
+  const int s0 = p8_start(g0, Gs, U) < tt * nu ? 1 : 0;
+  const int nbm = (p.M + W4 - 1) / W4, nbn = (p.N + W4 - 1) / W4;
+  int bm, bn;
+  w4_tile_coords(tl.dp_tiles + tt, nbm, nbn, bm, bn);
+  const long row0 = (long)bm * W4 + wr * 128, col0 = (long)bn * W4 + wc * 128 + hf * 64;
+  switch (I) {
+    case 0: p8_fixup_rows<ACT, OUT, 0>(p, tl.slab, g0, np, s0, wave, row0, col0, lane); break;
+    case 1: p8_fixup_rows<ACT, OUT, 1>(p, tl.slab, g0, np, s0, wave, row0, col0, lane); break;
+    case 2: p8_fixup_rows<ACT, OUT, 2>(p, tl.slab, g0, np, s0, wave, row0, col0, lane); break;
+    case 3: p8_fixup_rows<ACT, OUT, 3>(p, tl.slab, g0, np, s0, wave, row0, col0, lane); break;
+    case 4: p8_fixup_rows<ACT, OUT, 4>(p, tl.slab, g0, np, s0, wave, row0, col0, lane); break;
+    case 5: p8_fixup_rows<ACT, OUT, 5>(p, tl.slab, g0, np, s0, wave, row0, col0, lane); break;
+    case 6: p8_fixup_rows<ACT, OUT, 6>(p, tl.slab, g0, np, s0, wave, row0, col0, lane); break;
+    default: p8_fixup_rows<ACT, OUT, 7>(p, tl.slab, g0, np, s0, wave, row0, col0, lane); break;
+  }
+}
+
+int launch_p8_fixup(const GemmArgs& a, int act, int out, const P8Tail& tl, hipStream_t st) {
+  const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
+  const dim3 grid((unsigned)(ntile - tl.dp_tiles), 8);
+  const int nu = a.K / W4_KT / 2;
+  if (act != ACT_NONE) return set_error("p8 fixup: ACT_NONE only");
+  if (out == OUT_BF16) hipLaunchKernelGGL((p8_fixup_kernel<ACT_NONE, OUT_BF16>), grid, dim3(512), 0, st, a, tl, nu);
+  else if (out == OUT_F32) hipLaunchKernelGGL((p8_fixup_kernel<ACT_NONE, OUT_F32>), grid, dim3(512), 0, st, a, tl, nu);
+  else hipLaunchKernelGGL((p8_fixup_kernel<ACT_NONE, OUT_F32_BFR>), grid, dim3(512), 0, st, a, tl, nu);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("p8 fixup launch failed");
+}
+
 // the p8 path takes what the w4 path takes, at K >= 128 (a tile's first and last k-step pairs are peeled)
 bool p8_supported(const GemmArgs& a, int act, int out) { return a.K >= 128 && w4_supported(a, act, out); }
 
@@ -780,40 +782,40 @@ size_t p8_tail_scratch_bytes() {
 }
 
 // the stream-K plan of a launch.  Cost model of the tail round, in K-tiles of one workgroup (a 256x256x64 step,
-// ~1.7 us): unsplit, nt; split over Gs workgroups, ceil(U / Gs) plus, where a tile is cut, one partial write
-// and (pieces - 1) partial reads by its reducer, each ~HANDOFF K-tiles (a 256-KiB slab at the ~70 GB/s one
-// workgroup moves across XCDs: ~3.7 us).  The cheapest Gs is taken when it saves >= 10 % of the round.
-constexpr double P8_HANDOFF_KTILES = 2.4;
-static P8Tail p8_tail_plan(const GemmArgs& a, long ntile, long G, int act, int out) {
+// ~1.3 us): unsplit, nt; split over Gs workgroups, ceil(U / Gs) plus the partial writes of a workgroup's (at most
+// two) cut pieces (a 256-KiB slab each, ~1 K-tile) and the fixup launch (~5 K-tiles).  The cheapest Gs is taken
+// when it saves >= 10 % of the round.
+size_t p8_slab_bytes(long G) { return (size_t)G * 2 * 8 * P8_WAVE_FLOATS * sizeof(float); }
+P8Tail p8_tail_plan_ws(const GemmArgs& a, long ntile, long G, void* slab, long max_t0, long max_t1) {
   P8Tail tl;
-  void* ws = a.tail_ws ? a.tail_ws : tail_scope();   // (the scope is lent only under PTK_STREAMK=1)
-  if (!ws || act != ACT_NONE || (out != OUT_BF16 && out != OUT_F32 && out != OUT_F32_BFR)) return tl;
   const long R = ntile / G, T = ntile - R * G, nt = a.K / W4_KT;
-  if (T == 0 || T * 8 * 4 > (long)P8_CNT_BYTES || (nt & 1)) return tl;
-  // only few tail tiles -- a grid of at most 64 tiles, or one full round plus at most 24: where the tail split
-  // measured faster than the same launch unsplit (tools/sk_ab.py, profiles/r04_sk_ab.txt: Stage 2's weight grads
-  // and M = 14 336 projections at 0.43-0.80 of the time).  With more tail tiles the pieces of a tile stream
-  // different K ranges at the same time, the L2 sharing of a lock-step round is lost, and every Stage-1 shape
-  // measured slower (1.1-1.4x)
-  if (!((R == 0 && T <= 64) || (R == 1 && T <= 24))) return tl;
+  if (!slab || T == 0 || (nt & 1)) return tl;
+  if (!((R == 0 && T <= max_t0) || (R == 1 && T <= max_t1))) return tl;
   const long U = T * (nt / 2);                                // tail units: pairs of K-tiles
   double best = (double)nt * 0.9;
   long bestG = 0;
   for (long gs = T + 1; gs <= G; ++gs) {
     const long per = (U + gs - 1) / gs;                       // units of the busiest workgroup
-    const long lo = U / gs;                                   // units of the least busy (>= 1 needed)
-    if (lo < 1) break;
-    const long pieces = (nt / 2 + lo - 1) / lo + 1;           // most pieces one tile can be cut into
-    const double cost = 2.0 * (double)per + P8_HANDOFF_KTILES * (double)pieces;
+    if (U / gs < 1) break;                                    // (every workgroup >= 1 unit)
+    const double cost = 2.0 * (double)per + 2.0 + 5.0;
     if (cost < best - 1e-9) { best = cost; bestG = gs; }
   }
   if (!bestG || R + 3 > 64 || G > 1023 || ntile > 65535) return tl;   // the kernel's per-lane segment table
   tl.dp_tiles = (int)(R * G);
   tl.units = (int)U;
   tl.gsplit = (int)bestG;
-  tl.cnt = (uint32_t*)ws;
-  tl.slab = (float*)((char*)ws + P8_CNT_BYTES);
+  tl.slab = (float*)slab;
   return tl;
+}
+
+// the 8-wave kernel's plan: the scratch of the descriptor or the model-level scope (slabs after the counters).
+// A grid smaller than one round, or one full round plus at most 24 tiles: with more tail tiles after full rounds
+// the pieces of a tile stream different K ranges at the same time, the L2 sharing of a lock-step round is lost,
+// and every Stage-1 shape measured slower (r04: 1.1-1.4x; tools/sk_ab.py)
+static P8Tail p8_tail_plan(const GemmArgs& a, long ntile, long G, int act, int out) {
+  void* ws = a.tail_ws ? a.tail_ws : tail_scope();   // (the scope is lent only under PTK_STREAMK=1)
+  if (!ws || act != ACT_NONE || (out != OUT_BF16 && out != OUT_F32 && out != OUT_F32_BFR)) return P8Tail{};
+  return p8_tail_plan_ws(a, ntile, G, (char*)ws + P8_CNT_BYTES, G, 24);
 }
 
 // The model-level calls lend their tail scratch only under PTK_STREAMK=1: on the whole step the stream-K tail
@@ -874,9 +876,16 @@ int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk)
 #define PTK_P8SK_CASE(ACT_, OUT_)                                                                     \
   if (act == ACT_ && out == OUT_) {                                                                   \
     hipLaunchKernelGGL((gemm_p8_kernel<ACT_, OUT_, true>), dim3((unsigned)grid), dim3(512), 0, st, a, ab, bb, tl, 0u); \
-    return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");                  \
+    if (hipGetLastError() != hipSuccess) return set_error("gemm_p8 launch failed");                  \
+    return launch_p8_fixup(a, act, out, tl, st);                                                      \
   }
   if (tl.units) {
+    if (act == ACT_NONE && lean_epilogue_ok(a, act, out, cb)) {   // whole tiles take the lean epilogue
+      hipLaunchKernelGGL((gemm_p8_kernel<ACT_NONE, OUT_BF16, true, true>), dim3((unsigned)grid), dim3(512), 0, st, a,
+                         ab, bb, tl, cb);
+      if (hipGetLastError() != hipSuccess) return set_error("gemm_p8 launch failed");
+      return launch_p8_fixup(a, act, out, tl, st);
+    }
     PTK_P8SK_CASE(ACT_NONE, OUT_BF16)
     PTK_P8SK_CASE(ACT_NONE, OUT_F32)
     PTK_P8SK_CASE(ACT_NONE, OUT_F32_BFR)

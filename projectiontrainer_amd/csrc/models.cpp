@@ -234,6 +234,9 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
   // split-K partials (gemm_split): 2 slices of the largest [M, H] / [2I, H] output, 4 of the small dW ones
   w.sk_floats = std::max(std::max(2 * M * H, 2 * 2 * I * H), 4 * std::max(Dqkv, H) * H);
   if (train) w.sk_floats = std::max(w.sk_floats, V * H);   // the tied embedding's fp32 dW before its accumulate
+  // the stream-K slabs: the TN weight grads' and the long-K projections' (gemm_split)
+  w.sk_floats = std::max(w.sk_floats, (long)(p8_tail_scratch_bytes() / sizeof(float)) + 64);
+  if (train) w.sk_floats = std::max(w.sk_floats, (long)(tn_slab_bytes() / sizeof(float)));
   w.skpart = bp.take<float>(w.sk_floats);
   w.tail = bp.take<char>(p8_tail_scratch_bytes_models());
   return w;
@@ -250,6 +253,16 @@ int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStr
   // Stage 2's weight grads and M = 14 336 projections) before any host-side split
   if (a.M >= 1024 && a.N >= 256 && a.N <= 16384 && p8_supported(a, ACT_NONE, out) && p8_tail_split(a, ACT_NONE, out))
     return launch_gemm(a, ACT_NONE, out, 1, st);
+  // long-K GEMMs whose 256x256 tiles leave a thin last round (Stage 2's d(gate|up) dX and down projection at M =
+  // 14 336: 280 tiles = 256 + 24): the 8-wave kernel's stream-K tail over the split-K scratch, its pieces summed by
+  // p8_fixup_kernel (r05, tools/sk_ab.py same box: 419 / 216 us vs 662 / 298 unsplit; the 2-slice 128x128 split
+  // below ran them at ~390 + 26 us on average)
+  if (a.K >= 4096 && part && (size_t)part_floats * sizeof(float) >= p8_tail_scratch_bytes() && a.M >= 1024 &&
+      a.N >= 256 && a.N <= 16384) {
+    GemmArgs b = a;
+    b.tail_ws = part;
+    if (p8_supported(b, ACT_NONE, out) && p8_tail_split(b, ACT_NONE, out)) return launch_gemm(b, ACT_NONE, out, 1, st);
+  }
   const long nbig = (long)((a.M + 255) / 256) * ((a.N + 255) / 256);
   int S = 1, kmin = 1024;
   if (a.K >= 4096 && nbig <= 64) S = 4;
@@ -283,12 +296,43 @@ int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStr
                               bf ? a.resid16 : nullptr, a.ld_resid16, st);
 }
 
-// dW (+)= dY^T X over K token rows: both operands are token-major, so each is first transposed to a
-// K-contiguous feature-major copy (rows gathered through a map, zero-padded to a multiple of 64), then one
-// MFMA GEMM accumulates into the bf16 .grad (bf16(grad + bf16(acc)), autograd's accumulation).
+// dW (+)= dY^T X over K token rows into the bf16 .grad (bf16(grad + bf16(acc)), autograd's accumulation).  Both
+// operands are token-major.  Ungathered rows (identity maps, rows % 64 == 0): the persistent TN GEMM reads them
+// where they lie, K slices as fp32 partials summed in slice order (gemm_tn.hip).  Otherwise (the loss rows of the
+// last layer, ragged row counts, PTK_WGRAD_TN=0) each is transposed to a K-contiguous feature-major copy (rows
+// gathered through the map, zero-padded to a multiple of 64) for the NT GEMMs.
+static int wgrad_tn_mode() {
+  static const int m = [] { const char* e = getenv("PTK_WGRAD_TN"); return e ? atoi(e) : 1; }();
+  return m;
+}
 int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* x, long ldx, RowMap xmap, int Nx,
-                int rows, bf16_t* TA, bf16_t* TB, void* grad, float* skpart, long sk_floats, hipStream_t st) {
+                int rows, bf16_t* TA, bf16_t* TB, void* grad, float* skpart, long sk_floats, hipStream_t st,
+                int tn = -1) {
   if (!grad) return 0;
+  if (tn < 0) tn = wgrad_tn_mode();
+  if (tn && ymap.g == 0 && ymap.off == 0 && xmap.g == 0 && xmap.off == 0 && rows > 0) {
+    GemmArgs g = gemm(dy, lddy, x, ldx, grad, Nx, Ny, Nx, rows);   // A = dY [rows][Ny], B = X [rows][Nx]
+    g.bf16_linear = 1;
+    g.resid16 = (const bf16_t*)grad;
+    g.ld_resid16 = Nx;
+    // with a slab for the stream-K tail (the fp32 scratch): one slice, the tail round's K-tiles spread over the
+    // CUs; otherwise equal K slices summed by splitk_reduce
+    if (skpart && (size_t)sk_floats * sizeof(float) >= tn_slab_bytes() && tn_supported(g, OUT_BF16, 1))
+      return gemm_tn(g, OUT_BF16, 1, skpart, st);
+    const int S = skpart ? tn_slices(g, sk_floats) : (tn_supported(g, OUT_BF16, 1) ? 1 : 0);
+    if (S == 1) return gemm_tn(g, OUT_BF16, 1, nullptr, st);
+    if (S > 1) {
+      GemmArgs b = g;
+      b.C = skpart;
+      b.ldc = Nx;
+      b.bf16_linear = 0;
+      b.resid16 = nullptr;
+      b.ld_resid16 = 0;
+      CK(gemm_tn(b, OUT_F32, S, nullptr, st));
+      return launch_splitk_reduce(skpart, S, Ny, Nx, grad, Nx, 1, (const bf16_t*)grad, Nx, st);
+    }
+  }
+  if (tn == 2) return set_error("weight_grad: the TN path does not take Ny %d Nx %d rows %d", Ny, Nx, rows);
   const int Kp = (rows + 63) / 64 * 64;
   CK(launch_transpose_rows(dy, lddy, ymap, rows, Ny, TA, Kp, Kp, st));
   CK(launch_transpose_rows(x, ldx, xmap, rows, Nx, TB, Kp, Kp, st));
@@ -302,6 +346,18 @@ int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* 
 }  // namespace
 
 extern "C" {
+
+int ptk_weight_grad_bf16(const void* dy, int64_t lddy, int y_map_g, int64_t y_map_gs, int64_t y_map_off, int Ny,
+                         const void* x, int64_t ldx, int x_map_g, int64_t x_map_gs, int64_t x_map_off, int Nx, int rows,
+                         void* grad, void* ta, void* tb, float* part, int64_t part_floats, int mode, void* stream) {
+  if (mode < 0 || mode > 2) return set_error("weight_grad: mode %d (0 auto, 1 transposes, 2 TN)", mode);
+  if (Ny <= 0 || Nx <= 0 || rows <= 0) return 0;
+  const RowMap ym{y_map_g, 0, y_map_gs, y_map_off}, xm{x_map_g, 0, x_map_gs, x_map_off};
+  const bool tn_ok = mode != 1 && ym.g == 0 && ym.off == 0 && xm.g == 0 && xm.off == 0;
+  if (!tn_ok && (!ta || !tb)) return set_error("weight_grad: the transpose path needs ta / tb scratch");
+  return weight_grad((const bf16_t*)dy, lddy, ym, Ny, (const bf16_t*)x, ldx, xm, Nx, rows, (bf16_t*)ta, (bf16_t*)tb,
+                     grad, part, part_floats, (hipStream_t)stream, mode == 0 ? -1 : (mode == 1 ? 0 : 2));
+}
 
 size_t ptk_siglip_workspace_bytes(const ptk_siglip_config* c, int batch) {
   Bump bp(nullptr);

@@ -71,7 +71,19 @@ int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk)
 bool dual_supported(const GemmArgs& a, int act, int out);
 // the persistent kernels would take their lean bf16 epilogue for this plain bf16 GEMM (gemm_w4.hip lean_epilogue_ok)
 bool lean_epilogue_candidate(const GemmArgs& a);
+bool lean_epilogue_ok(const GemmArgs& a, int act, int out, uint32_t& c_bytes);   // + c_bytes: C's extent (store rsrc)
 int launch_gemm_dual(const GemmArgs& a, int act, int out, hipStream_t st, bool solo);   // solo: 256x128 tiles, 2 WGs/CU
+// persistent TN GEMM (gemm_tn.hip): C[M,N] = A[K,M]^T B[K,N] on the token-major operands of a weight grad, lda / ldb
+// their row strides.  OUT_BF16: slices == 1 and the weight-grad accumulate (bf16_linear + resid16 == C), with the
+// stream-K tail of the 8-wave kernel when `slab` (tn_slab_bytes() bytes) is given and the plan splits; OUT_F32:
+// fp32 partials of `slices` equal K slices at C + z M ldc.  tn_slices: the slice count the cost model picks for
+// the weight-grad form without a slab (partials within part_floats), 0 when the TN path does not take the shape.
+// gemm_tn (gemm.hip) launches with the census (GEMM_PATH_TN) and live timers
+bool tn_supported(const GemmArgs& a, int out, int slices);
+int tn_slices(const GemmArgs& a, long part_floats);
+size_t tn_slab_bytes();
+int launch_gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st);
+int gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st);
 // stream-K tail of the persistent 8-wave kernel: scratch bytes (arrival counters, then partial slabs), the
 // workgroups its plan spreads a GEMM's tail over (0: no split), and the thread-local scratch a model-level
 // call lends to every GEMM it launches (the counters are zeroed when the scope opens)

@@ -146,6 +146,30 @@ def transpose_rows(x, rows, rows_pad, map_g=0, map_gs=0, map_off=0, ld_out=None)
     return out
 
 
+def weight_grad(dy, x, grad, rows=None, ymap=(0, 0, 0), xmap=(0, 0, 0), part=None, mode=0):
+    """Stage-2 weight grad of one nn.Linear into its bf16 .grad (ptk_weight_grad_bf16): grad [Ny, Nx] =
+    bf16(grad + bf16(dY^T X)) over `rows` token rows of dy [.., Ny] / x [.., Nx] (row maps (g, gs, off) as
+    transpose_rows').  part: fp32 scratch for K-slice partials (None: one slice); mode 0 auto, 1 the transpose path,
+    2 the TN path only.  Returns grad."""
+    for t in (dy, x, grad):
+        if t.dtype != torch.bfloat16 or t.dim() != 2 or t.stride(1) != 1:
+            raise L.PtkError("weight_grad: dy, x, grad must be 2-D bf16 tensors with unit column stride")
+    Ny, Nx = dy.shape[1], x.shape[1]
+    if tuple(grad.shape) != (Ny, Nx) or grad.stride(0) != Nx:
+        raise L.PtkError("weight_grad: grad must be a contiguous [Ny, Nx] tensor")
+    rows = dy.shape[0] if rows is None else rows
+    kp = (rows + 63) // 64 * 64
+    ta = tb = None
+    if mode == 1 or ymap[0] or ymap[2] or xmap[0] or xmap[2] or rows % 64:
+        ta = torch.empty((Ny, kp), dtype=torch.bfloat16, device=dy.device)
+        tb = torch.empty((Nx, kp), dtype=torch.bfloat16, device=dy.device)
+    pf = 0 if part is None else part.numel()
+    check(L.lib().ptk_weight_grad_bf16(ptr(dy), dy.stride(0), ymap[0], ymap[1], ymap[2], Ny, ptr(x), x.stride(0),
+                                       xmap[0], xmap[1], xmap[2], Nx, rows, ptr(grad), ptr(ta), ptr(tb), ptr(part),
+                                       pf, mode, L.stream_ptr(dy.device)), "weight_grad")
+    return grad
+
+
 def transpose(x, rows_pad=None, out=None):
     """[Z, rows, cols] or [rows, cols] bf16 -> [.., cols, rows_pad] (zero-padded); out: preallocated result."""
     squeeze = x.dim() == 2

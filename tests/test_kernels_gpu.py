@@ -649,3 +649,65 @@ def test_gemm_stream_k_tail_vs_fp32(gpu, M, N, K, kind):
     # against the unsplit kernel: equal up to the fp32 summation order of the K pieces (and one bf16 rounding)
     d0 = (C1.float() - C0.float()).abs().max().item()
     assert d0 <= 2e-2 * max(1.0, C0.float().abs().max().item()), d0
+
+
+# Stage-2 weight grads on the token-major TN path (gemm_tn.hip): the cfg4 dW shapes (K = 14 336 token rows) with the
+# stream-K tail over a slab (dW_qkv 30 tiles, dW_o 20, dW_down 135: all tail; dW_gate|up 270 = one round + 14),
+# with equal K slices (no slab: partials summed by splitk_reduce) and unsplit, a partial last M tile (Ny 1000),
+# padded row strides, the minimum K (128)
+WG_CASES = [(1536, 1152, 14336, 0, "slab"), (1152, 1024, 14336, 0, "slab"), (1152, 6912, 14336, 0, "slab"),
+            (13824, 1152, 14336, 0, "slab"), (1536, 1152, 14336, 0, "slices"), (1152, 6912, 4096, 0, "slices"),
+            (13824, 1152, 2048, 0, "none"), (1000, 320, 640, 8, "slab"), (1000, 320, 640, 8, "slices"),
+            (256, 128, 128, 0, "none"), (2304, 1152, 1024, 24, "slices")]
+
+
+@pytest.mark.parametrize("Ny,Nx,rows,ld_extra,split", WG_CASES)
+def test_weight_grad_tn_vs_fp32(gpu, Ny, Nx, rows, ld_extra, split):
+    """grad = bf16(grad + bf16(dY^T X)) on the TN path against torch fp32 of the same products (one bf16 rounding
+    of the product, one of the sum: rtol 1e-2 at the product's scale), against the transposed-operand path (same
+    products, another fp32 summation order), bit for bit against itself (stream-K pieces and K slices summed in K
+    order); the census shows the TN kernel ran and nothing else."""
+    Kn, L = _k()
+    dy = rnd(rows, Ny + ld_extra, dev=gpu, seed=101)[:, :Ny]
+    x = rnd(rows, Nx + ld_extra, dev=gpu, seed=102, scale=0.05)[:, :Nx]
+    g0 = rnd(Ny, Nx, dev=gpu, seed=103)
+    slab = torch.cuda.get_device_properties(gpu).multi_processor_count * 2 * 8 * 128 * 64
+    part = {"slab": torch.empty(max(slab, 8 * Ny * Nx), dtype=torch.float32, device=gpu),
+            "slices": torch.empty(min(8 * Ny * Nx, slab - 4), dtype=torch.float32, device=gpu),
+            "none": None}[split]
+    L.gemm_path_counts(reset=True)
+    g1 = Kn.weight_grad(dy, x, g0.clone(), part=part, mode=2)
+    paths = L.gemm_path_counts(reset=True)
+    g2 = Kn.weight_grad(dy, x, g0.clone(), part=part, mode=2)
+    gt = Kn.weight_grad(dy, x, g0.clone(), part=part, mode=1)
+    torch.cuda.synchronize()
+    assert set(paths) == {("tn", L.ACT_NONE)}, paths
+    assert torch.equal(g1, g2)
+    prod = dy.float().t() @ x.float()
+    ref = (g0.float() + prod.to(torch.bfloat16).float()).to(torch.bfloat16).float()
+    scale = max(prod.abs().max().item(), g0.float().abs().max().item())
+    torch.testing.assert_close(g1.float(), ref, rtol=1e-2, atol=1e-2 * scale)
+    # against the transposed-operand path: the same products, another fp32 summation order
+    d = (g1.float() - gt.float()).abs().max().item()
+    assert d <= 1e-2 * scale, d
+    # the bulk of the elements equal to the fp32 reference after its two roundings
+    assert (g1.float() == ref).float().mean().item() > 0.9
+
+
+def test_weight_grad_tn_gated_shapes(gpu):
+    """Shapes the TN path does not take run the transpose path in auto mode and fail loudly in TN-only mode:
+    ragged rows (not a multiple of 64), gathered rows, N % 64 != 0."""
+    Kn, L = _k()
+    dy, x = rnd(200, 256, dev=gpu, seed=104), rnd(200, 128, dev=gpu, seed=105)
+    g0 = torch.zeros(256, 128, dtype=torch.bfloat16, device=gpu)
+    L.gemm_path_counts(reset=True)
+    g = Kn.weight_grad(dy, x, g0.clone(), mode=0)
+    paths = L.gemm_path_counts(reset=True)
+    assert ("tn", L.ACT_NONE) not in paths, paths
+    torch.testing.assert_close(g.float(), (dy.float().t() @ x.float()).to(torch.bfloat16).float(), rtol=1e-2,
+                               atol=1e-2)
+    with pytest.raises(L.PtkError):
+        Kn.weight_grad(dy, x, g0.clone(), mode=2)
+    dy2, x2 = rnd(256, 256, dev=gpu, seed=106), rnd(256, 96, dev=gpu, seed=107)
+    with pytest.raises(L.PtkError):
+        Kn.weight_grad(dy2, x2, torch.zeros(256, 96, dtype=torch.bfloat16, device=gpu), mode=2)
