@@ -431,6 +431,18 @@ constexpr int P8_PIECES = 4;   // LDS-DMA pieces per wave per k-step
 // the fixup spreads the same loads over 8 waves x 8 row blocks per tile.  No wave waits for another workgroup.
 
 
+// PTK_P8_CREAD (A/B builds only): the fragment reads as compiler-visible LDS loads (hipcc places them and counts
+// their waits) instead of the asm reads with the counted lgkmcnt ladder -- gemm_tn.hip's form
+#ifdef PTK_P8_CREAD
+#define P8_DSREAD(DST, ADDR, OFF) \
+  (DST) = *reinterpret_cast<const __attribute__((address_space(3))) bf16x8_t*>((uintptr_t)((ADDR) + (OFF)))
+#define P8_LGKM(N) do { } while (0)
+#define P8_BARRIER() do { __builtin_amdgcn_s_barrier(); asm volatile("" ::: "memory"); } while (0)
+#else
+#define P8_BARRIER() __builtin_amdgcn_s_barrier()
+#define P8_DSREAD(DST, ADDR, OFF) W4_DSREAD(DST, ADDR, OFF)
+#define P8_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
+#endif
 template <int ACT, int OUT, bool SK, bool LEAN = false>
 __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes, P8Tail tl,
                                                          uint32_t c_bytes) {
@@ -543,10 +555,10 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
   auto read_frags = [&](uint32_t rs) __attribute__((always_inline)) {
     const uint32_t ba = frag_a + rs, bb = frag_b + rs;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) W4_DSREAD(fa[r], ba, r * 1024);
+    for (int r = 0; r < 8; ++r) P8_DSREAD(fa[r], ba, r * 1024);
 #pragma unroll
-    for (int r = 0; r < 4; ++r) W4_DSREAD(fb0[r], bb, r * 1024);
-    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    for (int r = 0; r < 4; ++r) P8_DSREAD(fb0[r], bb, r * 1024);
+    P8_LGKM(0);
     asm volatile("" : "+v"(fa[0]), "+v"(fa[1]), "+v"(fa[2]), "+v"(fa[3]), "+v"(fa[4]), "+v"(fa[5]),
                  "+v"(fa[6]), "+v"(fa[7]));
     asm volatile("" : "+v"(fb0[0]), "+v"(fb0[1]), "+v"(fb0[2]), "+v"(fb0[3]));
@@ -567,13 +579,13 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     const uint32_t sa = dsa + dks * (W4_KS * 2), sb = dsb + dks * (W4_KS * 2);
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
-      if (q == 0) asm volatile("s_waitcnt lgkmcnt(6)" ::: "memory");
-      else if (q < 3) asm volatile("s_waitcnt lgkmcnt(8)" ::: "memory");
-      else if (q == 3) asm volatile("s_waitcnt lgkmcnt(9)" ::: "memory");
-      else asm volatile("s_waitcnt lgkmcnt(10)" ::: "memory");
+      if (q == 0) P8_LGKM(6);
+      else if (q < 3) P8_LGKM(8);
+      else if (q == 3) P8_LGKM(9);
+      else P8_LGKM(10);
       asm volatile("" : "+v"(fa[q]));
       if (q == 0) asm volatile("" : "+v"(FB[0]), "+v"(FB[1]), "+v"(FB[2]), "+v"(FB[3]));
-      if (rd && q < 4) W4_DSREAD(NB[q], bb, q * 1024);
+      if (rd && q < 4) P8_DSREAD(NB[q], bb, q * 1024);
       if ((q & 1) == half) {
         const int pc = q >> 1;   // pieces A0 B0 A1 B1
         if (pc & 1) W4_DMA(rsb, offb[pc >> 1], sb, db + (pc >> 1) * 1024);
@@ -586,9 +598,9 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
         else W4_MFMA(acc[q][jj], FB[jj], fa[q]);
       }
       if (PTK_P8_MPRIO) asm volatile("s_setprio 0" ::: "memory");
-      if (rd && q >= 1) W4_DSREAD(fa[q - 1], ba, (q - 1) * 1024);   // one group after its last reader
+      if (rd && q >= 1) P8_DSREAD(fa[q - 1], ba, (q - 1) * 1024);   // one group after its last reader
     }
-    if (rd) W4_DSREAD(fa[7], ba, 7 * 1024);
+    if (rd) P8_DSREAD(fa[7], ba, 7 * 1024);
   };
 
   // stream-K piece of a cut tail tile: the wave's 128x64 fp32 partial to its workgroup's slot (slot 0 for the
@@ -623,9 +635,9 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       dma_advance();
     }
     asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
+    P8_BARRIER();
     read_frags(0);
-    __builtin_amdgcn_s_barrier();
+    P8_BARRIER();
     // ring invariant as gemm_w4_kernel's (k-step i's fragments in registers, i+1 / i+2 published, i+3 in
     // flight, i+4 issued into the slot of i-1); vmcnt(4) before each pair's barrier leaves only the youngest
     // k-step's 4 pieces in flight
@@ -644,7 +656,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       if (!lst) rs = slot_next(rs);   // last pair: rs stays on the next segment's first k-step
       ws = slot_next(ws);
       asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
-      __builtin_amdgcn_s_barrier();
+      P8_BARRIER();
     };
     for (int s = 0; s < nseg; ++s) {
       int t, k0, k1, tt;
@@ -677,7 +689,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       // one the NEXT pair's second k-step restages (k-step i+6 lands in the slot of i+1), so a barrier keeps
       // a wave that finished its epilogue early from overwriting it before every wave has read it
       read_frags(rs);
-      __builtin_amdgcn_s_barrier();
+      P8_BARRIER();
       rs = slot_next(rs);
     }
   };
