@@ -323,7 +323,7 @@ __global__ void __launch_bounds__(512, 1) gemm_tn_kernel(GemmArgs p, uint32_t a_
 }
 
 // the TN path takes: 16-B aligned operands with 16-B k-rows, K split into `slices` equal slices of >= 128 rows (a
-// multiple of 64), N % 64 == 0, byte extents below 2^31; OUT_BF16 only with the lean epilogue's form (the weight-grad
+// multiple of 64), N % 64 == 0, operand extents below 4 GiB and C's below 2^31; OUT_BF16 only with the lean epilogue's form (the weight-grad
 // accumulate: bf16_linear + resid16), OUT_F32 the partials of a K split ([slices][M][ldc])
 bool tn_supported(const GemmArgs& a, int out, int slices) {
   if (slices < 1 || a.K % (W4_KT * slices) || a.K / slices < 2 * W4_KT) return false;
@@ -331,8 +331,10 @@ bool tn_supported(const GemmArgs& a, int out, int slices) {
   if (((uintptr_t)a.A | (uintptr_t)a.B | (uintptr_t)a.C) & 15) return false;
   if (a.amap.g || a.amap.off || a.bias || a.rowadd || a.resid || a.aux || a.aux_in || a.row_stats || a.alpha != 1.f)
     return false;
+  // operand extents below 4 GiB less 1 MiB: 32-bit buffer offsets and num_records (the tied lm_head's dW reads the
+  // 2 GiB d(logits) [4 096][262 144]); the last tile's read past its k-row never wraps
   const double ab = (double)a.K * a.lda * 2, bb = (double)a.K * a.ldb * 2;
-  if (ab >= 2147483000.0 || bb >= 2147483000.0) return false;
+  if (ab >= 4293918720.0 || bb >= 4293918720.0) return false;
   if (out == OUT_BF16) {
     uint32_t cb = 0;
     return slices == 1 && lean_epilogue_candidate(a) && lean_epilogue_ok(a, ACT_NONE, OUT_BF16, cb);

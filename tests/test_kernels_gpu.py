@@ -658,7 +658,8 @@ def test_gemm_stream_k_tail_vs_fp32(gpu, M, N, K, kind):
 WG_CASES = [(1536, 1152, 14336, 0, "slab"), (1152, 1024, 14336, 0, "slab"), (1152, 6912, 14336, 0, "slab"),
             (13824, 1152, 14336, 0, "slab"), (1536, 1152, 14336, 0, "slices"), (1152, 6912, 4096, 0, "slices"),
             (13824, 1152, 2048, 0, "none"), (1000, 320, 640, 8, "slab"), (1000, 320, 640, 8, "slices"),
-            (256, 128, 128, 0, "none"), (2304, 1152, 1024, 24, "slices")]
+            (256, 128, 128, 0, "none"), (2304, 1152, 1024, 24, "slices"),
+            (262144, 1152, 4096, 0, "slab")]   # the tied lm_head's dW: a 2 GiB d(logits) operand (32-bit offsets)
 
 
 @pytest.mark.parametrize("Ny,Nx,rows,ld_extra,split", WG_CASES)
