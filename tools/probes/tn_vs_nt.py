@@ -18,7 +18,10 @@ def t_ms(fn, reps):
     return e0.elapsed_time(e1) / reps
 
 
-for M, N, Kd in [(8192, 8192, 8192), (4096, 4096, 16384), (12800, 1280, 13824), (6400, 6400, 1152)]:
+SIZES = [(8192, 8192, 8192), (4096, 4096, 16384), (12800, 1280, 13824), (6400, 6400, 1152)]
+if len(sys.argv) > 1:   # e.g. 8192,8192,8192 (profiling passes: one size)
+    SIZES = [tuple(int(v) for v in a.split(",")) for a in sys.argv[1:]]
+for M, N, Kd in SIZES:
     # NT: C[M,N] = A[M,K] B[N,K]^T on the 8-wave kernel;  TN: grad[M,N] += dY[K,M]^T X[K,N] (one slice, no slab)
     A = torch.randn(M, Kd, device=dev).bfloat16()
     B = (torch.randn(N, Kd, device=dev) * 0.05).bfloat16()
