@@ -820,7 +820,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // scratch lent by the model-level call (or in the descriptor), runs on the persistent 8-wave kernel with that
   // round's K-tiles spread over the CUs (r04: the N = 1024 / 1152 / 1536 projections, the long-K d(gate|up) dX
   // and down projection, the projector's fc2 and weight grads)
-  const int sk = (g_force_tiles == 0 || g_force_tiles == 32 || g_force_tiles == 256) && batch == 1 && act == ACT_NONE && a.M >= 1024 &&
+  const int sk = (g_force_tiles == 0 || g_force_tiles == 32) && batch == 1 && act == ACT_NONE && a.M >= 1024 &&
                  a.N >= 256 && a.N <= 16384 && p8_supported(a, act, out) ? p8_tail_split(a, act, out) : 0;
   // two-group persistent kernel (gemm_dual.hip): PTK_DUAL=1 puts every persistent (w4 / p8) shape on it (A/B)
   static const bool dual_env = [] { const char* e = getenv("PTK_DUAL"); return e && e[0] == '1'; }();
@@ -834,14 +834,12 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
   }
-  // PTK_P8W=1: the 8-wave kernel over 64-deep whole-line LDS images (gemm_p8w.hip; A/B, bit-identical)
-  static const bool p8w_env = [] { const char* e = getenv("PTK_P8W"); return e && e[0] == '1'; }();
-  if (batch == 1 && (g_force_tiles == 32 || g_force_tiles == 256 || p8_auto || sk) && p8_supported(a, act, out)) {
+  if (batch == 1 && (g_force_tiles == 32 || p8_auto || sk) && p8_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);
     count_path(sk ? GEMM_PATH_P8SK : GEMM_PATH_P8, act);
-    const int rc = launch_gemm_p8(a, act, out, st, sk != 0, p8w_env || g_force_tiles == 256);
+    const int rc = launch_gemm_p8(a, act, out, st, sk != 0);
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
   }

@@ -36,8 +36,6 @@ P8Tail p8_tail_plan_ws(const GemmArgs& a, long ntile, long G, void* ws, long max
 size_t p8_slab_bytes(long G);
 // the cut tail tiles' pieces summed in K order + the tile epilogue (ACT_NONE; the general epilogue's forms)
 int launch_p8_fixup(const GemmArgs& a, int act, int out, const P8Tail& tl, hipStream_t st);
-// the 8-wave kernel over 64-deep whole-line LDS images (gemm_p8w.hip), the same tail plan
-int launch_gemm_p8w(const GemmArgs& a, int act, int out, hipStream_t st, const P8Tail& tl);
 
 namespace {
 constexpr int W4 = 256;                  // output tile edge

@@ -856,12 +856,11 @@ int p8_tail_split(const GemmArgs& a, int act, int out) {
   return p8_tail_plan(a, ntile, g_num_cu, act, out).gsplit;
 }
 
-int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk, bool wide) {
+int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk) {
   num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   // the stream-K plan only where launch_gemm's gates chose the tail split (its census counts it as p8sk)
   const P8Tail tl = sk ? p8_tail_plan(a, ntile, g_num_cu, act, out) : P8Tail{};
-  if (wide) return launch_gemm_p8w(a, act, out, st, tl);   // the whole-line variant (gemm_p8w.hip)
   long grid = tl.units ? g_num_cu : std::min<long>(ntile, g_num_cu);
 #ifdef PTK_P8_STAMPS
   if (const char* e = getenv("PTK_GEMM_GRID")) grid = std::min<long>(grid, atol(e));   // diagnostic: fewer CUs

@@ -66,7 +66,7 @@ double w4_round_fill(long M, long N);
 int device_cus();   // compute units of the current device (cached)
 // persistent 8-wave variant (gemm_w4.hip): the w4 tiles and ring with two waves per SIMD
 bool p8_supported(const GemmArgs& a, int act, int out);
-int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk, bool wide = false);
+int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk);
 // persistent two-group kernel (gemm_dual.hip): 256x128 tiles, one group's epilogue beside the other's K loop
 bool dual_supported(const GemmArgs& a, int act, int out);
 // the persistent kernels would take their lean bf16 epilogue for this plain bf16 GEMM (gemm_w4.hip lean_epilogue_ok)

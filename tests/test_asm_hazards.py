@@ -121,7 +121,7 @@ def hazards(body):
 
 
 # every HIP source of libptk.so (capi / models / comm are host code)
-PRODUCT_SOURCES = ["flash.hip", "gemm_w4.hip", "gemm_p8w.hip", "gemm_dual.hip", "gemm_tn.hip", "gemm.hip", "norm.hip", "attn.hip", "misc.hip", "image.hip",
+PRODUCT_SOURCES = ["flash.hip", "gemm_w4.hip", "gemm_dual.hip", "gemm_tn.hip", "gemm.hip", "norm.hip", "attn.hip", "misc.hip", "image.hip",
                    "train.hip"]
 _ASM_CACHE = {}
 
@@ -148,7 +148,7 @@ def asm_dir(tmp_path_factory):
     return tmp_path_factory.mktemp("asm")
 
 
-@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip", "gemm_p8w.hip", "gemm_dual.hip", "gemm_tn.hip"])
+@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip", "gemm_dual.hip", "gemm_tn.hip"])
 def test_inline_asm_mfma_hazards(src, asm_dir):
     asm = product_asm(src, asm_dir)
     bad = []
@@ -178,9 +178,6 @@ SPILL_BUDGET = {   # kernel symbol substring -> (sgpr_spill_count, vgpr_spill_co
     # the stream-K tail variants' bookkeeping (r05: 24 -> 0-1 with the in-kernel reducer moved to p8_fixup_kernel)
     "gemm_p8_kernelILi0ELi0ELb1E": (1, 0, 0),
     "gemm_tn_kernelILi0ELb1E": (3, 0, 0),
-    "gemm_p8w_kernelILi0ELi0ELb1ELb1E": (2, 0, 0),
-    "gemm_p8w_kernelILi2ELi0ELb0E": (6, 0, 0),
-    "gemm_p8w_kernelILi4ELi0ELb0E": (2, 0, 0),
     "gemm_p8_kernelILi1ELi0ELb0E": (4, 0, 0),
     "gemm_p8_kernelILi2ELi0ELb0E": (28, 0, 0),
     "gemm_p8_kernelILi4ELi0ELb0E": (20, 0, 0),
@@ -248,7 +245,7 @@ def test_kernel_spills_within_budget(src, asm_dir):
     assert not bad, "\n".join(bad[:20])
 
 
-@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip", "gemm_p8w.hip", "gemm_dual.hip", "gemm_tn.hip"])
+@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip", "gemm_dual.hip", "gemm_tn.hip"])
 def test_asm_never_writes_m0(src, asm_dir):
     """LDS-DMA asm takes its LDS address through the {m0} constraint (hipcc writes M0 and knows the asm reads
     it); an M0 write hidden inside an asm statement would break any M0 value hipcc keeps live."""

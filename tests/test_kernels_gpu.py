@@ -504,9 +504,7 @@ def test_gemm_p8_matches_w4(gpu, M, N, K):
     bias = rnd(N, dev=gpu, dtype=torch.float32, seed=15)
     res = rnd(M, N, dev=gpu, dtype=torch.float32, seed=16)
     outs = []
-    # 128: the two-group tiles as one-group workgroups, two per CU; 256: the 8-wave kernel over 64-deep whole-line
-    # LDS images (gemm_p8w.hip, census "p8")
-    modes = {8: "w4", 32: "p8", 64: "dual", 128: "dual", 256: "p8"}
+    modes = {8: "w4", 32: "p8", 64: "dual", 128: "dual"}   # 128: the two-group tiles as one-group workgroups, two per CU
     for md in modes:
         L.lib().ptk_gemm_force_small_tiles(md)
         L.gemm_path_counts(reset=True)
