@@ -1291,7 +1291,18 @@ PTK_DEV int swz_dual(int r) { return ((r & 3) << 2) | ((r >> 2) & 3); }
 #ifndef DQ_RA
 #define DQ_RA 2   // dQ kernel: LDS fragment reads issued this many MFMAs ahead of their use
 #endif
-__global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a) {
+typedef const FlashBwdArgs __attribute__((address_space(4)))* fb_kargs_ptr_t;
+PTK_DEV const FlashBwdArgs& fb_kernarg() {   // fa_kernarg's laundered pointer for the backward arguments
+#if defined(__HIP_DEVICE_COMPILE__)
+  fb_kargs_ptr_t pk = (fb_kargs_ptr_t)__builtin_amdgcn_kernarg_segment_ptr();
+  asm volatile("" : "+s"(pk));
+  return *(const FlashBwdArgs*)pk;
+#else
+  __builtin_unreachable();
+#endif
+}
+
+__global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a, int nz, int nitems) {
   constexpr int D = 256, KT = 32, NB = 4;
   constexpr int TILE = KT * D * 2;
   typedef __attribute__((ext_vector_type(16))) float f32x16_t;
@@ -1304,66 +1315,74 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int h = lane >> 5, c32 = lane & 31;
-  const int nqb = (a.rows + 127) / 128, nz = gridDim.x / nqb;
-  const long z = blockIdx.x % nz;
-  const int r0 = (nqb - 1 - (int)(blockIdx.x / nz)) * 128;   // heaviest (latest) row blocks first
-  const bf16_t* K = a.K + z * (long)a.nkeys * D;
-  const bf16_t* V = a.V + z * (long)a.nkeys * D;
-  const long b = z / a.zdiv;
-  const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
-  const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
-  int k_hi = a.nkeys, k_lo = 0;
-  if (a.causal) {
-    k_hi = min(k_hi, pos_hi + 1);
-    if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
-  }
-  const int t_lo = k_lo / KT, t_hi = (k_hi + KT - 1) / KT;
-
-  // ---- Q, dO fragments (B operands, k-step ks: lane holds row c32, d 16 ks + 8 h .. +7), LSE, delta
-  const int wrow0 = r0 + wave * 32;
-  const int qrow = wrow0 + c32;
-  const int qrow_c = min(qrow, a.rows - 1);
-  const int qpos = qrow_c / a.qdiv;
-  bf16x8_t qf[16], df[16];
-  const long qoff = (z * a.rows + qrow_c) * (long)D + 8 * h;
-#pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    qf[ks] = *reinterpret_cast<const bf16x8_t*>(a.Q + qoff + 16 * ks);
-    df[ks] = *reinterpret_cast<const bf16x8_t*>(a.dO + qoff + 16 * ks);
-  }
+  const int nqb = (a.rows + 127) / 128;
   const float L2E = 1.4426950408889634f;
-  const float lse2 = a.lse[z * a.rows + qrow_c] * L2E;
-  float dlt;
-  {
+  const float sl2 = a.scale * L2E;
+  const int causal = a.causal != 0, nowin = a.window <= 0;
+
+  // ---- work items (row block of 128 query rows, z), heaviest (latest) row blocks first, in
+  // attn_fwd256w_kernel's snake order over rounds of the persistent grid.  Per-item state (begin_item, load_qdo):
+  long z = 0;
+  int t_lo = 0, t_hi = 0, wrow0 = 0, qrow = 0, qpos = 0, wpos_lo = 0, wpos_hi = 0;
+  float lse2 = 0.f, dlt = 0.f;
+  fa_u32x4_t rsk, rsv;
+  bf16x8_t qf[16], df[16], of[16];   // Q, dO fragments (B operands, k-step ks: row c32, d 16 ks + 8 h .. +7); O
+  auto begin_item = [&](int item) __attribute__((always_inline)) {
+    const FlashBwdArgs& a = fb_kernarg();
+    z = item % nz;
+    const int r0 = (nqb - 1 - item / nz) * 128;
+    const long b = z / a.zdiv;
+    const int* kvl = a.key_valid ? a.key_valid + b * a.nkeys : nullptr;
+    const int pos_lo = r0 / a.qdiv, pos_hi = min(r0 + 127, a.rows - 1) / a.qdiv;
+    int k_hi = a.nkeys, k_lo = 0;
+    if (a.causal) {
+      k_hi = min(k_hi, pos_hi + 1);
+      if (a.window > 0) k_lo = max(0, pos_lo - a.window + 1);
+    }
+    t_lo = k_lo / KT;
+    t_hi = (k_hi + KT - 1) / KT;
+    wrow0 = r0 + wave * 32;
+    qrow = wrow0 + c32;
+    wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
+    wpos_hi = min(wrow0 + 31, a.rows - 1) / a.qdiv;
+    fa_key_masks<4>(kvl, a.nkeys, t_lo, t_hi, wave, lane, kmask_s);
+    rsk = fa_rsrc(a.K + z * (long)a.nkeys * D, (uint32_t)((long)a.nkeys * D * 2));
+    rsv = fa_rsrc(a.V + z * (long)a.nkeys * D, (uint32_t)((long)a.nkeys * D * 2));
+  };
+  // the item's Q, dO, O fragments and LSE (loads left in flight); delta = rowsum(dO O) once they landed
+  auto load_qdo = [&]() __attribute__((always_inline)) {
+    const FlashBwdArgs& a = fb_kernarg();
+    const int qrow_c = min(qrow, a.rows - 1);
+    qpos = qrow_c / a.qdiv;
+    const long qoff = (z * a.rows + qrow_c) * (long)D + 8 * h;
+#pragma unroll
+    for (int ks = 0; ks < 16; ++ks) {
+      qf[ks] = *reinterpret_cast<const bf16x8_t*>(a.Q + qoff + 16 * ks);
+      df[ks] = *reinterpret_cast<const bf16x8_t*>(a.dO + qoff + 16 * ks);
+    }
+    lse2 = a.lse[z * a.rows + qrow_c] * L2E;
     const long z0 = z / a.zin, z1 = z - z0 * a.zin;
     const bf16_t* orow = a.O + z0 * a.sO0 + z1 * a.sO1 + map_row(a.omap, qrow_c) * a.ldo + 8 * h;
-    bf16x8_t of[16];
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks) of[ks] = *reinterpret_cast<const bf16x8_t*>(orow + 16 * ks);
-    fa_key_masks<4>(kvl, a.nkeys, t_lo, t_hi, wave, lane, kmask_s);   // (its loads join those in flight)
+  };
+  auto finish_qdo = [&]() __attribute__((always_inline)) {
     float acc0 = 0.f;
 #pragma unroll
     for (int ks = 0; ks < 16; ++ks)
 #pragma unroll
       for (int e = 0; e < 8; ++e) acc0 += bf2f((bf16_t)of[ks][e]) * bf2f((bf16_t)df[ks][e]);
     dlt = xor32_sum(acc0);
+    const FlashBwdArgs& a = fb_kernarg();
     if (h == 0 && qrow < a.rows) a.delta[z * a.rows + qrow] = dlt;
-  }
 #pragma unroll
-  for (int ks = 0; ks < 16; ++ks) {
-    fa_pin(qf[ks]);
-    fa_pin(df[ks]);
-  }
-  __syncthreads();   // key masks published (no LDS-DMA in flight yet)
-  FA_STAMP(1);
-  const float sl2 = a.scale * L2E;
-  const int causal = a.causal != 0, nowin = a.window <= 0;
-  const int wpos_lo = min(wrow0, a.rows - 1) / a.qdiv;
-  const int wpos_hi = min(wrow0 + 31, a.rows - 1) / a.qdiv;
+    for (int ks = 0; ks < 16; ++ks) {
+      fa_pin(qf[ks]);
+      fa_pin(df[ks]);
+    }
+  };
 
   // ---- DMA: wave w stages rows 8w..8w+7 of each tile (4 pieces of 2 rows x 512 B per tensor)
-  const fa_u32x4_t rsk = fa_rsrc(K, (uint32_t)((long)a.nkeys * D * 2));
-  const fa_u32x4_t rsv = fa_rsrc(V, (uint32_t)((long)a.nkeys * D * 2));
   uint32_t dk[4], dv[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -1380,6 +1399,13 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
     for (int j = 0; j < 4; ++j) FA_DMA(dk[j], so, rsk, lds_k + bb * 2 * TILE + j * 1024);
 #pragma unroll
     for (int j = 0; j < 4; ++j) FA_DMA(dv[j], so, rsv, lds_v + bb * 2 * TILE + j * 1024);
+  };
+  // the first three tiles of the item into ring slots 0..2 (past the last tile: re-loads of it, never read)
+  auto stage_first = [&]() __attribute__((always_inline)) {
+    if (t_lo < t_hi) {
+#pragma unroll
+      for (int i = 0; i < 3; ++i) stage(i, min(t_lo + i, t_hi - 1));
+    }
   };
 
   // ---- LDS read addresses.  Row reads (K and V, k-step ks): row c32, logical chunk 2ks + h: 8 bases for
@@ -1415,8 +1441,6 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
   };
 
   f32x16_t acc[8];   // dQ^T: d block db, lane = query column
-#pragma unroll
-  for (int i = 0; i < 8; ++i) acc[i] = (f32x16_t){};
 
   // visibility of tile t for this row (all ones when the tile is interior for the wave)
   auto vis_of = [&](int t) __attribute__((always_inline)) {
@@ -1498,20 +1522,21 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
     }
   };
 
-  if (t_lo < t_hi) {
-#pragma unroll
-    for (int i = 0; i < 3; ++i) stage(i, min(t_lo + i, t_hi - 1));
-    asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    __builtin_amdgcn_s_barrier();
-    asm volatile("" ::: "memory");
-  }
+  // Persistent items (attn_fwd256w_kernel's scheme): after an item's last dQ MFMAs, a barrier (every wave is done
+  // with the ring and the key-mask table), then the next item's key masks, Q / dO / O loads and first three K / V
+  // tiles are issued BEFORE this item's dQ epilogue, so their latency runs under its scaling and stores; the next
+  // item's delta follows the epilogue.
+  int item = blockIdx.x, round_k = 0;
+  begin_item(item);
+  load_qdo();
+  finish_qdo();
+  __syncthreads();   // key masks published (no LDS-DMA in flight yet)
+  FA_STAMP(1);
+  stage_first();
   using T_ = std::true_type;
   using F_ = std::false_type;
-  f32x16_t sa, pa, sb = (f32x16_t){}, pb = (f32x16_t){};
+  f32x16_t sa, pa, sb, pb;
   bf16x8_t dsf[2];
-  phase_a(T_{}, F_{}, 0, sa, pa, sb, pb, 0u, dsf);
-  asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // its MFMA results -> the first VALU reads
-  FA_STAMP(2);
   auto slot = [&](int t) { return (uint32_t)((t - t_lo) & (NB - 1)) * (uint32_t)(2 * TILE); };
   auto iter = [&](int t, f32x16_t& s_c, f32x16_t& p_c, f32x16_t& s_n, f32x16_t& p_n) __attribute__((always_inline)) {
     const uint32_t vis = vis_of(t);
@@ -1521,41 +1546,74 @@ __global__ void __launch_bounds__(256, 1) attn_bwd_dq256w_kernel(FlashBwdArgs a)
     phase_a(T_{}, T_{}, slot(t + 1), s_n, p_n, s_c, p_c, vis, dsf);
     phase_b(T_{}, slot(t), dsf, (t - t_lo + 3) & (NB - 1), min(t + 3, t_hi - 1));
   };
-  int t = t_lo;
-  for (; t + 2 < t_hi; t += 2) {
-    iter(t, sa, pa, sb, pb);
-    iter(t + 1, sb, pb, sa, pa);
-  }
-  if (t + 1 < t_hi) {
-    iter(t, sa, pa, sb, pb);
-    ++t;
-    sa = sb;
-    pa = pb;
-  }
-  if (t < t_hi) {
-    phase_a(F_{}, T_{}, 0, sb, pb, sa, pa, vis_of(t), dsf);
-    phase_b(F_{}, slot(t), dsf, 0, 0);
-  }
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // no LDS-DMA may land after the workgroup exits
-  FA_STAMP(3);
-
-  // ---- dQ[q][d] = scale dQ^T[d][q] (bf16), 16-B stores after one permlane32 swap per register pair
-  if (qrow >= a.rows) return;
-  bf16_t* op = a.dQ + (z * a.rows + qrow) * (long)D + 8 * h;
-#pragma unroll
-  for (int db = 0; db < 8; ++db) {
-#pragma unroll
-    for (int m = 0; m < 2; ++m) {
-      uint32_t w[4];
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        const int r = 8 * m + 2 * k;
-        w[k] = (uint32_t)f2bf(acc[db][r] * a.scale) | ((uint32_t)f2bf(acc[db][r + 1] * a.scale) << 16);
-      }
-      const auto s0 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
-      const auto s1 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
-      *reinterpret_cast<uint4*>(op + 32 * db + 16 * m) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+  for (;;) {
+    if (t_lo < t_hi) {
+      asm volatile("s_waitcnt vmcnt(16)" ::: "memory");   // tile t_lo landed (t_lo + 1, + 2 in flight)
+      __builtin_amdgcn_s_barrier();
+      asm volatile("" ::: "memory");
     }
+#pragma unroll
+    for (int i = 0; i < 8; ++i) acc[i] = (f32x16_t){};
+    sb = (f32x16_t){};
+    pb = (f32x16_t){};
+    phase_a(T_{}, F_{}, 0, sa, pa, sb, pb, 0u, dsf);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 7" ::: "memory");   // its MFMA results -> the first VALU reads
+    FA_STAMP(2);
+    int t = t_lo;
+    for (; t + 2 < t_hi; t += 2) {
+      iter(t, sa, pa, sb, pb);
+      iter(t + 1, sb, pb, sa, pa);
+    }
+    if (t + 1 < t_hi) {
+      iter(t, sa, pa, sb, pb);
+      ++t;
+      sa = sb;
+      pa = pb;
+    }
+    if (t < t_hi) {
+      phase_a(F_{}, T_{}, 0, sb, pb, sa, pa, vis_of(t), dsf);
+      phase_b(F_{}, slot(t), dsf, 0, 0);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // (the item's stream is done; nothing else in flight)
+    FA_STAMP(3);
+
+    // ---- dQ[q][d] = scale dQ^T[d][q] (bf16), 16-B stores after one permlane32 swap per register pair; the
+    // output address is taken before the next item's state replaces this one's
+    const FlashBwdArgs& ka = fb_kernarg();
+    const bool row_ok = qrow < ka.rows;
+    bf16_t* op = ka.dQ + (z * ka.rows + (row_ok ? qrow : 0)) * (long)D + 8 * h;
+    ++round_k;
+    const int next = round_k * (int)gridDim.x +
+                     ((round_k & 1) ? (int)gridDim.x - 1 - (int)blockIdx.x : (int)blockIdx.x);
+    if (next < nitems) {
+      __builtin_amdgcn_s_barrier();   // every wave is past its last read of the ring and of the mask table
+      begin_item(next);
+      load_qdo();
+      stage_first();
+    }
+    if (row_ok) {
+#pragma unroll
+      for (int db = 0; db < 8; ++db) {
+#pragma unroll
+        for (int m = 0; m < 2; ++m) {
+          uint32_t w[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int r = 8 * m + 2 * k;
+            w[k] = (uint32_t)f2bf(acc[db][r] * ka.scale) | ((uint32_t)f2bf(acc[db][r + 1] * ka.scale) << 16);
+          }
+          const auto s0 = __builtin_amdgcn_permlane32_swap(w[0], w[2], false, false);
+          const auto s1 = __builtin_amdgcn_permlane32_swap(w[1], w[3], false, false);
+          *reinterpret_cast<uint4*>(op + 32 * db + 16 * m) = make_uint4(s0[0], s1[0], s0[1], s1[1]);
+        }
+      }
+    }
+    if (next >= nitems) break;
+    item = next;
+    finish_qdo();
+    // the next item's key masks published; raw barrier: its LDS-DMA stays in flight (a __syncthreads would drain it)
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_s_barrier();
   }
   FA_STAMPS_WRITE(1, t_hi - t_lo);
 }
@@ -2456,7 +2514,14 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs*
       // the dQ kernel computes delta and runs first; past the 4096-key mask table the generic dQ kernel runs
       // after a separate delta pass and the dK/dV kernel
       const bool dq_new = (a.nkeys + 31) / 32 <= FA_MAXT;
-      if (dq_new) hipLaunchKernelGGL(attn_bwd_dq256w_kernel, gq, dim3(256), 0, st, b);
+      if (dq_new) {
+        // persistent grid (attn_fwd256w_kernel's: one workgroup per CU over the row blocks heaviest first, the next
+        // item's prologue beside this one's epilogue); PTK_ATTN_PERSIST=0: one workgroup per item
+        static const bool persist = [] { const char* e = getenv("PTK_ATTN_PERSIST"); return !(e && e[0] == '0'); }();
+        const long nblk = (long)gq.x;
+        const long g = persist ? std::min<long>(nblk, num_cus()) : nblk;
+        hipLaunchKernelGGL(attn_bwd_dq256w_kernel, dim3((unsigned)g), dim3(256), 0, st, b, nz, (int)nblk);
+      }
       else hipLaunchKernelGGL(attn_delta_kernel<256>, gd, dim3(256), 0, st, b, nz);
       // 32 keys per wave (one wave per SIMD) measured 209 us vs 252 us for 16 keys per wave (two per
       // SIMD, which spills the precomputed transposed-read addresses) at cfg2

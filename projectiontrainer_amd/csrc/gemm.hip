@@ -815,7 +815,12 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
                         // projection at 69 % round fill (Gemma q|k|v 90.7 vs 95.3 us, profiles/r05_dual_solo_probe.txt);
                         // the N 1024 ones stay on 128x128 (dO 66.0 vs 63.2, SigLIP fc2 187 vs 171)
                         (act == ACT_NONE && out == OUT_BF16 && a.N >= 1536 && a.K <= 2048 &&
-                         w4_round_fill(a.M, a.N) >= 0.65 && lean_epilogue_candidate(a)));
+                         w4_round_fill(a.M, a.N) >= 0.65 && lean_epilogue_candidate(a)) ||
+                        // r05: a plain bf16 grid of one partial round of 256x256 tiles beats the 128x128 kernel's
+                        // ~1.1 rounds of two blocks per CU (tools/sk_ab.py, Stage 2's SigLIP at M = 9 216: o 31.3 vs
+                        // 41.8 us, fc2 85.1 vs 109.1; its down projection at bs 8 133.6 vs 177.8)
+                        (act == ACT_NONE && out == OUT_BF16 && a.K <= 8192 &&
+                         (long)((a.M + 255) / 256) * ((a.N + 255) / 256) <= device_cus() && lean_epilogue_candidate(a)));
   // the stream-K tail (gemm_w4.hip P8Tail): a plain GEMM whose last tile round fills the CUs badly, with tail
   // scratch lent by the model-level call (or in the descriptor), runs on the persistent 8-wave kernel with that
   // round's K-tiles spread over the CUs (r04: the N = 1024 / 1152 / 1536 projections, the long-K d(gate|up) dX

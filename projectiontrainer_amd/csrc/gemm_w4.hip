@@ -821,33 +821,38 @@ P8Tail p8_tail_plan_ws(const GemmArgs& a, long ntile, long G, void* slab, long m
 }
 
 // the 8-wave kernel's plan: the scratch of the descriptor or the model-level scope (slabs after the counters).
-// A grid smaller than one round, or one full round plus at most 24 tiles: with more tail tiles after full rounds
-// the pieces of a tile stream different K ranges at the same time, the L2 sharing of a lock-step round is lost,
-// and every Stage-1 shape measured slower (r04: 1.1-1.4x; tools/sk_ab.py)
+// Long K only (K >= 4096: the fixup launch and the partial writes cost a few K-tiles), and a tail the split
+// shortens without losing the lock-step L2 sharing of a round: a grid of at most 64 tiles, or one full round plus
+// at most 128.  Measured (tools/sk_ab.py, r05, same box): SigLIP fc2 0.90x, projector fc2 0.91x, Stage 2's
+// down / d(gate|up) dX 0.72 / 0.63x, projector dW1 (160 tiles, no full round) 0.90x; slower where many tiles
+// share no full round (projector dW2 200 tiles 1.31x, the Stage-2 SigLIP fc2 144 tiles 1.11x, Gemma's 440-tile
+// projections with 184 tail tiles 1.06-1.08x)
 static P8Tail p8_tail_plan(const GemmArgs& a, long ntile, long G, int act, int out) {
-  void* ws = a.tail_ws ? a.tail_ws : tail_scope();   // (the scope is lent only under PTK_STREAMK=1)
+  void* ws = a.tail_ws ? a.tail_ws : tail_scope();
   if (!ws || act != ACT_NONE || (out != OUT_BF16 && out != OUT_F32 && out != OUT_F32_BFR)) return P8Tail{};
-  return p8_tail_plan_ws(a, ntile, G, (char*)ws + P8_CNT_BYTES, G, 24);
+  if (a.K < 4096) return P8Tail{};
+#ifndef PTK_SK_MAXT1
+#define PTK_SK_MAXT1 128   // A/B builds (make ablib AB_DEFS=-DPTK_SK_MAXT1=..) vary the one-round-plus-tail limit
+#endif
+  return p8_tail_plan_ws(a, ntile, G, (char*)ws + P8_CNT_BYTES, 64, PTK_SK_MAXT1);
 }
 
-// The model-level calls lend their tail scratch only under PTK_STREAMK=1: on the whole step the stream-K tail
-// measured slower than the dispatch without it (r04, same box: Stage-2 cfg4 130.7 vs 137.0 img/s against its
-// split-K 128x128 weight grads; no Stage-1 shape qualifies), so it stays an opt-in of the model path and a
-// per-call option of ptk_gemm (ptk_gemm_desc.tail_ws)
+// The model-level calls lend their tail scratch to every GEMM they launch (PTK_STREAMK=0: never, an A/B of the
+// default dispatch without the tail; r04's opt-in predates the parallel fixup)
 static bool streamk_models() {
-  static const bool v = [] { const char* e = getenv("PTK_STREAMK"); return e && e[0] == '1'; }();
+  static const bool v = [] { const char* e = getenv("PTK_STREAMK"); return !(e && e[0] == '0'); }();
   return v;
 }
 static thread_local void* g_tail_scope = nullptr;
 void* tail_scope() { return g_tail_scope; }
 TailScratchScope::TailScratchScope(void* ws, hipStream_t st) : prev(g_tail_scope) {
   if (!streamk_models()) ws = nullptr;
-  g_tail_scope = ws;
-  if (ws) status = launch_zero(ws, P8_CNT_BYTES, st);
+  g_tail_scope = ws;   // (the counters ahead of the slabs are unused since the fixup kernel: no zero-fill)
+  (void)st;
 }
 TailScratchScope::~TailScratchScope() { g_tail_scope = prev; }
 
-// the model-level workspaces reserve tail scratch only when it will be lent (PTK_STREAMK=1)
+// the model-level workspaces reserve tail scratch when it will be lent
 size_t p8_tail_scratch_bytes_models() { return streamk_models() ? p8_tail_scratch_bytes() : 0; }
 
 int p8_tail_split(const GemmArgs& a, int act, int out) {

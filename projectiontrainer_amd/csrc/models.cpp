@@ -263,6 +263,11 @@ int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStr
     b.tail_ws = part;
     if (p8_supported(b, ACT_NONE, out) && p8_tail_split(b, ACT_NONE, out)) return launch_gemm(b, ACT_NONE, out, 1, st);
   }
+  // one partial round of 256x256 tiles: the 8-wave kernel unsplit (launch_gemm's single-round rule) beats the
+  // split-K 128x128 slices (Stage 2 at bs 8: the down projection 133.6 vs 177.8 us)
+  if (a.M >= 4096 && (long)((a.M + 255) / 256) * ((a.N + 255) / 256) <= device_cus() && out == OUT_BF16 &&
+      p8_supported(a, ACT_NONE, out) && lean_epilogue_candidate(a))
+    return launch_gemm(a, ACT_NONE, out, 1, st);
   const long nbig = (long)((a.M + 255) / 256) * ((a.N + 255) / 256);
   int S = 1, kmin = 1024;
   if (a.K >= 4096 && nbig <= 64) S = 4;

@@ -172,6 +172,7 @@ SPILL_BUDGET = {   # kernel symbol substring -> (sgpr_spill_count, vgpr_spill_co
     # the persistent d-256 forward: the per-item state and arguments live across the item loop; every spill
     # reload sits in the per-item code (the K / V tile loop has none: v_readlane count 0 there, r05)
     "attn_fwd256w_kernel": (52, 0, 0),
+    "attn_bwd_dq256w_kernel": (38, 0, 0),   # the persistent dQ's per-item state (r05; none in the K/V tile loop)
     "attn_bwd_dkv256_kernelILi32E": (15, 13, 56),
     # the persistent kernels' epilogues read their arguments through a laundered kernarg pointer
     # (gemm_w4.hip kernarg_args, scalar loads): 0 spills, except the GELU-erf epilogues (the projector's) and

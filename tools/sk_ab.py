@@ -18,7 +18,8 @@ SHAPES = [  # name, M, N, K, out, epilogue kind
     ("proj_dW2", 1152, 10240, 18432, "f32", ""), ("proj_dW1", 10240, 1024, 18432, "f32", ""),
     ("s2_dW_qkv", 1536, 1152, 14336, "bf16", "acc"), ("s2_dW_gu", 13824, 1152, 14336, "bf16", "acc"),
     ("s2_dW_down", 1152, 6912, 14336, "bf16", "acc"), ("s2_down", 14336, 1152, 6912, "bf16", ""),
-    ("s2_dgu_dX", 14336, 1152, 13824, "bf16", ""),
+    ("s2_dgu_dX", 14336, 1152, 13824, "bf16", ""), ("s2_sig_fc2", 9216, 1024, 4096, "bf16", "siglip"),
+    ("s2_sig_o", 9216, 1024, 1024, "bf16", "siglip"), ("s2b8_down", 7168, 1152, 6912, "bf16", ""),
 ]
 only = sys.argv[1:]
 tail = torch.zeros(L.lib().ptk_gemm_tail_scratch_bytes(), dtype=torch.uint8, device=dev)
