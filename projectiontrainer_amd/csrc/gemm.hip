@@ -918,6 +918,18 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   return set_error("gemm: unsupported (act=%d, out=%d)", act, out);
 }
 
+// the K-sliced 8-wave GEMM (gemm_w4.hip launch_gemm_p8_kslices) with launch_gemm's census ("p8") and timers
+int gemm_p8_kslices(const GemmArgs& a, int slices, hipStream_t st) {
+  if (a.M <= 0 || a.N <= 0) return 0;
+  hipEvent_t e0 = nullptr, e1 = nullptr;
+  if (g_timing && (g_timing_mask & 1)) { e0 = next_event(ACT_NONE); e1 = next_event(ACT_NONE); }
+  if (e0) (void)hipEventRecord(e0, st);
+  count_path(GEMM_PATH_P8, ACT_NONE);
+  const int rc = launch_gemm_p8_kslices(a, slices, st);
+  if (e1) (void)hipEventRecord(e1, st);
+  return rc;
+}
+
 // the token-major weight-grad GEMM (gemm_tn.hip) with launch_gemm's census and live timers (class ACT_NONE)
 int gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st) {
   if (a.M <= 0 || a.N <= 0) return 0;

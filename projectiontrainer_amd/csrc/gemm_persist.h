@@ -28,6 +28,10 @@ struct P8Tail {
   int units = 0;              // U = tail tiles x K-tile pairs (0: no tail split)
   int gsplit = 0;             // Gs: workgroups sharing the tail
   float* slab = nullptr;      // [G][2 slots][8 waves][128 x 64] fp32 partials
+  // K slices as extra row tiles (no tail split): the grid's M = zslices x the real M; virtual row tile bm covers
+  // real rows (bm % (nbm / zslices)) x 256 and K rows [z K, (z + 1) K) of the operands (z = bm / (nbm / zslices)),
+  // so slice z's fp32 partial lands at output rows z M_real .. (gemm_p8_kslices)
+  int zslices = 1;
 };
 constexpr size_t P8_WAVE_FLOATS = 128 * 64;
 // the plan of a GEMM with ntile tiles on a grid of G over scratch ws (nullptr: no split); the tail is split only

@@ -530,9 +530,15 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     segment(s, t, k0, k1, tt);
     int bm, bn;
     w4_tile_coords(t, nbm, nbn, bm, bn);
-    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * W4 + (int)p.amap.off) * (uint32_t)p.lda * 2u +
+    uint32_t kz = 0;   // K slices as row tiles (P8Tail::zslices): byte offset of slice z's K range
+    if (!SK && tl.zslices > 1) {
+      const int nbz = nbm / tl.zslices, z = bm / nbz;
+      bm -= z * nbz;
+      kz = (uint32_t)z * (uint32_t)p.K * 2u;
+    }
+    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * W4 + (int)p.amap.off) * (uint32_t)p.lda * 2u + kz +
                                          (uint32_t)k0 * (W4_KT * 2));
-    dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * W4) * (uint32_t)p.ldb * 2u + (uint32_t)k0 * (W4_KT * 2));
+    dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * W4) * (uint32_t)p.ldb * 2u + kz + (uint32_t)k0 * (W4_KT * 2));
     dlen = 2 * (k1 - k0);
   };
   auto dma_advance = [&]() {
@@ -859,6 +865,31 @@ int p8_tail_split(const GemmArgs& a, int act, int out) {
   num_cu();
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   return p8_tail_plan(a, ntile, g_num_cu, act, out).gsplit;
+}
+
+// K-sliced plain fp32 GEMM on the 8-wave kernel (P8Tail::zslices): C[z][M][N] = A[:, zK:(z+1)K] B[:, zK:(z+1)K]^T
+// for z < slices, a.K the slice depth; the slices run as S x M rows of persistent tiles in lock-step rounds
+// (every slice's tiles share their operand panels through L2), the caller sums the partials.  Plain fp32 out,
+// M % 256 == 0 (no tile straddles two slices), byte offsets within 4 GiB.
+int launch_gemm_p8_kslices(const GemmArgs& a, int slices, hipStream_t st) {
+  num_cu();
+  if (slices < 1 || a.M % W4 || a.K < 128 || a.K % W4_KT || a.cmap.g || a.cmap.off || a.amap.g || a.amap.off ||
+      a.bias || a.rowadd || a.resid || a.resid16 || a.aux || a.row_stats)
+    return set_error("gemm_p8_kslices: unsupported operands");
+  if ((double)a.M * a.lda * 2 + (double)slices * a.K * 2 >= 4293918720.0 ||
+      (double)a.N * a.ldb * 2 + (double)slices * a.K * 2 >= 4293918720.0)
+    return set_error("gemm_p8_kslices: operands past 4 GiB");
+  GemmArgs g = a;
+  g.M = a.M * slices;
+  P8Tail tl;
+  tl.zslices = slices;
+  const long ntile = (long)(g.M / W4) * ((g.N + W4 - 1) / W4);
+  const long grid = std::min<long>(ntile, g_num_cu);
+  const uint32_t ab = (uint32_t)std::min<double>((double)a.M * a.lda * 2, 4294967040.0);
+  const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 4294967040.0);
+  hipLaunchKernelGGL((gemm_p8_kernel<ACT_NONE, OUT_F32, false>), dim3((unsigned)grid), dim3(512), 0, st, g, ab, bb, tl,
+                     0u);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8_kslices launch failed");
 }
 
 int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk) {

@@ -49,6 +49,7 @@ float bfround_host(float f) {
 }
 
 constexpr int LM_SPLITK = 8;   // split-K for the vocab-long lm_head dX GEMM (R x H output, K = V)
+constexpr int LM_KSLICES = 16; // its K slices on the 8-wave kernel (R % 256 == 0, V % 1024 == 0)
 
 #define CK(x) \
   do {        \
@@ -219,7 +220,7 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
   if (V % 64 == 0) w.ce_stats = bp.take<float>(R * (V / 64) * 2);
   w.row_loss = bp.take<float>(R);
   w.dxf = bp.take<float>(R * H);
-  w.dxf_part = bp.take<float>((long)(LM_SPLITK + 1) * R * H);   // + one slot for a vocab remainder
+  w.dxf_part = bp.take<float>((long)std::max(LM_SPLITK + 1, LM_KSLICES) * R * H);   // (+ a vocab remainder slot)
   w.count = bp.take<float>(4);
   w.gscale = bp.take<float>(4);
   if (train) {
@@ -580,7 +581,13 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
   sq.next("gemma.lm_head_bwd");
   // tied lm_head weight grad: dE += dlogits^T . xf (the logits rows outside the loss rows have zero grad)
   if (train) CK(weight_grad(w.logits, V, ident, V, w.xf, H, ident, H, R, w.TL, w.TX, gr->embed, w.skpart, w.sk_floats, st));
-  {  // d(xf) = dlogits . E, K = vocab: split-K over LM_SPLITK equal slices (fp32 partials, ordered sum);
+  if (R % 256 == 0 && V % (64 * LM_KSLICES) == 0) {
+    // d(xf) = dlogits . E, K = vocab, as LM_KSLICES K slices of 256x256 tiles on the 8-wave kernel: 80 tiles x 16
+    // slices = 5 lock-step rounds at cfg2 (the 128x128 8-slice split ran 2.8 ms); fp32 partials, ordered sum
+    GemmArgs g = gemm(w.logits, V, wt->embed_t, V, w.dxf_part, H, R, H, V / LM_KSLICES);
+    CK(gemm_p8_kslices(g, LM_KSLICES, st));
+    CK(launch_sum_partials(w.dxf_part, LM_KSLICES, (long)R * H, w.dxf, st));
+  } else {  // d(xf) = dlogits . E, K = vocab: split-K over LM_SPLITK equal slices (fp32 partials, ordered sum);
      // a vocab that is not a multiple of 64 * LM_SPLITK (Gemma3-4B: 262 208 = 4 097 x 64) leaves a
      // remainder slice, computed into one more partial
     const int kc = V / (64 * LM_SPLITK) * 64, rem = V - LM_SPLITK * kc;
