@@ -839,12 +839,23 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
   }
-  if (batch == 1 && (g_force_tiles == 32 || p8_auto || sk) && p8_supported(a, act, out)) {
+  // 224- / 192-row tiles on the 8-wave kernel where their rounds undercut the 256-row ones (p8_tile_height:
+  // Gemma3's N 1152 / 1536 / 1024 projections at M 22 528, SigLIP's q|k|v, o and fc1 at M 18 432), ahead of the
+  // 4-wave and 128x128 kernels; force modes 512 / 1024 put every plain / GELU-tanh single GEMM on 224 / 192 rows
+  // (tests).  PTK_TM224=0: 256-row tiles only (A/B)
+  static const bool tm_env = [] { const char* e = getenv("PTK_TM224"); return !(e && e[0] == '0'); }();
+  const bool short_ok = batch == 1 && !sk && p8_supported(a, act, out) &&
+                        (act == ACT_NONE || (act == ACT_GELU_TANH && out == OUT_BF16));
+  int tm = 256;
+  if (short_ok && g_force_tiles == 0 && tm_env && a.M >= 4096) tm = p8_tile_height(a, act, out);
+  else if (short_ok && g_force_tiles == 512) tm = 224;
+  else if (short_ok && g_force_tiles == 1024) tm = 192;
+  if (batch == 1 && (g_force_tiles == 32 || p8_auto || sk || tm != 256) && p8_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
     if (e0) (void)hipEventRecord(e0, st);
     count_path(sk ? GEMM_PATH_P8SK : GEMM_PATH_P8, act);
-    const int rc = launch_gemm_p8(a, act, out, st, sk != 0);
+    const int rc = launch_gemm_p8(a, act, out, st, sk != 0, tm);
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
   }

@@ -443,14 +443,22 @@ constexpr int P8_PIECES = 4;   // LDS-DMA pieces per wave per k-step
 #define P8_DSREAD(DST, ADDR, OFF) W4_DSREAD(DST, ADDR, OFF)
 #define P8_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
 #endif
-template <int ACT, int OUT, bool SK, bool LEAN = false>
+// TM: output tile height, 256, 224 or 192.  Shorter tiles (TM / 32 row blocks of 16 per wave, the A image's
+// last rows unused, waves 0 .. TM / 32 - 1 staging A, the others only B) fill the rounds of the persistent grid
+// better where 256-row tiles leave a thin last round: Gemma3's N 1152 / 1024 projections at M 22 528 (440 -> 505
+// tiles of 7/8 the work on 2 rounds), N 1536 (3 rounds either way, 7/8 the work), SigLIP's q|k|v at M 18 432,
+// its fc1 on 192-row tiles (5 rounds of 256 -> 6 of 192) -- launch_gemm: p8_tile_height
+template <int ACT, int OUT, bool SK, bool LEAN = false, int TM = 256>
 __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes, P8Tail tl,
                                                          uint32_t c_bytes) {
+  static_assert(TM == 256 || ((TM == 224 || TM == 192) && !SK), "shorter tiles: whole tiles only");
+  constexpr int RB = TM / 32;   // 16-row blocks per wave
   __shared__ __attribute__((aligned(16))) char smem[W4_NSLOT * W4_SLOT];   // 160 KiB: the k-step ring
   const int lane = threadIdx.x & 63;
   const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int hf = wave >> 2, wq = wave & 3, wr = wq >> 1, wc = wq & 1;
-  const int nbm = (p.M + W4 - 1) / W4, nbn = (p.N + W4 - 1) / W4;
+  const bool a_dma = TM == 256 || wave < RB;   // (shorter tiles: waves RB .. 7 stage no A rows)
+  const int nbm = (p.M + TM - 1) / TM, nbn = (p.N + W4 - 1) / W4;
   const int ntile = nbm * nbn;
   const int G = gridDim.x;
   int loc;
@@ -536,7 +544,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       bm -= z * nbz;
       kz = (uint32_t)z * (uint32_t)p.K * 2u;
     }
-    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * W4 + (int)p.amap.off) * (uint32_t)p.lda * 2u + kz +
+    dsa = __builtin_amdgcn_readfirstlane((uint32_t)(bm * TM + (int)p.amap.off) * (uint32_t)p.lda * 2u + kz +
                                          (uint32_t)k0 * (W4_KT * 2));
     dsb = __builtin_amdgcn_readfirstlane((uint32_t)(bn * W4) * (uint32_t)p.ldb * 2u + kz + (uint32_t)k0 * (W4_KT * 2));
     dlen = 2 * (k1 - k0);
@@ -552,7 +560,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
   auto slot_next = [](uint32_t s) { s += W4_SLOT; return s == W4_NSLOT * W4_SLOT ? 0u : s; };
 
   const int frag_off = (lane & 15) * 64 + (((lane >> 4) ^ ((lane >> 1) & 2)) << 4);
-  const uint32_t frag_a = lds_addr(smem) + wr * 128 * 64 + frag_off;
+  const uint32_t frag_a = lds_addr(smem) + wr * (TM / 2) * 64 + frag_off;
   const uint32_t frag_b = lds_addr(smem) + W4_SOPB + (wc * 128 + hf * 64) * 64 + frag_off;
   bf16x8_t fa[8], fb0[4], fb1[4];
   f32x4_t acc[8][4];
@@ -561,7 +569,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
   auto read_frags = [&](uint32_t rs) __attribute__((always_inline)) {
     const uint32_t ba = frag_a + rs, bb = frag_b + rs;
 #pragma unroll
-    for (int r = 0; r < 8; ++r) P8_DSREAD(fa[r], ba, r * 1024);
+    for (int r = 0; r < RB; ++r) P8_DSREAD(fa[r], ba, r * 1024);
 #pragma unroll
     for (int r = 0; r < 4; ++r) P8_DSREAD(fb0[r], bb, r * 1024);
     P8_LGKM(0);
@@ -584,18 +592,35 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
     const uint32_t da = lds_dma + ws, db = da + W4_SOPB;
     const uint32_t sa = dsa + dks * (W4_KS * 2), sb = dsb + dks * (W4_KS * 2);
 #pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      if (q == 0) P8_LGKM(6);
-      else if (q < 3) P8_LGKM(8);
-      else if (q == 3) P8_LGKM(9);
-      else P8_LGKM(10);
+    for (int q = 0; q < RB; ++q) {
+      // n_q = RB - 2, RB, RB, RB + 1, RB + 2, .. (8 groups: 6, 8, 8, 9, 10, 10, 10, 10; each A read fewer, one less)
+      if constexpr (RB == 8) {
+        if (q == 0) P8_LGKM(6);
+        else if (q < 3) P8_LGKM(8);
+        else if (q == 3) P8_LGKM(9);
+        else P8_LGKM(10);
+      } else if constexpr (RB == 7) {
+        if (q == 0) P8_LGKM(5);
+        else if (q < 3) P8_LGKM(7);
+        else if (q == 3) P8_LGKM(8);
+        else P8_LGKM(9);
+      } else {
+        if (q == 0) P8_LGKM(4);
+        else if (q < 3) P8_LGKM(6);
+        else if (q == 3) P8_LGKM(7);
+        else P8_LGKM(8);
+      }
       asm volatile("" : "+v"(fa[q]));
       if (q == 0) asm volatile("" : "+v"(FB[0]), "+v"(FB[1]), "+v"(FB[2]), "+v"(FB[3]));
       if (rd && q < 4) P8_DSREAD(NB[q], bb, q * 1024);
-      if ((q & 1) == half) {
-        const int pc = q >> 1;   // pieces A0 B0 A1 B1
-        if (pc & 1) W4_DMA(rsb, offb[pc >> 1], sb, db + (pc >> 1) * 1024);
-        else W4_DMA(rsa, offa[pc >> 1], sa, da + (pc >> 1) * 1024);
+      // pieces A0 B0 A1 B1: piece pc in group min(2 pc + half, RB - 1) -- the even (waves 0-3) or odd (waves 4-7)
+      // groups, the pieces past the last group in it
+#pragma unroll
+      for (int pc = 0; pc < 4; ++pc) {
+        if (q == (2 * pc + half < RB - 1 ? 2 * pc + half : RB - 1)) {
+          if (pc & 1) W4_DMA(rsb, offb[pc >> 1], sb, db + (pc >> 1) * 1024);
+          else if (a_dma) W4_DMA(rsa, offa[pc >> 1], sa, da + (pc >> 1) * 1024);
+        }
       }
       if (PTK_P8_MPRIO) asm volatile("s_setprio 1" ::: "memory");
 #pragma unroll
@@ -606,7 +631,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       if (PTK_P8_MPRIO) asm volatile("s_setprio 0" ::: "memory");
       if (rd && q >= 1) P8_DSREAD(fa[q - 1], ba, (q - 1) * 1024);   // one group after its last reader
     }
-    if (rd) P8_DSREAD(fa[7], ba, 7 * 1024);
+    if (rd) P8_DSREAD(fa[RB - 1], ba, (RB - 1) * 1024);
   };
 
   // stream-K piece of a cut tail tile: the wave's 128x64 fp32 partial to its workgroup's slot (slot 0 for the
@@ -625,6 +650,11 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
   unsigned int stv_[4] = {0u, 0u, 0u, 0u};
   const int em_ = g_p8_epi_mode;
 #endif
+  // the wait that leaves only the youngest k-step's pieces in flight: 4 per wave, 2 for the B-only waves
+  auto vm_wait = [&]() __attribute__((always_inline)) {
+    if (TM != 256 && !a_dma) asm volatile("s_waitcnt vmcnt(2)" ::: "memory");
+    else asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+  };
   auto run = [&](auto half_c) __attribute__((always_inline)) {
     if (PTK_P8_PRIO && decltype(half_c)::value) __builtin_amdgcn_s_setprio(PTK_P8_PRIO);
     // prologue: k-steps 0..3 into slots 0..3; 0..2 landed and published; fragments of k-step 0 read
@@ -635,12 +665,12 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       const uint32_t sa = dsa + dks * (W4_KS * 2), sb = dsb + dks * (W4_KS * 2);
 #pragma unroll
       for (int j = 0; j < 2; ++j) {
-        W4_DMA(rsa, offa[j], sa, da + j * 1024);
+        if (a_dma) W4_DMA(rsa, offa[j], sa, da + j * 1024);
         W4_DMA(rsb, offb[j], sb, db + j * 1024);
       }
       dma_advance();
     }
-    asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+    vm_wait();
     P8_BARRIER();
     read_frags(0);
     P8_BARRIER();
@@ -661,7 +691,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       dma_advance();
       if (!lst) rs = slot_next(rs);   // last pair: rs stays on the next segment's first k-step
       ws = slot_next(ws);
-      asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      vm_wait();
       P8_BARRIER();
     };
     for (int s = 0; s < nseg; ++s) {
@@ -676,7 +706,7 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
       asm volatile("s_nop 7\n\ts_nop 7" ::: "memory");   // MFMA D -> accumulator read wait states
       int bm, bn;
       w4_tile_coords(t, nbm, nbn, bm, bn);
-      const long row0 = (long)bm * W4 + wr * 128, col0 = (long)bn * W4 + wc * 128 + hf * 64;
+      const long row0 = (long)bm * TM + wr * (TM / 2), col0 = (long)bn * W4 + wc * 128 + hf * 64;
       if (!SK || tt < 0) {
 #ifdef PTK_P8_STAMPS
         if (em_ != 1)
@@ -684,8 +714,8 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
         {
           if constexpr (LEAN && ACT == ACT_GEGLU_BWD)
             w4_epilogue_lean_glu<ACT, 4>(kernarg_args(), acc, row0, col0, lane, c_bytes);
-          else if constexpr (LEAN) w4_epilogue_lean<ACT, 4>(kernarg_args(), acc, row0, col0, lane, c_bytes);
-          else w4_epilogue<ACT, OUT, 4>(kernarg_args(), acc, row0, col0, lane);
+          else if constexpr (LEAN) w4_epilogue_lean<ACT, 4, RB>(kernarg_args(), acc, row0, col0, lane, c_bytes);
+          else w4_epilogue<ACT, OUT, 4, RB>(kernarg_args(), acc, row0, col0, lane);
         }
       } else if constexpr (SK) {
         tail_store((int)((__builtin_amdgcn_readlane(segC, s) >> 21) & 1u));
@@ -892,8 +922,65 @@ int launch_gemm_p8_kslices(const GemmArgs& a, int slices, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8_kslices launch failed");
 }
 
-int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk) {
+// the tile height of a plain / GELU-tanh 8-wave GEMM without a stream-K tail: the TM of {256, 224, 192} with the
+// lowest tile rounds x (TM + 128), when it undercuts 256 by >= 5 % (else 256).  The 128 rows' worth per round is
+// what shorter tiles do not shed (prologue, epilogue, the DMA / LDS work per MFMA): fitted to tools/p8_probe.py
+// (r05, same box): Gemma o 59.6 / 54.1 / 68.5 us at 256 / 224 / 192 rows, dO 65.8 / 59.5 / 54.4, q|k|v 90.7 / 88.0
+// / 81.4, down 340 / 312 / 407, SigLIP fc1 149 / 157 / 153 (5 rounds of 256 vs 6 of 192: kept at 256)
+int p8_tile_height(const GemmArgs& a, int act, int out) {
   num_cu();
+  if (!(act == ACT_NONE || (act == ACT_GELU_TANH && out == OUT_BF16))) return 256;
+  const long nbn = (a.N + W4 - 1) / W4, cu = g_num_cu;
+  auto cost = [&](long tm) { return (double)((((a.M + tm - 1) / tm) * nbn + cu - 1) / cu) * (double)(tm + 128); };
+  const double c256 = cost(256);
+  int best = 256;
+  double bc = 0.95 * c256;
+  for (int tm : {224, 192}) {
+    const double c = cost(tm);
+    if (c < bc) { bc = c; best = tm; }
+  }
+  return best;
+}
+
+template <int TM>
+static int launch_p8_short(const GemmArgs& a, int act, int out, hipStream_t st, long grid) {
+  const uint32_t ab = (uint32_t)std::min<double>((double)(a.M + a.amap.off) * a.lda * 2, 2147483000.0);
+  const uint32_t bb = (uint32_t)std::min<double>((double)a.N * a.ldb * 2, 2147483000.0);
+  const P8Tail tl{};
+  uint32_t cb = 0;
+  if (lean_epilogue_ok(a, act, out, cb)) {
+    if (act == ACT_NONE)
+      hipLaunchKernelGGL((gemm_p8_kernel<ACT_NONE, OUT_BF16, false, true, TM>), dim3((unsigned)grid), dim3(512), 0,
+                         st, a, ab, bb, tl, cb);
+    else
+      hipLaunchKernelGGL((gemm_p8_kernel<ACT_GELU_TANH, OUT_BF16, false, true, TM>), dim3((unsigned)grid),
+                         dim3(512), 0, st, a, ab, bb, tl, cb);
+  } else if (act == ACT_GELU_TANH) {
+    hipLaunchKernelGGL((gemm_p8_kernel<ACT_GELU_TANH, OUT_BF16, false, false, TM>), dim3((unsigned)grid), dim3(512),
+                       0, st, a, ab, bb, tl, 0u);
+  } else if (out == OUT_BF16) {
+    hipLaunchKernelGGL((gemm_p8_kernel<ACT_NONE, OUT_BF16, false, false, TM>), dim3((unsigned)grid), dim3(512), 0,
+                       st, a, ab, bb, tl, 0u);
+  } else if (out == OUT_F32) {
+    hipLaunchKernelGGL((gemm_p8_kernel<ACT_NONE, OUT_F32, false, false, TM>), dim3((unsigned)grid), dim3(512), 0,
+                       st, a, ab, bb, tl, 0u);
+  } else {
+    hipLaunchKernelGGL((gemm_p8_kernel<ACT_NONE, OUT_F32_BFR, false, false, TM>), dim3((unsigned)grid), dim3(512),
+                       0, st, a, ab, bb, tl, 0u);
+  }
+  return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8 launch failed");
+}
+
+int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk, int tm) {
+  num_cu();
+  if (tm != 256 && !sk) {
+    if (!(act == ACT_NONE || (act == ACT_GELU_TANH && out == OUT_BF16)))
+      return set_error("gemm_p8: %d-row tiles take the plain / GELU-tanh epilogues only", tm);
+    if (tm != 224 && tm != 192) return set_error("gemm_p8: tile height %d (256, 224, 192)", tm);
+    const long ntm = (long)((a.M + tm - 1) / tm) * ((a.N + W4 - 1) / W4);
+    const long grid = std::min<long>(ntm, g_num_cu);
+    return tm == 224 ? launch_p8_short<224>(a, act, out, st, grid) : launch_p8_short<192>(a, act, out, st, grid);
+  }
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   // the stream-K plan only where launch_gemm's gates chose the tail split (its census counts it as p8sk)
   const P8Tail tl = sk ? p8_tail_plan(a, ntile, g_num_cu, act, out) : P8Tail{};

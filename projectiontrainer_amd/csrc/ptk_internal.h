@@ -66,7 +66,8 @@ double w4_round_fill(long M, long N);
 int device_cus();   // compute units of the current device (cached)
 // persistent 8-wave variant (gemm_w4.hip): the w4 tiles and ring with two waves per SIMD
 bool p8_supported(const GemmArgs& a, int act, int out);
-int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk);
+int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk, int tm = 256);
+int p8_tile_height(const GemmArgs& a, int act, int out);   // 256, or 224 / 192 where shorter tiles fill the rounds
 int launch_gemm_p8_kslices(const GemmArgs& a, int slices, hipStream_t st);   // K slices as row tiles (fp32 partials)
 int gemm_p8_kslices(const GemmArgs& a, int slices, hipStream_t st);          // + census / timers (gemm.hip)
 // persistent two-group kernel (gemm_dual.hip): 256x128 tiles, one group's epilogue beside the other's K loop

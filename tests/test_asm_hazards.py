@@ -179,9 +179,12 @@ SPILL_BUDGET = {   # kernel symbol substring -> (sgpr_spill_count, vgpr_spill_co
     # the stream-K tail variants' bookkeeping (r05: 24 -> 0-1 with the in-kernel reducer moved to p8_fixup_kernel)
     "gemm_p8_kernelILi0ELi0ELb1E": (1, 0, 0),
     "gemm_tn_kernelILi0ELb1E": (3, 0, 0),
+    "Lb0ELi224E": (1, 0, 0),   # the 8-wave kernel's 224- / 192-row tiles, general epilogues
+    "Lb0ELi192E": (1, 0, 0),
     "gemm_p8_kernelILi1ELi0ELb0E": (4, 0, 0),
-    "gemm_p8_kernelILi2ELi0ELb0E": (28, 0, 0),
-    "gemm_p8_kernelILi4ELi0ELb0E": (20, 0, 0),
+    # GELU-erf epilogues: 28 / 20 -> 31 / 28 with the K-slice (zslices) DMA offsets (r05); none in the K loop
+    "gemm_p8_kernelILi2ELi0ELb0E": (31, 0, 0),
+    "gemm_p8_kernelILi4ELi0ELb0E": (28, 0, 0),
     # the 4-wave kernel's GELU-erf epilogues (not dispatched: the projector's GELU-erf shapes run on p8), with the
     # whole-line stores' row-pair exchange
     "gemm_w4_kernelILi2ELi0E": (18, 0, 0),

@@ -544,6 +544,45 @@ def test_gemm_p8_matches_w4(gpu, M, N, K):
     torch.testing.assert_close(outs[2]["f32"], ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
 
 
+@pytest.mark.parametrize("M,N,K", [(22528, 1152, 1152), (1000, 1024, 1152), (4500, 1536, 640), (18432, 3072, 1024),
+                                   (224, 256, 128), (230, 320, 192)])
+def test_gemm_p8_tm224_matches_p8(gpu, M, N, K):
+    """The 8-wave kernel's 224- and 192-row tiles (forced modes 512 / 1024: 7 / 6 row blocks per wave, the waves
+    past them staging only B, ragged M) against its 256-row tiles (mode 32): the same k-step order per output element, so the plain bf16 / fp32 /
+    fp32-rounded, bias + residual, bias + bf16(linear) + bf16 residual in place, identity group row map and
+    GELU-tanh epilogues are bit-identical; the census shows the p8 family ran."""
+    Kn, L = _k()
+    A, B = rnd(M, K, dev=gpu, seed=21), rnd(N, K, dev=gpu, seed=22, scale=0.05)
+    bias = rnd(N, dev=gpu, dtype=torch.float32, seed=25)
+    res = rnd(M, N, dev=gpu, dtype=torch.float32, seed=26)
+    outs = []
+    for md in (32, 512, 1024):
+        L.lib().ptk_gemm_force_small_tiles(md)
+        L.gemm_path_counts(reset=True)
+        try:
+            o = {"f32": Kn.gemm(A, B, out_dtype=torch.float32), "bf16": Kn.gemm(A, B),
+                 "f32r": Kn.gemm(A, B, C=torch.empty(M, N, device=gpu), out_mode=L.OUT_F32_BF16ROUND)}
+            C = res.clone()
+            Kn.gemm(A, B, C=C, bias=bias, resid=C)
+            o["resid"] = C
+            o["gelu_tanh"] = Kn.gemm(A, B, bias=bias, act=L.ACT_GELU_TANH)
+            C16 = res.to(torch.bfloat16)
+            Kn.gemm(A, B, C=C16, bias=bias, resid16=C16, bf16_linear=True)
+            o["resid16"] = C16
+            o["gmap"] = Kn.gemm(A, B, C=torch.zeros(M, N, dtype=torch.bfloat16, device=gpu), cmap=(112, 0, 112, 0))
+            torch.cuda.synchronize()
+            paths = {p for p, _ in L.gemm_path_counts(reset=True)}
+            assert paths == {"p8"}, paths
+            outs.append(o)
+        finally:
+            L.lib().ptk_gemm_force_small_tiles(0)
+    for other in outs[1:]:
+        for k in outs[0]:
+            assert torch.equal(outs[0][k], other[k]), (k, (outs[0][k].float() - other[k].float()).abs().max())
+    ref = A.float() @ B.float().T
+    torch.testing.assert_close(outs[2]["f32"], ref, rtol=2e-3, atol=2e-3 * math.sqrt(K))
+
+
 def test_projector_module_autograd(gpu):
     """MLPProjector as an nn.Module under autograd (the public API, Stage1/projectors.py:22-29): output,
     parameter grads and the INPUT grad vs torch fp32 autograd of the same Sequential(Linear, GELU, Linear);
