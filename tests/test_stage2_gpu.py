@@ -355,8 +355,9 @@ def test_stage2_architecture_scale_vs_oracle(gpu, bs):
     exists at these sizes, so the bars are SURVEY.md:297's with rel-L2 on the weight grads widened to 6e-2
     (the bf16-vs-fp32 distance the s2_tiny twins show, tests/golden/s2_tiny*.npz: up to 0.05); params
     after AdamW within 2.5 lr + 1 bf16 ulp (Adam moves each weight by ~lr; bf16 parameters).
-    bs 8 (M = 7 168 token rows) is the smallest batch whose GEMM dispatch census equals the benchmarked bs-16
-    micro-batch's (tools/census_probe2.py stage2: bs 2-6 and 10-14 each differ by a family): the weight grads
+    bs 8 (M = 7 168 token rows) is the smallest batch whose GEMM dispatch census covers the benchmarked bs-16
+    micro-batch's but for the split-K family exempted below (tools/census_probe2.py stage2, r05: bs 6 misses two
+    more families; bs 8, 10 and 12 miss only that one): the weight grads
     over K = 7 168 tokens run the benchmarked paths (transposes, the stream-K / split-K GEMMs and their
     reductions), asserted through ptk_gemm_path_counts."""
     from oracle import stage2_ref as S
@@ -397,7 +398,13 @@ def test_stage2_architecture_scale_vs_oracle(gpu, bs):
     if bs == 8:
         bench = _stage2_bench_census(gpu)
         record(t, "paths", n_bench=len(bench), n_here=len(paths), missing=len(bench - paths))
-        assert bench <= paths, ("kernel families of the bs-16 micro-batch not exercised", sorted(bench - paths))
+        # the one family bs 8 cannot reach: the batched 128x128 split-K slices, which at bs 16 run only the last
+        # layer's weight grads over its K = R = 4 096 gathered loss rows (gemm_split S = 2 for K >= 4 096; 2 048
+        # rows at bs 8).  Since the lm_head dX moved to K slices on the 8-wave kernel (r05) nothing else uses
+        # them here; the kernel is exercised by test_kernels_gpu.py's batched GEMMs (batch = B x heads)
+        exempt = {("nt128b", 0)}
+        assert bench - exempt <= paths, ("kernel families of the bs-16 micro-batch not exercised",
+                                         sorted(bench - paths))
     torch.set_num_threads(min(16, torch.get_num_threads()))
     st = S.Stage2State(lp)
     ref_loss = S.stage2_loss({k: torch.from_numpy(v) for k, v in vp.items()}, cfg.vision, st.params, cfg.text,
