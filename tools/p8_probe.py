@@ -71,7 +71,7 @@ def timed(A, B, kw, act, odt, C, reps):
 
 
 only = set(a for a in sys.argv[1:] if not a.startswith("-"))
-TAGS = {8: "w4", 32: "p8", 64: "dual", 128: "solo", 256: "p8w", 512: "p8t224", 1024: "p8t192", 0: "auto"}
+TAGS = {8: "w4", 32: "p8", 64: "dual", 128: "solo", 256: "p8w", 512: "p8t224", 1024: "p8t192", 2048: "w4r", 0: "auto"}
 modes = tuple(int(x) for x in os.environ.get("MODES", "8,32,64,0").split(","))
 for name, m, n, k, act, odt, *extra in SHAPES:
     if only and name not in only:
@@ -86,6 +86,17 @@ for name, m, n, k, act, odt, *extra in SHAPES:
             timed(A, B, kw, act, odt, C, 1)
             res[md].append(timed(A, B, kw, act, odt, C, reps))
     L.lib().ptk_gemm_force_small_tiles(0)
+    eq = {}
+    if os.environ.get("CHECK") == "1":   # each mode's output against the first mode's, bitwise
+        outs = []
+        for md in modes:
+            L.lib().ptk_gemm_force_small_tiles(md)
+            Cm = torch.full_like(C, float("nan"))
+            K.gemm(A, B, C=Cm, out_dtype=odt, act=act, **kw)
+            outs.append(Cm)
+        L.lib().ptk_gemm_force_small_tiles(0)
+        torch.cuda.synchronize()
+        eq = {"eq_" + TAGS[md]: bool(torch.equal(outs[0], o)) for md, o in zip(modes[1:], outs[1:])}
     fl = 2.0 * m * n * k
     out = {"name": name, "M": m, "N": n, "K": k}
     for md in modes:
@@ -93,6 +104,7 @@ for name, m, n, k, act, odt, *extra in SHAPES:
         ms = min(res[md])
         out[tag + "_us"] = round(ms * 1e3, 1)
         out[tag + "_TF"] = round(fl / ms / 1e9, 1)
+    out.update(eq)
     print(json.dumps(out), flush=True)
     del A, B, C, kw
     torch.cuda.empty_cache()
