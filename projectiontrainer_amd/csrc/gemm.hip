@@ -859,18 +859,6 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
     if (e1) (void)hipEventRecord(e1, st);
     return rc;
   }
-  // the 4-wave kernel with register-staged operands (gemm_w4r.hip): force mode 2048, or PTK_W4R=1 for every w4
-  // shape (A/B)
-  static const bool w4r_env = [] { const char* e = getenv("PTK_W4R"); return e && e[0] == '1'; }();
-  if (batch == 1 && (g_force_tiles == 2048 || (w4_auto && w4r_env)) && w4_supported(a, act, out)) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
-    if (e0) (void)hipEventRecord(e0, st);
-    count_path(GEMM_PATH_W4, act);
-    const int rc = launch_gemm_w4r(a, act, out, st);
-    if (e1) (void)hipEventRecord(e1, st);
-    return rc;
-  }
   if (batch == 1 && (g_force_tiles == 8 || w4_auto) && w4_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }

@@ -61,7 +61,6 @@ int path_counts(int64_t* out, int reset);   // out [GEMM_NPATH][8] launches per 
 // persistent 256x256 4-wave GEMM (gemm_w4.hip): batch 1 only; w4_supported says whether a shape qualifies
 bool w4_supported(const GemmArgs& a, int act, int out);
 int launch_gemm_w4(const GemmArgs& a, int act, int out, hipStream_t st, int max_grid);
-int launch_gemm_w4r(const GemmArgs& a, int act, int out, hipStream_t st);   // register-staged stream (A/B)
 // fraction of the persistent grid's tile rounds that hold work: ntile / (ceil(ntile / CUs) * CUs)
 double w4_round_fill(long M, long N);
 int device_cus();   // compute units of the current device (cached)
