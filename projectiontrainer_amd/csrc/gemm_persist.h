@@ -523,12 +523,15 @@ PTK_DEV void w4_epilogue_lean(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row
 
 // Lean GEGLU-backward epilogue (lean_glu_ok): w4_gbwd_rows' values and whole-line dg | du stores, the saved g, u
 // loaded by buffer loads one row block ahead (rows past M read as zero and their stores are dropped)
+#ifndef PTK_GBWD_AHEAD
+#define PTK_GBWD_AHEAD 2   // row blocks of saved g, u in flight in the lean GEGLU-backward epilogue (A/B builds)
+#endif
 struct LeanGbwd {
   __amdgpu_buffer_rsrc_t rgi, rui, rc;
   uint32_t vin, ldin_bytes, vout, ldc_bytes;
 };
-template <int I, int NP>
-PTK_DEV void w4_gbwd_load_lean(const LeanGbwd& e, u16x8_t (&G)[NP], u16x8_t (&U)[NP]) {
+template <int NP>
+PTK_DEV void w4_gbwd_load_lean(const LeanGbwd& e, int I, u16x8_t (&G)[NP], u16x8_t (&U)[NP]) {
 #pragma unroll
   for (int pp = 0; pp < NP; ++pp) {
     const uint32_t o = e.vin + (uint32_t)(16 * I) * e.ldin_bytes + 64u * pp;
@@ -536,8 +539,8 @@ PTK_DEV void w4_gbwd_load_lean(const LeanGbwd& e, u16x8_t (&G)[NP], u16x8_t (&U)
     U[pp] = __builtin_bit_cast(u16x8_t, __builtin_amdgcn_raw_buffer_load_b128(e.rui, o, 0, 0));
   }
 }
-template <int I, int NP>
-PTK_DEV void w4_gbwd_rows_lean(f32x4_t (&a)[2 * NP], const LeanGbwd& e, const u16x8_t (&G)[NP],
+template <int NP>
+PTK_DEV void w4_gbwd_rows_lean(f32x4_t (&a)[2 * NP], const LeanGbwd& e, int I, const u16x8_t (&G)[NP],
                                const u16x8_t (&U)[NP]) {
 #pragma unroll
   for (int j = 0; j < 2 * NP; ++j) asm volatile("" : "+a"(a[j]) :: "memory");
@@ -593,23 +596,16 @@ PTK_DEV void w4_epilogue_lean_glu(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long
     const bool lo = (lane & 8) == 0;
     e.vout = (crow0 + (lane & 7)) * ldc_bytes +
              (uint32_t)(2 * col0 + 8 * (4 * (cb >> 4) + ((cb >> 3) & 1) + (lo ? 0 : 2))) * 2u;
-    u16x8_t G0[NP], U0[NP], G1[NP], U1[NP];
-    w4_gbwd_load_lean<0, NP>(e, G0, U0);
-    w4_gbwd_load_lean<1, NP>(e, G1, U1);
-    w4_gbwd_rows_lean<0, NP>(acc[0], e, G0, U0);
-    w4_gbwd_load_lean<2, NP>(e, G0, U0);
-    w4_gbwd_rows_lean<1, NP>(acc[1], e, G1, U1);
-    w4_gbwd_load_lean<3, NP>(e, G1, U1);
-    w4_gbwd_rows_lean<2, NP>(acc[2], e, G0, U0);
-    w4_gbwd_load_lean<4, NP>(e, G0, U0);
-    w4_gbwd_rows_lean<3, NP>(acc[3], e, G1, U1);
-    w4_gbwd_load_lean<5, NP>(e, G1, U1);
-    w4_gbwd_rows_lean<4, NP>(acc[4], e, G0, U0);
-    w4_gbwd_load_lean<6, NP>(e, G0, U0);
-    w4_gbwd_rows_lean<5, NP>(acc[5], e, G1, U1);
-    w4_gbwd_load_lean<7, NP>(e, G1, U1);
-    w4_gbwd_rows_lean<6, NP>(acc[6], e, G0, U0);
-    w4_gbwd_rows_lean<7, NP>(acc[7], e, G1, U1);
+    // the saved g, u of row block i + D load while row block i computes (D row blocks in flight)
+    constexpr int D = PTK_GBWD_AHEAD;
+    u16x8_t G[D][NP], U[D][NP];
+#pragma unroll
+    for (int i = 0; i < D; ++i) w4_gbwd_load_lean<NP>(e, i, G[i], U[i]);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      w4_gbwd_rows_lean<NP>(acc[i], e, i, G[i % D], U[i % D]);
+      if (i + D < 8) w4_gbwd_load_lean<NP>(e, i + D, G[i % D], U[i % D]);
+    }
   }
 }
 
