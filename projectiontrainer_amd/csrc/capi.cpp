@@ -225,9 +225,22 @@ int projector_bwd_stage(const ptk_projector* p, int rows, const void* x, const v
   bf16_t* xT = (bf16_t*)w; w += align256((size_t)Dv * Rp * 2);
   float* part = (float*)w;
   const long part_floats = 64L * (I > Dl ? I : Dl);   // the colsum partials of ptk_projector_workspace_bytes
+  // the weight grads on the TN GEMM (gemm_tn.hip), which reads the token-major operands where they lie: K = Rp,
+  // the rows R .. Rp - 1 past the operands' buffer ranges read as zero.  PTK_WGRAD_TN=0 (or operands the TN path
+  // does not take): transposed copies for the NT GEMMs
+  auto tn_wgrad = [&](const void* A, int lda, const void* B, int ldb, float* C, int M, int N) -> int {
+    if (!wgrad_tn_enabled()) return 1;
+    GemmArgs g;
+    g.A = (const bf16_t*)A; g.B = (const bf16_t*)B; g.C = C; g.M = M; g.N = N; g.K = Rp;
+    g.lda = lda; g.ldb = ldb; g.ldc = N;
+    if (!tn_supported(g, OUT_F32, 1)) return 1;
+    return gemm_tn(g, OUT_F32, 1, nullptr, st, R) ? -1 : 0;
+  };
   if (stage == 0) {
     // db2 = colsum(dy); dW2 = dy^T . h  (contraction over tokens)
     if (launch_colsum_bf16((const bf16_t*)dy, R, Dl, db2, part, part_floats, st)) return -1;
+    const int tn = tn_wgrad(dy, Dl, h, I, dw2, Dl, I);
+    if (tn <= 0) return tn;
     if (launch_transpose((const bf16_t*)dy, Dl, 0, 0, 1, dyT, Rp, 0, 0, 1, R, Dl, Rp, st)) return -1;
     if (launch_transpose((const bf16_t*)h, I, 0, 0, 1, T, Rp, 0, 0, 1, R, I, Rp, st)) return -1;
     GemmArgs g;
@@ -241,6 +254,8 @@ int projector_bwd_stage(const ptk_projector* p, int rows, const void* x, const v
   if (launch_gemm(g2, ACT_GELU_ERF_BWD, OUT_BF16, 1, st)) return -1;
   // db1 = colsum(dA); dW1 = dA^T . x
   if (launch_colsum_bf16(dA, R, I, db1, part, part_floats, st)) return -1;
+  const int tn = tn_wgrad(dA, I, x, Dv, dw1, I, Dv);
+  if (tn <= 0) return tn;
   if (launch_transpose(dA, I, 0, 0, 1, T, Rp, 0, 0, 1, R, I, Rp, st)) return -1;
   if (launch_transpose((const bf16_t*)x, Dv, 0, 0, 1, xT, Rp, 0, 0, 1, R, Dv, Rp, st)) return -1;
   GemmArgs g3;

@@ -942,13 +942,13 @@ int gemm_p8_kslices(const GemmArgs& a, int slices, hipStream_t st) {
 }
 
 // the token-major weight-grad GEMM (gemm_tn.hip) with launch_gemm's census and live timers (class ACT_NONE)
-int gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st) {
+int gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st, long k_rows) {
   if (a.M <= 0 || a.N <= 0) return 0;
   hipEvent_t e0 = nullptr, e1 = nullptr;
   if (g_timing && (g_timing_mask & 1)) { e0 = next_event(ACT_NONE); e1 = next_event(ACT_NONE); }
   if (e0) (void)hipEventRecord(e0, st);
   count_path(GEMM_PATH_TN, ACT_NONE);
-  const int rc = launch_gemm_tn(a, out, slices, slab, st);
+  const int rc = launch_gemm_tn(a, out, slices, slab, st, k_rows);
   if (e1) (void)hipEventRecord(e1, st);
   return rc;
 }

@@ -383,12 +383,15 @@ P8Tail tn_tail_plan(const GemmArgs& a, void* slab) {
   return p8_tail_plan_ws(a, ntile, device_cus(), slab, 256, 64);
 }
 
-int launch_gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st) {
+int launch_gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st, long k_rows) {
   if (!tn_supported(a, out, slices)) return set_error("gemm_tn: unsupported operands (M %d N %d K %d slices %d)", a.M, a.N, a.K, slices);
+  if (k_rows < 0) k_rows = a.K;
+  if (k_rows > a.K || k_rows <= a.K - W4_KT) return set_error("gemm_tn: k_rows %ld outside (K - 64, K] (K %d)", k_rows, a.K);
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4) * slices;
   const P8Tail tl = slices == 1 && slab ? tn_tail_plan(a, slab) : P8Tail{};
   const long grid = tl.units ? device_cus() : std::min<long>(ntile, device_cus());
-  const uint32_t ab = (uint32_t)((double)a.K * a.lda * 2), bb = (uint32_t)((double)a.K * a.ldb * 2);
+  // num_records end at row k_rows: a K padded to a multiple of 64 reads its last rows as zero
+  const uint32_t ab = (uint32_t)((double)k_rows * a.lda * 2), bb = (uint32_t)((double)k_rows * a.ldb * 2);
   uint32_t cb = 0;
   if (out == OUT_BF16) {
     lean_epilogue_ok(a, ACT_NONE, OUT_BF16, cb);

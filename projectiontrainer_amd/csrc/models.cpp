@@ -311,6 +311,11 @@ static int wgrad_tn_mode() {
   static const int m = [] { const char* e = getenv("PTK_WGRAD_TN"); return e ? atoi(e) : 1; }();
   return m;
 }
+}  // namespace
+namespace ptk {
+int wgrad_tn_enabled() { return wgrad_tn_mode() != 0; }
+}  // namespace ptk
+namespace {
 int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* x, long ldx, RowMap xmap, int Nx,
                 int rows, bf16_t* TA, bf16_t* TB, void* grad, float* skpart, long sk_floats, hipStream_t st,
                 int tn = -1) {

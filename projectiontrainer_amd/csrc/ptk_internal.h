@@ -85,8 +85,11 @@ int launch_gemm_dual(const GemmArgs& a, int act, int out, hipStream_t st, bool s
 bool tn_supported(const GemmArgs& a, int out, int slices);
 int tn_slices(const GemmArgs& a, long part_floats);
 size_t tn_slab_bytes();
-int launch_gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st);
-int gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st);
+// k_rows (>= 0): the operands' real row count when K is padded up to a multiple of 64 (rows k_rows .. K - 1 are
+// past the buffer ranges and read as zero)
+int launch_gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st, long k_rows = -1);
+int gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st, long k_rows = -1);
+int wgrad_tn_enabled();   // PTK_WGRAD_TN != 0 (models.cpp)
 // stream-K tail of the persistent 8-wave kernel: scratch bytes (arrival counters, then partial slabs), the
 // workgroups its plan spreads a GEMM's tail over (0: no split), and the thread-local scratch a model-level
 // call lends to every GEMM it launches (the counters are zeroed when the scope opens)

@@ -612,6 +612,36 @@ def test_projector_module_autograd(gpu):
         assert F.cosine_similarity(g.flatten(), p.grad.flatten(), dim=0) > 0.999
 
 
+@pytest.mark.parametrize("rows", [2 * 575, 3 * 64])
+def test_projector_weight_grads_tn_vs_fp32(gpu, rows):
+    """The projector's weight grads at cfg2 widths (Stage1/projectors.py:16-20: 1024 -> 10240 -> 1152) on the TN GEMM
+    (token-major dY / h / dA / x read in place, K = rows padded to a multiple of 64 with the pad rows read as zero:
+    2 x 575 = 1150 tokens, and an exact multiple) against torch fp32 autograd of the same Sequential; the census
+    asserts the TN path ran.  bf16 operands (autocast semantics) bound the difference."""
+    from projectiontrainer_amd import _lib as L
+    from projectiontrainer_amd.projectors import MLPProjector
+    torch.manual_seed(0)
+    Dv, Dl = 1024, 1152
+    proj = MLPProjector(Dv, Dl)
+    ref = torch.nn.Sequential(torch.nn.Linear(Dv, 10 * Dv), torch.nn.GELU(), torch.nn.Linear(10 * Dv, Dl))
+    ref.load_state_dict(proj.model.state_dict())
+    proj.to(gpu)
+    ref = ref.to(gpu)
+    x = rnd(1, rows, Dv, dev=gpu, dtype=torch.float32, seed=95).requires_grad_(True)
+    w = rnd(1, rows, Dl, dev=gpu, dtype=torch.float32, seed=96)
+    L.gemm_path_counts(reset=True)
+    (proj(x) * w).sum().backward()
+    torch.cuda.synchronize()
+    paths = {p for p, _ in L.gemm_path_counts(reset=True)}
+    assert "tn" in paths, paths
+    (ref(x) * w).sum().backward()
+    for g, p in zip(proj.grads(), [ref[0].weight, ref[0].bias, ref[2].weight, ref[2].bias]):
+        g, r = g.float().reshape(p.shape), p.grad.float()
+        rel = float((g - r).norm() / r.norm())
+        assert rel < 1.5e-2, rel
+        assert F.cosine_similarity(g.flatten(), r.flatten(), dim=0) > 0.9999
+
+
 def test_projector_module_device_move(gpu):
     """Moving the module drops every device-resident cache (bf16 shadows, W1^T, backward workspace, grad scratch,
     tail scratch): autograd backward, a move to the CPU and back, and the same backward again give the same grads
