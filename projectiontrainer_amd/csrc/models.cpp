@@ -303,8 +303,8 @@ int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStr
 }
 
 // dW (+)= dY^T X over K token rows into the bf16 .grad (bf16(grad + bf16(acc)), autograd's accumulation).  Both
-// operands are token-major.  Ungathered rows (identity maps, rows % 64 == 0): the persistent TN GEMM reads them
-// where they lie, K slices as fp32 partials summed in slice order (gemm_tn.hip).  Otherwise (the loss rows of the
+// operands are token-major.  Ungathered rows (identity maps): the persistent TN GEMM reads them where they lie
+// (a ragged row count padded to 64 with zero rows), K slices as fp32 partials summed in slice order (gemm_tn.hip).  Otherwise (the loss rows of the
 // last layer, ragged row counts, PTK_WGRAD_TN=0) each is transposed to a K-contiguous feature-major copy (rows
 // gathered through the map, zero-padded to a multiple of 64) for the NT GEMMs.
 static int wgrad_tn_mode() {
@@ -322,16 +322,19 @@ int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* 
   if (!grad) return 0;
   if (tn < 0) tn = wgrad_tn_mode();
   if (tn && ymap.g == 0 && ymap.off == 0 && xmap.g == 0 && xmap.off == 0 && rows > 0) {
-    GemmArgs g = gemm(dy, lddy, x, ldx, grad, Nx, Ny, Nx, rows);   // A = dY [rows][Ny], B = X [rows][Nx]
+    // A = dY [rows][Ny], B = X [rows][Nx]; K = rows padded to a multiple of 64, the pad rows past the operands'
+    // buffer ranges read as zero
+    const int Kp = (rows + 63) / 64 * 64;
+    GemmArgs g = gemm(dy, lddy, x, ldx, grad, Nx, Ny, Nx, Kp);
     g.bf16_linear = 1;
     g.resid16 = (const bf16_t*)grad;
     g.ld_resid16 = Nx;
     // with a slab for the stream-K tail (the fp32 scratch): one slice, the tail round's K-tiles spread over the
     // CUs; otherwise equal K slices summed by splitk_reduce
     if (skpart && (size_t)sk_floats * sizeof(float) >= tn_slab_bytes() && tn_supported(g, OUT_BF16, 1))
-      return gemm_tn(g, OUT_BF16, 1, skpart, st);
+      return gemm_tn(g, OUT_BF16, 1, skpart, st, rows);
     const int S = skpart ? tn_slices(g, sk_floats) : (tn_supported(g, OUT_BF16, 1) ? 1 : 0);
-    if (S == 1) return gemm_tn(g, OUT_BF16, 1, nullptr, st);
+    if (S == 1) return gemm_tn(g, OUT_BF16, 1, nullptr, st, rows);
     if (S > 1) {
       GemmArgs b = g;
       b.C = skpart;
@@ -339,7 +342,7 @@ int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* 
       b.bf16_linear = 0;
       b.resid16 = nullptr;
       b.ld_resid16 = 0;
-      CK(gemm_tn(b, OUT_F32, S, nullptr, st));
+      CK(gemm_tn(b, OUT_F32, S, nullptr, st, rows));
       return launch_splitk_reduce(skpart, S, Ny, Nx, grad, Nx, 1, (const bf16_t*)grad, Nx, st);
     }
   }

@@ -728,7 +728,9 @@ WG_CASES = [(1536, 1152, 14336, 0, "slab"), (1152, 1024, 14336, 0, "slab"), (115
             (13824, 1152, 14336, 0, "slab"), (1536, 1152, 14336, 0, "slices"), (1152, 6912, 4096, 0, "slices"),
             (13824, 1152, 2048, 0, "none"), (1000, 320, 640, 8, "slab"), (1000, 320, 640, 8, "slices"),
             (256, 128, 128, 0, "none"), (2304, 1152, 1024, 24, "slices"),
-            (262144, 1152, 4096, 0, "slab")]   # the tied lm_head's dW: a 2 GiB d(logits) operand (32-bit offsets)
+            (262144, 1152, 4096, 0, "slab"),   # the tied lm_head's dW: a 2 GiB d(logits) operand (32-bit offsets)
+            # ragged token counts: K padded to a multiple of 64, the pad rows read as zero
+            (1152, 1024, 1150, 0, "none"), (1000, 320, 650, 8, "slices"), (1536, 1152, 7150, 0, "slab")]
 
 
 @pytest.mark.parametrize("Ny,Nx,rows,ld_extra,split", WG_CASES)
@@ -766,9 +768,9 @@ def test_weight_grad_tn_vs_fp32(gpu, Ny, Nx, rows, ld_extra, split):
 
 def test_weight_grad_tn_gated_shapes(gpu):
     """Shapes the TN path does not take run the transpose path in auto mode and fail loudly in TN-only mode:
-    ragged rows (not a multiple of 64), gathered rows, N % 64 != 0."""
+    fewer than 65 token rows (K padded to 64 is below the kernel's two K-tiles), gathered rows, N % 64 != 0."""
     Kn, L = _k()
-    dy, x = rnd(200, 256, dev=gpu, seed=104), rnd(200, 128, dev=gpu, seed=105)
+    dy, x = rnd(40, 256, dev=gpu, seed=104), rnd(40, 128, dev=gpu, seed=105)
     g0 = torch.zeros(256, 128, dtype=torch.bfloat16, device=gpu)
     L.gemm_path_counts(reset=True)
     g = Kn.weight_grad(dy, x, g0.clone(), mode=0)
