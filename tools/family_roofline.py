@@ -27,31 +27,37 @@ def roles(cfg):
     M_v, M_g = B * N, B * S
     attn_g = sum(2 * 2 * attention_pairs(S, t.sliding_window if t.is_sliding(i) else None) * t.head_dim *
                  t.num_attention_heads * B for i in range(L))
-    # family -> list of (role, launches per step, FLOPs per launch)
+    Mp, Ip = B * cfg.num_vision_tokens, cfg.expansion_factor * D   # projector rows (575 per image), hidden
+    # family -> list of (role, launches per step, FLOPs per launch); the r05 dispatch (tests/test_stage1_gpu.py
+    # census): plain bf16 projections on the lean 8-wave kernel with 224- / 192-row tiles (p8_tile_height),
+    # SigLIP fc2 with the stream-K tail + fixup, projector weight grads on the TN kernel, lm_head dX as K slices
     return {
-        # r05: the plain bf16 projections run the lean epilogue (gemm_p8_kernel<0, 0, false, true>), Gemma q|k|v
-        # moved here from the 128x128 kernel
-        "gemm_p8_kernel<0, 0, false, true>": [
+        "gemm_p8_kernel<0, 0, false, true, 224>": [
             ("SigLIP q|k|v", Lv, 2 * M_v * D * 3 * D),
-            ("Gemma q|k|v", L, 2 * M_g * H * (q + 2 * kv)),
             ("Gemma o", L, 2 * M_g * q * H),
-            ("Gemma d(gate|up) dX", L - 1, 2 * M_g * 2 * I * H),
-            ("Gemma d(q|k|v) dX", L, 2 * M_g * (q + 2 * kv) * H)],
+            ("Gemma d(q|k|v) dX", L, 2 * M_g * (q + 2 * kv) * H),
+            ("Gemma down", L - 1, 2 * M_g * I * H),
+            ("Gemma d(gate|up) dX", L - 1, 2 * M_g * 2 * I * H)],
+        "gemm_p8_kernel<0, 0, false, true, 192>": [
+            ("Gemma q|k|v", L, 2 * M_g * H * (q + 2 * kv)),
+            ("Gemma dO", L, 2 * M_g * H * q),
+            ("SigLIP o", Lv, 2 * M_v * D * D)],
         "gemm_w4_kernel<3, 0,": [("Gemma gate|up + GEGLU", L - 1, 2 * M_g * 2 * I * H)],
         "gemm_w4_kernel<5, 0,": [("Gemma dh + GEGLU backward", L - 1, 2 * M_g * I * H)],
-        "gemm_w4_kernel<0, 0,": [("Gemma down", L - 1, 2 * M_g * I * H)],
-        "gemm_nt_kernel<0, 0>": [
-            ("SigLIP o", Lv, 2 * M_v * D * D),
-            ("SigLIP fc2", Lv, 2 * M_v * Iv * D),
-            ("Gemma dO", L, 2 * M_g * H * q)],
         "gemm_p8_kernel<1, 0": [("SigLIP fc1 + GELU-tanh", Lv, 2 * M_v * D * Iv)],
+        "gemm_p8_kernel<0, 0, true, true|p8_fixup_kernel<0, 0>": [("SigLIP fc2 (stream-K tail + fixup)", Lv,
+                                                                   2 * M_v * Iv * D)],
+        "gemm_p8_kernel<2, 0": [("projector fc1 + GELU-erf", 1, 2 * Mp * D * Ip)],
+        "gemm_p8_kernel<0, 2, true": [("projector fc2", 1, 2 * Mp * Ip * H)],
+        "gemm_p8_kernel<4, 0": [("projector dA + GELU-erf backward", 1, 2 * Mp * H * Ip)],
+        "gemm_tn_kernel<1, false>": [("projector dW1, dW2 (TN)", 2, 2 * Mp * D * Ip)],
         "attn_fwd64_kernel": [("SigLIP attention", Lv, 2 * 2 * N * N * D * B)],
         "attn_fwd256w_kernel": [("Gemma attention forward", L, attn_g / L)],
         # the backward's four algorithmic products (dP, dV, dQ, dK) over both kernels' time (dQ recomputes S, dP)
         "attn_bwd_dkv256b_kernel|attn_bwd_dq256w_kernel": [("Gemma attention backward (dK / dV + dQ)", 2 * L,
                                                             attn_g / L)],
-        "gemm_big_kernel<0, 0>": [("lm_head forward", 1, 2 * B * T * H * t.vocab_size)],
-        "gemm_nt_kernel<0, 1>": [("lm_head dX (split-K)", 1, 2 * B * T * H * t.vocab_size)],
+        "gemm_big_kernel<0, 0>": [("lm_head forward (+ softmax statistics)", 1, 2 * B * T * H * t.vocab_size)],
+        "gemm_p8_kernel<0, 1, false, false, 256>": [("lm_head dX (16 K slices)", 1, 2 * B * T * H * t.vocab_size)],
     }
 
 
