@@ -1,7 +1,7 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 300 python -u -m pytest tests -m gpu -x -q --timeout 200 --timeout-method thread -k "stage2_vs_reference or norm_wgrad or rms" > gpurun_out/r5n_tests.log 2>&1 || { echo tests failed; tail -20 gpurun_out/r5n_tests.log; exit 1; }
-tail -1 gpurun_out/r5n_tests.log
-CONFIG=cfg4 ROUNDS=2 STEPS=2 timeout -k 10 1000 bash tools/ab.sh new ablibs/libptk_wg1.so > gpurun_out/r5n_ab.log 2>&1 || { echo ab failed; tail -5 gpurun_out/r5n_ab.log; exit 1; }
-cat gpurun_out/r5n_ab.log
+R=$(pwd)
+(cd /tmp && export TMPDIR=/tmp && timeout -s KILL 300 rocprofv3 --kernel-trace --pmc SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAVES GRBM_GUI_ACTIVE --output-format csv -d $R/gpurun_out/r05_sq -o run -- python3 $R/bench.py --steps 2 --warmup 1 --no-cpu-baseline) > gpurun_out/r05_sq.log 2>&1 || { echo pmc failed; tail -5 gpurun_out/r05_sq.log; exit 1; }
+python3 tools/pmc_summary.py gpurun_out/r05_sq/run_counter_collection.csv --top 16 > gpurun_out/r05_sq_summary.md 2>&1 || { echo summary failed; tail -5 gpurun_out/r05_sq_summary.md; exit 1; }
+cat gpurun_out/r05_sq_summary.md
