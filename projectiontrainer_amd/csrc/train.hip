@@ -80,7 +80,12 @@ int launch_transpose_rows(const bf16_t* in, long ld_in, RowMap map, int rows, in
 // partial[blk][c] = sum over the block's rows of dy[r,c] * x[xmap(r),c] * rstd[r]; dy optionally rounded to
 // bf16 first (the post-norms' output grads arrive as bf16 in the reference's autocast graph).
 // 256 threads own float4 column groups c = 4 t + 1024 j; WG_ROWS rows per block.
-constexpr int WG_ROWS = 32;
+#ifndef PTK_WG_ROWS
+#define PTK_WG_ROWS 8
+#endif
+constexpr int WG_ROWS = PTK_WG_ROWS;   // rows per block of the partial sums: 8 gives 1 792 blocks at cfg4's 14 336
+                                       // rows (32: 448 blocks, 7 waves per CU, ~2.6 TB/s); cfg4 161.3 -> 163.4 img/s
+                                       // (profiles/r05_wgrad_rows_ab.txt)
 PTK_DEV float4 ldv4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 PTK_DEV float4 ldv4(const bf16_t* p) {
   u16x4_t u = *reinterpret_cast<const u16x4_t*>(p);
@@ -205,7 +210,10 @@ int launch_rms_wgrad_bdy(const float* x, long ldx, RowMap xmap, const float* rst
 // dQ is in the attention layout [B, Hkv, S, G, D], dK in [B, Hkv, S, D]; qkv rows are token-major.
 // D = 256: one wave per token (4 lanes-elements each: lane l owns d = 4l..4l+3, its RoPE partner d +- 128 is
 // lane l +- 32, loaded directly), QK_ROWS tokens per block; per-block partials [blk][D], fixed-order finish.
-constexpr int QK_ROWS = 32;
+#ifndef PTK_QK_ROWS
+#define PTK_QK_ROWS 8
+#endif
+constexpr int QK_ROWS = PTK_QK_ROWS;   // tokens per block of the partial sums (8: with WG_ROWS 8, +0.25 % on cfg4)
 PTK_DEV float4 ldb4(const bf16_t* p) {
   u16x4_t u = *reinterpret_cast<const u16x4_t*>(p);
   return make_float4(bf2f(u[0]), bf2f(u[1]), bf2f(u[2]), bf2f(u[3]));

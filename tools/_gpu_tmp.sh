@@ -1,9 +1,5 @@
 set -o pipefail
 mkdir -p gpurun_out
 export PYTHONUNBUFFERED=1
-timeout -k 10 400 python -u bench.py --config cfg5 --steps 5 --warmup 2 --no-cpu-baseline > gpurun_out/r05_final_cfg5.log 2>&1 || { echo cfg5 failed; tail -5 gpurun_out/r05_final_cfg5.log; exit 1; }
-tail -1 gpurun_out/r05_final_cfg5.log | cut -c1-200
-for r in 1 2 3; do
-timeout -k 10 300 python -u bench.py --steps 20 --warmup 5 --no-cpu-baseline > gpurun_out/r05_rep_$r.log 2>&1 || { echo bench failed; tail -5 gpurun_out/r05_rep_$r.log; exit 1; }
-tail -1 gpurun_out/r05_rep_$r.log | cut -c1-120
-done
+timeout -k 10 900 python -u -m pytest tests -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r5wg_tests.log 2>&1 || { echo tests failed; tail -20 gpurun_out/r5wg_tests.log; exit 1; }
+tail -1 gpurun_out/r5wg_tests.log
