@@ -81,8 +81,12 @@ int launch_transpose_rows(const bf16_t* in, long ld_in, RowMap map, int rows, in
 // bf16 first (the post-norms' output grads arrive as bf16 in the reference's autocast graph).
 // 256 threads own float4 column groups c = 4 t + 1024 j; WG_ROWS rows per block.
 #ifndef PTK_WG_ROWS
-#define PTK_WG_ROWS 8
+#define PTK_WG_ROWS 32
 #endif
+#ifndef PTK_WG_GROUPS
+#define PTK_WG_GROUPS 4
+#endif
+constexpr int WG_GROUPS = PTK_WG_GROUPS;   // row groups (256 threads each) per block of the partial sums
 constexpr int WG_ROWS = PTK_WG_ROWS;   // rows per block of the partial sums: 8 gives 1 792 blocks at cfg4's 14 336
                                        // rows (32: 448 blocks, 7 waves per CU, ~2.6 TB/s); cfg4 161.3 -> 163.4 img/s
                                        // (profiles/r05_wgrad_rows_ab.txt)
@@ -93,21 +97,27 @@ PTK_DEV float4 ldv4(const bf16_t* p) {
 }
 
 template <typename TX, typename TD, int NJ>
-__global__ void __launch_bounds__(256) rms_wgrad_partial_kernel(const TX* __restrict__ x, long ldx, RowMap xmap,
-                                                                const float* __restrict__ rstd,
-                                                                const TD* __restrict__ dy, long lddy, int dy_round,
-                                                                int rows, int cols, float* __restrict__ partial) {
+__global__ void __launch_bounds__(256 * WG_GROUPS) rms_wgrad_partial_kernel(const TX* __restrict__ x, long ldx,
+                                                                            RowMap xmap, const float* __restrict__ rstd,
+                                                                            const TD* __restrict__ dy, long lddy,
+                                                                            int dy_round, int rows, int cols,
+                                                                            float* __restrict__ partial) {
+  // WG_GROUPS row groups of 256 threads: group g sums rows r0 + g, r0 + g + WG_GROUPS, ... of the block's WG_ROWS
+  // (more waves per CU on the memory stream without more partial rows), then the groups' sums are added in group
+  // order through LDS
+  __shared__ float4 red[WG_GROUPS > 1 ? WG_GROUPS - 1 : 1][NJ][256];
+  const int t = threadIdx.x & 255, grp = threadIdx.x >> 8;
   float4 acc[NJ];
 #pragma unroll
   for (int j = 0; j < NJ; ++j) acc[j] = make_float4(0.f, 0.f, 0.f, 0.f);
   const int r0 = blockIdx.x * WG_ROWS, r1 = min(rows, r0 + WG_ROWS);
-  for (int r = r0; r < r1; ++r) {
+  for (int r = r0 + grp; r < r1; r += WG_GROUPS) {
     const float rs = rstd[r];
     const TX* xr = x + map_row(xmap, r) * ldx;
     const TD* dr = dy + (long)r * lddy;
 #pragma unroll
     for (int j = 0; j < NJ; ++j) {
-      const int c = threadIdx.x * 4 + 1024 * j;
+      const int c = t * 4 + 1024 * j;
       if (c < cols) {
         float4 xv = ldv4(xr + c), dv = ldv4(dr + c);
         if (dy_round) dv = make_float4(bfround(dv.x), bfround(dv.y), bfround(dv.z), bfround(dv.w));
@@ -118,9 +128,23 @@ __global__ void __launch_bounds__(256) rms_wgrad_partial_kernel(const TX* __rest
       }
     }
   }
+  if constexpr (WG_GROUPS > 1) {
+    if (grp > 0)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) red[grp - 1][j][t] = acc[j];
+    __syncthreads();
+    if (grp > 0) return;
+#pragma unroll
+    for (int g = 0; g < WG_GROUPS - 1; ++g)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const float4 v = red[g][j][t];
+        acc[j].x += v.x; acc[j].y += v.y; acc[j].z += v.z; acc[j].w += v.w;
+      }
+  }
 #pragma unroll
   for (int j = 0; j < NJ; ++j) {
-    const int c = threadIdx.x * 4 + 1024 * j;
+    const int c = t * 4 + 1024 * j;
     if (c < cols) *reinterpret_cast<float4*>(partial + (long)blockIdx.x * cols + c) = acc[j];
   }
 }
@@ -175,10 +199,10 @@ static int rms_wgrad_t(const TX* x, long ldx, RowMap xmap, const float* rstd, co
   const int nj = (cols + 1023) / 1024;
   const dim3 g((unsigned)nblk);
   switch (nj) {
-    case 1: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 1>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
-    case 2: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 2>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
-    case 3: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 3>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
-    default: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 4>), g, dim3(256), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
+    case 1: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 1>), g, dim3(256 * WG_GROUPS), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
+    case 2: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 2>), g, dim3(256 * WG_GROUPS), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
+    case 3: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 3>), g, dim3(256 * WG_GROUPS), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
+    default: hipLaunchKernelGGL((rms_wgrad_partial_kernel<TX, TD, 4>), g, dim3(256 * WG_GROUPS), 0, st, x, ldx, xmap, rstd, dy, lddy, dy_round, rows, cols, partial); break;
   }
   wgrad_finish(partial, nblk, cols, grad, partial + (long)nblk * cols, st);
   RET_OK("rms_wgrad");
