@@ -79,17 +79,18 @@ int launch_transpose_rows(const bf16_t* in, long ld_in, RowMap map, int rows, in
 // ---------------------------------------------------------------- RMSNorm weight grads
 // partial[blk][c] = sum over the block's rows of dy[r,c] * x[xmap(r),c] * rstd[r]; dy optionally rounded to
 // bf16 first (the post-norms' output grads arrive as bf16 in the reference's autocast graph).
-// 256 threads own float4 column groups c = 4 t + 1024 j; WG_ROWS rows per block.
+// 256 threads own float4 column groups c = 4 t + 1024 j; WG_ROWS rows per block, split over WG_GROUPS row groups.
+// One group of 256 threads per 32-row block (448 blocks at cfg4's 14 336 rows, 7 waves per CU) streamed at
+// ~2.6 TB/s; 8-row blocks (4x the waves) took cfg4 161.3 -> 163.4 img/s, and 4 row groups per 32-row block (the
+// same waves, a quarter of the partial rows, one colsum level less) +0.4 % more (profiles/r05_wgrad_rows_ab.txt)
 #ifndef PTK_WG_ROWS
 #define PTK_WG_ROWS 32
 #endif
 #ifndef PTK_WG_GROUPS
 #define PTK_WG_GROUPS 4
 #endif
-constexpr int WG_GROUPS = PTK_WG_GROUPS;   // row groups (256 threads each) per block of the partial sums
-constexpr int WG_ROWS = PTK_WG_ROWS;   // rows per block of the partial sums: 8 gives 1 792 blocks at cfg4's 14 336
-                                       // rows (32: 448 blocks, 7 waves per CU, ~2.6 TB/s); cfg4 161.3 -> 163.4 img/s
-                                       // (profiles/r05_wgrad_rows_ab.txt)
+constexpr int WG_GROUPS = PTK_WG_GROUPS;
+constexpr int WG_ROWS = PTK_WG_ROWS;
 PTK_DEV float4 ldv4(const float* p) { return *reinterpret_cast<const float4*>(p); }
 PTK_DEV float4 ldv4(const bf16_t* p) {
   u16x4_t u = *reinterpret_cast<const u16x4_t*>(p);
