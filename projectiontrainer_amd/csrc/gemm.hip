@@ -850,6 +850,7 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   if (short_ok && g_force_tiles == 0 && tm_env && a.M >= 4096) tm = p8_tile_height(a, act, out);
   else if (short_ok && g_force_tiles == 512) tm = 224;
   else if (short_ok && g_force_tiles == 1024) tm = 192;
+  else if (short_ok && g_force_tiles == 4096) tm = 160;
   if (batch == 1 && (g_force_tiles == 32 || p8_auto || sk || tm != 256) && p8_supported(a, act, out)) {
     hipEvent_t e0 = nullptr, e1 = nullptr;
     if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }

@@ -481,7 +481,7 @@ PTK_DEV void w4_rows_lean(f32x4_t (&a)[NJ], const LeanEpi& e, const float (&bias
     __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v_t, d2), e.rc, v1 + 8u * e.ldc_bytes, 0, 0);
   }
 }
-template <int ACT, int NJ, int RB = 8>   // RB: 16-row blocks per wave (7: the 224-row tiles)
+template <int ACT, int NJ, int RB = 8>   // RB: 16-row blocks per wave (7, 6, 5: the 224- / 192- / 160-row tiles)
 PTK_DEV void w4_epilogue_lean(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, long col0, int lane,
                               uint32_t c_bytes) {
   if (col0 >= p.N) return;
@@ -516,7 +516,7 @@ PTK_DEV void w4_epilogue_lean(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row
   w4_rows_lean<ACT, 2, NJ>(acc[2], e, bias);
   w4_rows_lean<ACT, 3, NJ>(acc[3], e, bias);
   w4_rows_lean<ACT, 4, NJ>(acc[4], e, bias);
-  w4_rows_lean<ACT, 5, NJ>(acc[5], e, bias);
+  if constexpr (RB > 5) w4_rows_lean<ACT, 5, NJ>(acc[5], e, bias);
   if constexpr (RB > 6) w4_rows_lean<ACT, 6, NJ>(acc[6], e, bias);
   if constexpr (RB > 7) w4_rows_lean<ACT, 7, NJ>(acc[7], e, bias);
 }
@@ -640,7 +640,7 @@ PTK_DEV void w4_epilogue(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row0, lo
   w4_rows<ACT, OUT, 2, NJ>(p, acc[2], row0, col0, lane, sink);
   w4_rows<ACT, OUT, 3, NJ>(p, acc[3], row0, col0, lane, sink);
   w4_rows<ACT, OUT, 4, NJ>(p, acc[4], row0, col0, lane, sink);
-  w4_rows<ACT, OUT, 5, NJ>(p, acc[5], row0, col0, lane, sink);
+  if constexpr (RB > 5) w4_rows<ACT, OUT, 5, NJ>(p, acc[5], row0, col0, lane, sink);
   if constexpr (RB > 6) w4_rows<ACT, OUT, 6, NJ>(p, acc[6], row0, col0, lane, sink);
   if constexpr (RB > 7) w4_rows<ACT, OUT, 7, NJ>(p, acc[7], row0, col0, lane, sink);
 }

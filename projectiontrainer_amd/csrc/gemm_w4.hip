@@ -443,7 +443,7 @@ constexpr int P8_PIECES = 4;   // LDS-DMA pieces per wave per k-step
 #define P8_DSREAD(DST, ADDR, OFF) W4_DSREAD(DST, ADDR, OFF)
 #define P8_LGKM(N) asm volatile("s_waitcnt lgkmcnt(" #N ")" ::: "memory")
 #endif
-// TM: output tile height, 256, 224 or 192.  Shorter tiles (TM / 32 row blocks of 16 per wave, the A image's
+// TM: output tile height, 256, 224, 192 or 160.  Shorter tiles (TM / 32 row blocks of 16 per wave, the A image's
 // last rows unused, waves 0 .. TM / 32 - 1 staging A, the others only B) fill the rounds of the persistent grid
 // better where 256-row tiles leave a thin last round: Gemma3's N 1152 / 1024 projections at M 22 528 (440 -> 505
 // tiles of 7/8 the work on 2 rounds), N 1536 (3 rounds either way, 7/8 the work), SigLIP's q|k|v at M 18 432,
@@ -451,7 +451,7 @@ constexpr int P8_PIECES = 4;   // LDS-DMA pieces per wave per k-step
 template <int ACT, int OUT, bool SK, bool LEAN = false, int TM = 256>
 __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_bytes, uint32_t b_bytes, P8Tail tl,
                                                          uint32_t c_bytes) {
-  static_assert(TM == 256 || ((TM == 224 || TM == 192) && !SK), "shorter tiles: whole tiles only");
+  static_assert(TM == 256 || ((TM == 224 || TM == 192 || TM == 160) && !SK), "shorter tiles: whole tiles only");
   constexpr int RB = TM / 32;   // 16-row blocks per wave
   __shared__ __attribute__((aligned(16))) char smem[W4_NSLOT * W4_SLOT];   // 160 KiB: the k-step ring
   const int lane = threadIdx.x & 63;
@@ -604,11 +604,17 @@ __global__ void __launch_bounds__(512, 1) gemm_p8_kernel(GemmArgs p, uint32_t a_
         else if (q < 3) P8_LGKM(7);
         else if (q == 3) P8_LGKM(8);
         else P8_LGKM(9);
-      } else {
+      } else if constexpr (RB == 6) {
         if (q == 0) P8_LGKM(4);
         else if (q < 3) P8_LGKM(6);
         else if (q == 3) P8_LGKM(7);
         else P8_LGKM(8);
+      } else {
+        static_assert(RB == 5, "tile heights 256, 224, 192, 160");
+        if (q == 0) P8_LGKM(3);
+        else if (q < 3) P8_LGKM(5);
+        else if (q == 3) P8_LGKM(6);
+        else P8_LGKM(7);
       }
       asm volatile("" : "+v"(fa[q]));
       if (q == 0) asm volatile("" : "+v"(FB[0]), "+v"(FB[1]), "+v"(FB[2]), "+v"(FB[3]));
@@ -922,11 +928,12 @@ int launch_gemm_p8_kslices(const GemmArgs& a, int slices, hipStream_t st) {
   return hipGetLastError() == hipSuccess ? 0 : set_error("gemm_p8_kslices launch failed");
 }
 
-// the tile height of a plain / GELU-tanh 8-wave GEMM without a stream-K tail: the TM of {256, 224, 192} with the
+// the tile height of a plain / GELU-tanh 8-wave GEMM without a stream-K tail: the TM of {256, 224, 192, 160} with the
 // lowest tile rounds x (TM + 128), when it undercuts 256 by >= 5 % (else 256).  The 128 rows' worth per round is
 // what shorter tiles do not shed (prologue, epilogue, the DMA / LDS work per MFMA): fitted to tools/p8_probe.py
 // (r05, same box): Gemma o 59.6 / 54.1 / 68.5 us at 256 / 224 / 192 rows, dO 65.8 / 59.5 / 54.4, q|k|v 90.7 / 88.0
-// / 81.4, down 340 / 312 / 407, SigLIP fc1 149 / 157 / 153 (5 rounds of 256 vs 6 of 192: kept at 256)
+// / 81.4, down 340 / 312 / 407, SigLIP fc1 149 / 157 / 153 (5 rounds of 256 vs 6 of 192: kept at 256); 160 rows:
+// SigLIP o 52.1 -> 46.4 us (2 rounds of 160 vs 2 of 192), Gemma dO stays at 192 (57.6 vs 70.9), profiles/r05_tm160_ab.txt
 int p8_tile_height(const GemmArgs& a, int act, int out) {
   num_cu();
   if (!(act == ACT_NONE || (act == ACT_GELU_TANH && out == OUT_BF16))) return 256;
@@ -935,7 +942,7 @@ int p8_tile_height(const GemmArgs& a, int act, int out) {
   const double c256 = cost(256);
   int best = 256;
   double bc = 0.95 * c256;
-  for (int tm : {224, 192}) {
+  for (int tm : {224, 192, 160}) {
     const double c = cost(tm);
     if (c < bc) { bc = c; best = tm; }
   }
@@ -976,10 +983,12 @@ int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk,
   if (tm != 256 && !sk) {
     if (!(act == ACT_NONE || (act == ACT_GELU_TANH && out == OUT_BF16)))
       return set_error("gemm_p8: %d-row tiles take the plain / GELU-tanh epilogues only", tm);
-    if (tm != 224 && tm != 192) return set_error("gemm_p8: tile height %d (256, 224, 192)", tm);
+    if (tm != 224 && tm != 192 && tm != 160) return set_error("gemm_p8: tile height %d (256, 224, 192, 160)", tm);
     const long ntm = (long)((a.M + tm - 1) / tm) * ((a.N + W4 - 1) / W4);
     const long grid = std::min<long>(ntm, g_num_cu);
-    return tm == 224 ? launch_p8_short<224>(a, act, out, st, grid) : launch_p8_short<192>(a, act, out, st, grid);
+    if (tm == 224) return launch_p8_short<224>(a, act, out, st, grid);
+    if (tm == 192) return launch_p8_short<192>(a, act, out, st, grid);
+    return launch_p8_short<160>(a, act, out, st, grid);
   }
   const long ntile = (long)((a.M + W4 - 1) / W4) * ((a.N + W4 - 1) / W4);
   // the stream-K plan only where launch_gemm's gates chose the tail split (its census counts it as p8sk)

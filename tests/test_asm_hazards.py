@@ -181,6 +181,7 @@ SPILL_BUDGET = {   # kernel symbol substring -> (sgpr_spill_count, vgpr_spill_co
     "gemm_tn_kernelILi0ELb1E": (3, 0, 0),
     "Lb0ELi224E": (1, 0, 0),   # the 8-wave kernel's 224- / 192-row tiles, general epilogues
     "Lb0ELi192E": (1, 0, 0),
+    "Lb0ELi160E": (3, 0, 0),   # (the general GELU-tanh epilogue of the 160-row tiles: 3)
     "gemm_p8_kernelILi1ELi0ELb0E": (4, 0, 0),
     # GELU-erf epilogues: 28 / 20 -> 31 / 28 with the K-slice (zslices) DMA offsets (r05); none in the K loop
     "gemm_p8_kernelILi2ELi0ELb0E": (31, 0, 0),

@@ -547,7 +547,7 @@ def test_gemm_p8_matches_w4(gpu, M, N, K):
 @pytest.mark.parametrize("M,N,K", [(22528, 1152, 1152), (1000, 1024, 1152), (4500, 1536, 640), (18432, 3072, 1024),
                                    (224, 256, 128), (230, 320, 192)])
 def test_gemm_p8_tm224_matches_p8(gpu, M, N, K):
-    """The 8-wave kernel's 224- and 192-row tiles (forced modes 512 / 1024: 7 / 6 row blocks per wave, the waves
+    """The 8-wave kernel's 224-, 192- and 160-row tiles (forced modes 512 / 1024 / 4096: 7 / 6 / 5 row blocks per wave, the waves
     past them staging only B, ragged M) against its 256-row tiles (mode 32): the same k-step order per output element, so the plain bf16 / fp32 /
     fp32-rounded, bias + residual, bias + bf16(linear) + bf16 residual in place, identity group row map and
     GELU-tanh epilogues are bit-identical; the census shows the p8 family ran."""
@@ -556,7 +556,7 @@ def test_gemm_p8_tm224_matches_p8(gpu, M, N, K):
     bias = rnd(N, dev=gpu, dtype=torch.float32, seed=25)
     res = rnd(M, N, dev=gpu, dtype=torch.float32, seed=26)
     outs = []
-    for md in (32, 512, 1024):
+    for md in (32, 512, 1024, 4096):
         L.lib().ptk_gemm_force_small_tiles(md)
         L.gemm_path_counts(reset=True)
         try:

@@ -71,7 +71,7 @@ def timed(A, B, kw, act, odt, C, reps):
 
 
 only = set(a for a in sys.argv[1:] if not a.startswith("-"))
-TAGS = {8: "w4", 32: "p8", 64: "dual", 128: "solo", 256: "p8w", 512: "p8t224", 1024: "p8t192", 2048: "w4r", 0: "auto"}
+TAGS = {8: "w4", 32: "p8", 64: "dual", 128: "solo", 256: "p8w", 512: "p8t224", 1024: "p8t192", 4096: "p8t160", 0: "auto"}
 modes = tuple(int(x) for x in os.environ.get("MODES", "8,32,64,0").split(","))
 for name, m, n, k, act, odt, *extra in SHAPES:
     if only and name not in only:
