@@ -929,10 +929,11 @@ int launch_gemm_p8_kslices(const GemmArgs& a, int slices, hipStream_t st) {
 }
 
 // the tile height of a plain / GELU-tanh 8-wave GEMM without a stream-K tail: the TM of {256, 224, 192, 160} with the
-// lowest tile rounds x (TM + 128), when it undercuts 256 by >= 5 % (else 256).  The 128 rows' worth per round is
-// what shorter tiles do not shed (prologue, epilogue, the DMA / LDS work per MFMA): fitted to tools/p8_probe.py
+// lowest tile rounds x (TM + 128), a tie with 256 rows going to the shorter tile (SigLIP fc1: 6 rounds of 192 = 5 of
+// 256; +0.15 % on the cfg2 step over three same-box alternations, profiles/r05_tm160_ab.txt; with a 5 % margin it
+// stayed at 256).  The 128 rows' worth per round is what shorter tiles do not shed (prologue, epilogue, the DMA / LDS work per MFMA): fitted to tools/p8_probe.py
 // (r05, same box): Gemma o 59.6 / 54.1 / 68.5 us at 256 / 224 / 192 rows, dO 65.8 / 59.5 / 54.4, q|k|v 90.7 / 88.0
-// / 81.4, down 340 / 312 / 407, SigLIP fc1 149 / 157 / 153 (5 rounds of 256 vs 6 of 192: kept at 256); 160 rows:
+// / 81.4, down 340 / 312 / 407, SigLIP fc1 149 / 157 / 153 (on another box 154.7 at 256, 148.1 at 192); 160 rows:
 // SigLIP o 52.1 -> 46.4 us (2 rounds of 160 vs 2 of 192), Gemma dO stays at 192 (57.6 vs 70.9), profiles/r05_tm160_ab.txt
 int p8_tile_height(const GemmArgs& a, int act, int out) {
   num_cu();
@@ -941,10 +942,10 @@ int p8_tile_height(const GemmArgs& a, int act, int out) {
   auto cost = [&](long tm) { return (double)((((a.M + tm - 1) / tm) * nbn + cu - 1) / cu) * (double)(tm + 128); };
   const double c256 = cost(256);
   int best = 256;
-  double bc = 0.95 * c256;
+  double bc = c256;
   for (int tm : {224, 192, 160}) {
     const double c = cost(tm);
-    if (c < bc) { bc = c; best = tm; }
+    if (c < bc || (c == bc && best == 256)) { bc = c; best = tm; }   // a tie with 256 rows goes to the shorter tile
   }
   return best;
 }
