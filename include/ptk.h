@@ -67,11 +67,11 @@ typedef struct {
   int64_t ld_rowadd;
   const float* resid;
   int64_t ld_resid;
-  void* aux;                 /* GELU_ERF: pre-activation out; GEGLU: gate out */
-  void* aux2;                /* GEGLU: up out */
+  void* aux;                 /* GELU_ERF: pre-activation out; GEGLU: a = bf16(gelu_tanh(gate)) out */
+  void* aux2;                /* GEGLU: b = bf16(gelu_tanh'(gate) * up) out (h = bf16(a * up) is C) */
   int64_t ld_aux;
-  const void* aux_in;        /* GELU_ERF_BWD: pre-activation; GEGLU_BWD: gate */
-  const void* aux_in2;       /* GEGLU_BWD: up */
+  const void* aux_in;        /* GELU_ERF_BWD: pre-activation; GEGLU_BWD: the forward's a (du = bf16(dh) * a) */
+  const void* aux_in2;       /* GEGLU_BWD: the forward's b (dg = bf16(dh) * b) */
   int64_t ld_aux_in;
   ptk_rowmap amap;
   ptk_rowmap cmap;
@@ -146,13 +146,15 @@ int ptk_gemm_timer_enable(int on);   /* 0 off, 1 every class, (1 << 8) | class m
 /* Tile-path test hook: 0 = shape heuristic, 1 = every GEMM on the 128x128 kernel,
    2 / 4 = every single-batch GEMM on the 256x256 / barrier-staggered 256x256 kernel,
    8 / 32 = every single-batch GEMM the persistent 4-wave / 8-wave (two waves per SIMD) 256x256 kernel
-   supports on it, 64 = the same on the persistent two-group 256x128 kernel (gemm_dual.hip). */
+   supports on it, 512 / 1024 / 4096 = every plain / GELU-tanh single-batch GEMM on the 8-wave kernel with
+   224- / 192- / 160-row tiles.  Any other mode is an error (64 / 128, the two-group 256x128 kernel, left the
+   library in round 6). */
 int ptk_gemm_force_small_tiles(int mode);
 int ptk_gemm_timer_read(int act_class, double* total_ms, int* count);
 /* Dispatch census (tests): counts[path * 8 + act] = GEMM launches since the last reset per kernel family
  * (0 128x128, 1 256x256 8-wave, 2 staggered 256x256 8-wave, 3 persistent 4-wave, 4 128x128 batched (split-K
  * slices, batch > 1), 5 persistent 8-wave with a stream-K tail round, 6 persistent 8-wave, 7 token-major weight
- * grad, 8 persistent two-group 256x128) and epilogue class (PTK_ACT_*): PTK_GEMM_NPATHS * 8 counts (ABI 5: 9 paths)
+ * grad, 8 unused since round 6) and epilogue class (PTK_ACT_*): PTK_GEMM_NPATHS * 8 counts (ABI 5: 9 paths)
  * class (PTK_ACT_*); counts may be
  * NULL; reset != 0 zeroes them afterwards.  Host-side counters, no GPU work. */
 #define PTK_GEMM_NPATHS 9

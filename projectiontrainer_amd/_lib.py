@@ -233,7 +233,7 @@ def ptr(t) -> int | None:
 
 
 # nt128b: batched / split-K slices of the 128x128 kernel; p8sk: the persistent 8-wave kernel with a stream-K tail
-GEMM_PATHS = ("nt128", "big", "big2", "w4", "nt128b", "p8sk", "p8", "tn", "dual")
+GEMM_PATHS = ("nt128", "big", "big2", "w4", "nt128b", "p8sk", "p8", "tn", "unused8")
 
 
 def gemm_path_counts(reset=False):

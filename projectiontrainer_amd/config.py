@@ -137,6 +137,11 @@ PRESETS = {
     # > the 512-key sliding window, the step's per-layer shapes at bs 2)
     "cfg2w": Stage1Config(vision=SiglipVisionConfig(num_hidden_layers=2),
                           text=Gemma3TextConfig(num_hidden_layers=6), batch_size=2, text_len=128),
+    # cfg5 WIDTHS at reduced depth (the same recipe at SigLIP-L/16-384 + Gemma3-4B widths: hidden 2560, GQA 8:4,
+    # linear RoPE x8 on the one global layer of 6, vocab 262 208; bs 1, T 256 as cfg5's caption length)
+    "cfg5w": Stage1Config(vision=SiglipVisionConfig(num_hidden_layers=2),
+                          text=GEMMA3_4B.__class__(**{**GEMMA3_4B.__dict__, "num_hidden_layers": 6}), batch_size=1,
+                          text_len=256),
     "tiny": Stage1Config(vision=SIGLIP_TINY, text=GEMMA3_TINY, batch_size=3, text_len=16),
     "tiny_gqa": Stage1Config(vision=SIGLIP_TINY, text=GEMMA3_TINY_GQA, batch_size=3, text_len=16),
 }

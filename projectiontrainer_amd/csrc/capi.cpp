@@ -118,8 +118,9 @@ int ptk_cast_f32_bf16(const float* in, void* out, int64_t n, void* stream) {
 }
 
 int ptk_gemm_force_small_tiles(int mode) {
-  if (mode != 0 && mode != 1 && mode != 2 && mode != 4 && mode != 8 && mode != 32 && mode != 64 && mode != 128 && mode != 512 && mode != 1024 && mode != 4096)
-    return set_error("gemm tile mode %d not in {0, 1, 2, 4, 8, 32, 64, 128}", mode);
+  if (mode != 0 && mode != 1 && mode != 2 && mode != 4 && mode != 8 && mode != 32 && mode != 512 && mode != 1024 &&
+      mode != 4096)
+    return set_error("gemm tile mode %d not in {0, 1, 2, 4, 8, 32, 512, 1024, 4096}", mode);
   force_small_tiles(mode);
   return 0;
 }

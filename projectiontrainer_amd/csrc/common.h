@@ -144,6 +144,28 @@ PTK_DEV f32x2_t bfround2(f32x2_t v) {
 }
 // two bf16 packed in a dword (element 0 in the low half) -> two f32
 PTK_DEV f32x2_t bf2x2(uint32_t w) { return f32x2_t{__uint_as_float(w << 16), __uint_as_float(w & 0xffff0000u)}; }
+PTK_DEV uint32_t pkbf2(f32x2_t v) { return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2_t)); }
+
+// GEGLU (TF gemma3 :131-133: h = gelu_tanh(gate) * up, bf16 ops) from the bf16-rounded g, u of two lanes, with the
+// two bf16 factors its backward needs saved instead of g and u:
+//   a = bf16(gelu(g))            (du = bf16(dh * a): the reference's MulBackward on the bf16 act output)
+//   b = bf16(gelu'(g) * u)       (dg = bf16(dh * b); the reference rounds bf16(dh * u) before gelu', so dg differs
+//                                 from it by which of the two products is rounded -- one bf16 rounding either way)
+//   h = bf16(a * u)
+// so the backward epilogue is two multiplies per element, no transcendental (the tanh-GELU value and derivative
+// come from the forward's one exp / rcp pair, gelu_tanh_fg2).  Packed dwords, element 0 in the low half.
+PTK_DEV void geglu_fwd2(f32x2_t g, f32x2_t u, uint32_t& a, uint32_t& b, uint32_t& h) {
+  f32x2_t f, df;
+  gelu_tanh_fg2(g, f, df);
+  a = pkbf2(f);
+  h = pkbf2(bf2x2(a) * u);
+  b = pkbf2(df * u);
+}
+// the backward from the saved factors: dg = dh * b, du = dh * a (dh already bf16-rounded; stored rounded)
+PTK_DEV void geglu_bwd2(f32x2_t d, uint32_t a, uint32_t b, f32x2_t& dg, f32x2_t& du) {
+  dg = d * bf2x2(b);
+  du = d * bf2x2(a);
+}
 PTK_DEV float gelu_tanh_grad(float x) {
   float f, df;
   gelu_tanh_fg(x, f, df);

@@ -2516,8 +2516,8 @@ int launch_attn_bwd(const FlashBwdArgs& a, int nz, hipStream_t st, FlashBwdArgs*
       const bool dq_new = (a.nkeys + 31) / 32 <= FA_MAXT;
       if (dq_new) {
         // persistent grid (attn_fwd256w_kernel's: one workgroup per CU over the row blocks heaviest first, the next
-        // item's prologue beside this one's epilogue); PTK_ATTN_PERSIST=0: one workgroup per item
-        static const bool persist = [] { const char* e = getenv("PTK_ATTN_PERSIST"); return !(e && e[0] == '0'); }();
+        // item's prologue beside this one's epilogue); PTK_ATTN_PERSIST=0 (A/B builds): one workgroup per item
+        const bool persist = PTK_AB("PTK_ATTN_PERSIST", 1) != 0;
         const long nblk = (long)gq.x;
         const long g = persist ? std::min<long>(nblk, num_cus()) : nblk;
         hipLaunchKernelGGL(attn_bwd_dq256w_kernel, dim3((unsigned)g), dim3(256), 0, st, b, nz, (int)nblk);
@@ -2569,8 +2569,8 @@ int launch_attn_fwd(const FlashArgs& a, int nz, hipStream_t st) {
         hipLaunchKernelGGL((attn_fwd_kernel<256, 1>), grid, dim3(512), 0, st, a);
       else {
         // persistent grid (one workgroup per CU walking the row blocks heaviest first, the next item's prologue
-        // beside this one's epilogue); PTK_ATTN_PERSIST=0: one workgroup per item (A/B, bit-identical)
-        static const bool persist = [] { const char* e = getenv("PTK_ATTN_PERSIST"); return !(e && e[0] == '0'); }();
+        // beside this one's epilogue); PTK_ATTN_PERSIST=0 (A/B builds): one workgroup per item (A/B, bit-identical)
+        const bool persist = PTK_AB("PTK_ATTN_PERSIST", 1) != 0;
         const long g = persist ? std::min<long>(nblk, num_cus()) : nblk;
         hipLaunchKernelGGL(attn_fwd256w_kernel, dim3((unsigned)g), dim3(256), 0, st, a, nz, (int)nblk);
       }

@@ -804,8 +804,8 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // 90 -> 87 us, o 58 -> 56, SigLIP q|k|v 111 -> 109, fc1 157 -> 151), the projector fc1 with the GELU-erf
   // epilogue (674 -> 583 us) and its backward (dA, 858 -> 703 us) and the long-K d(gate|up) dX (K 13 824, N <= 2048: 700 -> 672 us); w4 keeps the
   // GEGLU / GEGLU-backward epilogues and the K 6 912 down projection (697 / 486 / 330 us vs 723 / 500 / 342).
-  // PTK_P8=1 puts every w4 shape on it (A/B)
-  static const bool p8_env = [] { const char* e = getenv("PTK_P8"); return e && e[0] == '1'; }();
+  // PTK_P8=1 (A/B builds, PTK_AB) puts every w4 shape on it
+  const bool p8_env = PTK_AB("PTK_P8", 0) == 1;
   const bool p8_auto = g_force_tiles == 0 && a.M >= 4096 && a.N <= 16384 &&
                        ((w4_auto && (p8_env || (act != ACT_GEGLU && act != ACT_GEGLU_BWD && a.K <= 2048))) ||
                         ((act == ACT_GELU_ERF || act == ACT_GELU_ERF_BWD) && out == OUT_BF16 && a.K <= 2048 &&
@@ -827,23 +827,13 @@ int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st) 
   // and down projection, the projector's fc2 and weight grads)
   const int sk = (g_force_tiles == 0 || g_force_tiles == 32) && batch == 1 && act == ACT_NONE && a.M >= 1024 &&
                  a.N >= 256 && a.N <= 16384 && p8_supported(a, act, out) ? p8_tail_split(a, act, out) : 0;
-  // two-group persistent kernel (gemm_dual.hip): PTK_DUAL=1 puts every persistent (w4 / p8) shape on it (A/B)
-  static const bool dual_env = [] { const char* e = getenv("PTK_DUAL"); return e && e[0] == '1'; }();
-  const bool dual_auto = g_force_tiles == 0 && !sk && dual_env && (p8_auto || w4_auto);
-  if (batch == 1 && (g_force_tiles == 64 || g_force_tiles == 128 || dual_auto) && dual_supported(a, act, out)) {
-    hipEvent_t e0 = nullptr, e1 = nullptr;
-    if (g_timing && ((g_timing_mask >> act) & 1)) { e0 = next_event(act); e1 = next_event(act); }
-    if (e0) (void)hipEventRecord(e0, st);
-    count_path(GEMM_PATH_DUAL, act);
-    const int rc = launch_gemm_dual(a, act, out, st, g_force_tiles == 128);
-    if (e1) (void)hipEventRecord(e1, st);
-    return rc;
-  }
+  // (the two-group persistent kernel on 256x128 tiles, gemm_dual.hip, measured 17-44 % slower than the 8-wave
+  // kernel in round 5, profiles/r05_dual_probe.txt, and was removed from the tree in round 6)
   // 224- / 192-row tiles on the 8-wave kernel where their rounds undercut the 256-row ones (p8_tile_height:
   // Gemma3's N 1152 / 1536 / 1024 projections at M 22 528, SigLIP's q|k|v, o and fc1 at M 18 432), ahead of the
   // 4-wave and 128x128 kernels; force modes 512 / 1024 put every plain / GELU-tanh single GEMM on 224 / 192 rows
-  // (tests).  PTK_TM224=0: 256-row tiles only (A/B)
-  static const bool tm_env = [] { const char* e = getenv("PTK_TM224"); return !(e && e[0] == '0'); }();
+  // (tests).  PTK_TM224=0 (A/B builds, PTK_AB): 256-row tiles only
+  const bool tm_env = PTK_AB("PTK_TM224", 1) != 0;
   const bool short_ok = batch == 1 && !sk && p8_supported(a, act, out) &&
                         (act == ACT_NONE || (act == ACT_GELU_TANH && out == OUT_BF16));
   int tm = 256;

@@ -162,48 +162,42 @@ PTK_DEV void epi_scalar(const GemmArgs& p, char* Cz, long r, long c, float v) {
 }
 
 // GEGLU: GEMM cols [32q, 32q+16) = gate[16q..], [32q+16, 32q+32) = up[16q..] (interleaved
-// weights); writes h = bf16(gelu_tanh(g)) * u and the bf16 g, u side outputs (TF gemma3 :131-133).
+// weights); writes h = bf16(bf16(gelu_tanh(g)) * u) and the backward's bf16 factors a = gelu(g) (aux) and
+// b = gelu'(g) * u (aux2) (common.h geglu_fwd2; TF gemma3 :131-133)
 PTK_DEV void geglu_vec4(const GemmArgs& p, char* Cz, long r, long hc, float4 g, float4 u) {
-  float4 h;
+  uint32_t a[2], b[2], h[2];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    el(g, e) = bfround(el(g, e));
-    el(u, e) = bfround(el(u, e));
-    el(h, e) = bfround(gelu_tanh(el(g, e))) * el(u, e);
-  }
-  if (p.aux) stbf4(p.aux + r * p.ld_aux + hc, g);
-  if (p.aux2) stbf4(p.aux2 + r * p.ld_aux + hc, u);
+  for (int e = 0; e < 4; e += 2)
+    geglu_fwd2(bfround2(f32x2_t{el(g, e), el(g, e + 1)}), bfround2(f32x2_t{el(u, e), el(u, e + 1)}), a[e / 2],
+               b[e / 2], h[e / 2]);
+  if (p.aux) *reinterpret_cast<uint2*>(p.aux + r * p.ld_aux + hc) = uint2{a[0], a[1]};
+  if (p.aux2) *reinterpret_cast<uint2*>(p.aux2 + r * p.ld_aux + hc) = uint2{b[0], b[1]};
   const long cr = map_row(p.cmap, r);
-  if (cr >= 0) stbf4(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + hc, h);
+  if (cr >= 0) *reinterpret_cast<uint2*>(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + hc) = uint2{h[0], h[1]};
 }
 
 PTK_DEV void geglu_vec8(const GemmArgs& p, char* Cz, long r, long hc, const float* g, const float* u) {
-  float gg[8], uu[8], h[8];
+  uint32_t a[4], b[4], h[4];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    gg[e] = bfround(g[e]);
-    uu[e] = bfround(u[e]);
-    h[e] = bfround(gelu_tanh(gg[e])) * uu[e];
-  }
-  if (p.aux) stbf8(p.aux + r * p.ld_aux + hc, gg);
-  if (p.aux2) stbf8(p.aux2 + r * p.ld_aux + hc, uu);
+  for (int e = 0; e < 8; e += 2)
+    geglu_fwd2(bfround2(f32x2_t{g[e], g[e + 1]}), bfround2(f32x2_t{u[e], u[e + 1]}), a[e / 2], b[e / 2], h[e / 2]);
+  if (p.aux) *reinterpret_cast<uint4*>(p.aux + r * p.ld_aux + hc) = uint4{a[0], a[1], a[2], a[3]};
+  if (p.aux2) *reinterpret_cast<uint4*>(p.aux2 + r * p.ld_aux + hc) = uint4{b[0], b[1], b[2], b[3]};
   const long cr = map_row(p.cmap, r);
-  if (cr >= 0) stbf8(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + hc, h);
+  if (cr >= 0) *reinterpret_cast<uint4*>(reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + hc) = uint4{h[0], h[1], h[2], h[3]};
 }
 
-// GEGLU backward: GEMM output = dh [M, I]; writes dg, du into the interleaved [M, 2I] layout.
+// GEGLU backward: GEMM output = dh [M, I]; the forward's factors a (aux_in), b (aux_in2); writes dg = dh * b,
+// du = dh * a into the interleaved [M, 2I] layout
 PTK_DEV void geglu_bwd_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 dh) {
-  const float4 g = ldbf4(p.aux_in + r * p.ld_aux_in + c);
-  const float4 u = ldbf4(p.aux_in2 + r * p.ld_aux_in + c);
+  const uint2 a = *reinterpret_cast<const uint2*>(p.aux_in + r * p.ld_aux_in + c);
+  const uint2 b = *reinterpret_cast<const uint2*>(p.aux_in2 + r * p.ld_aux_in + c);
   float4 dg, du;
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    const float d = bfround(el(dh, e));
-    float f, df;
-    gelu_tanh_fg(el(g, e), f, df);
-    el(dg, e) = bfround(d * el(u, e)) * df;
-    el(du, e) = d * bfround(f);
-  }
+  f32x2_t g0, g1, u0, u1;
+  geglu_bwd2(bfround2(f32x2_t{dh.x, dh.y}), a.x, b.x, g0, u0);
+  geglu_bwd2(bfround2(f32x2_t{dh.z, dh.w}), a.y, b.y, g1, u1);
+  dg = make_float4(g0.x, g0.y, g1.x, g1.y);
+  du = make_float4(u0.x, u0.y, u1.x, u1.y);
   const long cr = map_row(p.cmap, r);
   if (cr < 0) return;
   bf16_t* C = reinterpret_cast<bf16_t*>(Cz) + cr * p.ldc + (c >> 4) * 32 + (c & 15);
@@ -214,16 +208,18 @@ PTK_DEV void geglu_bwd_vec4(const GemmArgs& p, char* Cz, long r, long c, float4 
 // 8-wide GEGLU backward: 16-B loads of g, u and 16-B stores of dg, du (8 columns stay inside one
 // 16-column interleave group)
 PTK_DEV void geglu_bwd_vec8(const GemmArgs& p, char* Cz, long r, long c, const float* dh) {
-  float g[8], u[8], dg[8], du[8];
-  ldbf8(p.aux_in + r * p.ld_aux_in + c, g);
-  ldbf8(p.aux_in2 + r * p.ld_aux_in + c, u);
+  const uint4 a = *reinterpret_cast<const uint4*>(p.aux_in + r * p.ld_aux_in + c);
+  const uint4 b = *reinterpret_cast<const uint4*>(p.aux_in2 + r * p.ld_aux_in + c);
+  const uint32_t av[4] = {a.x, a.y, a.z, a.w}, bv[4] = {b.x, b.y, b.z, b.w};
+  float dg[8], du[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const float d = bfround(dh[e]);
-    float f, df;
-    gelu_tanh_fg(g[e], f, df);
-    dg[e] = bfround(d * u[e]) * df;
-    du[e] = d * bfround(f);
+  for (int e = 0; e < 8; e += 2) {
+    f32x2_t x, y;
+    geglu_bwd2(bfround2(f32x2_t{dh[e], dh[e + 1]}), av[e / 2], bv[e / 2], x, y);
+    dg[e] = x.x;
+    dg[e + 1] = x.y;
+    du[e] = y.x;
+    du[e + 1] = y.y;
   }
   const long cr = map_row(p.cmap, r);
   if (cr < 0) return;

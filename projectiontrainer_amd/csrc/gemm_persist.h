@@ -1,5 +1,5 @@
-// Shared pieces of the persistent GEMM kernels (gemm_w4.hip: 4-wave and 8-wave 256x256; gemm_dual.hip: two
-// 4-wave groups on 256x128 tiles): tile constants, the register epilogues (plain / GELU / GEGLU / GEGLU backward,
+// Shared pieces of the persistent GEMM kernels (gemm_w4.hip: 4-wave and 8-wave 256x256; gemm_tn.hip: the token-major
+// weight-grad kernel): tile constants, the register epilogues (plain / GELU / GEGLU / GEGLU backward,
 // whole-line bf16 stores), the grouped tile order, the laundered kernarg pointer and the inline-asm MFMA /
 // ds_read / LDS-DMA primitives.  Included by the .hip files only (device code, anonymous namespace).
 #pragma once
@@ -243,14 +243,11 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
         swap16(u0, u1);
         const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
         const float u[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-        uint32_t gp[4], up[4], hp[4];
+        uint32_t gp[4], up[4], hp[4];   // gp / up: the backward's factors a = gelu(g), b = gelu'(g) u
 #pragma unroll
-        for (int e = 0; e < 8; e += 2) {
-          gp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{g[e], g[e + 1]}, bf16x2_t));
-          up[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{u[e], u[e + 1]}, bf16x2_t));
-          const f32x2_t hh = bfround2(gelu_tanh2(bf2x2(gp[e / 2]))) * bf2x2(up[e / 2]);
-          hp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(hh, bf16x2_t));
-        }
+        for (int e = 0; e < 8; e += 2)
+          geglu_fwd2(bfround2(f32x2_t{g[e], g[e + 1]}), bfround2(f32x2_t{u[e], u[e + 1]}), gp[e / 2], up[e / 2],
+                     hp[e / 2]);
         G[pp] = uint4{gp[0], gp[1], gp[2], gp[3]};
         U[pp] = uint4{up[0], up[1], up[2], up[3]};
         H[pp] = uint4{hp[0], hp[1], hp[2], hp[3]};
@@ -284,15 +281,12 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
       swap16(u0, u1);
       const float g[8] = {g0[0], g0[1], g0[2], g0[3], g1[0], g1[1], g1[2], g1[3]};
       const float u[8] = {u0[0], u0[1], u0[2], u0[3], u1[0], u1[1], u1[2], u1[3]};
-      // g, u rounded to bf16 once: the packed dwords are stored as they are and unpacked for the math
+      // g, u rounded to bf16 once; stored: h and the backward's factors a = gelu(g) (aux), b = gelu'(g) u (aux2)
       uint32_t gp[4], up[4], hp[4];
 #pragma unroll
-      for (int e = 0; e < 8; e += 2) {
-        gp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{g[e], g[e + 1]}, bf16x2_t));
-        up[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(f32x2_t{u[e], u[e + 1]}, bf16x2_t));
-        const f32x2_t hh = bfround2(gelu_tanh2(bf2x2(gp[e / 2]))) * bf2x2(up[e / 2]);
-        hp[e / 2] = __builtin_bit_cast(uint32_t, __builtin_convertvector(hh, bf16x2_t));
-      }
+      for (int e = 0; e < 8; e += 2)
+        geglu_fwd2(bfround2(f32x2_t{g[e], g[e + 1]}), bfround2(f32x2_t{u[e], u[e + 1]}), gp[e / 2], up[e / 2],
+                   hp[e / 2]);
       const long hc = col0 / 2 + 32 * pp + cb;
       const bool cin = 2 * hc < p.N;
       const bool rv = w.rv && cin, sv = w.cv && cin;
@@ -340,8 +334,9 @@ PTK_DEV void w4_rows(const GemmArgs& p, f32x4_t (&a)[NJ], long row0, long col0, 
 }
 
 // GEGLU backward (GEMM output = dh [M, I]; writes dg, du into the interleaved [M, 2I] layout, as
-// geglu_bwd_kernel does): the saved g and u of row block I, 8 columns per lane and column pair pp,
-// loaded one row block ahead of their use so their latency runs under the previous block's math
+// geglu_bwd_kernel does): the forward's saved factors a = gelu(g) (aux_in), b = gelu'(g) u (aux_in2) of row block
+// I, 8 columns per lane and column pair pp, loaded one row block ahead of their use so their latency runs under
+// the previous block's math (G holds a, U holds b)
 template <int I, int NP = 4>
 PTK_DEV void w4_gbwd_load(const GemmArgs& p, long row0, long col0, int lane, u16x8_t (&G)[NP], u16x8_t (&U)[NP]) {
   const int q = lane >> 4;
@@ -374,11 +369,9 @@ PTK_DEV void w4_gbwd_rows(const GemmArgs& p, f32x4_t (&a)[2 * NP], long row0, lo
     const uint32_t gv[4] = {gw.x, gw.y, gw.z, gw.w}, uv[4] = {uw.x, uw.y, uw.z, uw.w};
     float dg[8], du[8];
 #pragma unroll
-    for (int e = 0; e < 8; e += 2) {   // packed pairs: the same per-element math as gelu_tanh_fg
-      const f32x2_t d = bfround2(f32x2_t{v[e], v[e + 1]}), g = bf2x2(gv[e / 2]), u = bf2x2(uv[e / 2]);
-      f32x2_t f, df;
-      gelu_tanh_fg2(g, f, df);
-      const f32x2_t a = bfround2(d * u) * df, b = d * bfround2(f);
+    for (int e = 0; e < 8; e += 2) {   // the forward's factors (G: a = gelu(g), U: b = gelu'(g) u): two multiplies
+      f32x2_t a, b;
+      geglu_bwd2(bfround2(f32x2_t{v[e], v[e + 1]}), gv[e / 2], uv[e / 2], a, b);
       dg[e] = a.x;
       dg[e + 1] = a.y;
       du[e] = b.x;
@@ -521,8 +514,8 @@ PTK_DEV void w4_epilogue_lean(const GemmArgs& p, f32x4_t (&acc)[8][NJ], long row
   if constexpr (RB > 7) w4_rows_lean<ACT, 7, NJ>(acc[7], e, bias);
 }
 
-// Lean GEGLU-backward epilogue (lean_glu_ok): w4_gbwd_rows' values and whole-line dg | du stores, the saved g, u
-// loaded by buffer loads one row block ahead (rows past M read as zero and their stores are dropped)
+// Lean GEGLU-backward epilogue (lean_glu_ok): w4_gbwd_rows' values and whole-line dg | du stores, the saved factors
+// a, b loaded by buffer loads one row block ahead (rows past M read as zero and their stores are dropped)
 #ifndef PTK_GBWD_AHEAD
 #define PTK_GBWD_AHEAD 2   // row blocks of saved g, u in flight in the lean GEGLU-backward epilogue (A/B builds)
 #endif
@@ -554,10 +547,8 @@ PTK_DEV void w4_gbwd_rows_lean(f32x4_t (&a)[2 * NP], const LeanGbwd& e, int I, c
     float dg[8], du[8];
 #pragma unroll
     for (int k = 0; k < 8; k += 2) {   // w4_gbwd_rows' math
-      const f32x2_t d = bfround2(f32x2_t{v[k], v[k + 1]}), g = bf2x2(gv[k / 2]), u = bf2x2(uv[k / 2]);
-      f32x2_t f, df;
-      gelu_tanh_fg2(g, f, df);
-      const f32x2_t aa = bfround2(d * u) * df, bb = d * bfround2(f);
+      f32x2_t aa, bb;
+      geglu_bwd2(bfround2(f32x2_t{v[k], v[k + 1]}), gv[k / 2], uv[k / 2], aa, bb);
       dg[k] = aa.x;
       dg[k + 1] = aa.y;
       du[k] = bb.x;

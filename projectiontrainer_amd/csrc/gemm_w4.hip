@@ -317,12 +317,9 @@ double w4_round_fill(long M, long N) {
 // a bias, the bf16-linear rounding and a bf16 residual (row-aligned with C, 16-B rows); a C row map that is an
 // offset (cmap.g == 0, or a group map without skipped rows whose group stride equals its size: the identity
 // plus cmap.off); whole 64-column wave ranges; C's extent (rows cmap.off .. M + cmap.off) below 2^31 bytes.
-// c_bytes = that extent (num_records of the store resource: rows past M are dropped).  PTK_LEAN_EPI=0 keeps the
-// general epilogue (A/B; bit-identical either way)
-static bool lean_on() {
-  static const bool on = [] { const char* e = getenv("PTK_LEAN_EPI"); return !(e && e[0] == '0'); }();
-  return on;
-}
+// c_bytes = that extent (num_records of the store resource: rows past M are dropped).  PTK_LEAN_EPI=0 (A/B builds,
+// PTK_AB) keeps the general epilogue (bit-identical either way)
+static bool lean_on() { return PTK_AB("PTK_LEAN_EPI", 1) != 0; }
 // the lean GEGLU-backward epilogue (w4_epilogue_lean_glu): the saved g, u inputs with 16-B rows, no other epilogue
 // input, an offset C row map, whole 128-column wave ranges, extents below 2^31 bytes
 static bool lean_glu_ok(const GemmArgs& a, int act, int out, uint32_t& c_bytes) {
@@ -879,12 +876,10 @@ static P8Tail p8_tail_plan(const GemmArgs& a, long ntile, long G, int act, int o
   return p8_tail_plan_ws(a, ntile, G, (char*)ws + P8_CNT_BYTES, 64, PTK_SK_MAXT1);
 }
 
-// The model-level calls lend their tail scratch to every GEMM they launch (PTK_STREAMK=0: never, an A/B of the
-// default dispatch without the tail; r04's opt-in predates the parallel fixup)
-static bool streamk_models() {
-  static const bool v = [] { const char* e = getenv("PTK_STREAMK"); return !(e && e[0] == '0'); }();
-  return v;
-}
+// The model-level calls lend their tail scratch to every GEMM they launch (PTK_STREAMK=0 in an A/B build, PTK_AB:
+// never, the default dispatch without the tail; r04's opt-in predates the parallel fixup)
+static bool streamk_models() { return PTK_AB("PTK_STREAMK", 1) != 0; }
+bool streamk_enabled() { return streamk_models(); }
 static thread_local void* g_tail_scope = nullptr;
 void* tail_scope() { return g_tail_scope; }
 TailScratchScope::TailScratchScope(void* ws, hipStream_t st) : prev(g_tail_scope) {

@@ -516,9 +516,10 @@ int launch_sum_partials(const float* part, int nsplit, long n, float* out, hipSt
 }  // namespace ptk
 
 namespace ptk {
-// GEGLU backward as a streaming pass (TF gemma3 :131-133 autograd, bf16 ops):
-//   dg = bf16(bf16(dh * u) * gelu_tanh'(g)),  du = bf16(dh * bf16(gelu_tanh(g)))
-// dh, g, u [M, I] bf16 -> dgu [M, 2I] bf16 in the interleaved gate/up layout (16-column groups).
+// GEGLU backward as a streaming pass (TF gemma3 :131-133 autograd, bf16 ops) from the forward's saved factors
+// (common.h geglu_fwd2: a = bf16(gelu_tanh(g)), b = bf16(gelu_tanh'(g) * u)):
+//   dg = bf16(dh * b),  du = bf16(dh * a)
+// dh, a, b [M, I] bf16 -> dgu [M, 2I] bf16 in the interleaved gate/up layout (16-column groups).
 __global__ void __launch_bounds__(256) geglu_bwd_kernel(const bf16_t* __restrict__ dh, const bf16_t* __restrict__ g,
                                                         const bf16_t* __restrict__ u, bf16_t* __restrict__ dgu,
                                                         long n8, int I) {
@@ -530,14 +531,12 @@ __global__ void __launch_bounds__(256) geglu_bwd_kernel(const bf16_t* __restrict
   const u16x8_t vd = *reinterpret_cast<const u16x8_t*>(dh + e0);
   const u16x8_t vg = *reinterpret_cast<const u16x8_t*>(g + e0);
   const u16x8_t vu = *reinterpret_cast<const u16x8_t*>(u + e0);
-  u16x8_t og, ou;
+  u16x8_t og, ou;   // (vg: the factor a, vu: the factor b)
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
-    const float d = bf2f(vd[k]), gg = bf2f(vg[k]), uu = bf2f(vu[k]);
-    float f, df;
-    gelu_tanh_fg(gg, f, df);
-    og[k] = f2bf(bfround(d * uu) * df);
-    ou[k] = f2bf(d * bfround(f));
+    const float d = bf2f(vd[k]);
+    og[k] = f2bf(d * bf2f(vu[k]));
+    ou[k] = f2bf(d * bf2f(vg[k]));
   }
   bf16_t* o = dgu + r * 2L * I + (c >> 4) * 32 + (c & 15);
   *reinterpret_cast<u16x8_t*>(o) = og;

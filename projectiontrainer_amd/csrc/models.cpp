@@ -63,7 +63,7 @@ constexpr int LM_KSLICES = 16; // its K slices on the 8-wave kernel (R % 256 == 
   } while (0)
 
 static bool geglu_split() {
-  static const int v = [] { const char* e = getenv("PTK_GEGLU_SPLIT"); return e && e[0] == '1' ? 1 : 0; }();
+  const int v = PTK_AB("PTK_GEGLU_SPLIT", 0) == 1;   // A/B builds only
   return v != 0;
 }
 // PTK_DKV_REDUCE_SPLIT=1: separate attn_dkv_reduce_kernel pass (A/B) instead of summing the split-slab
@@ -123,7 +123,9 @@ SiglipWs siglip_layout(Bump& bp, const ptk_siglip_config* c, int B) {
 // ------------------------------------------------------------------ Gemma3
 struct GemmaLayerSave {
   float *x2, *rstd_in, *rstd_ao, *rstd_pre, *rstd_dn, *rstd_q, *rstd_k;
-  bf16_t *qkv, *Q, *K, *V, *O, *ao, *g, *u, *dn;
+  // glu_a, glu_b: the GEGLU backward's factors the gate|up epilogue saves, bf16 gelu(gate) and gelu'(gate) * up
+  // (common.h geglu_fwd2)
+  bf16_t *qkv, *Q, *K, *V, *O, *ao, *glu_a, *glu_b, *dn;
   float* lse;
   // unfrozen LLM only: the GEMM inputs the weight grads contract with (input-norm / pre-ff-norm outputs,
   // GEGLU output); the frozen path keeps them in one scratch buffer
@@ -171,8 +173,8 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
     s.lse = bp.take<float>(Z * SG);
     s.O = bp.take<bf16_t>(M * Dq);
     s.ao = bp.take<bf16_t>(M * H);
-    s.g = bp.take<bf16_t>(M * I);
-    s.u = bp.take<bf16_t>(M * I);
+    s.glu_a = bp.take<bf16_t>(M * I);
+    s.glu_b = bp.take<bf16_t>(M * I);
     s.dn = bp.take<bf16_t>(M * H);
     if (train) {
       s.xn_in = bp.take<bf16_t>(M * H);
@@ -258,15 +260,16 @@ int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStr
   // 14 336: 280 tiles = 256 + 24): the 8-wave kernel's stream-K tail over the split-K scratch, its pieces summed by
   // p8_fixup_kernel (r05, tools/sk_ab.py same box: 419 / 216 us vs 662 / 298 unsplit; the 2-slice 128x128 split
   // below ran them at ~390 + 26 us on average)
-  if (a.K >= 4096 && part && (size_t)part_floats * sizeof(float) >= p8_tail_scratch_bytes() && a.M >= 1024 &&
-      a.N >= 256 && a.N <= 16384) {
+  if (streamk_enabled() && a.K >= 4096 && part && (size_t)part_floats * sizeof(float) >= p8_tail_scratch_bytes() &&
+      a.M >= 1024 && a.N >= 256 && a.N <= 16384) {
     GemmArgs b = a;
     b.tail_ws = part;
     if (p8_supported(b, ACT_NONE, out) && p8_tail_split(b, ACT_NONE, out)) return launch_gemm(b, ACT_NONE, out, 1, st);
   }
   // one partial round of 256x256 tiles: the 8-wave kernel unsplit (launch_gemm's single-round rule) beats the
-  // split-K 128x128 slices (Stage 2 at bs 8: the down projection 133.6 vs 177.8 us)
-  if (a.M >= 4096 && (long)((a.M + 255) / 256) * ((a.N + 255) / 256) <= device_cus() && out == OUT_BF16 &&
+  // split-K 128x128 slices (Stage 2 at bs 8: the down projection 133.6 vs 177.8 us); K <= 8192 as launch_gemm's own
+  // single-round rule, so a longer K (Gemma3-4B's down projection, K 10 240) keeps the split
+  if (a.M >= 4096 && a.K <= 8192 && (long)((a.M + 255) / 256) * ((a.N + 255) / 256) <= device_cus() && out == OUT_BF16 &&
       p8_supported(a, ACT_NONE, out) && lean_epilogue_candidate(a))
     return launch_gemm(a, ACT_NONE, out, 1, st);
   const long nbig = (long)((a.M + 255) / 256) * ((a.N + 255) / 256);
@@ -307,10 +310,7 @@ int gemm_split(const GemmArgs& a, int out, float* part, long part_floats, hipStr
 // (a ragged row count padded to 64 with zero rows), K slices as fp32 partials summed in slice order (gemm_tn.hip).  Otherwise (the loss rows of the
 // last layer, ragged row counts, PTK_WGRAD_TN=0) each is transposed to a K-contiguous feature-major copy (rows
 // gathered through the map, zero-padded to a multiple of 64) for the NT GEMMs.
-static int wgrad_tn_mode() {
-  static const int m = [] { const char* e = getenv("PTK_WGRAD_TN"); return e ? atoi(e) : 1; }();
-  return m;
-}
+static int wgrad_tn_mode() { return PTK_AB("PTK_WGRAD_TN", 1); }   // A/B builds: PTK_WGRAD_TN=0 / 2
 }  // namespace
 namespace ptk {
 int wgrad_tn_enabled() { return wgrad_tn_mode() != 0; }
@@ -347,6 +347,12 @@ int weight_grad(const bf16_t* dy, long lddy, RowMap ymap, int Ny, const bf16_t* 
     }
   }
   if (tn == 2) return set_error("weight_grad: the TN path does not take Ny %d Nx %d rows %d", Ny, Nx, rows);
+  // the transpose path: decided here on the host, so scratch that was left out because the caller expected the
+  // TN path (identity maps) is caught before any launch (tn_supported rejects e.g. Ny / Nx % 64, 64 rows, unaligned
+  // pointers or operands past 4 GiB)
+  if (!TA || !TB)
+    return set_error("weight_grad: Ny %d Nx %d rows %d take the transpose path, which needs ta / tb scratch", Ny, Nx,
+                     rows);
   const int Kp = (rows + 63) / 64 * 64;
   CK(launch_transpose_rows(dy, lddy, ymap, rows, Ny, TA, Kp, Kp, st));
   CK(launch_transpose_rows(x, ldx, xmap, rows, Nx, TB, Kp, Kp, st));
@@ -543,15 +549,15 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
     sq.next("gemma.fwd.mlp");
     if (l + 1 < nl) {
       GemmArgs g = gemm(xff, H, L.wgu, H, hh, I, M, 2 * I, H);
-      g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
+      g.aux = sv.glu_a; g.aux2 = sv.glu_b; g.ld_aux = I;
       CK(launch_gemm(g, ACT_GEGLU, OUT_BF16, 1, st));
       CK(gemm_split(gemm(hh, I, L.wd, I, sv.dn, H, M, H, I), OUT_BF16, w.skpart, w.sk_floats, st));
     } else {
-      // last layer: only the loss rows reach the loss, so its MLP runs on those R rows (h, g, u compact);
+      // last layer: only the loss rows reach the loss, so its MLP runs on those R rows (h, glu_a, glu_b compact);
       // the other rows of dn are zero (their residual output is never read, their gradient is zero)
       GemmArgs g = gemm(xff, H, L.wgu, H, hh, I, R, 2 * I, H);
       g.amap = lossmap;
-      g.aux = sv.g; g.aux2 = sv.u; g.ld_aux = I;
+      g.aux = sv.glu_a; g.aux2 = sv.glu_b; g.ld_aux = I;
       CK(launch_gemm(g, ACT_GEGLU, OUT_BF16, 1, st));
       CK(launch_zero(sv.dn, (size_t)M * H * sizeof(bf16_t), st));
       GemmArgs g2 = gemm(hh, I, L.wd, I, sv.dn, H, R, H, I);
@@ -638,26 +644,26 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
       CK(last ? weight_grad(w.dao, H, lossmap, H, sv.h, I, ident, I, R, w.TA, w.TB, GL->wd, w.skpart, w.sk_floats, st)
               : weight_grad(w.dao, H, ident, H, sv.h, I, ident, I, M, w.TA, w.TB, GL->wd, w.skpart, w.sk_floats, st));
     // d(gate|up) = GEGLU backward of dh = dd . Wd, fused into the persistent 4-wave GEMM's register
-    // epilogue (g, u loaded one row block ahead; dh never reaches HBM).  PTK_GEGLU_SPLIT=1: the plain
+    // epilogue (the saved factors loaded one row block ahead: dg = dh * b, du = dh * a; dh never reaches HBM).  PTK_GEGLU_SPLIT=1: the plain
     // GEMM + one streaming geglu_bwd pass instead (A/B)
     if (!last) {
       if (geglu_split()) {
         CK(launch_gemm(gemm(w.dao, H, L.wd_t, H, w.h, I, M, I, H), ACT_NONE, OUT_BF16, 1, st));
-        CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, M, I, st));
+        CK(launch_geglu_bwd(w.h, sv.glu_a, sv.glu_b, w.dgu, M, I, st));
       } else {
         GemmArgs g = gemm(w.dao, H, L.wd_t, H, w.dgu, 2 * I, M, I, H);
-        g.aux_in = sv.g;
-        g.aux_in2 = sv.u;
+        g.aux_in = sv.glu_a;
+        g.aux_in2 = sv.glu_b;
         g.ld_aux_in = I;
         CK(launch_gemm(g, ACT_GEGLU_BWD, OUT_BF16, 1, st));
       }
       if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, ident, H, M, w.TA, w.TB, GL->wgu, w.skpart, w.sk_floats, st));
       CK(gemm_split(gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, M, H, 2 * I), OUT_BF16, w.skpart, w.sk_floats, st));
-    } else {   // last layer: MLP gradient is non-zero on the loss rows only (compact h, g, u, dgu)
+    } else {   // last layer: MLP gradient is non-zero on the loss rows only (compact h, glu_a, glu_b, dgu)
       GemmArgs g = gemm(w.dao, H, L.wd_t, H, w.h, I, R, I, H);
       g.amap = lossmap;
       CK(launch_gemm(g, ACT_NONE, OUT_BF16, 1, st));
-      CK(launch_geglu_bwd(w.h, sv.g, sv.u, w.dgu, R, I, st));
+      CK(launch_geglu_bwd(w.h, sv.glu_a, sv.glu_b, w.dgu, R, I, st));
       if (train) CK(weight_grad(w.dgu, 2 * I, ident, 2 * I, sv.xn_ff, H, lossmap, H, R, w.TA, w.TB, GL->wgu, w.skpart, w.sk_floats, st));
       CK(launch_zero(w.dtmp, (size_t)M * H * sizeof(bf16_t), st));
       GemmArgs g2 = gemm(w.dgu, 2 * I, L.wgu_t, 2 * I, w.dtmp, H, R, H, 2 * I);

@@ -10,6 +10,20 @@ namespace ptk {
 
 int set_error(const char* fmt, ...);   // records the thread-local message, returns -1
 
+// A/B switches (same-box measurements of a kernel choice): in the product library each is its compile-time default
+// -- no environment read, nothing for `strings libptk.so` to find.  A diagnostic build of one source with
+// -DPTK_AB_ENV (`make ablib AB_NAME=.. AB_SRC=gemm.hip AB_DEFS=-DPTK_AB_ENV`, `make diag`) reads the named variable
+// once instead (an integer; unset or empty keeps the default)
+#ifdef PTK_AB_ENV
+}  // namespace ptk
+#include <cstdlib>
+namespace ptk {
+inline int ab_env(const char* name, int dflt) { const char* e = getenv(name); return e && *e ? atoi(e) : dflt; }
+#define PTK_AB(NAME, DFLT) ([] { static const int v_ = ::ptk::ab_env(NAME, DFLT); return v_; }())
+#else
+#define PTK_AB(NAME, DFLT) (DFLT)
+#endif
+
 enum Act { ACT_NONE = 0, ACT_GELU_TANH = 1, ACT_GELU_ERF = 2, ACT_GEGLU = 3,
            ACT_GELU_ERF_BWD = 4, ACT_GEGLU_BWD = 5 };
 enum Out { OUT_BF16 = 0, OUT_F32 = 1, OUT_F32_BFR = 2 };
@@ -56,7 +70,7 @@ struct GemmArgs {
 int launch_gemm(const GemmArgs& a, int act, int out, int batch, hipStream_t st);
 // kernel families launch_gemm dispatches to (census: path_counts, ptk_gemm_path_counts)
 enum GemmPath { GEMM_PATH_NT = 0, GEMM_PATH_BIG = 1, GEMM_PATH_BIG2 = 2, GEMM_PATH_W4 = 3, GEMM_PATH_NTB = 4,
-                GEMM_PATH_P8SK = 5, GEMM_PATH_P8 = 6, GEMM_PATH_TN = 7, GEMM_PATH_DUAL = 8, GEMM_NPATH = 9 };
+                GEMM_PATH_P8SK = 5, GEMM_PATH_P8 = 6, GEMM_PATH_TN = 7, GEMM_NPATH = 9 };   // (8: unused since r06)
 int path_counts(int64_t* out, int reset);   // out [GEMM_NPATH][8] launches per (path, act class)
 // persistent 256x256 4-wave GEMM (gemm_w4.hip): batch 1 only; w4_supported says whether a shape qualifies
 bool w4_supported(const GemmArgs& a, int act, int out);
@@ -70,12 +84,9 @@ int launch_gemm_p8(const GemmArgs& a, int act, int out, hipStream_t st, bool sk,
 int p8_tile_height(const GemmArgs& a, int act, int out);   // 256, or 224 / 192 where shorter tiles fill the rounds
 int launch_gemm_p8_kslices(const GemmArgs& a, int slices, hipStream_t st);   // K slices as row tiles (fp32 partials)
 int gemm_p8_kslices(const GemmArgs& a, int slices, hipStream_t st);          // + census / timers (gemm.hip)
-// persistent two-group kernel (gemm_dual.hip): 256x128 tiles, one group's epilogue beside the other's K loop
-bool dual_supported(const GemmArgs& a, int act, int out);
 // the persistent kernels would take their lean bf16 epilogue for this plain bf16 GEMM (gemm_w4.hip lean_epilogue_ok)
 bool lean_epilogue_candidate(const GemmArgs& a);
 bool lean_epilogue_ok(const GemmArgs& a, int act, int out, uint32_t& c_bytes);   // + c_bytes: C's extent (store rsrc)
-int launch_gemm_dual(const GemmArgs& a, int act, int out, hipStream_t st, bool solo);   // solo: 256x128 tiles, 2 WGs/CU
 // persistent TN GEMM (gemm_tn.hip): C[M,N] = A[K,M]^T B[K,N] on the token-major operands of a weight grad, lda / ldb
 // their row strides.  OUT_BF16: slices == 1 and the weight-grad accumulate (bf16_linear + resid16 == C), with the
 // stream-K tail of the 8-wave kernel when `slab` (tn_slab_bytes() bytes) is given and the plan splits; OUT_F32:
@@ -89,12 +100,13 @@ size_t tn_slab_bytes();
 // past the buffer ranges and read as zero)
 int launch_gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st, long k_rows = -1);
 int gemm_tn(const GemmArgs& a, int out, int slices, void* slab, hipStream_t st, long k_rows = -1);
-int wgrad_tn_enabled();   // PTK_WGRAD_TN != 0 (models.cpp)
+int wgrad_tn_enabled();   // the TN weight-grad path is on (models.cpp; A/B switch PTK_WGRAD_TN)
 // stream-K tail of the persistent 8-wave kernel: scratch bytes (arrival counters, then partial slabs), the
 // workgroups its plan spreads a GEMM's tail over (0: no split), and the thread-local scratch a model-level
 // call lends to every GEMM it launches (the counters are zeroed when the scope opens)
 size_t p8_tail_scratch_bytes();
-size_t p8_tail_scratch_bytes_models();   // 0 unless PTK_STREAMK=1 (the model workspaces lend it only then)
+size_t p8_tail_scratch_bytes_models();   // 0 when the A/B build turns the tail off (PTK_STREAMK=0)
+bool streamk_enabled();                  // the stream-K tail is on (the product library: always)
 int p8_tail_split(const GemmArgs& a, int act, int out);
 void* tail_scope();
 struct TailScratchScope {

@@ -238,7 +238,8 @@ int launch_rms_wgrad_bdy(const float* x, long ldx, RowMap xmap, const float* rst
 #ifndef PTK_QK_ROWS
 #define PTK_QK_ROWS 8
 #endif
-constexpr int QK_ROWS = PTK_QK_ROWS;   // tokens per block of the partial sums (8: with WG_ROWS 8, +0.25 % on cfg4)
+constexpr int QK_ROWS = PTK_QK_ROWS;   // tokens per block of the partial sums (8 measured +0.25 % on cfg4 when the RMSNorm
+                                       // partials ran 8-row blocks; kept, not re-measured, with their final 32-row x 4-group form)
 PTK_DEV float4 ldb4(const bf16_t* p) {
   u16x4_t u = *reinterpret_cast<const u16x4_t*>(p);
   return make_float4(bf2f(u[0]), bf2f(u[1]), bf2f(u[2]), bf2f(u[3]));

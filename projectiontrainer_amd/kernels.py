@@ -160,7 +160,7 @@ def weight_grad(dy, x, grad, rows=None, ymap=(0, 0, 0), xmap=(0, 0, 0), part=Non
     rows = dy.shape[0] if rows is None else rows
     kp = (rows + 63) // 64 * 64
     ta = tb = None
-    if mode == 1 or ymap[0] or ymap[2] or xmap[0] or xmap[2] or rows % 64:
+    if mode != 2:   # the TN path is not guaranteed (shape, alignment, maps): the transpose fallback's scratch
         ta = torch.empty((Ny, kp), dtype=torch.bfloat16, device=dy.device)
         tb = torch.empty((Nx, kp), dtype=torch.bfloat16, device=dy.device)
     pf = 0 if part is None else part.numel()

@@ -11,7 +11,6 @@ torch.autograd.Function; there is no CPU path.
 """
 from __future__ import annotations
 
-import os
 
 import torch
 import torch.nn as nn
@@ -96,9 +95,8 @@ class MLPProjector(nn.Module):
             self._w2b = torch.empty(self.w2.shape, dtype=torch.bfloat16, device=self.flat.device)
             self._w2t = torch.empty((self.inter_dim, self.llm_dim), dtype=torch.bfloat16, device=self.flat.device)
             # stream-K tail scratch of the projector's GEMMs (ptk_projector.tail_ws; the fc2 projection's 104-tile
-            # tail round runs split); PTK_STREAMK=0 leaves it unallocated (the A/B without the tail)
-            self._tail = (torch.zeros(L.lib().ptk_gemm_tail_scratch_bytes(), dtype=torch.uint8,
-                                      device=self.flat.device) if os.environ.get("PTK_STREAMK") != "0" else None)
+            # tail round runs split)
+            self._tail = torch.zeros(L.lib().ptk_gemm_tail_scratch_bytes(), dtype=torch.uint8, device=self.flat.device)
         K.cast_bf16(self.w1.detach(), self._w1b)
         K.cast_bf16(self.w2.detach(), self._w2b)
         K.transpose(self._w2b, out=self._w2t)     # in place: no allocation per optimizer step

@@ -16,12 +16,12 @@ def oracle_ddp(rank, world, port, out_dir):
     """CPU/gloo: per-rank oracle grads on the rank's half batch -> allreduce_grads_
     (the engine's collective) -> clip + AdamW (oracle); dump flat grads/params."""
     _init(rank, world, port, "gloo")
-    torch.set_num_threads(2)
+    torch.set_num_threads(1 if world > 2 else 2)
     from oracle import stage1_ref as R
     from projectiontrainer_amd import dist as D
     from projectiontrainer_amd import weights as W
     from projectiontrainer_amd.config import PRESETS
-    cfg = PRESETS["tiny"].replace(batch_size=4)
+    cfg = PRESETS["tiny"].replace(batch_size=2 * world)
     vp, lp = W.siglip_vision_params(cfg.vision), W.gemma3_params(cfg.text)
     pp = W.projector_params(cfg.vision.hidden_size, cfg.text.hidden_size)
     px, ids, labels = W.synthetic_batch(cfg, seed=21)
@@ -38,8 +38,10 @@ def oracle_ddp(rank, world, port, out_dir):
 
 
 def engine_ddp(rank, world, port, out_dir):
-    """GPU/gloo on one device: the real Stage1Engine with world_size 2."""
+    """GPU/gloo on one device: the real Stage1Engine at world_size `world`, 2 samples per rank (the batch of
+    2 * world cut by rank), one step; the gathered per-rank losses (accelerator.gather, DistState.gather)."""
     _init(rank, world, port, "gloo")
+    from projectiontrainer_amd import dist as D
     from projectiontrainer_amd import weights as W
     from projectiontrainer_amd.config import PRESETS
     from projectiontrainer_amd.gemma3 import Gemma3CausalLM
@@ -47,7 +49,7 @@ def engine_ddp(rank, world, port, out_dir):
     from projectiontrainer_amd.siglip import SiglipVisionTower
     from projectiontrainer_amd.stage1 import Stage1Engine
     dev = torch.device("cuda:0")
-    cfg = PRESETS["tiny"].replace(batch_size=4)
+    cfg = PRESETS["tiny"].replace(batch_size=2 * world)
     vp, lp = W.siglip_vision_params(cfg.vision), W.gemma3_params(cfg.text)
     pp = W.projector_params(cfg.vision.hidden_size, cfg.text.hidden_size)
     px, ids, labels = W.synthetic_batch(cfg, seed=21)
@@ -60,9 +62,12 @@ def engine_ddp(rank, world, port, out_dir):
     sl = slice(2 * rank, 2 * rank + 2)
     eng.step(*(torch.from_numpy(t[sl]).to(dev) for t in (px, ids, labels)))
     torch.cuda.synchronize()
+    acc = D.DistState(1, backend="gloo", device=dev)
+    losses = acc.gather(eng.loss.detach().cpu())
     np.save(os.path.join(out_dir, f"grad{rank}.npy"), eng.proj.flat_grad.cpu().numpy())
     np.save(os.path.join(out_dir, f"param{rank}.npy"), eng.proj.flat.cpu().numpy())
     np.save(os.path.join(out_dir, f"sched{rank}.npy"), np.array([eng.sched_step, eng.last_lr]))
+    np.save(os.path.join(out_dir, f"loss{rank}.npy"), losses.numpy())
     dist.destroy_process_group()
 
 
@@ -182,15 +187,15 @@ def nccl_world1(rank, world, port, out_dir):
 
 
 def stage2_zero(rank, world, port, out_dir):
-    """GPU (one device shared) / gloo, world 2: Stage2Engine with ZeRO-1 sharding; each rank runs one half of a
-    batch, then the sharded optimizer step.  Saves the replica's flat parameters."""
+    """GPU (one device shared) / gloo, world 2 / 4 / 8: Stage2Engine with ZeRO-1 sharding; each rank runs its 2
+    samples of a batch of 2 * world, then the sharded optimizer step.  Saves the replica's flat parameters."""
     _init(rank, world, port, "gloo")
     import math
     from projectiontrainer_amd import weights as W
     from projectiontrainer_amd.config import PRESETS
     from projectiontrainer_amd.stage2 import synthetic_engine
     dev = torch.device("cuda:0")
-    cfg = PRESETS["tiny"].replace(batch_size=4, text_len=8 + 12, question_len=8)
+    cfg = PRESETS["tiny"].replace(batch_size=2 * world, text_len=8 + 12, question_len=8)
     torch.manual_seed(0)
     eng = synthetic_engine(cfg, dev, seed=3, world_size=world, rank=rank, learning_rate=1e-3, total_steps=10)
     px, q, a = (torch.from_numpy(t).to(dev) for t in W.synthetic_vqa_batch(cfg, seed=9))

@@ -24,6 +24,8 @@ Fixtures:
                       vocab 262144), bs 2, T 64, fp32 / bf16 as above
   cfg2w, cfg2w_bf16   BASELINE cfg2 WIDTHS (SigLIP-L/16-384 + Gemma3-1B, vocab 262144) at 2 + 6 layers
                       (one global Gemma layer), bs 2, T 128 (S 703 > the sliding window), fp32 / bf16
+  cfg5w, cfg5w_bf16   BASELINE cfg5 WIDTHS (SigLIP-L/16-384 + Gemma3-4B, vocab 262208) at 2 + 6 layers, bs 1,
+                      T 256, fp32 / bf16
 
 Large tensors are stored as a strided sub-sample `<key>@sub<sr>x<sc>` (every
 sr-th row, every sc-th column of the [rows, last-dim] view) plus the exact
@@ -201,6 +203,10 @@ FIXTURES = {   # name: (gas, batch seed, precision)
     # reference itself, and its bf16 twin measures the reference's own mixed-precision noise at those widths
     "cfg2w": (2, 15, "no"),
     "cfg2w_bf16": (2, 15, "bf16"),   # same batch as "cfg2w"
+    # cfg5 widths (SigLIP-L/16-384 + Gemma3-4B) at 2 + 6 layers, bs 1, T 256: the 4B per-layer shapes pinned to the
+    # reference, and the 4B-width twin noise the cfg5 full-depth bars derive from
+    "cfg5w": (2, 16, "no"),
+    "cfg5w_bf16": (2, 16, "bf16"),   # same batch as "cfg5w"
 }
 
 

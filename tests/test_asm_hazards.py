@@ -121,7 +121,7 @@ def hazards(body):
 
 
 # every HIP source of libptk.so (capi / models / comm are host code)
-PRODUCT_SOURCES = ["flash.hip", "gemm_w4.hip", "gemm_dual.hip", "gemm_tn.hip", "gemm.hip", "norm.hip", "attn.hip", "misc.hip", "image.hip",
+PRODUCT_SOURCES = ["flash.hip", "gemm_w4.hip", "gemm_tn.hip", "gemm.hip", "norm.hip", "attn.hip", "misc.hip", "image.hip",
                    "train.hip"]
 _ASM_CACHE = {}
 
@@ -148,7 +148,7 @@ def asm_dir(tmp_path_factory):
     return tmp_path_factory.mktemp("asm")
 
 
-@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip", "gemm_dual.hip", "gemm_tn.hip"])
+@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip", "gemm_tn.hip"])
 def test_inline_asm_mfma_hazards(src, asm_dir):
     asm = product_asm(src, asm_dir)
     bad = []
@@ -250,7 +250,7 @@ def test_kernel_spills_within_budget(src, asm_dir):
     assert not bad, "\n".join(bad[:20])
 
 
-@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip", "gemm_dual.hip", "gemm_tn.hip"])
+@pytest.mark.parametrize("src", ["flash.hip", "gemm_w4.hip", "gemm_tn.hip"])
 def test_asm_never_writes_m0(src, asm_dir):
     """LDS-DMA asm takes its LDS address through the {m0} constraint (hipcc writes M0 and knows the asm reads
     it); an M0 write hidden inside an asm statement would break any M0 value hipcc keeps live."""

@@ -7,7 +7,9 @@
    * BASELINE cfg1 dims (SigLIP-B/16-224 + the full 26-layer Gemma3-1B, vocab
      262144, bs 2, T 64), fp32 (cfg1) and bf16 (cfg1_bf16);
    * BASELINE cfg2 WIDTHS (SigLIP-L/16-384 + Gemma3-1B, vocab 262144) at 2 + 6 layers
-     (one global Gemma layer, S 703 > the sliding window), bs 2, T 128: cfg2w / cfg2w_bf16.
+     (one global Gemma layer, S 703 > the sliding window), bs 2, T 128: cfg2w / cfg2w_bf16;
+   * BASELINE cfg5 WIDTHS (SigLIP-L/16-384 + Gemma3-4B, vocab 262208, GQA 8:4, linear RoPE x8 on the
+     global layer) at 2 + 6 layers, bs 1, T 256: cfg5w / cfg5w_bf16.
 2. Against the CPU oracle at architecture-true sizes (SigLIP-L/16-384 and
    Gemma3-1B dims at full depth, S = 703 > sliding window 512, and T = 512).
 
@@ -19,7 +21,7 @@ path (bf16 GEMM operands, fp32 accumulation, SURVEY F8 flow) must agree with eit
 reference run within twice the distance between the two reference runs (two bf16
 implementations of one function each sit ~noise away from fp32), and within
 SURVEY.md:297's bar wherever that noise is below it:
-  loss |d| <= 2e-2 abs;
+  loss |d| <= max(2e-2, 2 * the twins' loss distance) abs;
   patch embeddings / projector output / d(projector output) / projector grads:
     rel-L2 <= max(2e-2, 2 * noise_rel_l2), cosine >= min(0.999, 1 - 4 * (1 - noise_cos)) (1 - cos
     ~ rel-L2^2 / 2, so both are a factor 2 on the distance);
@@ -128,7 +130,7 @@ def build_engine(name, gpu, gas, lr, total):
 
 
 @pytest.mark.parametrize("name", ["tiny", "tiny_gqa", "tiny_bf16", "tiny_gqa_bf16", "cfg1", "cfg1_bf16", "cfg2w",
-                                  "cfg2w_bf16"])
+                                  "cfg2w_bf16", "cfg5w", "cfg5w_bf16"])
 def test_two_steps_vs_reference_golden(gpu, name):
     d, meta = G.load(name)
     cfg, eng = build_engine(name, gpu, meta["gas"], meta["lr"], meta["max_train_steps"])
@@ -141,8 +143,12 @@ def test_two_steps_vs_reference_golden(gpu, name):
                                     torch.from_numpy(labels).to(gpu))
         torch.cuda.synchronize()
         dl = abs(float(loss) - float(d[f"s{s}_loss"]))
-        record(t, f"s{s}_loss", abs=dl)
-        assert dl <= LOSS_TOL, (float(loss), float(d[f"s{s}_loss"]))
+        # SURVEY.md:297's 2e-2, or twice the reference's own bf16-vs-fp32 loss distance where that is larger (cfg5w:
+        # 0.019 / 0.021 -- the 4B-width logits are larger, so their bf16 rounding moves the mean CE further)
+        tw, _ = G.load(name.replace("_bf16", "") + ("" if name.endswith("_bf16") else "_bf16"))
+        ltol = max(LOSS_TOL, 2.0 * abs(float(tw[f"s{s}_loss"]) - float(d[f"s{s}_loss"])))
+        record(t, f"s{s}_loss", abs=dl, tol=ltol)
+        assert dl <= ltol, (float(loss), float(d[f"s{s}_loss"]), ltol)
         vis = eng.vis.view(cfg.batch_size, N, -1)[:, 1:].float()
         compare(d, f"s{s}_patch", vis, RL2, cos=COS, test=t, name=name)
         xv = eng.x.view(cfg.batch_size, eng.Sp, -1)[:, :Nv]
@@ -192,6 +198,15 @@ def _bench_census(gpu, preset="cfg2"):
 
 # (preset, batch) whose compared step must run every kernel family of the benchmarked step (census asserted)
 CENSUS_CASES = {("cfg2", 30), ("cfg5", 8)}
+
+# rel-L2 of the HIP path against the reference's own fp32 train() on the width fixtures (test_two_steps_vs_reference
+# _golden, step 0; profiles/r06_width_fixtures_parity_metrics.jsonl): cfg2w for the Gemma3-1B cases, cfg5w for the 4B
+HIP_WIDTH_DIST = {
+    "cfg2": {"d_proj": 0.0177, "grad.model.0.weight": 0.0161, "grad.model.0.bias": 0.0144,
+             "grad.model.2.weight": 0.0210, "grad.model.2.bias": 0.0143},
+    "cfg5": {"d_proj": 0.0174, "grad.model.0.weight": 0.0128, "grad.model.0.bias": 0.0136,
+             "grad.model.2.weight": 0.0155, "grad.model.2.bias": 0.0135},
+}
 
 
 @pytest.mark.slow
@@ -264,12 +279,13 @@ def test_architecture_scale_vs_oracle(gpu, preset, bs, T, vl, tl):
     out = R.stage1_step(vp, cfg.vision, lp, cfg.text, st, (px, ids, labels), R.StepConfig(gradient_accumulation_steps=1),
                         embed_dtype=torch.bfloat16)
     t = f"arch[{preset}-bs{bs}-T{T}]"
-    # the bar is SURVEY.md:297's, widened on the backward quantities to twice the reference's own bf16-vs-fp32
-    # noise at cfg2 WIDTHS (the cfg2w / cfg2w_bf16 fixtures: SigLIP-L/16-384 + Gemma3-1B at 2 + 6 layers, bs 2,
-    # T 128, the reference's train() run both ways; 0.075 on d(projector output), 0.02-0.03 on the grads)
+    # the bar is SURVEY.md:297's (rel-L2 2e-2), widened on the backward quantities to twice the HIP path's own
+    # distance from the reference's fp32 run on the reference-generated fixture of the same widths (HIP_WIDTH_DIST:
+    # golden[cfg2w] / golden[cfg5w], step 0); the full-depth cfg2 runs (24 + 26 layers) measured 1.0-1.7x that
+    # 2 + 6-layer distance
     record(t, "loss", abs=abs(loss - float(out["loss"])))
     assert abs(loss - float(out["loss"])) <= LOSS_TOL, (loss, float(out["loss"]))
-    bar = lambda key: max(RL2, 2.0 * twin_noise("cfg2w", "s0_" + key)[0])
+    bar = lambda key: max(RL2, 2.0 * HIP_WIDTH_DIST[preset][key])
     for key, got, ref, rtol in (("patch", vis, out["patch"], RL2), ("proj", xv, out["proj"], RL2),
                                 ("d_proj", dxv, out["d_proj"], bar("d_proj"))) + tuple(
             ("grad." + k, gc, out["grads"][k], bar("grad." + k))

@@ -155,10 +155,18 @@ def test_stage2_state_roundtrip(gpu):
     assert torch.equal(llm.embed_t, llm.embed.t().contiguous())
 
 
-def test_stage2_zero1_two_ranks_match_single_process(gpu):
-    """ZeRO-1 (reduce-scatter of the bf16 grads, sharded bf16 AdamW, all-gather) at world 2 (gloo on one
-    device) gives bit-identical replicas equal to one process that accumulates both halves of the batch and
-    halves the grad (DDP's average; exact in bf16), then steps the whole buffer."""
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_stage2_zero1_ranks_match_single_process(gpu, world):
+    """ZeRO-1 (reduce-scatter of the bf16 grads, sharded bf16 AdamW, all-gather, the squared-norm all-reduce) at
+    world 2, 4 and 8 (gloo on one device; W = 8 is the cfg4 benchmark's rank count): replicas bit-identical, the flat
+    store padded to a multiple of 64 x W, every rank's optimizer shard its contiguous 1/W, and the result equal to one
+    process that accumulates all W parts of the batch, scales the grad by 1/W (DDP's average; exact in bf16 for a
+    power of two) and steps the whole buffer.  At W = 2 the two grad sums round identically, so every matrix and
+    norm weight is bit-identical; at W = 4 / 8 the single process rounds its bf16 grad after every micro-batch while
+    the exchange sums the ranks' bf16 grads in fp32 and rounds once (gloo; RCCL's bf16 ring rounds W - 1 times,
+    test_bf16_ring_sum_w8_within_twin_noise), so a grad may differ in its last bits: a first AdamW step moves a
+    weight by lr * g / (|g| + eps) ~ +-lr, so the params agree to one lr step where a tiny grad's sign flipped, and
+    to a bf16 ulp of the update elsewhere (median 0)."""
     import tempfile
     import torch.multiprocessing as mp
     from tests import dist_worker
@@ -167,41 +175,58 @@ def test_stage2_zero1_two_ranks_match_single_process(gpu):
     from projectiontrainer_amd.config import PRESETS
     from projectiontrainer_amd.stage2 import synthetic_engine
     with tempfile.TemporaryDirectory() as td:
-        mp.spawn(dist_worker.stage2_zero, args=(2, _port(), td), nprocs=2, join=True)
-        p0, p1 = np.load(f"{td}/s2param0.npy"), np.load(f"{td}/s2param1.npy")
+        mp.spawn(dist_worker.stage2_zero, args=(world, _port(), td), nprocs=world, join=True)
+        ps = [np.load(f"{td}/s2param{r}.npy") for r in range(world)]
         n0 = np.load(f"{td}/s2norm0.npy")
-        shards = [torch.load(f"{td}/opt{r}.pt", weights_only=True) for r in range(2)]
-    np.testing.assert_array_equal(p0, p1)
-    cfg = PRESETS["tiny"].replace(batch_size=4, text_len=8 + 12, question_len=8)
+        shards = [torch.load(f"{td}/opt{r}.pt", weights_only=True) for r in range(world)]
+    p0 = ps[0]
+    for r in range(1, world):
+        np.testing.assert_array_equal(p0, ps[r])
+    assert p0.size % (64 * world) == 0
+    per = p0.size // world
+    assert [sh["shard"] for sh in shards] == [(r * per, per) for r in range(world)]
+    assert all(sh["world"] == world and sh["rank"] == r for r, sh in enumerate(shards))
+    cfg = PRESETS["tiny"].replace(batch_size=2 * world, text_len=8 + 12, question_len=8)
     torch.manual_seed(0)
     eng = synthetic_engine(cfg, gpu, seed=3, learning_rate=1e-3, total_steps=10)
     px, q, a = (torch.from_numpy(t).to(gpu) for t in W.synthetic_vqa_batch(cfg, seed=9))
-    for r in range(2):
+    for r in range(world):
         sl = slice(2 * r, 2 * r + 2)
         eng.forward_backward(px[sl], q[sl], a[sl])
-    eng.state.grad.mul_(0.5)
+    eng.state.grad.mul_(1.0 / world)
     eng.optimizer_step()
     torch.cuda.synchronize()
+    assert eng.sched_step == 1     # one process: the scheduler once per optimizer step (F7: W at world W)
     flat = eng.state.flat.float().cpu().numpy()
     n = min(flat.size, p0.size)        # the stores differ only in their zero tail (shards padded per world)
     assert not flat[n:].any() and not p0[n:].any()
-    # every matrix and norm weight is bit-identical.  The tied embedding is not: each micro-batch adds two
-    # terms to its bf16 grad (lm_head GEMM, then the input-embedding scatter), so accumulating both halves
-    # in one process rounds ((G0 + L1) + E1) where the reduce-scatter rounds G0 + (L1 + E1) -- the same
-    # bf16 order dependence the reference has between DDP and accumulation.  There: within 2 lr (one Adam
-    # step moves a weight by ~lr).
+    # the tied embedding: each micro-batch adds two terms to its bf16 grad (lm_head GEMM, then the input-embedding
+    # scatter), so accumulating in one process rounds ((G0 + L1) + E1) where the exchange rounds G0 + (L1 + E1) --
+    # the same bf16 order dependence the reference has between DDP and accumulation.  There: within 2 lr.
     e0, e1 = eng.state.offsets["embed"][0], eng.state.offsets["embed"][0] + cfg.text.vocab_size * cfg.text.hidden_size
     mask = np.ones(n, dtype=bool)
     mask[e0:e1] = False
-    np.testing.assert_array_equal(flat[:n][mask], p0[:n][mask])
-    assert np.abs(flat[e0:e1] - p0[e0:e1]).max() <= 2e-3
-    np.testing.assert_allclose(float(eng.grad_norm), float(n0[0]), rtol=1e-6)
-    # the two ranks' saved optimizer shards together are the single process's AdamW moments
+    lr = 1e-3
+    assert np.abs(flat[e0:e1] - p0[e0:e1]).max() <= 2 * lr + 1e-3
+    if world == 2:
+        np.testing.assert_array_equal(flat[:n][mask], p0[:n][mask])
+        np.testing.assert_allclose(float(eng.grad_norm), float(n0[0]), rtol=1e-6)
+    else:
+        d = np.abs(flat[:n][mask] - p0[:n][mask])
+        assert d.max() <= 2 * lr + 1e-3, d.max()
+        assert np.median(d) == 0.0
+        assert (d > 0).mean() < 0.05, (d > 0).mean()
+        np.testing.assert_allclose(float(eng.grad_norm), float(n0[0]), rtol=2e-3)
+    # the W ranks' saved optimizer shards together are the single process's AdamW moments
     for key in ("exp_avg", "exp_avg_sq"):
         both = torch.cat([sh[key] for sh in shards]).float().numpy()
         one = getattr(eng, key).float().cpu().numpy()
-        np.testing.assert_array_equal(both[:n][mask], one[:n][mask])
-    assert [sh["shard"] for sh in shards] == [(0, p0.size // 2), (p0.size // 2, p0.size // 2)]
+        if world == 2:
+            np.testing.assert_array_equal(both[:n][mask], one[:n][mask])
+        else:
+            scale = np.abs(one[:n][mask]).max()
+            assert np.abs(both[:n][mask] - one[:n][mask]).max() <= 2e-2 * scale
+            assert np.median(np.abs(both[:n][mask] - one[:n][mask])) <= 1e-6 * scale
 
 
 def test_vqa_trainer_api_with_hf_models(gpu, tmp_path):

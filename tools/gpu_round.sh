@@ -2,7 +2,7 @@
 # Parametrised GPU-box checks of this tree (replaces the per-round one-off scripts).
 #   ROUND=r05 tools/gpu_round.sh [part ...]
 # parts (default: tests smoke bench prof): tests | smoke | bench | stages | cfg5 | cfg4 | prof | pmc
-#   tests   full `pytest -m gpu` (TESTS=<pytest args> selects a subset)
+#   tests   full `pytest -m gpu` (TESTS=<pytest args> / KEXPR=<-k expression> select a subset)
 #   smoke   __graft_entry__.smoke()
 #   bench   default bench.py line (with the CPU baseline)
 #   stages  bench.py --stage-timers (per-stage breakdown)
@@ -23,7 +23,9 @@ for part in "${PARTS[@]}"; do
   log=gpurun_out/${T}_$part.log
   case $part in
     tests)
-      timeout -k 10 900 python -u -m pytest tests -m gpu -v -x --timeout 600 --timeout-method thread ${TESTS:-} > $log 2>&1
+      KARGS=()
+      [ -n "${KEXPR:-}" ] && KARGS=(-k "$KEXPR")
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v -x --timeout 600 --timeout-method thread ${TESTS:-} "${KARGS[@]}" > $log 2>&1
       rc=$?; grep -E "passed|failed" $log | tail -1; grep -E "FAILED|Error" $log | head -5
       [ $rc -eq 0 ] || exit $rc ;;
     smoke)
