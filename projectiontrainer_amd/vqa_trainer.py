@@ -6,7 +6,11 @@ Same constructor signature, `.train()`, `.evaluate(epoch, global_step)`,
 Supported configuration: BASELINE cfg4 — the LLM unfrozen (`freeze_llm=False`,
 no QLoRA), projector and vision encoder frozen; anything else raises
 NotImplementedError (QLoRA/peft needs 4-bit kernels; a trainable vision
-encoder or projector needs their backward passes).
+encoder or projector needs their backward passes).  Note that the reference's
+own run script ships `ENABLE_QLORA=true` (`Stage2/run_vqa_train_stage2.sh:42`,
+a Qwen3-8B QLoRA run); cfg4 -- the benchmark this path is built for -- is the
+unfrozen-LLM form of the same trainer (`--unfreeze_llm`, `UNFREEZE_LLM` in that
+script, ignored there only because QLoRA is on).
 
 Kept reference semantics (Stage2/trainer.py:248-488):
   * batches dealt as accelerate's prepared DataLoader deals them (even_batches),
