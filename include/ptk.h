@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTK_ABI_VERSION 6
+#define PTK_ABI_VERSION 7
 
 int ptk_abi_version(void);
 const char* ptk_last_error(void);
@@ -351,6 +351,36 @@ typedef struct {
 size_t ptk_gemma3_train_workspace_bytes(const ptk_gemma3_config* c, int batch, int text_len, int seq_pad);
 int ptk_gemma3_train_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_batch* b,
                              const ptk_gemma3_grads* g, void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * KV-cache decode: the validation `generate` of Stage1/projector_trainer.py:386-393                       *
+ * (unwrapped_llm.generate(inputs_embeds=projected_embeds, attention_mask=ones, max_new_tokens=64,          *
+ * do_sample=True, pad_token_id, eos_token_id) -> GenerationMixin._sample with a cache).  Prefill of the    *
+ * prompt embeddings (all positions valid) into a per-layer K / V cache, then one token per step:           *
+ * embedding x bf16(sqrt H), the 26 layers on the training path's kernels with the step's query against     *
+ * the cache (sliding layers: the last `sliding_window` keys), final norm, tied lm_head (bf16 logits), and  *
+ * the sampling step (temperature, top-k with ties kept, a softmax draw; or greedy argmax).  A row that      *
+ * produced eos_token_id emits pad_token_id from then on.                                                    *
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int batch, prompt_len, max_new_tokens;
+  int do_sample;             /* 0: greedy argmax (first maximal index) */
+  int top_k;                 /* <= 0 or >= vocab: no top-k (HF GenerationConfig default: 50) */
+  float temperature;         /* > 0 when sampling (default 1) */
+  uint64_t seed;             /* the draw of step t, row b: a counter-based uniform of (seed, t, b) */
+  int64_t eos_token_id, pad_token_id;
+  int64_t prompt_batch_stride;   /* rows of prompt_embeds between consecutive samples (>= prompt_len) */
+} ptk_gemma3_generate_desc;
+
+size_t ptk_gemma3_generate_workspace_bytes(const ptk_gemma3_config* c, int batch, int prompt_len, int max_new_tokens);
+/* prompt_embeds: f32 rows [b * prompt_batch_stride + i], i < prompt_len, width hidden (the projector output as the
+ * Stage-1 engine lays it out in the LLM input).  out_ids: int64 [batch, max_new_tokens].  force_ids (optional,
+ * int64 [batch, max_new_tokens]): teacher forcing -- step t > 0 feeds force_ids[:, t-1] instead of the token drawn
+ * at t-1 (out_ids still records the draws).  step_logits (optional, bf16 [max_new_tokens][batch][vocab]): every
+ * step's logits.  Needs rope tables of prompt_len + max_new_tokens positions. */
+int ptk_gemma3_generate(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_generate_desc* g,
+                        const float* prompt_embeds, const int64_t* force_ids, int64_t* out_ids, void* step_logits,
+                        void* ws, size_t ws_bytes, void* stream);
 
 /* clip_grad_norm_ + AdamW over bf16 parameters (Stage2/trainer.py:426-443, optimizer :145-149).
  * ptk_bf16_grad_scale_sumsq: g = bf16(g * scale) in place (scale 1: untouched), *out = sum g^2 (fp32,

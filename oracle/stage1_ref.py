@@ -172,6 +172,38 @@ def embed_tokens(p, cfg: Gemma3TextConfig, token_ids, dtype=torch.float32):
     return E[token_ids] * scale
 
 
+def greedy_generate(p, cfg: Gemma3TextConfig, prompt_embeds, max_new_tokens, eos_token_id=None, pad_token_id=0,
+                    force_ids=None, dtype=torch.float32):
+    """`GenerationMixin._sample` with do_sample=False over `Gemma3ForCausalLM` from inputs_embeds and an all-ones
+    attention mask, as the reference's validation calls generate (Stage1/projector_trainer.py:386-393; greedy, so
+    deterministic): each step's logits are the tied lm_head of the last position's final-norm output (recomputed
+    over the whole sequence, no cache), the token is their argmax; a row that produced eos_token_id emits
+    pad_token_id afterwards and the loop stops once every row has.  New tokens enter as their embedding, the bf16
+    weight row times bf16(sqrt H) rounded to bf16 (Gemma3TextScaledWordEmbedding on bf16 weights).  force_ids
+    [B, max_new_tokens]: teacher forcing (step t appends force_ids[:, t-1]).  Returns (tokens [B, n], logits
+    [n, B, V] fp32)."""
+    B, P, _ = prompt_embeds.shape
+    E = _t(p, "model.embed_tokens.weight", dtype)
+    x = prompt_embeds.to(dtype)
+    unfinished = torch.ones(B, dtype=torch.bool)
+    toks, logs = [], []
+    for t in range(max_new_tokens):
+        h = gemma3_forward(p, cfg, x, torch.ones(B, x.shape[1], dtype=torch.long), dtype)
+        lg = F.linear(h[:, -1], E).float()
+        tok = lg.argmax(-1)
+        tok = torch.where(unfinished, tok, torch.full_like(tok, pad_token_id))
+        toks.append(tok)
+        logs.append(lg)
+        if eos_token_id is not None:
+            unfinished &= tok != eos_token_id
+            if not unfinished.any():
+                break
+        feed = tok if force_ids is None else torch.as_tensor(force_ids)[:, t]
+        e = embed_tokens(p, cfg, feed[:, None], torch.bfloat16).to(dtype)
+        x = torch.cat([x, e], dim=1)
+    return torch.stack(toks, 1), torch.stack(logs, 0)
+
+
 # --------------------------------------------------------------------------- step
 @dataclass
 class TrainState:

@@ -107,6 +107,12 @@ class Gemma3BatchC(C.Structure):
                 ("loss_scale", c_float), ("loss", c_void_p), ("label_offset", c_int)]
 
 
+class Gemma3GenerateC(C.Structure):
+    _fields_ = [("batch", c_int), ("prompt_len", c_int), ("max_new_tokens", c_int), ("do_sample", c_int),
+                ("top_k", c_int), ("temperature", c_float), ("seed", C.c_uint64), ("eos_token_id", c_int64),
+                ("pad_token_id", c_int64), ("prompt_batch_stride", c_int64)]
+
+
 class Gemma3LayerGradsC(C.Structure):
     _fields_ = [(n, c_void_p) for n in ("wqkv", "wo", "wgu", "wd", "ln_in", "ln_post_attn", "ln_pre_ff",
                                         "ln_post_ff", "q_norm", "k_norm")]
@@ -122,7 +128,7 @@ class ImageDesc(C.Structure):
                 ("coef_off", c_int64), ("tmp_off", c_int64)]
 
 
-ABI_VERSION = 6      # include/ptk.h PTK_ABI_VERSION
+ABI_VERSION = 7      # include/ptk.h PTK_ABI_VERSION
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -176,6 +182,9 @@ SIGNATURES = {
     "ptk_gemma3_train_fwd_bwd": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC),
                                          C.POINTER(Gemma3BatchC), C.POINTER(Gemma3GradsC), c_void_p, c_size_t,
                                          c_void_p]),
+    "ptk_gemma3_generate_workspace_bytes": (c_size_t, [C.POINTER(Gemma3ConfigC), c_int, c_int, c_int]),
+    "ptk_gemma3_generate": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC), C.POINTER(Gemma3GenerateC),
+                                    c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
     "ptk_bf16_sumsq_partial_floats": (c_int, []),
     "ptk_bf16_grad_scale_sumsq": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p]),
     "ptk_adamw_bf16": (c_int, [c_void_p] * 4 + [c_int64, c_void_p, c_float] + [C.c_double] * 5 +

@@ -732,6 +732,189 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
 
 }  // namespace
 
+namespace {
+
+// ------------------------------------------------------------------ Gemma3 KV-cache decode (generate)
+// Stage1/projector_trainer.py:386-393 -> GenerationMixin._sample over Gemma3ForCausalLM with a cache: a prefill of
+// the prompt embeddings, then one position per step.  Each layer is the training forward's launch sequence (same
+// kernels, same fp32 residual stream and bf16 GEMM operands) on the rows of the pass; the step's attention reads
+// the layer's K / V cache [B, Hkv, Smax, D] (the prefill writes its rows, each step appends one), over keys
+// [0, p] on full layers and the last `sliding_window` of them on sliding layers (TF/masking_utils.py:92-101:
+// key > p - W).
+struct GenPass {            // per-pass activations (rows = B * S)
+  float *xa, *xb, *x2, *rs1, *rs2, *rq, *rk;
+  bf16_t *xn, *qkv, *Q, *K, *V, *O, *ao, *h, *dn;
+  int32_t* kv;
+};
+struct GenWs {
+  GenPass pre, dec;
+  std::vector<bf16_t*> kc, vc;     // per layer [B, Hkv, Smax, D]
+  bf16_t *xf, *logits;
+  float* rstd_f;
+  int32_t* finished;
+  int64_t *next, *feed;
+  void* tail;
+};
+GenPass gen_pass(Bump& bp, const ptk_gemma3_config* c, long M) {
+  const long H = c->hidden, I = c->inter, D = c->head_dim, Hq = c->heads, Hkv = c->kv_heads;
+  const long Dq = Hq * D, Dqkv = (Hq + 2 * Hkv) * D;
+  GenPass g;
+  g.xa = bp.take<float>(M * H);
+  g.xb = bp.take<float>(M * H);
+  g.x2 = bp.take<float>(M * H);
+  g.rs1 = bp.take<float>(M);
+  g.rs2 = bp.take<float>(M);
+  g.rq = bp.take<float>(M * Hq);
+  g.rk = bp.take<float>(M * Hkv);
+  g.xn = bp.take<bf16_t>(M * H);
+  g.qkv = bp.take<bf16_t>(M * Dqkv);
+  g.Q = bp.take<bf16_t>(M * Dq);
+  g.K = bp.take<bf16_t>(M * Hkv * D);
+  g.V = bp.take<bf16_t>(M * Hkv * D);
+  g.O = bp.take<bf16_t>(M * Dq);
+  g.ao = bp.take<bf16_t>(M * H);
+  g.h = bp.take<bf16_t>(M * I);
+  g.dn = bp.take<bf16_t>(M * H);
+  g.kv = bp.take<int32_t>(M);
+  return g;
+}
+GenWs gen_layout(Bump& bp, const ptk_gemma3_config* c, int B, int P, int max_new) {
+  const long Pp = (P + 63) / 64 * 64, Smax = (P + max_new + 63) / 64 * 64;
+  const long Z = (long)B * c->kv_heads, D = c->head_dim;
+  GenWs w;
+  w.pre = gen_pass(bp, c, (long)B * Pp);
+  w.dec = gen_pass(bp, c, B);
+  for (int l = 0; l < c->layers; ++l) {
+    w.kc.push_back(bp.take<bf16_t>(Z * Smax * D));
+    w.vc.push_back(bp.take<bf16_t>(Z * Smax * D));
+  }
+  w.xf = bp.take<bf16_t>((long)B * c->hidden);
+  w.logits = bp.take<bf16_t>((long)B * c->vocab);
+  w.rstd_f = bp.take<float>(B);
+  w.finished = bp.take<int32_t>(B);
+  w.next = bp.take<int64_t>(B);
+  w.feed = bp.take<int64_t>(B);
+  w.tail = bp.take<char>(p8_tail_scratch_bytes_models());
+  return w;
+}
+
+// one decoder layer over the S positions of each of B rows of pass g (Sp = S rounded the pass's way: the prefill's
+// padded prompt, 1 for a decode step): x_in -> x_out (fp32), the layer's K / V appended to the cache at p0, the
+// queries attending cache keys [k_lo, p0 + S) (prefill: causal + window over its own rows, decode: the window
+// start k_lo); xn holds the layer's input norm on entry and the next layer's on exit (w_next: none -> untouched)
+int gen_layer(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, int l, GenPass& g, const float* x_in,
+              float* x_out, int B, int S, int Sp, int p0, bool prefill, int Smax, bf16_t* kc, bf16_t* vc,
+              hipStream_t st) {
+  const ptk_gemma3_layer& L = wt->layers[l];
+  const int H = c->hidden, I = c->inter, D = c->head_dim, Hq = c->heads, Hkv = c->kv_heads, G = Hq / Hkv;
+  const int M = B * Sp, Dq = Hq * D, Dqkv = (Hq + 2 * Hkv) * D, Z = B * Hkv;
+  const bool sliding = (l + 1) % c->sliding_pattern != 0;
+  const float* cs = (sliding ? wt->rope_cos_local : wt->rope_cos_global) + (long)p0 * (D / 2);
+  const float* sn = (sliding ? wt->rope_sin_local : wt->rope_sin_global) + (long)p0 * (D / 2);
+  CK(launch_gemm(gemm(g.xn, H, L.wqkv, H, g.qkv, Dqkv, M, Dqkv, H), ACT_NONE, OUT_BF16, 1, st));
+  AttnShape ash{B, Sp, Hq, Hkv, D};
+  CK(launch_qknorm_rope_fwd(g.qkv, L.q_norm, L.k_norm, cs, sn, ash, c->eps, g.Q, g.K, g.V, g.rq, g.rk, st));
+  CK(launch_kv_append(g.K, (long)Sp * D, kc, (long)Smax * D, Z, p0, S, D, st));
+  CK(launch_kv_append(g.V, (long)Sp * D, vc, (long)Smax * D, Z, p0, S, D, st));
+  {
+    FlashArgs fa;
+    fa.Q = g.Q; fa.O = g.O; fa.lse = nullptr;
+    fa.rows = Sp * G; fa.D = D;
+    fa.ldq = D; fa.ldk = D; fa.ldo = D;
+    fa.zin = Hkv; fa.zdiv = Hkv;
+    fa.sQ0 = (long)Hkv * Sp * G * D; fa.sQ1 = (long)Sp * G * D;
+    fa.sK0 = (long)Hkv * Smax * D; fa.sK1 = (long)Smax * D;
+    fa.sO0 = (long)Sp * Hq * D; fa.sO1 = (long)G * D;
+    fa.omap = RowMap{G, 0, Hq, 0};
+    fa.qdiv = G;
+    fa.scale = 1.0f / sqrtf(c->query_pre_attn_scalar);
+    if (prefill) {   // the prompt's own keys: causal, the window on sliding layers, padded rows masked
+      fa.K = g.K; fa.V = g.V;
+      fa.sK0 = (long)Hkv * Sp * D; fa.sK1 = (long)Sp * D;
+      fa.nkeys = Sp; fa.causal = 1; fa.window = sliding ? c->sliding_window : 0;
+      fa.key_valid = g.kv;
+    } else {         // one query position p0 against cache keys [k_lo, p0]
+      const int k_lo = (sliding && c->sliding_window > 0) ? std::max(0, p0 - c->sliding_window + 1) : 0;
+      fa.K = kc + (long)k_lo * D; fa.V = vc + (long)k_lo * D;
+      fa.nkeys = p0 + 1 - k_lo; fa.causal = 0; fa.window = 0;
+      fa.key_valid = nullptr;
+    }
+    CK(launch_attn_fwd(fa, Z, st));
+  }
+  CK(launch_gemm(gemm(g.O, Dq, L.wo, Dq, g.ao, H, M, H, Dq), ACT_NONE, OUT_BF16, 1, st));
+  CK(launch_residual_norm_fwd(g.ao, x_in, L.ln_post_attn, L.ln_pre_ff, g.x2, g.xn, g.rs1, g.rs2, M, H, c->eps, st));
+  {
+    GemmArgs gg = gemm(g.xn, H, L.wgu, H, g.h, I, M, 2 * I, H);   // (no saved GEGLU factors: no backward)
+    CK(launch_gemm(gg, ACT_GEGLU, OUT_BF16, 1, st));
+  }
+  CK(launch_gemm(gemm(g.h, I, L.wd, I, g.dn, H, M, H, I), ACT_NONE, OUT_BF16, 1, st));
+  const float* wnext = (l + 1 < c->layers) ? wt->layers[l + 1].ln_in : nullptr;
+  CK(launch_residual_norm_fwd(g.dn, g.x2, L.ln_post_ff, wnext, x_out, g.xn, g.rs1, g.rs2, M, H, c->eps, st));
+  return 0;
+}
+
+int gemma_generate(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_generate_desc* gd,
+                   const float* prompt, const int64_t* force, int64_t* out_ids, bf16_t* step_logits, void* ws,
+                   size_t ws_bytes, hipStream_t st) {
+  const int B = gd->batch, P = gd->prompt_len, NT = gd->max_new_tokens;
+  if (B <= 0 || P < 4 || NT <= 0) return set_error("generate: batch %d, prompt_len %d (>= 4), max_new_tokens %d", B, P, NT);
+  if (gd->prompt_batch_stride < P) return set_error("generate: prompt_batch_stride %ld < prompt_len %d",
+                                                    (long)gd->prompt_batch_stride, P);
+  if (P + NT > wt->rope_max_pos || (P + 63) / 64 * 64 > wt->rope_max_pos)
+    return set_error("generate: %d positions exceed the rope tables (%d)", P + NT, wt->rope_max_pos);
+  if (c->heads % c->kv_heads) return set_error("generate: heads %% kv_heads");
+  if (ws_bytes < ptk_gemma3_generate_workspace_bytes(c, B, P, NT)) return set_error("generate: workspace too small");
+  const int H = c->hidden, V = c->vocab, Pp = (P + 63) / 64 * 64, Smax = (P + NT + 63) / 64 * 64;
+  Bump bp(ws);
+  GenWs w = gen_layout(bp, c, B, P, NT);
+  TailScratchScope tail(w.tail, st);
+  CK(tail.status);
+  const float escale = bfround_host(sqrtf((float)H));
+  CK(launch_zero(w.finished, ((size_t)B * 4 + 15) / 16 * 16, st));
+  // logits row b -> sampled token, into out_ids[:, t]
+  auto head = [&](const float* x, RowMap map, int t) -> int {
+    CK(launch_rmsnorm_fwd(x, H, map, wt->final_norm, w.xf, w.rstd_f, B, H, c->eps, st));
+    CK(launch_gemm(gemm(w.xf, H, wt->embed, H, w.logits, V, B, V, H), ACT_NONE, OUT_BF16, 1, st));
+    if (step_logits)
+      CKH(hipMemcpyAsync(step_logits + (long)t * B * V, w.logits, (size_t)B * V * 2, hipMemcpyDeviceToDevice, st));
+    return launch_gen_sample(w.logits, V, B, V, gd->do_sample, gd->top_k, gd->temperature, gd->seed, t,
+                             (long)gd->eos_token_id, (long)gd->pad_token_id, w.finished, out_ids + t, NT, w.next, st);
+  };
+  // prefill: the prompt rows, padded per sample to Pp (masked keys), every layer's K / V into the cache
+  {
+    GenPass& g = w.pre;
+    CK(launch_gen_prompt(prompt, (long)gd->prompt_batch_stride, B, P, Pp, H, g.xa, g.kv, st));
+    CK(launch_rmsnorm_fwd(g.xa, H, RowMap{0, 0, 0, 0}, wt->layers[0].ln_in, g.xn, g.rs1, B * Pp, H, c->eps, st));
+    float *xi = g.xa, *xo = g.xb;
+    for (int l = 0; l < c->layers; ++l) {
+      CK(gen_layer(c, wt, l, g, xi, xo, B, P, Pp, 0, true, Smax, w.kc[l], w.vc[l], st));
+      std::swap(xi, xo);
+    }
+    CK(head(xi, RowMap{1, 0, Pp, P - 1}, 0));   // the last prompt position of each sample
+  }
+  // decode: step t feeds the token drawn at t - 1 (or force[:, t - 1]) at position P + t - 1
+  for (int t = 1; t < NT; ++t) {
+    GenPass& g = w.dec;
+    const int p = P + t - 1;
+    const int64_t* ids = w.next;
+    if (force) {
+      CKH(hipMemcpy2DAsync(w.feed, 8, force + (t - 1), (size_t)NT * 8, 8, B, hipMemcpyDeviceToDevice, st));
+      ids = w.feed;
+    }
+    CK(launch_build_llm_inputs((const bf16_t*)wt->embed, ids, B, 1, 0, 1, 1, H, escale, -1, g.xa, g.kv, st));
+    CK(launch_rmsnorm_fwd(g.xa, H, RowMap{0, 0, 0, 0}, wt->layers[0].ln_in, g.xn, g.rs1, B, H, c->eps, st));
+    float *xi = g.xa, *xo = g.xb;
+    for (int l = 0; l < c->layers; ++l) {
+      CK(gen_layer(c, wt, l, g, xi, xo, B, 1, 1, p, false, Smax, w.kc[l], w.vc[l], st));
+      std::swap(xi, xo);
+    }
+    CK(head(xi, RowMap{0, 0, 0, 0}, t));
+  }
+  return 0;
+}
+
+}  // namespace
+
 extern "C" {
 
 int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,
@@ -748,6 +931,20 @@ int ptk_gemma3_train_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weight
                              const ptk_gemma3_grads* g, void* ws, size_t ws_bytes, void* stream) {
   if (!g) return set_error("gemma3 train: grads is NULL");
   return gemma_run(c, wt, bt, g, ws, ws_bytes, (hipStream_t)stream);
+}
+
+size_t ptk_gemma3_generate_workspace_bytes(const ptk_gemma3_config* c, int batch, int prompt_len, int max_new_tokens) {
+  Bump bp(nullptr);
+  gen_layout(bp, c, batch, prompt_len, max_new_tokens);
+  return bp.off + 256;
+}
+
+int ptk_gemma3_generate(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_generate_desc* g,
+                        const float* prompt_embeds, const int64_t* force_ids, int64_t* out_ids, void* step_logits,
+                        void* ws, size_t ws_bytes, void* stream) {
+  if (!c || !w || !g || !prompt_embeds || !out_ids) return set_error("generate: NULL argument");
+  return gemma_generate(c, w, g, prompt_embeds, force_ids, out_ids, (bf16_t*)step_logits, ws, ws_bytes,
+                        (hipStream_t)stream);
 }
 
 int ptk_bf16_sumsq_partial_floats(void) { return scale_sumsq_partial_floats(); }

@@ -320,6 +320,14 @@ int launch_zero(void* p, size_t bytes, hipStream_t st);
 int launch_geglu_bwd(const bf16_t* dh, const bf16_t* g, const bf16_t* u, bf16_t* dgu, long M, int I, hipStream_t st);
 int launch_fill_normal_bf16(bf16_t* out, long n, uint64_t seed, float std, float mean, hipStream_t st);
 
+// ---- KV-cache decode (generate.hip) ----
+int launch_gen_prompt(const float* src, long ld_b, int B, int P, int Pp, int H, float* x, int32_t* kv, hipStream_t st);
+int launch_kv_append(const bf16_t* src, long src_z, bf16_t* dst, long dst_z, int Z, int p0, int n, int D,
+                     hipStream_t st);
+int launch_gen_sample(const bf16_t* logits, long ld, int B, int V, int do_sample, int top_k, float temperature,
+                      uint64_t seed, int step, long eos_id, long pad_id, int32_t* finished, int64_t* out, long ld_out,
+                      int64_t* next, hipStream_t st);
+
 // ---- unfrozen-LLM step (train.hip) ----
 // out [cols][rows_pad] bf16 = in[map(r)][c] (r < rows), zero for rows <= r < rows_pad
 int launch_transpose_rows(const bf16_t* in, long ld_in, RowMap map, int rows, int cols, bf16_t* out, long ld_out,

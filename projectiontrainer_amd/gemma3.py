@@ -204,3 +204,57 @@ class Gemma3CausalLM:
 
     def get_input_embeddings(self):
         return self.embed
+
+    def generate(self, inputs_embeds, max_new_tokens=64, do_sample=True, top_k=50, temperature=1.0,
+                 pad_token_id=None, eos_token_id=None, seed=0, prompt_len=None, batch=None, force_ids=None,
+                 return_logits=False):
+        """`Gemma3ForCausalLM.generate(inputs_embeds=, attention_mask=ones, max_new_tokens=, do_sample=, pad_token_id=,
+        eos_token_id=)` as the reference's validation calls it (Stage1/projector_trainer.py:386-393) on the KV-cache
+        decode of libptk (ptk_gemma3_generate): returns the NEW tokens, int64 [B, n], n = max_new_tokens or the step
+        at which every row has produced eos_token_id (HF's stopping; finished rows are padded with pad_token_id).
+        Sampling follows HF's defaults (GenerationConfig: temperature 1, top_k 50, top_p 1): the drawn tokens are
+        one draw of the same distribution, from a counter-based generator seeded by `seed` (torch.multinomial's
+        stream is not reproduced).
+        inputs_embeds: f32 [B, P, H], or [B * stride, H] rows with prompt_len = P and batch = B (the Stage-1
+        engine's LLM input, whose vision rows start each stride-row sample).  force_ids (int64 [B, max_new_tokens]): teacher forcing
+        (step t feeds force_ids[:, t-1]); return_logits: also the bf16 logits of every step [max_new_tokens, B, V]."""
+        if inputs_embeds.dtype != torch.float32 or not inputs_embeds.is_cuda or not inputs_embeds.is_contiguous():
+            raise L.PtkError("generate: inputs_embeds must be a contiguous f32 HIP tensor")
+        H = self.cfg.hidden_size
+        if inputs_embeds.dim() == 3:
+            B, P, _ = inputs_embeds.shape
+            stride = P
+        else:
+            if prompt_len is None or batch is None or inputs_embeds.shape[0] % batch:
+                raise L.PtkError("generate: 2-D inputs_embeds need prompt_len and batch (rows = batch x stride)")
+            P, B = int(prompt_len), int(batch)
+            stride = inputs_embeds.shape[0] // B
+        if inputs_embeds.shape[-1] != H:
+            raise L.PtkError(f"generate: inputs_embeds width {inputs_embeds.shape[-1]} != hidden {H}")
+        pad = self.cfg.pad_token_id if pad_token_id is None else int(pad_token_id)
+        eos = -1 if eos_token_id is None else int(eos_token_id)
+        desc = L.Gemma3GenerateC(B, P, max_new_tokens, int(bool(do_sample)), int(top_k or 0), float(temperature),
+                                 int(seed) & ((1 << 64) - 1), eos, pad, stride)
+        n = L.lib().ptk_gemma3_generate_workspace_bytes(self.c_cfg, B, P, max_new_tokens)
+        if getattr(self, "_gen_ws", None) is None or self._gen_ws.numel() < n:
+            self._gen_ws = None
+            self._gen_ws = torch.empty(n, dtype=torch.uint8, device=self.device)
+        out = torch.empty((B, max_new_tokens), dtype=torch.int64, device=self.device)
+        logits = (torch.empty((max_new_tokens, B, self.cfg.vocab_size), dtype=torch.bfloat16, device=self.device)
+                  if return_logits else None)
+        if force_ids is not None:
+            force_ids = force_ids.to(device=self.device, dtype=torch.int64).contiguous()
+            if tuple(force_ids.shape) != (B, max_new_tokens):
+                raise L.PtkError(f"generate: force_ids must be [{B}, {max_new_tokens}]")
+        L.check(L.lib().ptk_gemma3_generate(self.c_cfg, self.c_w, desc, inputs_embeds.data_ptr(),
+                                            0 if force_ids is None else force_ids.data_ptr(), out.data_ptr(),
+                                            0 if logits is None else logits.data_ptr(), self._gen_ws.data_ptr(),
+                                            self._gen_ws.numel(), L.stream_ptr(self.device)), "ptk_gemma3_generate")
+        n_out = max_new_tokens
+        if eos >= 0:   # HF stops after the step at which the last unfinished row produced EOS
+            done = (out == eos).cumsum(1) > 0
+            all_done = done.all(0).nonzero()
+            if all_done.numel():
+                n_out = int(all_done[0]) + 1
+        out = out[:, :n_out]
+        return (out, logits) if return_logits else out

@@ -16,8 +16,11 @@ What changes underneath:
     computed from the unsharded loader, cosine lambda without a clamp;
   * checkpoints are byte-compatible: `torch.save(state_dict)` with keys
     model.0/2.{weight,bias} + projector_config.json (`:455-521`).
-Validation by `generate` (`:292-448`) is out of scope; a validation loss is
-computed when val_dataset is given.
+Validation (`:292-448`) when val_dataset is given: the loss (forward + CE only) and, when the tokenizer can
+decode (`batch_decode`), the reference's last-word accuracy of `generate` from the projected embeddings
+(`:378-413`: max_new_tokens 64, do_sample=True with HF's default top-k 50 / temperature 1, pad / eos from the
+tokenizer) on libptk's KV-cache decode (`Gemma3CausalLM.generate`, `ptk_gemma3_generate`).  The draws come from
+a counter-based generator seeded per epoch and batch (`generate_seed`), not torch's multinomial stream.
 """
 from __future__ import annotations
 
@@ -25,6 +28,7 @@ import json
 import logging
 import math
 import os
+import re
 import time
 
 import torch
@@ -42,12 +46,21 @@ def _collate(items):
     return {k: torch.stack([it[k] for it in items]) for k in items[0]}
 
 
+def get_last_word(text):
+    """The reference's last-word extractor (Stage1/projector_trainer.py:132-137): the last \\w+ run, lower-cased."""
+    if not text or not isinstance(text, str):
+        return ""
+    words = re.findall(r"\b\w+\b", text.lower())
+    return words[-1] if words else ""
+
+
 class ProjectionTrainerStage1:
     def __init__(self, accelerator, vision_encoder, language_model, projection_layer, processor, tokenizer,
                  train_dataset, val_dataset=None, output_dir="./trained_projection_stage1", batch_size=8,
                  learning_rate=1e-4, weight_decay=0.01, num_epochs=10, gradient_accumulation_steps=1,
                  warmup_ratio=0.0, wandb_project="xray_projection_training", save_every_n_epochs=0,
-                 log_fn=None, seed=0, num_workers=8):
+                 log_fn=None, seed=0, num_workers=8, generate_max_new_tokens=64, generate_do_sample=True,
+                 generate_seed=0):
         if accelerator is None:
             accelerator = D.DistState(gradient_accumulation_steps)
         elif not isinstance(accelerator, D.DistState):
@@ -61,6 +74,9 @@ class ProjectionTrainerStage1:
         self.log_fn = log_fn
         self.seed = seed
         self.num_workers = num_workers   # decode threads for image datasets (the reference: 2 DataLoader workers, :60)
+        # validation generate (projector_trainer.py:386-393): max_new_tokens 64, do_sample True
+        self.generate_max_new_tokens, self.generate_do_sample = generate_max_new_tokens, generate_do_sample
+        self.generate_seed = generate_seed
         self._pre = None
         if acc.is_main_process:
             os.makedirs(output_dir, exist_ok=True)
@@ -158,8 +174,11 @@ class ProjectionTrainerStage1:
             if acc.is_main_process and self.save_every_n_epochs > 0 and (epoch + 1) % self.save_every_n_epochs == 0:
                 self.save_projection(epoch=epoch + 1)
             if self.val_dataset is not None:
-                vl = self.validation_loss()
-                self._log({"validation/loss": vl, "epoch": epoch + 1}, self.global_step)
+                vl, acc_pct = self.validate(epoch)
+                d = {"validation/loss": vl, "epoch": epoch + 1}
+                if acc_pct is not None:
+                    d["validation/last_word_accuracy"] = acc_pct
+                self._log(d, self.global_step)
                 if vl < best_val:
                     best_val = vl
                     self.save_projection(is_best=True)
@@ -168,14 +187,45 @@ class ProjectionTrainerStage1:
 
     def validation_loss(self):
         """Mean LM loss over the validation set: forward + CE only (no backward, no grad exchange)."""
+        return self.validate(0, generate=False)[0]
+
+    def validate(self, epoch, generate=True):
+        """The reference's validation pass (projector_trainer.py:292-421): per batch the LM loss (forward + CE), and
+        when the tokenizer decodes, generate(inputs_embeds=projected_embeds) -> last-word accuracy against the
+        caption (:378-413).  Returns (mean loss over all ranks' batches, accuracy in % or None)."""
+        tok = self.tokenizer
+        gen = generate and tok is not None and hasattr(tok, "batch_decode") and self.generate_max_new_tokens > 0
         tot, n = torch.zeros(1, device=self.device), 0
-        for batch in self._batches(self.val_dataset, 0, shuffle=False):
-            tot += self.engine.forward_loss(batch["pixel_values"], batch["token_ids"], batch["labels"])
+        correct, total = 0, 0
+        eng = self.engine
+        for bi, batch in enumerate(self._batches(self.val_dataset, 0, shuffle=False)):
+            tot += eng.forward_loss(batch["pixel_values"], batch["token_ids"], batch["labels"])
             n += 1
+            if not gen:
+                continue
+            B = batch["token_ids"].shape[0]
+            # the projected embeddings are the LLM input's first N - 1 rows of each sample (eng.x, [B * Sp, H])
+            ids = self.language_model.generate(
+                eng.x, prompt_len=eng.N - 1, batch=B, max_new_tokens=self.generate_max_new_tokens,
+                do_sample=self.generate_do_sample, pad_token_id=getattr(tok, "pad_token_id", None),
+                eos_token_id=getattr(tok, "eos_token_id", None),
+                seed=self.generate_seed + 1000003 * (epoch + 1) + 7919 * bi + 104729 * self.accelerator.process_index)
+            generated = tok.batch_decode(ids.cpu(), skip_special_tokens=True)
+            reference = tok.batch_decode(batch["token_ids"].cpu().numpy(), skip_special_tokens=True)
+            for ref_text, gen_text in zip(reference, generated):
+                r, g = get_last_word(ref_text), get_last_word(gen_text)
+                if r and g and r == g:
+                    correct += 1
+                total += 1
         cnt = torch.tensor([float(n)], device=self.device)
         self.accelerator.all_reduce_sum_(tot)
         self.accelerator.all_reduce_sum_(cnt)
-        return float(tot / cnt.clamp(min=1))
+        acc_pct = None
+        if gen:
+            c = torch.tensor([float(correct), float(total)], device=self.device)
+            self.accelerator.all_reduce_sum_(c)
+            acc_pct = float(c[0] / c[1].clamp(min=1) * 100.0)
+        return float(tot / cnt.clamp(min=1)), acc_pct
 
     def save_projection(self, epoch=None, is_best=False):
         """projector_{best,epoch_N,final}.bin + projector_config.json (projector_trainer.py:455-521)."""

@@ -69,6 +69,24 @@ int main(int argc, char** argv) {
         const size_t f = ptk_gemma3_workspace_bytes(c, b, t, sp), tr = ptk_gemma3_train_workspace_bytes(c, b, t, sp);
         EXPECT(f > 0 && tr >= f);
       }
+  // the KV-cache decode's layout (prefill rows, per-layer K / V caches, decode rows) and its host-side refusals
+  for (const ptk_gemma3_config* c : {&g1, &g4})
+    for (int b : {1, 32})
+      for (int nt : {1, 64}) {
+        const size_t a = ptk_gemma3_generate_workspace_bytes(c, b, 575, nt);
+        EXPECT(a > 0 && ptk_gemma3_generate_workspace_bytes(c, b, 575, nt + 64) > a);
+      }
+  {
+    ptk_gemma3_generate_desc gd{};
+    gd.batch = 2; gd.prompt_len = 575; gd.max_new_tokens = 64; gd.prompt_batch_stride = 100;   // stride < prompt
+    ptk_gemma3_weights gw{};
+    gw.rope_max_pos = 704;
+    int64_t dummy = 0;
+    EXPECT(ptk_gemma3_generate(&g1, &gw, &gd, (const float*)&dummy, nullptr, &dummy, nullptr, nullptr, 0, nullptr) < 0);
+    gd.prompt_batch_stride = 704; gd.max_new_tokens = 200;                                      // past the rope tables
+    EXPECT(ptk_gemma3_generate(&g1, &gw, &gd, (const float*)&dummy, nullptr, &dummy, nullptr, nullptr, 0, nullptr) < 0);
+    EXPECT(ptk_gemma3_generate(&g1, &gw, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr) < 0);
+  }
   ptk_projector pj{};
   pj.vision_dim = 1024; pj.inter_dim = 4096; pj.llm_dim = 1152;
   for (int rows : {1, 576, 18432}) EXPECT(ptk_projector_workspace_bytes(&pj, rows) > 0);

@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
         assert n in L.SIGNATURES, f"{n} missing from the ctypes binding"
-    assert lib.ptk_abi_version() == L.ABI_VERSION == 6
+    assert lib.ptk_abi_version() == L.ABI_VERSION == 7
 
 
 def test_error_reporting_without_gpu():
