@@ -28,9 +28,12 @@ def roles(cfg):
     attn_g = sum(2 * 2 * attention_pairs(S, t.sliding_window if t.is_sliding(i) else None) * t.head_dim *
                  t.num_attention_heads * B for i in range(L))
     Mp, Ip = B * cfg.num_vision_tokens, cfg.expansion_factor * D   # projector rows (575 per image), hidden
-    # family -> list of (role, launches per step, FLOPs per launch); the r05 dispatch (tests/test_stage1_gpu.py
-    # census): plain bf16 projections on the lean 8-wave kernel with 224- / 192-row tiles (p8_tile_height),
-    # SigLIP fc2 with the stream-K tail + fixup, projector weight grads on the TN kernel, lm_head dX as K slices
+    # family -> list of (role, launches per step, FLOPs per launch); the r06 dispatch (tests/test_stage1_gpu.py
+    # census): plain bf16 projections on the lean 8-wave kernel with 224- / 192- / 160-row tiles (p8_tile_height),
+    # SigLIP fc2 with the stream-K tail + fixup, projector weight grads on the TN kernel, lm_head dX as K slices,
+    # and the last Gemma3 layer's MLP on the B*T loss rows only (gemm_big GEGLU, 160-row p8 for down / dh /
+    # d(gate|up) dX, the standalone GEGLU backward)
+    R = B * T
     return {
         "gemm_p8_kernel<0, 0, false, true, 224>": [
             ("SigLIP q|k|v", Lv, 2 * M_v * D * 3 * D),
@@ -40,15 +43,18 @@ def roles(cfg):
             ("Gemma d(gate|up) dX", L - 1, 2 * M_g * 2 * I * H)],
         "gemm_p8_kernel<0, 0, false, true, 192>": [
             ("Gemma q|k|v", L, 2 * M_g * H * (q + 2 * kv)),
-            ("Gemma dO", L, 2 * M_g * H * q),
-            ("SigLIP o", Lv, 2 * M_v * D * D)],
+            ("Gemma dO", L, 2 * M_g * H * q)],
+        "gemm_p8_kernel<0, 0, false, true, 160>": [("SigLIP o", Lv, 2 * M_v * D * D)],
         "gemm_w4_kernel<3, 0,": [("Gemma gate|up + GEGLU", L - 1, 2 * M_g * 2 * I * H)],
         "gemm_w4_kernel<5, 0,": [("Gemma dh + GEGLU backward", L - 1, 2 * M_g * I * H)],
+        "gemm_big_kernel<3, 0>": [("last layer gate|up + GEGLU (loss rows)", 1, 2 * R * 2 * I * H)],
+        "gemm_p8_kernel<0, 0, false, false, 160>": [("last layer down, dh, d(gate|up) dX (loss rows)", 3,
+                                                     2 * R * I * H * 4 / 3)],
         "gemm_p8_kernel<1, 0": [("SigLIP fc1 + GELU-tanh", Lv, 2 * M_v * D * Iv)],
         "gemm_p8_kernel<0, 0, true, true|p8_fixup_kernel<0, 0>": [("SigLIP fc2 (stream-K tail + fixup)", Lv,
                                                                    2 * M_v * Iv * D)],
         "gemm_p8_kernel<2, 0": [("projector fc1 + GELU-erf", 1, 2 * Mp * D * Ip)],
-        "gemm_p8_kernel<0, 2, true": [("projector fc2", 1, 2 * Mp * Ip * H)],
+        "gemm_p8_kernel<0, 2, true|p8_fixup_kernel<0, 2>": [("projector fc2", 1, 2 * Mp * Ip * H)],
         "gemm_p8_kernel<4, 0": [("projector dA + GELU-erf backward", 1, 2 * Mp * H * Ip)],
         "gemm_tn_kernel<1, false>": [("projector dW1, dW2 (TN)", 2, 2 * Mp * D * Ip)],
         "attn_fwd64_kernel": [("SigLIP attention", Lv, 2 * 2 * N * N * D * B)],
