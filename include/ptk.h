@@ -22,7 +22,7 @@
 extern "C" {
 #endif
 
-#define PTK_ABI_VERSION 7
+#define PTK_ABI_VERSION 8
 
 int ptk_abi_version(void);
 const char* ptk_last_error(void);
@@ -381,6 +381,47 @@ size_t ptk_gemma3_generate_workspace_bytes(const ptk_gemma3_config* c, int batch
 int ptk_gemma3_generate(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_generate_desc* g,
                         const float* prompt_embeds, const int64_t* force_ids, int64_t* out_ids, void* step_logits,
                         void* ws, size_t ws_bytes, void* stream);
+
+/* ------------------------------------------------------------------------ *
+ * Stepwise KV-cache decode (ABI 8): Stage 2's validation generate (Stage2/trainer.py:596-626:            *
+ * generate(inputs_embeds=[projected image tokens | question], attention_mask with the padded question      *
+ * tokens 0, max_new_tokens=512, do_sample=True, num_beams=3, top_p=0.9, top_k=50) -> GenerationMixin.       *
+ * _beam_search).  The prefill runs the prompts once and gives each of its `prompt_repeat` rows (the beams)  *
+ * the prompt's cache and logits; each step feeds one token per row, after re-ordering the cache rows by    *
+ * src_rows (the beams the caller kept: _reorder_cache).  Masked prompt tokens are masked keys and position  *
+ * ids follow HF: cumsum(mask) - 1 over the prompt, then the row's valid count + step - 1.  The workspace    *
+ * holds the caches and the per-row state from the prefill to the last step.                               *
+ * ------------------------------------------------------------------------ */
+typedef struct {
+  int rows;                     /* decode rows = prompts x prompt_repeat */
+  int prompt_len, max_new_tokens;
+  int prompt_repeat;            /* consecutive rows sharing one prompt (num_beams) */
+  int64_t prompt_batch_stride;  /* rows of prompt_embeds between consecutive prompts (>= prompt_len) */
+} ptk_gemma3_decode_desc;
+
+size_t ptk_gemma3_decode_workspace_bytes(const ptk_gemma3_config* c, const ptk_gemma3_decode_desc* d);
+/* prompt_embeds f32 [prompts][prompt_batch_stride][hidden]; prompt_mask int32 [prompts][prompt_mask_ld] (1 = token,
+ * 0 = padding) or NULL (all valid); logits out: bf16 [rows][vocab], the last prompt position of each row's prompt */
+int ptk_gemma3_decode_prefill(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_decode_desc* d,
+                              const float* prompt_embeds, const int32_t* prompt_mask, int64_t prompt_mask_ld,
+                              void* logits, void* ws, size_t ws_bytes, void* stream);
+/* step 1 .. max_new_tokens - 1: ids int64 [rows] (the token each row appends), src_rows int32 [rows] or NULL (row r
+ * continues from row src_rows[r]'s cache before the token is appended); logits out: bf16 [rows][vocab] */
+int ptk_gemma3_decode_step(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_decode_desc* d,
+                           int step, const int64_t* ids, const int32_t* src_rows, void* logits, void* ws,
+                           size_t ws_bytes, void* stream);
+/* One beam-search selection (transformers GenerationMixin._get_top_k_continuations) for `batch` items of `beams`
+ * rows: log_softmax of the bf16 logits [batch * beams][ld]; with do_sample the warpers on the log probs in HF's
+ * order (temperature, top-k keeping ties and at least min_tokens_to_keep, top-p keeping min_tokens_to_keep; top_k
+ * in 1..512 when sampling), + beam_scores[row]; then per item n_cand (<= 32) candidates over beams x vocab:
+ * do_sample -> drawn without replacement from softmax(accumulated) (the n_cand largest accumulated + Gumbel noise
+ * of (seed, step, row, token): torch.multinomial's distribution; order = draw order), else the n_cand largest
+ * (descending).  Out [batch][n_cand]: token, beam (0..beams-1) and accumulated log prob; fewer candidates than
+ * n_cand with a finite score leave token -1. */
+int ptk_beam_candidates(const void* logits, int64_t ld, const float* beam_scores, int batch, int beams, int vocab,
+                        int do_sample, int top_k, float top_p, float temperature, int min_tokens_to_keep,
+                        uint64_t seed, int step, int n_cand, int64_t* tokens, int32_t* beam_idx, float* scores,
+                        void* stream);
 
 /* clip_grad_norm_ + AdamW over bf16 parameters (Stage2/trainer.py:426-443, optimizer :145-149).
  * ptk_bf16_grad_scale_sumsq: g = bf16(g * scale) in place (scale 1: untouched), *out = sum g^2 (fp32,

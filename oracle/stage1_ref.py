@@ -110,18 +110,24 @@ def attention_mask_4d(attention_mask, sliding_window: int | None):
     return m[None, None] & attention_mask.bool()[:, None, None, :]
 
 
-def gemma3_forward(p, cfg: Gemma3TextConfig, inputs_embeds, attention_mask, dtype=torch.float32):
+def gemma3_forward(p, cfg: Gemma3TextConfig, inputs_embeds, attention_mask, dtype=torch.float32, position_ids=None):
     """`Gemma3TextModel.forward` with inputs_embeds (:511-578); decoder layer
     :399-429 (sandwich norms), attention :341-383 (q/k RMSNorm, RoPE, GQA via
     repeat_kv, scale query_pre_attn_scalar**-0.5), gated GELU-tanh MLP :131-133.
-    position_ids = arange(S) (not pad-adjusted).  Returns the final-norm output."""
+    position_ids = arange(S) (not pad-adjusted; the training forward), or [B, S] (generate: HF derives them from the
+    attention mask).  Returns the final-norm output."""
     W = lambda n: _t(p, n, dtype)
     x = inputs_embeds.to(dtype)
     B, S, Hd = x.shape
     hd, nq, nkv = cfg.head_dim, cfg.num_attention_heads, cfg.num_key_value_heads
     eps = cfg.rms_norm_eps
     scale = cfg.query_pre_attn_scalar ** -0.5
-    rope = {s: rope_cos_sin(cfg, S, s) for s in (True, False)}
+    if position_ids is None:
+        rope = {s: rope_cos_sin(cfg, S, s) for s in (True, False)}
+    else:
+        pid = torch.as_tensor(position_ids).long()
+        n = int(pid.max()) + 1
+        rope = {s: tuple(t[pid][:, None] for t in rope_cos_sin(cfg, n, s)) for s in (True, False)}
     masks = {True: attention_mask_4d(attention_mask, cfg.sliding_window),
              False: attention_mask_4d(attention_mask, None)}
     for i in range(cfg.num_hidden_layers):

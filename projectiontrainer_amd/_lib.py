@@ -113,6 +113,11 @@ class Gemma3GenerateC(C.Structure):
                 ("pad_token_id", c_int64), ("prompt_batch_stride", c_int64)]
 
 
+class Gemma3DecodeC(C.Structure):
+    _fields_ = [("rows", c_int), ("prompt_len", c_int), ("max_new_tokens", c_int), ("prompt_repeat", c_int),
+                ("prompt_batch_stride", c_int64)]
+
+
 class Gemma3LayerGradsC(C.Structure):
     _fields_ = [(n, c_void_p) for n in ("wqkv", "wo", "wgu", "wd", "ln_in", "ln_post_attn", "ln_pre_ff",
                                         "ln_post_ff", "q_norm", "k_norm")]
@@ -128,7 +133,7 @@ class ImageDesc(C.Structure):
                 ("coef_off", c_int64), ("tmp_off", c_int64)]
 
 
-ABI_VERSION = 7      # include/ptk.h PTK_ABI_VERSION
+ABI_VERSION = 8      # include/ptk.h PTK_ABI_VERSION
 
 # exported symbol -> (restype, argtypes)
 SIGNATURES = {
@@ -185,6 +190,14 @@ SIGNATURES = {
     "ptk_gemma3_generate_workspace_bytes": (c_size_t, [C.POINTER(Gemma3ConfigC), c_int, c_int, c_int]),
     "ptk_gemma3_generate": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC), C.POINTER(Gemma3GenerateC),
                                     c_void_p, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "ptk_gemma3_decode_workspace_bytes": (c_size_t, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3DecodeC)]),
+    "ptk_gemma3_decode_prefill": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC),
+                                          C.POINTER(Gemma3DecodeC), c_void_p, c_void_p, c_int64, c_void_p, c_void_p,
+                                          c_size_t, c_void_p]),
+    "ptk_gemma3_decode_step": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC), C.POINTER(Gemma3DecodeC),
+                                       c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "ptk_beam_candidates": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
+                                    c_int, c_uint64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
     "ptk_bf16_sumsq_partial_floats": (c_int, []),
     "ptk_bf16_grad_scale_sumsq": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p]),
     "ptk_adamw_bf16": (c_int, [c_void_p] * 4 + [c_int64, c_void_p, c_float] + [C.c_double] * 5 +

@@ -31,11 +31,12 @@ __global__ void __launch_bounds__(256) qknorm_rope_fwd_kernel(const bf16_t* __re
   const int b = (int)(m / sh.S), s = (int)(m - (long)b * sh.S);
   const int G = sh.Hq / sh.Hkv;
   const int fi = (lane & 31) * EPL;   // frequency index (cos[i] == cos[i + D/2])
+  const long ps = sh.pos ? (long)sh.pos[m] : (long)s;   // the generate path's position ids
   float cs[EPL], sn[EPL], wq[EPL], wk[EPL];
 #pragma unroll
   for (int e = 0; e < EPL; ++e) {
-    cs[e] = cos_t[(long)s * (D / 2) + fi + e];
-    sn[e] = sin_t[(long)s * (D / 2) + fi + e];
+    cs[e] = cos_t[ps * (D / 2) + fi + e];
+    sn[e] = sin_t[ps * (D / 2) + fi + e];
     wq[e] = 1.f + qw[lane * EPL + e];
     wk[e] = 1.f + kw[lane * EPL + e];
   }

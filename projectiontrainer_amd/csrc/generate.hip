@@ -193,3 +193,341 @@ int launch_gen_sample(const bf16_t* logits, long ld, int B, int V, int do_sample
 }
 
 }  // namespace ptk
+
+// ================================================================== stepwise decode (beam search)
+// The pieces of ptk_gemma3_decode_prefill / _step (models.cpp): Stage 2's validation generate
+// (Stage2/trainer.py:596-626: inputs_embeds = [projected image tokens | question], attention_mask with the padded
+// question tokens 0, num_beams 3, do_sample, top_k 50, top_p 0.9) needs per-row prompt masks, the position ids HF
+// derives from them (GenerationMixin._prepare_position_ids_for_generation: cumsum(mask) - 1, masked -> 0), and the
+// cache rows re-ordered by the selected beams every step.
+
+namespace ptk {
+
+// prompt p = r / repeat -> decode row r: x rows r*Pp + i (i < P from src, else 0); key flag = (i < P) & mask[p][i]
+__global__ void __launch_bounds__(256) dec_prompt_kernel(const float* __restrict__ src, long ld_b,
+                                                         const int32_t* __restrict__ mask, long mask_ld, int repeat,
+                                                         int P, int Pp, int H, float* __restrict__ x,
+                                                         int32_t* __restrict__ kv) {
+  const long row = blockIdx.x;
+  const int r = (int)(row / Pp), i = (int)(row - (long)r * Pp), pr = r / repeat;
+  const bool in = i < P;
+  if (threadIdx.x == 0) kv[row] = in && (!mask || mask[(long)pr * mask_ld + i] != 0);
+  float* xr = x + row * H;
+  const float* sr = src + ((long)pr * ld_b + (in ? i : 0)) * H;
+  for (int c = threadIdx.x * 4; c < H; c += 1024)
+    *reinterpret_cast<float4*>(xr + c) = in ? *reinterpret_cast<const float4*>(sr + c) : make_float4(0, 0, 0, 0);
+}
+
+// one wave per decode row: position ids of the prompt slots (cumsum of the key flags - 1, 0 where masked), the
+// row's slot-valid flags for the cache (slots < P), its valid count (the next position)
+__global__ void __launch_bounds__(64) dec_positions_kernel(const int32_t* __restrict__ kv, int P, int Pp, int Smax,
+                                                           int32_t* __restrict__ pos, int32_t* __restrict__ slot_ok,
+                                                           int32_t* __restrict__ nvalid) {
+  const int r = blockIdx.x, lane = threadIdx.x;
+  int base = 0;
+  for (int i0 = 0; i0 < Pp; i0 += 64) {
+    const int i = i0 + lane;
+    const int v = i < Pp ? kv[(long)r * Pp + i] : 0;
+    const uint64_t m = __ballot(v != 0);
+    const int before = __popcll(m & ((1ull << lane) - 1ull));
+    if (i < Pp) pos[(long)r * Pp + i] = v ? base + before : 0;
+    if (i < P) slot_ok[(long)r * Smax + i] = v;
+    base += __popcll(m);
+  }
+  for (int i = P + lane; i < Smax; i += 64) slot_ok[(long)r * Smax + i] = 0;
+  if (lane == 0) nvalid[r] = base;
+}
+
+// decode step t (slot p0 = P + t - 1): the new token's slot becomes valid, its position is the row's valid count
+// + t - 1, and the key flags of cache slots [k_lo, k_lo + nk) (nk a multiple of 4, slots past p0 masked) are
+// copied out contiguous for the attention call
+__global__ void __launch_bounds__(256) dec_step_prep_kernel(int32_t* __restrict__ slot_ok, const int32_t* __restrict__ nvalid,
+                                                            int Smax, int p0, int t, int k_lo, int nk,
+                                                            int32_t* __restrict__ pos, int32_t* __restrict__ kmask) {
+  const int r = blockIdx.x;
+  const int32_t* so = slot_ok + (long)r * Smax;
+  for (int j = threadIdx.x; j < nk; j += 256) {
+    const int s = k_lo + j;
+    kmask[(long)r * nk + j] = s < p0 ? so[s] : (s == p0 ? 1 : 0);
+  }
+  if (threadIdx.x == 0) {
+    slot_ok[(long)r * Smax + p0] = 1;
+    pos[r] = nvalid[r] + t - 1;
+  }
+}
+
+// out row r = in row src[r] (16-B chunks; rows of `row_bytes`, a multiple of 16)
+__global__ void __launch_bounds__(256) dec_gather_rows_kernel(const uint4* __restrict__ in, uint4* __restrict__ out,
+                                                              const int32_t* __restrict__ src, long chunks_per_row,
+                                                              long total) {
+  const long i = (long)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const long r = i / chunks_per_row, c = i - r * chunks_per_row;
+  out[i] = in[(long)src[r] * chunks_per_row + c];
+}
+
+int launch_dec_prompt(const float* src, long ld_b, const int32_t* mask, long mask_ld, int repeat, int rows, int P,
+                      int Pp, int H, float* x, int32_t* kv, hipStream_t st) {
+  if (H % 4 || P > Pp || repeat < 1) return set_error("decode: prompt layout (H %% 4, P <= Pp, repeat >= 1)");
+  hipLaunchKernelGGL(dec_prompt_kernel, dim3((unsigned)((long)rows * Pp)), dim3(256), 0, st, src, ld_b, mask, mask_ld,
+                     repeat, P, Pp, H, x, kv);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("dec_prompt launch failed");
+}
+int launch_dec_positions(const int32_t* kv, int rows, int P, int Pp, int Smax, int32_t* pos, int32_t* slot_ok,
+                         int32_t* nvalid, hipStream_t st) {
+  hipLaunchKernelGGL(dec_positions_kernel, dim3((unsigned)rows), dim3(64), 0, st, kv, P, Pp, Smax, pos, slot_ok, nvalid);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("dec_positions launch failed");
+}
+int launch_dec_step_prep(int32_t* slot_ok, const int32_t* nvalid, int rows, int Smax, int p0, int t, int k_lo, int nk,
+                         int32_t* pos, int32_t* kmask, hipStream_t st) {
+  if (nk % 4 || k_lo + nk > Smax || p0 >= Smax) return set_error("decode: step layout (nk %d, k_lo %d, p0 %d)", nk, k_lo, p0);
+  hipLaunchKernelGGL(dec_step_prep_kernel, dim3((unsigned)rows), dim3(256), 0, st, slot_ok, nvalid, Smax, p0, t, k_lo,
+                     nk, pos, kmask);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("dec_step_prep launch failed");
+}
+int launch_dec_gather_rows(const void* in, void* out, const int32_t* src, int rows, long row_bytes, hipStream_t st) {
+  if (row_bytes % 16) return set_error("decode: gathered rows must be multiples of 16 B");
+  const long cpr = row_bytes / 16, total = cpr * rows;
+  if (total <= 0) return 0;
+  hipLaunchKernelGGL(dec_gather_rows_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st,
+                     (const uint4*)in, (uint4*)out, src, cpr, total);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("dec_gather_rows launch failed");
+}
+
+__global__ void __launch_bounds__(256) dec_gather_i32_kernel(const int32_t* __restrict__ in, int32_t* __restrict__ out,
+                                                              const int32_t* __restrict__ src, int rows) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r < rows) out[r] = in[src[r]];
+}
+__global__ void __launch_bounds__(256) dec_repeat_index_kernel(int32_t* __restrict__ src, int rows, int repeat) {
+  const int r = blockIdx.x * 256 + threadIdx.x;
+  if (r < rows) src[r] = r / repeat;
+}
+int launch_dec_gather_i32(const int32_t* in, int32_t* out, const int32_t* src, int rows, hipStream_t st) {
+  hipLaunchKernelGGL(dec_gather_i32_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, in, out, src, rows);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("dec_gather_i32 launch failed");
+}
+int launch_dec_repeat_index(int32_t* src, int rows, int repeat, hipStream_t st) {
+  hipLaunchKernelGGL(dec_repeat_index_kernel, dim3((unsigned)((rows + 255) / 256)), dim3(256), 0, st, src, rows, repeat);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("dec_repeat_index launch failed");
+}
+
+// ------------------------------------------------------------------ beam candidates
+// GenerationMixin._beam_search, one step (b, c of its loop: transformers/generation/utils.py _get_top_k_continuations):
+// per decode row (batch item b, beam k) log_probs = log_softmax(fp32 logits); with do_sample the warpers act on
+// them in HF's order -- temperature (/T), top-k (keep >= the k-th largest, k = max(top_k, min_keep)), top-p (sort
+// ascending, cumulative softmax, drop where <= 1 - top_p, keep the last min_keep) -- the rest -inf; + the beam's
+// running score; then over the beams x vocab of item b:
+//   do_sample: n_cand draws without replacement from softmax(accumulated) (torch.multinomial), taken as the
+//              n_cand largest accumulated + Gumbel noise (the same distribution; order = draw order);
+//   greedy:    the n_cand largest accumulated (torch.topk, descending).
+// Out per item: tokens, beam (0..K-1) and the accumulated log prob (without the noise) of each candidate.
+constexpr int BC_T = 1024;     // threads per item
+constexpr int BC_LIST = 1024;  // kept entries per row (top-k with ties); more -> error flag (token -1)
+
+PTK_DEV float bc_gumbel(uint64_t seed, int step, int row, int tok) {
+  uint64_t z = seed ^ (0x9e3779b97f4a7c15ull * (uint64_t)(1 + step));
+  z += 0xbf58476d1ce4e5b9ull * (uint64_t)(1 + row) + 0x94d049bb133111ebull * (uint64_t)(1 + tok);
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  z ^= z >> 31;
+  const float u = ((float)(z >> 40) + 0.5f) * (1.0f / 16777216.0f);   // (0, 1)
+  return -__logf(-__logf(u));
+}
+
+__global__ void __launch_bounds__(BC_T) beam_cand_kernel(const bf16_t* __restrict__ logits, long ld,
+                                                         const float* __restrict__ beam_scores, int K, int V,
+                                                         int do_sample, int top_k, float top_p, float temperature,
+                                                         int min_keep, uint64_t seed, int step, int n_cand,
+                                                         int64_t* __restrict__ out_tok, int32_t* __restrict__ out_beam,
+                                                         float* __restrict__ out_score) {
+  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  constexpr int NW = BC_T / 64;
+  __shared__ uint32_t hist[256];
+  __shared__ float redf[NW];
+  __shared__ int redi[NW];
+  __shared__ uint32_t sel[2];
+  __shared__ int cnt;
+  __shared__ float ls[BC_LIST];      // kept entries of the row: log prob (processed)
+  __shared__ int lt[BC_LIST];        //                              token
+  __shared__ float best_key[32], best_acc[32];
+  __shared__ int best_tok[32], best_beam[32];
+  __shared__ int nbest;
+  if (tid == 0) nbest = 0;
+  const float inv_t = (do_sample && temperature > 0.f) ? 1.f / temperature : 1.f;
+  int bad = 0;
+  for (int k = 0; k < K; ++k) {
+    const int rowi = b * K + k;
+    const uint16_t* row = reinterpret_cast<const uint16_t*>(logits) + (long)rowi * ld;
+    // log_softmax statistics (fp32 over the bf16 logits)
+    float mx = -INFINITY;
+    for (int i = tid; i < V; i += BC_T) mx = fmaxf(mx, bf2f(row[i]));
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+    if (lane == 0) redf[wave] = mx;
+    __syncthreads();
+    mx = redf[0];
+    for (int w = 1; w < NW; ++w) mx = fmaxf(mx, redf[w]);
+    __syncthreads();
+    float se = 0.f;
+    for (int i = tid; i < V; i += BC_T) se += __expf(bf2f(row[i]) - mx);
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) se += __shfl_xor(se, o, 64);
+    if (lane == 0) redf[wave] = se;
+    __syncthreads();
+    se = 0.f;
+    for (int w = 0; w < NW; ++w) se += redf[w];
+    const float lse = mx + __logf(se);
+    __syncthreads();
+    // the row's kept set: the kk largest logits (ties kept) -- log_softmax and /T preserve the order
+    const int kk = do_sample ? (top_k > 0 ? max(top_k, min_keep) : V) : n_cand;
+    uint32_t thr = 0;
+    if (kk < V) {
+      uint32_t need = (uint32_t)kk, hi = 0;
+      for (int pass = 0; pass < 2; ++pass) {
+        for (int i = tid; i < 256; i += BC_T) hist[i] = 0;
+        __syncthreads();
+        for (int i = tid; i < V; i += BC_T) {
+          const uint32_t key = bf_key(row[i]);
+          if (pass == 0) atomicAdd(&hist[key >> 8], 1u);
+          else if ((key >> 8) == hi) atomicAdd(&hist[key & 255u], 1u);
+        }
+        __syncthreads();
+        if (tid == 0) {
+          uint32_t acc = 0;
+          int bin = 255;
+          for (; bin > 0; --bin) {
+            if (acc + hist[bin] >= need) break;
+            acc += hist[bin];
+          }
+          sel[0] = (uint32_t)bin;
+          sel[1] = need - acc;
+        }
+        __syncthreads();
+        if (pass == 0) { hi = sel[0]; need = sel[1]; }
+        else thr = (hi << 8) | sel[0];
+        __syncthreads();
+      }
+    }
+    if (tid == 0) cnt = 0;
+    __syncthreads();
+    for (int i = tid; i < V; i += BC_T) {
+      const uint16_t u = row[i];
+      if (bf_key(u) >= thr) {
+        const int slot = atomicAdd(&cnt, 1);
+        if (slot < BC_LIST) { ls[slot] = (bf2f(u) - lse) * inv_t; lt[slot] = i; }
+      }
+    }
+    __syncthreads();
+    int n = cnt;
+    if (n > BC_LIST) { bad = 1; n = BC_LIST; }
+    // top-p over the kept entries: bitonic sort ascending by score (then token), cumulative softmax
+    if (do_sample && top_p < 1.f) {
+      int np2 = 1;
+      while (np2 < n) np2 <<= 1;
+      for (int i = n + tid; i < np2; i += BC_T) { ls[i] = INFINITY; lt[i] = 0x7fffffff; }
+      __syncthreads();
+      for (int size = 2; size <= np2; size <<= 1)
+        for (int stride = size >> 1; stride > 0; stride >>= 1) {
+          for (int i = tid; i < np2; i += BC_T) {
+            const int j = i ^ stride;
+            if (j > i) {
+              const bool up = (i & size) == 0;
+              const float a = ls[i], c = ls[j];
+              const bool gt = a > c || (a == c && lt[i] > lt[j]);
+              if (gt == up) { ls[i] = c; ls[j] = a; const int tt = lt[i]; lt[i] = lt[j]; lt[j] = tt; }
+            }
+          }
+          __syncthreads();
+        }
+      if (tid == 0) {   // (n <= 1024 entries, once per row and step)
+        const float top = ls[n - 1];
+        float tot = 0.f;
+        for (int i = 0; i < n; ++i) tot += __expf(ls[i] - top);
+        float cum = 0.f;
+        int first = 0;
+        for (int i = 0; i < n; ++i) {
+          cum += __expf(ls[i] - top);
+          if (cum / tot <= 1.f - top_p) first = i + 1;
+        }
+        first = min(first, max(0, n - min_keep));
+        cnt = first;   // kept: [first, n)
+      }
+      __syncthreads();
+    } else if (tid == 0) {
+      cnt = 0;
+    }
+    __syncthreads();
+    const int first = cnt;
+    // candidates of this row: accumulated = processed log prob + the beam's score; selection key (+ Gumbel noise)
+    const float bs = beam_scores[rowi];
+    for (int i = first + tid; i < n; i += BC_T) {
+      const float acc = ls[i] + bs;
+      ls[i] = acc;
+    }
+    __syncthreads();
+    // merge into the item's running best n_cand: n_cand rounds of an arg-max over this row's entries
+    for (int rnd = 0; rnd < n_cand; ++rnd) {
+      float bk = -INFINITY;
+      int bi = -1;
+      for (int i = first + tid; i < n; i += BC_T) {
+        if (lt[i] < 0) continue;   // taken
+        const float key = do_sample ? ls[i] + bc_gumbel(seed, step, rowi, lt[i]) : ls[i];
+        if (key > bk || (key == bk && (bi < 0 || lt[i] < lt[bi]))) { bk = key; bi = i; }
+      }
+#pragma unroll
+      for (int o = 32; o >= 1; o >>= 1) {
+        const float ok = __shfl_xor(bk, o, 64);
+        const int oi = __shfl_xor(bi, o, 64);
+        if (ok > bk || (ok == bk && oi >= 0 && (bi < 0 || lt[oi] < lt[bi]))) { bk = ok; bi = oi; }
+      }
+      if (lane == 0) { redf[wave] = bk; redi[wave] = bi; }
+      __syncthreads();
+      if (tid == 0) {
+        float k0 = redf[0];
+        int i0 = redi[0];
+        for (int w = 1; w < NW; ++w)
+          if (redf[w] > k0 || (redf[w] == k0 && redi[w] >= 0 && (i0 < 0 || lt[redi[w]] < lt[i0]))) { k0 = redf[w]; i0 = redi[w]; }
+        if (i0 >= 0 && k0 > -INFINITY) {
+          // insert into the running list (descending by key), keep n_cand
+          int m = nbest;
+          int pos = m;
+          while (pos > 0 && best_key[pos - 1] < k0) --pos;
+          if (pos < n_cand) {
+            for (int q = min(m, n_cand - 1); q > pos; --q) {
+              best_key[q] = best_key[q - 1]; best_acc[q] = best_acc[q - 1];
+              best_tok[q] = best_tok[q - 1]; best_beam[q] = best_beam[q - 1];
+            }
+            best_key[pos] = k0; best_acc[pos] = ls[i0]; best_tok[pos] = lt[i0]; best_beam[pos] = k;
+            nbest = min(m + 1, n_cand);
+          }
+          lt[i0] = -1;
+        }
+      }
+      __syncthreads();
+    }
+    __syncthreads();
+  }
+  if (tid < n_cand) {
+    const bool ok = tid < nbest && !bad;
+    out_tok[(long)b * n_cand + tid] = ok ? best_tok[tid] : -1;
+    out_beam[(long)b * n_cand + tid] = ok ? best_beam[tid] : -1;
+    out_score[(long)b * n_cand + tid] = ok ? best_acc[tid] : -INFINITY;
+  }
+}
+
+int launch_beam_candidates(const bf16_t* logits, long ld, const float* beam_scores, int batch, int K, int V,
+                           int do_sample, int top_k, float top_p, float temperature, int min_keep, uint64_t seed,
+                           int step, int n_cand, int64_t* tok, int32_t* beam, float* score, hipStream_t st) {
+  if (batch <= 0 || K <= 0 || V <= 0 || n_cand <= 0 || n_cand > 32)
+    return set_error("beam_candidates: batch %d, beams %d, vocab %d, n_cand %d (1..32)", batch, K, V, n_cand);
+  if (do_sample && !(temperature > 0.f)) return set_error("beam_candidates: temperature must be > 0 when sampling");
+  if (do_sample && !(top_p > 0.f && top_p <= 1.f)) return set_error("beam_candidates: top_p must be in (0, 1]");
+  if (do_sample && !(top_k > 0 && top_k <= BC_LIST / 2) && V > BC_LIST / 2)
+    return set_error("beam_candidates: sampling needs 0 < top_k <= %d (the kept set lives in LDS)", BC_LIST / 2);
+  hipLaunchKernelGGL(beam_cand_kernel, dim3((unsigned)batch), dim3(BC_T), 0, st, logits, ld, beam_scores, K, V,
+                     do_sample, top_k, top_p, temperature, min_keep, seed, step, n_cand, tok, beam, score);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("beam_candidates launch failed");
+}
+
+}  // namespace ptk

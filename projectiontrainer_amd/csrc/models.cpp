@@ -802,17 +802,27 @@ GenWs gen_layout(Bump& bp, const ptk_gemma3_config* c, int B, int P, int max_new
 // padded prompt, 1 for a decode step): x_in -> x_out (fp32), the layer's K / V appended to the cache at p0, the
 // queries attending cache keys [k_lo, p0 + S) (prefill: causal + window over its own rows, decode: the window
 // start k_lo); xn holds the layer's input norm on entry and the next layer's on exit (w_next: none -> untouched)
+// The stepwise decode's extras (DecMasks, null for ptk_gemma3_generate): RoPE positions per token (pos: the prefill's
+// cumsum positions, a decode step's per-row position) and the decode step's key flags over cache slots
+// [k_lo, k_lo + nk) for sliding (0) and full (1) layers.
+struct DecMasks {
+  const int32_t* pos;
+  const int32_t* kmask[2];
+  int k_lo[2], nk[2];
+};
 int gen_layer(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, int l, GenPass& g, const float* x_in,
               float* x_out, int B, int S, int Sp, int p0, bool prefill, int Smax, bf16_t* kc, bf16_t* vc,
-              hipStream_t st) {
+              hipStream_t st, const DecMasks* dm = nullptr) {
   const ptk_gemma3_layer& L = wt->layers[l];
   const int H = c->hidden, I = c->inter, D = c->head_dim, Hq = c->heads, Hkv = c->kv_heads, G = Hq / Hkv;
   const int M = B * Sp, Dq = Hq * D, Dqkv = (Hq + 2 * Hkv) * D, Z = B * Hkv;
   const bool sliding = (l + 1) % c->sliding_pattern != 0;
-  const float* cs = (sliding ? wt->rope_cos_local : wt->rope_cos_global) + (long)p0 * (D / 2);
-  const float* sn = (sliding ? wt->rope_sin_local : wt->rope_sin_global) + (long)p0 * (D / 2);
+  const long pofs = (dm && dm->pos) ? 0 : (long)p0 * (D / 2);   // per-token positions index the whole table
+  const float* cs = (sliding ? wt->rope_cos_local : wt->rope_cos_global) + pofs;
+  const float* sn = (sliding ? wt->rope_sin_local : wt->rope_sin_global) + pofs;
   CK(launch_gemm(gemm(g.xn, H, L.wqkv, H, g.qkv, Dqkv, M, Dqkv, H), ACT_NONE, OUT_BF16, 1, st));
   AttnShape ash{B, Sp, Hq, Hkv, D};
+  if (dm) ash.pos = dm->pos;
   CK(launch_qknorm_rope_fwd(g.qkv, L.q_norm, L.k_norm, cs, sn, ash, c->eps, g.Q, g.K, g.V, g.rq, g.rk, st));
   CK(launch_kv_append(g.K, (long)Sp * D, kc, (long)Smax * D, Z, p0, S, D, st));
   CK(launch_kv_append(g.V, (long)Sp * D, vc, (long)Smax * D, Z, p0, S, D, st));
@@ -833,6 +843,11 @@ int gen_layer(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, int l, G
       fa.sK0 = (long)Hkv * Sp * D; fa.sK1 = (long)Sp * D;
       fa.nkeys = Sp; fa.causal = 1; fa.window = sliding ? c->sliding_window : 0;
       fa.key_valid = g.kv;
+    } else if (dm) {  // one query per row against cache slots [k_lo, k_lo + nk), the row's key flags
+      const int w = sliding ? 0 : 1;
+      fa.K = kc + (long)dm->k_lo[w] * D; fa.V = vc + (long)dm->k_lo[w] * D;
+      fa.nkeys = dm->nk[w]; fa.causal = 0; fa.window = 0;
+      fa.key_valid = dm->kmask[w];
     } else {         // one query position p0 against cache keys [k_lo, p0]
       const int k_lo = (sliding && c->sliding_window > 0) ? std::max(0, p0 - c->sliding_window + 1) : 0;
       fa.K = kc + (long)k_lo * D; fa.V = vc + (long)k_lo * D;
@@ -913,9 +928,186 @@ int gemma_generate(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, con
   return 0;
 }
 
+// ------------------------------------------------------------------ stepwise decode (beam search)
+// The stepwise form of the decode: ptk_gemma3_decode_prefill once, then ptk_gemma3_decode_step per token, the
+// caller choosing the tokens and (beam search) the cache rows each step takes from.  The workspace carries the
+// caches and per-row state between calls.  Rows = prompts x repeat (beams): the prefill runs on the prompts and
+// copies each one's caches, flags and logits to its `repeat` rows (GenerationMixin._expand_inputs_for_generation).
+struct DecWs {
+  GenPass pre, dec;
+  std::vector<bf16_t*> kc, vc;     // per layer [rows, Hkv, Smax, D]
+  bf16_t *tmp, *xf, *logits_pre;   // tmp: one cache tensor (row gathers)
+  float* rstd_f;
+  int32_t *pos_pre, *pos_dec, *slot_ok, *slot_tmp, *nvalid, *nvalid_tmp, *kmask[2], *rep_src;
+  void* tail;
+  int Pp, Smax, prompts;
+};
+DecWs dec_layout(Bump& bp, const ptk_gemma3_config* c, const ptk_gemma3_decode_desc* d) {
+  DecWs w;
+  const int rows = d->rows, P = d->prompt_len, R = d->prompt_repeat;
+  w.prompts = R > 0 ? rows / R : rows;
+  w.Pp = (P + 63) / 64 * 64;
+  w.Smax = (P + d->max_new_tokens + 4 + 63) / 64 * 64;   // + 4: a step's key window rounds up to 4 slots
+  const long Z = (long)rows * c->kv_heads, D = c->head_dim, cache = Z * w.Smax * D;
+  w.pre = gen_pass(bp, c, (long)w.prompts * w.Pp);
+  w.dec = gen_pass(bp, c, rows);
+  for (int l = 0; l < c->layers; ++l) {
+    w.kc.push_back(bp.take<bf16_t>(cache));
+    w.vc.push_back(bp.take<bf16_t>(cache));
+  }
+  w.tmp = bp.take<bf16_t>(cache);
+  w.xf = bp.take<bf16_t>((long)rows * c->hidden);
+  w.logits_pre = bp.take<bf16_t>((long)w.prompts * c->vocab);
+  w.rstd_f = bp.take<float>(rows);
+  w.pos_pre = bp.take<int32_t>((long)w.prompts * w.Pp);
+  w.pos_dec = bp.take<int32_t>(rows);
+  w.slot_ok = bp.take<int32_t>((long)rows * w.Smax);
+  w.slot_tmp = bp.take<int32_t>((long)rows * w.Smax);
+  w.nvalid = bp.take<int32_t>(rows + 4);
+  w.nvalid_tmp = bp.take<int32_t>(rows + 4);
+  w.kmask[0] = bp.take<int32_t>((long)rows * w.Smax);
+  w.kmask[1] = bp.take<int32_t>((long)rows * w.Smax);
+  w.rep_src = bp.take<int32_t>(rows);
+  w.tail = bp.take<char>(p8_tail_scratch_bytes_models());
+  return w;
+}
+int dec_check(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_decode_desc* d, size_t ws_bytes) {
+  if (!c || !wt || !d) return set_error("decode: NULL argument");
+  const int rows = d->rows, P = d->prompt_len, NT = d->max_new_tokens, R = d->prompt_repeat;
+  if (rows <= 0 || R <= 0 || rows % R || P < 4 || NT <= 0)
+    return set_error("decode: rows %d, prompt_repeat %d (divides rows), prompt_len %d (>= 4), max_new_tokens %d", rows,
+                     R, P, NT);
+  if (d->prompt_batch_stride < P) return set_error("decode: prompt_batch_stride %ld < prompt_len %d",
+                                                   (long)d->prompt_batch_stride, P);
+  if (P + NT > wt->rope_max_pos || (P + 63) / 64 * 64 > wt->rope_max_pos)
+    return set_error("decode: %d positions exceed the rope tables (%d)", P + NT, wt->rope_max_pos);
+  if (c->heads % c->kv_heads) return set_error("decode: heads %% kv_heads");
+  if (ws_bytes < ptk_gemma3_decode_workspace_bytes(c, d)) return set_error("decode: workspace too small");
+  return 0;
+}
+// every cache row r <- row src[r] (through tmp), and the rows' slot flags and valid counts
+int dec_gather(const ptk_gemma3_config* c, DecWs& w, const int32_t* src, int rows, hipStream_t st) {
+  const long row_bytes = (long)c->kv_heads * w.Smax * c->head_dim * 2;
+  for (int l = 0; l < c->layers; ++l)
+    for (bf16_t* t : {w.kc[l], w.vc[l]}) {
+      CK(launch_dec_gather_rows(t, w.tmp, src, rows, row_bytes, st));
+      CKH(hipMemcpyAsync(t, w.tmp, (size_t)rows * row_bytes, hipMemcpyDeviceToDevice, st));
+    }
+  CK(launch_dec_gather_rows(w.slot_ok, w.slot_tmp, src, rows, (long)w.Smax * 4, st));
+  CKH(hipMemcpyAsync(w.slot_ok, w.slot_tmp, (size_t)rows * w.Smax * 4, hipMemcpyDeviceToDevice, st));
+  CK(launch_dec_gather_i32(w.nvalid, w.nvalid_tmp, src, rows, st));
+  CKH(hipMemcpyAsync(w.nvalid, w.nvalid_tmp, (size_t)rows * 4, hipMemcpyDeviceToDevice, st));
+  return 0;
+}
+int gemma_decode_prefill(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_decode_desc* d,
+                         const float* prompt, const int32_t* mask, long mask_ld, bf16_t* logits, void* ws,
+                         size_t ws_bytes, hipStream_t st) {
+  CK(dec_check(c, wt, d, ws_bytes));
+  const int rows = d->rows, P = d->prompt_len, R = d->prompt_repeat, H = c->hidden, V = c->vocab;
+  Bump bp(ws);
+  DecWs w = dec_layout(bp, c, d);
+  const int Bp = w.prompts, Pp = w.Pp, Smax = w.Smax;
+  TailScratchScope tail(w.tail, st);
+  CK(tail.status);
+  const long cache_bytes = (long)rows * c->kv_heads * Smax * c->head_dim * 2;
+  for (int l = 0; l < c->layers; ++l) {   // slots past a step's position are read (masked) by the key window
+    CK(launch_zero(w.kc[l], (size_t)cache_bytes, st));
+    CK(launch_zero(w.vc[l], (size_t)cache_bytes, st));
+  }
+  GenPass& g = w.pre;
+  CK(launch_dec_prompt(prompt, (long)d->prompt_batch_stride, mask, mask_ld, 1, Bp, P, Pp, H, g.xa, g.kv, st));
+  CK(launch_dec_positions(g.kv, Bp, P, Pp, Smax, w.pos_pre, w.slot_ok, w.nvalid, st));
+  CK(launch_rmsnorm_fwd(g.xa, H, RowMap{0, 0, 0, 0}, wt->layers[0].ln_in, g.xn, g.rs1, Bp * Pp, H, c->eps, st));
+  DecMasks dm{};
+  dm.pos = w.pos_pre;
+  float *xi = g.xa, *xo = g.xb;
+  for (int l = 0; l < c->layers; ++l) {
+    CK(gen_layer(c, wt, l, g, xi, xo, Bp, P, Pp, 0, true, Smax, w.kc[l], w.vc[l], st, &dm));
+    std::swap(xi, xo);
+  }
+  CK(launch_rmsnorm_fwd(xi, H, RowMap{1, 0, Pp, P - 1}, wt->final_norm, w.xf, w.rstd_f, Bp, H, c->eps, st));
+  bf16_t* lg = R == 1 ? logits : w.logits_pre;
+  CK(launch_gemm(gemm(w.xf, H, wt->embed, H, lg, V, Bp, V, H), ACT_NONE, OUT_BF16, 1, st));
+  if (R > 1) {   // prompt b -> rows b*R .. b*R + R - 1
+    CK(launch_dec_repeat_index(w.rep_src, rows, R, st));
+    CK(launch_dec_gather_rows(w.logits_pre, logits, w.rep_src, rows, (long)V * 2, st));
+    CK(dec_gather(c, w, w.rep_src, rows, st));
+  }
+  return 0;
+}
+int gemma_decode_step(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_decode_desc* d,
+                      int t, const int64_t* ids, const int32_t* src_rows, bf16_t* logits, void* ws, size_t ws_bytes,
+                      hipStream_t st) {
+  CK(dec_check(c, wt, d, ws_bytes));
+  const int rows = d->rows, P = d->prompt_len, H = c->hidden, V = c->vocab;
+  if (t < 1 || t >= d->max_new_tokens) return set_error("decode: step %d outside 1..%d", t, d->max_new_tokens - 1);
+  if (!ids) return set_error("decode: ids is NULL");
+  Bump bp(ws);
+  DecWs w = dec_layout(bp, c, d);
+  TailScratchScope tail(w.tail, st);
+  CK(tail.status);
+  if (src_rows) CK(dec_gather(c, w, src_rows, rows, st));
+  const int p0 = P + t - 1;
+  DecMasks dm{};
+  dm.pos = w.pos_dec;
+  for (int k = 0; k < 2; ++k) {   // 0: sliding layers (the last `sliding_window` slots), 1: full layers
+    const int lo = (k == 0 && c->sliding_window > 0) ? std::max(0, p0 - c->sliding_window + 1) : 0;
+    dm.k_lo[k] = lo;
+    dm.nk[k] = (p0 + 1 - lo + 3) / 4 * 4;
+    dm.kmask[k] = w.kmask[k];
+    CK(launch_dec_step_prep(w.slot_ok, w.nvalid, rows, w.Smax, p0, t, lo, dm.nk[k], w.pos_dec, w.kmask[k], st));
+  }
+  GenPass& g = w.dec;
+  const float escale = bfround_host(sqrtf((float)H));
+  CK(launch_build_llm_inputs((const bf16_t*)wt->embed, ids, rows, 1, 0, 1, 1, H, escale, -1, g.xa, g.kv, st));
+  CK(launch_rmsnorm_fwd(g.xa, H, RowMap{0, 0, 0, 0}, wt->layers[0].ln_in, g.xn, g.rs1, rows, H, c->eps, st));
+  float *xi = g.xa, *xo = g.xb;
+  for (int l = 0; l < c->layers; ++l) {
+    CK(gen_layer(c, wt, l, g, xi, xo, rows, 1, 1, p0, false, w.Smax, w.kc[l], w.vc[l], st, &dm));
+    std::swap(xi, xo);
+  }
+  CK(launch_rmsnorm_fwd(xi, H, RowMap{0, 0, 0, 0}, wt->final_norm, w.xf, w.rstd_f, rows, H, c->eps, st));
+  CK(launch_gemm(gemm(w.xf, H, wt->embed, H, logits, V, rows, V, H), ACT_NONE, OUT_BF16, 1, st));
+  return 0;
+}
+
 }  // namespace
 
 extern "C" {
+
+size_t ptk_gemma3_decode_workspace_bytes(const ptk_gemma3_config* c, const ptk_gemma3_decode_desc* d) {
+  if (!c || !d || d->rows <= 0 || d->prompt_repeat <= 0) return 0;
+  Bump bp(nullptr);
+  dec_layout(bp, c, d);
+  return bp.off + 256;
+}
+
+int ptk_gemma3_decode_prefill(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_decode_desc* d,
+                              const float* prompt_embeds, const int32_t* prompt_mask, int64_t prompt_mask_ld,
+                              void* logits, void* ws, size_t ws_bytes, void* stream) {
+  if (!prompt_embeds || !logits || !ws) return set_error("decode_prefill: NULL argument");
+  if (prompt_mask && d && prompt_mask_ld < d->prompt_len) return set_error("decode_prefill: prompt_mask_ld < prompt_len");
+  return gemma_decode_prefill(c, w, d, prompt_embeds, prompt_mask, (long)prompt_mask_ld, (bf16_t*)logits, ws, ws_bytes,
+                              (hipStream_t)stream);
+}
+
+int ptk_gemma3_decode_step(const ptk_gemma3_config* c, const ptk_gemma3_weights* w, const ptk_gemma3_decode_desc* d,
+                           int step, const int64_t* ids, const int32_t* src_rows, void* logits, void* ws,
+                           size_t ws_bytes, void* stream) {
+  if (!logits || !ws) return set_error("decode_step: NULL argument");
+  return gemma_decode_step(c, w, d, step, ids, src_rows, (bf16_t*)logits, ws, ws_bytes, (hipStream_t)stream);
+}
+
+int ptk_beam_candidates(const void* logits, int64_t ld, const float* beam_scores, int batch, int beams, int vocab,
+                        int do_sample, int top_k, float top_p, float temperature, int min_tokens_to_keep,
+                        uint64_t seed, int step, int n_cand, int64_t* tokens, int32_t* beam_idx, float* scores,
+                        void* stream) {
+  if (!logits || !beam_scores || !tokens || !beam_idx || !scores) return set_error("beam_candidates: NULL argument");
+  if (ld < vocab) return set_error("beam_candidates: ld < vocab");
+  return launch_beam_candidates((const bf16_t*)logits, (long)ld, beam_scores, batch, beams, vocab, do_sample, top_k,
+                                top_p, temperature, min_tokens_to_keep, seed, step, n_cand, tokens, beam_idx, scores,
+                                (hipStream_t)stream);
+}
 
 int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,
                             void* ws, size_t ws_bytes, void* stream) {

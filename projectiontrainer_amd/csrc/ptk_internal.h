@@ -180,6 +180,7 @@ int launch_rmsnorm_bwd_scatter(const float* x, RowMap xmap, const float* w, cons
 // ---- attention helpers (attn.hip) ----
 struct AttnShape {
   int B, S, Hq, Hkv, D;     // S = padded sequence length (multiple of 64)
+  const int32_t* pos = nullptr;   // forward only: RoPE position of token b*S + s ([B*S]); null: s
 };
 int launch_qknorm_rope_fwd(const bf16_t* qkv, const float* qw, const float* kw, const float* cos_t,
                            const float* sin_t, AttnShape s, float eps, bf16_t* Q, bf16_t* K, bf16_t* V,
@@ -327,6 +328,19 @@ int launch_kv_append(const bf16_t* src, long src_z, bf16_t* dst, long dst_z, int
 int launch_gen_sample(const bf16_t* logits, long ld, int B, int V, int do_sample, int top_k, float temperature,
                       uint64_t seed, int step, long eos_id, long pad_id, int32_t* finished, int64_t* out, long ld_out,
                       int64_t* next, hipStream_t st);
+// stepwise decode (ptk_gemma3_decode_prefill / _step) and beam candidates (ptk_beam_candidates)
+int launch_dec_prompt(const float* src, long ld_b, const int32_t* mask, long mask_ld, int repeat, int rows, int P,
+                      int Pp, int H, float* x, int32_t* kv, hipStream_t st);
+int launch_dec_positions(const int32_t* kv, int rows, int P, int Pp, int Smax, int32_t* pos, int32_t* slot_ok,
+                         int32_t* nvalid, hipStream_t st);
+int launch_dec_step_prep(int32_t* slot_ok, const int32_t* nvalid, int rows, int Smax, int p0, int t, int k_lo, int nk,
+                         int32_t* pos, int32_t* kmask, hipStream_t st);
+int launch_dec_gather_rows(const void* in, void* out, const int32_t* src, int rows, long row_bytes, hipStream_t st);
+int launch_dec_gather_i32(const int32_t* in, int32_t* out, const int32_t* src, int rows, hipStream_t st);
+int launch_dec_repeat_index(int32_t* src, int rows, int repeat, hipStream_t st);
+int launch_beam_candidates(const bf16_t* logits, long ld, const float* beam_scores, int batch, int K, int V,
+                           int do_sample, int top_k, float top_p, float temperature, int min_keep, uint64_t seed,
+                           int step, int n_cand, int64_t* tok, int32_t* beam, float* score, hipStream_t st);
 
 // ---- unfrozen-LLM step (train.hip) ----
 // out [cols][rows_pad] bf16 = in[map(r)][c] (r < rows), zero for rows <= r < rows_pad

@@ -63,6 +63,14 @@ class DistState:
         if self.num_processes > 1:
             dist.barrier()
 
+    def gather_object(self, obj):
+        """accelerate.utils.gather_object for a list: every rank's list, concatenated in rank order."""
+        if self.num_processes == 1:
+            return list(obj)
+        parts = [None] * self.num_processes
+        dist.all_gather_object(parts, obj)
+        return [x for part in parts for x in part]
+
 
 def from_accelerator(acc) -> DistState:
     """Wrap an accelerate.Accelerator (process group already initialised by it)."""
@@ -74,6 +82,7 @@ def from_accelerator(acc) -> DistState:
     st.process_index = acc.process_index
     st.device = torch.device(acc.device)
     st.all_reduce_sum_ = DistState.all_reduce_sum_.__get__(st)
+    st.gather_object = DistState.gather_object.__get__(st)
     return st
 
 

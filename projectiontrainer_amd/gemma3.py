@@ -258,3 +258,91 @@ class Gemma3CausalLM:
                 n_out = int(all_done[0]) + 1
         out = out[:, :n_out]
         return (out, logits) if return_logits else out
+
+    # ------------------------------------------------------------------ beam search (stepwise decode)
+    def decode_begin(self, inputs_embeds, attention_mask=None, repeat=1, max_new_tokens=512):
+        """Prefill of the stepwise decode (ptk_gemma3_decode_prefill): prompts [B, P, H] f32 with an optional
+        attention mask [B, P] (0 = padding: a masked key, and HF's position ids cumsum(mask) - 1), each prompt
+        given to `repeat` consecutive rows.  Returns the first logits, bf16 [B * repeat, V]."""
+        if inputs_embeds.dtype != torch.float32 or not inputs_embeds.is_cuda or inputs_embeds.dim() != 3:
+            raise L.PtkError("decode: inputs_embeds must be an f32 HIP tensor [B, P, H]")
+        x = inputs_embeds.contiguous()
+        B, P, H = x.shape
+        if H != self.cfg.hidden_size:
+            raise L.PtkError(f"decode: inputs_embeds width {H} != hidden {self.cfg.hidden_size}")
+        self._dec = L.Gemma3DecodeC(B * repeat, P, max_new_tokens, repeat, P)
+        n = L.lib().ptk_gemma3_decode_workspace_bytes(self.c_cfg, self._dec)
+        if getattr(self, "_dec_ws", None) is None or self._dec_ws.numel() < n:
+            self._dec_ws = None
+            self._dec_ws = torch.empty(n, dtype=torch.uint8, device=self.device)
+        mask = None
+        if attention_mask is not None:
+            mask = attention_mask.to(device=self.device, dtype=torch.int32).contiguous()
+            if tuple(mask.shape) != (B, P):
+                raise L.PtkError(f"decode: attention_mask must be [{B}, {P}]")
+        self._dec_x = x   # keep the prompt alive for the call
+        logits = torch.empty((B * repeat, self.cfg.vocab_size), dtype=torch.bfloat16, device=self.device)
+        L.check(L.lib().ptk_gemma3_decode_prefill(self.c_cfg, self.c_w, self._dec, x.data_ptr(),
+                                                  0 if mask is None else mask.data_ptr(), P, logits.data_ptr(),
+                                                  self._dec_ws.data_ptr(), self._dec_ws.numel(),
+                                                  L.stream_ptr(self.device)), "ptk_gemma3_decode_prefill")
+        return logits
+
+    def decode_next(self, step, ids, src_rows=None):
+        """Decode step `step` (1..max_new_tokens-1): every row appends ids[row] after taking the cache of row
+        src_rows[row] (beam re-ordering; None keeps each row's own).  Returns the logits bf16 [rows, V]."""
+        rows = self._dec.rows
+        ids = ids.to(device=self.device, dtype=torch.int64).contiguous()
+        src = None if src_rows is None else src_rows.to(device=self.device, dtype=torch.int32).contiguous()
+        if ids.numel() != rows or (src is not None and src.numel() != rows):
+            raise L.PtkError(f"decode: ids / src_rows must hold {rows} rows")
+        logits = torch.empty((rows, self.cfg.vocab_size), dtype=torch.bfloat16, device=self.device)
+        L.check(L.lib().ptk_gemma3_decode_step(self.c_cfg, self.c_w, self._dec, int(step), ids.data_ptr(),
+                                               0 if src is None else src.data_ptr(), logits.data_ptr(),
+                                               self._dec_ws.data_ptr(), self._dec_ws.numel(),
+                                               L.stream_ptr(self.device)), "ptk_gemma3_decode_step")
+        return logits
+
+    def beam_candidates(self, logits, beam_scores, beams, n_cand, do_sample, top_k, top_p, temperature, seed, step,
+                        min_tokens_to_keep):
+        """ptk_beam_candidates over logits [B * beams, V]: (tokens int64, beam int32, accumulated f32) [B, n_cand]."""
+        rows, V = logits.shape
+        B = rows // beams
+        tok = torch.empty((B, n_cand), dtype=torch.int64, device=self.device)
+        bi = torch.empty((B, n_cand), dtype=torch.int32, device=self.device)
+        sc = torch.empty((B, n_cand), dtype=torch.float32, device=self.device)
+        bs = beam_scores.to(device=self.device, dtype=torch.float32).contiguous()
+        L.check(L.lib().ptk_beam_candidates(logits.data_ptr(), V, bs.data_ptr(), B, beams, V, int(bool(do_sample)),
+                                            int(top_k or 0), float(top_p), float(temperature), int(min_tokens_to_keep),
+                                            int(seed) & ((1 << 64) - 1), int(step), int(n_cand), tok.data_ptr(),
+                                            bi.data_ptr(), sc.data_ptr(), L.stream_ptr(self.device)),
+                "ptk_beam_candidates")
+        return tok, bi, sc
+
+    def beam_generate(self, inputs_embeds, attention_mask=None, num_beams=3, max_new_tokens=512, do_sample=True,
+                      top_k=50, top_p=1.0, temperature=1.0, eos_token_id=None, pad_token_id=None,
+                      length_penalty=1.0, early_stopping=False, seed=0):
+        """`generate(inputs_embeds=, attention_mask=, num_beams=, do_sample=, top_k=, top_p=, ...)` with beams, as
+        Stage 2's validation calls it (Stage2/trainer.py:596-626 -> GenerationMixin._beam_search): the stepwise
+        KV-cache decode, ptk_beam_candidates for the continuations of each step (sampled without replacement from
+        the joint beam x vocab distribution, or the best with do_sample=False) and the host bookkeeping of
+        projectiontrainer_amd/beam.py.  Returns the new tokens of the best hypothesis per prompt, int64 [B, n]."""
+        from .beam import BeamSearch
+        B = inputs_embeds.shape[0]
+        K = int(num_beams)
+        n_eos = 0 if eos_token_id is None else 1
+        n_cand = max(2, 1 + n_eos) * K
+        min_keep = (1 + n_eos) if K > 1 else 1
+        pad = self.cfg.pad_token_id if pad_token_id is None else int(pad_token_id)
+        bs = BeamSearch(B, K, max_new_tokens, eos_token_id, pad, length_penalty, early_stopping)
+        logits = self.decode_begin(inputs_embeds, attention_mask, repeat=K, max_new_tokens=max_new_tokens)
+        step = 0
+        while True:
+            tok, bi, sc = self.beam_candidates(logits, bs.run_score.reshape(-1), K, n_cand, do_sample, top_k, top_p,
+                                               temperature, seed, step, min_keep)
+            ids, rows = bs.step(tok, bi, sc)
+            if bs.finished:
+                break
+            step += 1
+            logits = self.decode_next(step, ids, rows)
+        return bs.result().to(self.device)

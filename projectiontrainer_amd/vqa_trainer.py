@@ -24,8 +24,11 @@ Kept reference semantics (Stage2/trainer.py:248-488):
   * logging keys `train/batch_loss` (every micro-batch), `train/step_loss` (sync
     micro-batches), `train/loss` = sum of sync losses / len(train_loader) per
     epoch, `val/loss`.
-Validation by sampled `generate` (:595-647) is out of scope: `evaluate` computes
-the validation loss only.  `save_model` writes the fine-tuned LLM as HF-named
+`evaluate` computes the validation loss and, with a tokenizer that decodes, the reference's generated examples
+(:595-700): `generate(inputs_embeds=[projected image | question], attention_mask, max_new_tokens=512,
+do_sample=True, num_beams=3, top_p=0.9, top_k=50)` on libptk's stepwise KV-cache decode with beam sampling
+(`Gemma3CausalLM.beam_generate`), decoded and written to `validation_examples/epoch_{n}_examples.txt` and
+`all_validation_examples.txt` in the reference's format (at most 20 examples, gathered over the ranks).  `save_model` writes the fine-tuned LLM as HF-named
 bf16 tensors (`language_model/model.safetensors`, accelerate's save_model
 layout) plus the optimizer state of this rank (`optimizer_rank{r}.pt`).
 """
@@ -68,7 +71,9 @@ class VQATrainerStage2:
                  val_dataset, output_dir: str, batch_size: int, learning_rate: float, weight_decay: float,
                  num_epochs: int, gradient_accumulation_steps: int, warmup_ratio: float, freeze_vision_encoder: bool,
                  freeze_projection_layer: bool, freeze_llm: bool, enable_qlora: bool, train_ve_first_epoch: bool,
-                 wandb_project: str, log_fn=None, seed: int = 0):
+                 wandb_project: str, log_fn=None, seed: int = 0, generate_max_new_tokens: int = 512,
+                 generate_num_beams: int = 3, generate_do_sample: bool = True, generate_top_k: int = 50,
+                 generate_top_p: float = 0.9, generate_seed: int = 0):
         if enable_qlora:
             raise NotImplementedError("VQATrainerStage2 (HIP): QLoRA / 4-bit LLMs are not supported; run with the "
                                       "dense bf16 LLM and --unfreeze_llm")
@@ -86,6 +91,10 @@ class VQATrainerStage2:
         self.train_dataset, self.val_dataset = train_dataset, val_dataset
         self.wandb_project, self.log_fn, self.seed = wandb_project, log_fn, seed
         self.gas = gradient_accumulation_steps
+        # the validation generate of Stage2/trainer.py:603-613
+        self.gen_kwargs = dict(max_new_tokens=generate_max_new_tokens, num_beams=generate_num_beams,
+                               do_sample=generate_do_sample, top_k=generate_top_k, top_p=generate_top_p)
+        self.generate_seed = generate_seed
         self.validation_dir = os.path.join(output_dir, "validation_examples")
         if acc.is_main_process:
             os.makedirs(self.validation_dir, exist_ok=True)
@@ -162,8 +171,8 @@ class VQATrainerStage2:
         logger.info("Process %d: Stage 2 training complete!", acc.process_index)
 
     def evaluate(self, epoch, global_step):
-        """Validation loss (Stage2/trainer.py:490-593; the sampled generate() is out of scope): forward + CE
-        only, as under the reference's torch.no_grad (no grads touched).  As the reference, the batches are
+        """Validation loss (Stage2/trainer.py:490-593): forward + CE only, as under the reference's torch.no_grad
+        (no grads touched); then, with a tokenizer that decodes, the generated examples (:595-700).  As the reference, the batches are
         collated with the tokenizer padding on the LEFT (restored afterwards) and a missing pad token falls
         back to eos (:499-507)."""
         tok = self.tokenizer
@@ -175,19 +184,68 @@ class VQATrainerStage2:
             tok.pad_token_id = tok.eos_token_id
         eng_pad = self.engine.pad_token_id
         self.engine.pad_token_id = int(tok.pad_token_id)
+        examples = []
+        can_decode = hasattr(tok, "batch_decode")
         try:
             tot, n = 0.0, 0
-            for batch in self._batches(self.val_dataset, 0, shuffle=False):
-                loss = self.engine.forward_loss(batch["pixel_values"], batch["question_input_ids"],
-                                                batch["answer_input_ids"])
+            for bi, batch in enumerate(self._batches(self.val_dataset, 0, shuffle=False)):
+                q, a = batch["question_input_ids"], batch["answer_input_ids"]
+                loss = self.engine.forward_loss(batch["pixel_values"], q, a)
                 tot += float(self.accelerator.gather(loss).mean())
                 n += 1
+                if can_decode:
+                    try:   # (the reference logs a failed generation and goes on, :645-646)
+                        preds = self._generate_batch(q, seed=self.generate_seed + 7919 * bi + epoch)
+                        dp = tok.batch_decode(preds.cpu(), skip_special_tokens=True)
+                        dq = tok.batch_decode(q.cpu(), skip_special_tokens=True)
+                        da = tok.batch_decode(a.cpu(), skip_special_tokens=True)
+                        examples += [{"epoch": epoch + 1, "question": dq[j], "ground_truth": da[j],
+                                      "prediction": dp[j]} for j in range(len(dp))]
+                    except Exception as e:  # noqa: BLE001
+                        logger.error("Error during validation generation/logging: %s", e, exc_info=True)
         finally:
             tok.padding_side = side
             self.engine.pad_token_id = eng_pad
+        acc = self.accelerator
+        acc.wait_for_everyone()
+        if can_decode:
+            gathered = acc.gather_object(examples)[:min(20, len(self.val_dataset))]
+            if acc.is_main_process and gathered:
+                self._write_examples(epoch, gathered)
         avg = tot / max(1, n)
         self._log({"val/loss": avg, "epoch": epoch + 1}, global_step)
         return avg
+
+    def _generate_batch(self, question_ids, seed=0):
+        """The validation generate of one batch (Stage2/trainer.py:596-626): prompt = the projected image tokens
+        of the batch just evaluated (the engine's LLM input rows) followed by the question embeddings, attention
+        mask 1 on the image tokens and (question != pad) on the question."""
+        eng = self.engine
+        B, Tq = question_ids.shape
+        P = eng.N - 1 + Tq
+        x = eng.x.view(B, eng.Sp, -1)[:, :P].contiguous()   # forward_loss built [projected | question | answer]
+        mask = torch.ones(B, P, dtype=torch.int32, device=self.device)
+        mask[:, eng.N - 1:] = (question_ids.to(self.device) != int(self.tokenizer.pad_token_id)).int()
+        return self.language_model.beam_generate(x, mask, eos_token_id=getattr(self.tokenizer, "eos_token_id", None),
+                                                 pad_token_id=int(self.tokenizer.pad_token_id), seed=seed,
+                                                 **self.gen_kwargs)
+
+    def _write_examples(self, epoch, examples):
+        """validation_examples/epoch_{n}_examples.txt and all_validation_examples.txt (Stage2/trainer.py:672-700)."""
+        def body():
+            out = []
+            for i, ex in enumerate(examples):
+                out.append(f"Example {i + 1}:\nQuestion: {ex['question']}\nGround Truth: {ex['ground_truth']}\n"
+                           f"Prediction: {ex['prediction']}\n{'=' * 80}\n\n")
+            return "".join(out)
+        try:
+            with open(os.path.join(self.validation_dir, f"epoch_{epoch + 1}_examples.txt"), "w", encoding="utf-8") as f:
+                f.write(f"Validation Examples for Epoch {epoch + 1}\n{'=' * 80}\n\n" + body())
+            with open(os.path.join(self.validation_dir, "all_validation_examples.txt"), "a" if epoch > 0 else "w",
+                      encoding="utf-8") as f:
+                f.write(f"\nValidation Examples for Epoch {epoch + 1}\n{'=' * 80}\n\n" + body())
+        except OSError as e:
+            logger.error("Failed to save validation examples to file: %s", e, exc_info=True)
 
     def save_model(self, path):
         """Called on EVERY rank.  Main process: language_model/model.safetensors (HF names, bf16) and the

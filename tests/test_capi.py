@@ -27,7 +27,7 @@ def test_library_exports_every_declared_symbol():
     for n in names:
         assert hasattr(lib, n), n
         assert n in L.SIGNATURES, f"{n} missing from the ctypes binding"
-    assert lib.ptk_abi_version() == L.ABI_VERSION == 7
+    assert lib.ptk_abi_version() == L.ABI_VERSION == 8
 
 
 def test_error_reporting_without_gpu():
@@ -56,6 +56,8 @@ STRUCTS = {
     "ptk_gemma3_layer_grads": ("Gemma3LayerGradsC", None),
     "ptk_gemma3_grads": ("Gemma3GradsC", None),
     "ptk_image_desc": ("ImageDesc", None),
+    "ptk_gemma3_generate_desc": ("Gemma3GenerateC", None),
+    "ptk_gemma3_decode_desc": ("Gemma3DecodeC", None),
 }
 
 
