@@ -87,6 +87,33 @@ int main(int argc, char** argv) {
     EXPECT(ptk_gemma3_generate(&g1, &gw, &gd, (const float*)&dummy, nullptr, &dummy, nullptr, nullptr, 0, nullptr) < 0);
     EXPECT(ptk_gemma3_generate(&g1, &gw, nullptr, nullptr, nullptr, nullptr, nullptr, nullptr, 0, nullptr) < 0);
   }
+  // the stepwise decode (beam search): layout monotone in rows and new tokens, host-side refusals before any launch
+  for (const ptk_gemma3_config* c : {&g1, &g4})
+    for (int rows : {3, 48})
+      for (int nt : {2, 512}) {
+        ptk_gemma3_decode_desc dd{rows, 639, nt, 3, 704};
+        const size_t a = ptk_gemma3_decode_workspace_bytes(c, &dd);
+        dd.max_new_tokens = nt + 64;
+        EXPECT(a > 0 && ptk_gemma3_decode_workspace_bytes(c, &dd) > a);
+      }
+  {
+    ptk_gemma3_weights gw{};
+    gw.rope_max_pos = 4096;
+    ptk_gemma3_decode_desc dd{4, 639, 8, 3, 704};   // rows not a multiple of prompt_repeat
+    int64_t dummy = 0;
+    EXPECT(ptk_gemma3_decode_prefill(&g1, &gw, &dd, (const float*)&dummy, nullptr, 0, &dummy, &dummy, 1 << 20, nullptr) < 0);
+    dd.rows = 6; dd.prompt_batch_stride = 100;      // stride < prompt
+    EXPECT(ptk_gemma3_decode_prefill(&g1, &gw, &dd, (const float*)&dummy, nullptr, 0, &dummy, &dummy, 1 << 20, nullptr) < 0);
+    dd.prompt_batch_stride = 704;                   // workspace too small
+    EXPECT(ptk_gemma3_decode_prefill(&g1, &gw, &dd, (const float*)&dummy, nullptr, 0, &dummy, &dummy, 1 << 20, nullptr) < 0);
+    EXPECT(ptk_gemma3_decode_step(&g1, &gw, &dd, 0, &dummy, nullptr, &dummy, &dummy, (size_t)1 << 40, nullptr) < 0);  // step 0
+    EXPECT(ptk_gemma3_decode_step(&g1, &gw, &dd, 8, &dummy, nullptr, &dummy, &dummy, (size_t)1 << 40, nullptr) < 0);  // past the last
+    float sc = 0.f;
+    int32_t bi = 0;
+    EXPECT(ptk_beam_candidates(&dummy, 512, &sc, 1, 3, 512, 0, 0, 1.f, 1.f, 1, 0, 0, 64, &dummy, &bi, &sc, nullptr) < 0);  // n_cand > 32
+    EXPECT(ptk_beam_candidates(&dummy, 262144, &sc, 1, 3, 262144, 1, 0, 0.9f, 1.f, 2, 0, 0, 6, &dummy, &bi, &sc, nullptr) < 0);  // no top-k
+    EXPECT(ptk_beam_candidates(&dummy, 512, &sc, 1, 3, 512, 1, 50, 0.9f, 0.f, 2, 0, 0, 6, &dummy, &bi, &sc, nullptr) < 0);  // T = 0
+  }
   ptk_projector pj{};
   pj.vision_dim = 1024; pj.inter_dim = 4096; pj.llm_dim = 1152;
   for (int rows : {1, 576, 18432}) EXPECT(ptk_projector_workspace_bytes(&pj, rows) > 0);
