@@ -370,6 +370,7 @@ typedef struct {
   uint64_t seed;             /* the draw of step t, row b: a counter-based uniform of (seed, t, b) */
   int64_t eos_token_id, pad_token_id;
   int64_t prompt_batch_stride;   /* rows of prompt_embeds between consecutive samples (>= prompt_len) */
+  float top_p;               /* (0, 1]; < 1: TopPLogitsWarper after top-k (needs 0 < top_k <= 512); 0 reads as 1 */
 } ptk_gemma3_generate_desc;
 
 size_t ptk_gemma3_generate_workspace_bytes(const ptk_gemma3_config* c, int batch, int prompt_len, int max_new_tokens);

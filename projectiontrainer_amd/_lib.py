@@ -110,7 +110,7 @@ class Gemma3BatchC(C.Structure):
 class Gemma3GenerateC(C.Structure):
     _fields_ = [("batch", c_int), ("prompt_len", c_int), ("max_new_tokens", c_int), ("do_sample", c_int),
                 ("top_k", c_int), ("temperature", c_float), ("seed", C.c_uint64), ("eos_token_id", c_int64),
-                ("pad_token_id", c_int64), ("prompt_batch_stride", c_int64)]
+                ("pad_token_id", c_int64), ("prompt_batch_stride", c_int64), ("top_p", c_float)]
 
 
 class Gemma3DecodeC(C.Structure):

@@ -74,9 +74,10 @@ constexpr int GS_T = 1024;   // threads per row
 //   draw i with probability exp(z_i - z_max) / sum over the kept (inverse CDF in index order of one uniform).
 // finished[b] != 0: the token is pad_id; a row whose token is eos_id becomes finished.  tok -> out[b * ld_out]
 // and next[b].
+constexpr int GS_LIST = 1024;   // kept entries sorted for top-p
 __global__ void __launch_bounds__(GS_T) gen_sample_kernel(const bf16_t* __restrict__ logits, long ld, int V,
-                                                          int do_sample, int top_k, float temperature, uint64_t seed,
-                                                          int step, long eos_id, long pad_id,
+                                                          int do_sample, int top_k, float temperature, float top_p,
+                                                          uint64_t seed, int step, long eos_id, long pad_id,
                                                           int32_t* __restrict__ finished, int64_t* __restrict__ out,
                                                           long ld_out, int64_t* __restrict__ next) {
   const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -142,8 +143,67 @@ __global__ void __launch_bounds__(GS_T) gen_sample_kernel(const bf16_t* __restri
           __syncthreads();
         }
       }
-      // the kept mass over a contiguous chunk per thread, in index order
       const float inv_t = 1.f / temperature;
+      if (top_p < 1.f) {
+        // TopPLogitsWarper (min_tokens_to_keep 1): the kept set sorted ascending by logit in LDS (bitonic), the
+        // cumulative softmax of z = x / T, entries with cumulative mass <= 1 - top_p dropped; then the draw by
+        // inverse CDF over what is left (sorted order: the same law as a draw in index order)
+        __shared__ float ls[GS_LIST];
+        __shared__ int lt[GS_LIST];
+        __shared__ int cnt;
+        if (tid == 0) cnt = 0;
+        __syncthreads();
+        for (int i = tid; i < V; i += GS_T) {
+          const uint16_t u = row[i];
+          if (bf_key(u) >= thr) {
+            const int slot = atomicAdd(&cnt, 1);
+            if (slot < GS_LIST) { ls[slot] = (bf2f(u) - mx) * inv_t; lt[slot] = i; }
+          }
+        }
+        __syncthreads();
+        const int n = min(cnt, GS_LIST);
+        int np2 = 1;
+        while (np2 < n) np2 <<= 1;
+        for (int i = n + tid; i < np2; i += GS_T) { ls[i] = INFINITY; lt[i] = 0x7fffffff; }
+        __syncthreads();
+        for (int size = 2; size <= np2; size <<= 1)
+          for (int stride = size >> 1; stride > 0; stride >>= 1) {
+            for (int i = tid; i < np2; i += GS_T) {
+              const int j = i ^ stride;
+              if (j > i) {
+                const bool up = (i & size) == 0;
+                const float a = ls[i], c = ls[j];
+                const bool gt = a > c || (a == c && lt[i] > lt[j]);
+                if (gt == up) { ls[i] = c; ls[j] = a; const int tt = lt[i]; lt[i] = lt[j]; lt[j] = tt; }
+              }
+            }
+            __syncthreads();
+          }
+        if (tid == 0) {   // (<= 1024 entries, once per row and token)
+          float tot = 0.f;
+          for (int i = 0; i < n; ++i) tot += __expf(ls[i]);   // z <= 0 (the row max at 0)
+          float cum = 0.f;
+          int first = 0;
+          for (int i = 0; i < n; ++i) {
+            cum += __expf(ls[i]);
+            if (cum / tot <= 1.f - top_p) first = i + 1;
+          }
+          first = min(first, n - 1);
+          float kept = 0.f;
+          for (int i = first; i < n; ++i) kept += __expf(ls[i]);
+          const float target = gen_uniform(seed, step, b) * kept;
+          float s = 0.f;
+          int pick = lt[n - 1];
+          for (int i = first; i < n; ++i) {
+            s += __expf(ls[i]);
+            if (target < s) { pick = lt[i]; break; }
+          }
+          redi[0] = cnt > GS_LIST ? -1 : pick;
+        }
+        __syncthreads();
+        tok = redi[0] >= 0 ? redi[0] : mi;
+      } else {
+      // the kept mass over a contiguous chunk per thread, in index order
       const int chunk = (V + GS_T - 1) / GS_T, c0 = tid * chunk, c1 = min(V, c0 + chunk);
       float part = 0.f;
       for (int i = c0; i < c1; ++i) {
@@ -175,6 +235,7 @@ __global__ void __launch_bounds__(GS_T) gen_sample_kernel(const bf16_t* __restri
       }
       __syncthreads();
       tok = redi[0] >= 0 ? redi[0] : mi;   // (rounding left the target past the total: the maximum)
+      }
     }
   }
   if (tid == 0) {
@@ -184,11 +245,14 @@ __global__ void __launch_bounds__(GS_T) gen_sample_kernel(const bf16_t* __restri
   }
 }
 int launch_gen_sample(const bf16_t* logits, long ld, int B, int V, int do_sample, int top_k, float temperature,
-                      uint64_t seed, int step, long eos_id, long pad_id, int32_t* finished, int64_t* out, long ld_out,
-                      int64_t* next, hipStream_t st) {
+                      float top_p, uint64_t seed, int step, long eos_id, long pad_id, int32_t* finished, int64_t* out,
+                      long ld_out, int64_t* next, hipStream_t st) {
   if (do_sample && !(temperature > 0.f)) return set_error("generate: temperature must be > 0 when sampling");
+  if (do_sample && !(top_p > 0.f && top_p <= 1.f)) return set_error("generate: top_p must be in (0, 1]");
+  if (do_sample && top_p < 1.f && !(top_k > 0 && top_k <= GS_LIST / 2) && V > GS_LIST / 2)
+    return set_error("generate: top_p < 1 needs 0 < top_k <= %d (the kept set is sorted in LDS)", GS_LIST / 2);
   hipLaunchKernelGGL(gen_sample_kernel, dim3((unsigned)B), dim3(GS_T), 0, st, logits, ld, V, do_sample, top_k,
-                     temperature, seed, step, eos_id, pad_id, finished, out, ld_out, next);
+                     temperature, do_sample ? top_p : 1.f, seed, step, eos_id, pad_id, finished, out, ld_out, next);
   return hipGetLastError() == hipSuccess ? 0 : set_error("gen_sample launch failed");
 }
 

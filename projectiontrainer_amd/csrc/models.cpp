@@ -892,7 +892,8 @@ int gemma_generate(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, con
     CK(launch_gemm(gemm(w.xf, H, wt->embed, H, w.logits, V, B, V, H), ACT_NONE, OUT_BF16, 1, st));
     if (step_logits)
       CKH(hipMemcpyAsync(step_logits + (long)t * B * V, w.logits, (size_t)B * V * 2, hipMemcpyDeviceToDevice, st));
-    return launch_gen_sample(w.logits, V, B, V, gd->do_sample, gd->top_k, gd->temperature, gd->seed, t,
+    return launch_gen_sample(w.logits, V, B, V, gd->do_sample, gd->top_k, gd->temperature,
+                             gd->top_p > 0.f ? gd->top_p : 1.f, gd->seed, t,
                              (long)gd->eos_token_id, (long)gd->pad_token_id, w.finished, out_ids + t, NT, w.next, st);
   };
   // prefill: the prompt rows, padded per sample to Pp (masked keys), every layer's K / V into the cache

@@ -326,8 +326,8 @@ int launch_gen_prompt(const float* src, long ld_b, int B, int P, int Pp, int H, 
 int launch_kv_append(const bf16_t* src, long src_z, bf16_t* dst, long dst_z, int Z, int p0, int n, int D,
                      hipStream_t st);
 int launch_gen_sample(const bf16_t* logits, long ld, int B, int V, int do_sample, int top_k, float temperature,
-                      uint64_t seed, int step, long eos_id, long pad_id, int32_t* finished, int64_t* out, long ld_out,
-                      int64_t* next, hipStream_t st);
+                      float top_p, uint64_t seed, int step, long eos_id, long pad_id, int32_t* finished, int64_t* out,
+                      long ld_out, int64_t* next, hipStream_t st);
 // stepwise decode (ptk_gemma3_decode_prefill / _step) and beam candidates (ptk_beam_candidates)
 int launch_dec_prompt(const float* src, long ld_b, const int32_t* mask, long mask_ld, int repeat, int rows, int P,
                       int Pp, int H, float* x, int32_t* kv, hipStream_t st);

@@ -132,7 +132,14 @@ class Gemma3CausalLM:
         cls.check_not_quantized(model)
         cfg = cls.config_from_hf(model.config)
         sd = {k: v.detach().float() for k, v in model.state_dict().items()}
-        return cls(cfg, sd, device, max_pos)
+        lm = cls(cfg, sd, device, max_pos)
+        # generate() without explicit sampling arguments uses the checkpoint's generation_config, as HF does (the
+        # public gemma-3-1b-it ships top_k 64, top_p 0.95)
+        gc = getattr(model, "generation_config", None)
+        if gc is not None:
+            lm.generation_defaults = {k: getattr(gc, k) for k in ("top_k", "top_p", "temperature")
+                                      if getattr(gc, k, None) is not None}
+        return lm
 
     @classmethod
     def random_init(cls, cfg: Gemma3TextConfig, device="cuda", seed=1, max_pos=2048):
@@ -205,16 +212,19 @@ class Gemma3CausalLM:
     def get_input_embeddings(self):
         return self.embed
 
-    def generate(self, inputs_embeds, max_new_tokens=64, do_sample=True, top_k=50, temperature=1.0,
+    generation_defaults: dict = {}   # HF GenerationConfig defaults unless the checkpoint ships its own
+
+    def generate(self, inputs_embeds, max_new_tokens=64, do_sample=True, top_k=None, temperature=None,
                  pad_token_id=None, eos_token_id=None, seed=0, prompt_len=None, batch=None, force_ids=None,
-                 return_logits=False):
+                 return_logits=False, top_p=None):
         """`Gemma3ForCausalLM.generate(inputs_embeds=, attention_mask=ones, max_new_tokens=, do_sample=, pad_token_id=,
         eos_token_id=)` as the reference's validation calls it (Stage1/projector_trainer.py:386-393) on the KV-cache
         decode of libptk (ptk_gemma3_generate): returns the NEW tokens, int64 [B, n], n = max_new_tokens or the step
         at which every row has produced eos_token_id (HF's stopping; finished rows are padded with pad_token_id).
-        Sampling follows HF's defaults (GenerationConfig: temperature 1, top_k 50, top_p 1): the drawn tokens are
-        one draw of the same distribution, from a counter-based generator seeded by `seed` (torch.multinomial's
-        stream is not reproduced).
+        Sampling follows HF's processors with the checkpoint's generation config where from_hf found one, else
+        GenerationConfig's defaults (temperature 1, top_k 50, top_p 1); explicit arguments win.  The drawn tokens
+        are one draw of the same distribution, from a counter-based generator seeded by `seed`
+        (torch.multinomial's stream is not reproduced).
         inputs_embeds: f32 [B, P, H], or [B * stride, H] rows with prompt_len = P and batch = B (the Stage-1
         engine's LLM input, whose vision rows start each stride-row sample).  force_ids (int64 [B, max_new_tokens]): teacher forcing
         (step t feeds force_ids[:, t-1]); return_logits: also the bf16 logits of every step [max_new_tokens, B, V]."""
@@ -233,8 +243,12 @@ class Gemma3CausalLM:
             raise L.PtkError(f"generate: inputs_embeds width {inputs_embeds.shape[-1]} != hidden {H}")
         pad = self.cfg.pad_token_id if pad_token_id is None else int(pad_token_id)
         eos = -1 if eos_token_id is None else int(eos_token_id)
+        dflt = self.generation_defaults
+        top_k = dflt.get("top_k", 50) if top_k is None else top_k
+        top_p = dflt.get("top_p", 1.0) if top_p is None else top_p
+        temperature = dflt.get("temperature", 1.0) if temperature is None else temperature
         desc = L.Gemma3GenerateC(B, P, max_new_tokens, int(bool(do_sample)), int(top_k or 0), float(temperature),
-                                 int(seed) & ((1 << 64) - 1), eos, pad, stride)
+                                 int(seed) & ((1 << 64) - 1), eos, pad, stride, float(top_p))
         n = L.lib().ptk_gemma3_generate_workspace_bytes(self.c_cfg, B, P, max_new_tokens)
         if getattr(self, "_gen_ws", None) is None or self._gen_ws.numel() < n:
             self._gen_ws = None

@@ -138,6 +138,27 @@ def test_generate_sampling_distribution(gpu):
     assert (~keep[wide]).any()
 
 
+def test_generate_sampling_top_p(gpu):
+    """do_sample with top_k 64 and top_p 0.95 (the public gemma-3-1b-it generation config) and T 0.8: the draws stay
+    inside HF's processed support (TopKLogitsWarper then TopPLogitsWarper, min_tokens_to_keep 1) and their
+    histogram matches softmax over it (TV within 3x its expectation, 4096 rows)."""
+    from oracle import beam_ref as BR
+    cfg, lpb, lm = _model("tiny", gpu)
+    g = torch.Generator().manual_seed(8)
+    x = (torch.randn(1, 20, cfg.hidden_size, generator=g)).expand(4096, 20, cfg.hidden_size).contiguous().to(gpu)
+    ids, logits = lm.generate(x, max_new_tokens=1, do_sample=True, top_k=64, top_p=0.95, temperature=0.8, seed=5,
+                              return_logits=True)
+    ids = ids[:, 0].cpu()
+    lp = BR.processed_log_probs(logits[0, 0:1].float().cpu(), True, 64, 0.95, 0.8, 1)[0]
+    assert torch.isfinite(lp[ids]).all()
+    p = torch.softmax(lp.double(), -1)
+    emp = torch.bincount(ids, minlength=lp.numel()).double() / ids.numel()
+    tv = 0.5 * float((emp - p).abs().sum())
+    bar = 3.0 * 0.5 * float((2.0 * p * (1 - p) / (np.pi * ids.numel())).sqrt().sum())
+    assert tv < bar, (tv, bar)
+    assert int(torch.isfinite(lp).sum()) < 64     # top-p removed part of the top-k set
+
+
 def test_trainer_validation_generate(gpu, tmp_path):
     """ProjectionTrainerStage1 with a validation set and a tokenizer that decodes: the reference's validation logs
     (projector_trainer.py:423-431) -- validation/loss and validation/last_word_accuracy -- from generate on the
