@@ -418,11 +418,21 @@ int ptk_gemma3_decode_step(const ptk_gemma3_config* c, const ptk_gemma3_weights*
  * do_sample -> drawn without replacement from softmax(accumulated) (the n_cand largest accumulated + Gumbel noise
  * of (seed, step, row, token): torch.multinomial's distribution; order = draw order), else the n_cand largest
  * (descending).  Out [batch][n_cand]: token, beam (0..beams-1) and accumulated log prob; fewer candidates than
- * n_cand with a finite score leave token -1. */
+ * n_cand with a finite score leave token -1.  beams <= 8; ws: ptk_beam_candidates_workspace_bytes(batch, beams,
+ * n_cand) bytes (one workgroup per row writes its best n_cand there, a second pass merges each item's rows). */
+size_t ptk_beam_candidates_workspace_bytes(int batch, int beams, int n_cand);
 int ptk_beam_candidates(const void* logits, int64_t ld, const float* beam_scores, int batch, int beams, int vocab,
                         int do_sample, int top_k, float top_p, float temperature, int min_tokens_to_keep,
                         uint64_t seed, int step, int n_cand, int64_t* tokens, int32_t* beam_idx, float* scores,
-                        void* stream);
+                        void* ws, size_t ws_bytes, void* stream);
+
+/* The decode steps' skinny GEMM (unit-test surface; the decode calls it internally): C[M][N] bf16 =
+ * A[M][K] . B[N][K]^T for M <= 64, N % 128 == 0, K % 32 == 0 (K >= 64), act PTK_ACT_NONE or PTK_ACT_GEGLU
+ * (interleaved gate|up columns -> N / 2 output columns); part: fp32 K-split partials of
+ * ptk_gemm_skinny_part_bytes(M, N, K) bytes (0: none needed). */
+size_t ptk_gemm_skinny_part_bytes(int M, int N, int K);
+int ptk_gemm_skinny(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
+                    int act, void* part, size_t part_bytes, void* stream);
 
 /* clip_grad_norm_ + AdamW over bf16 parameters (Stage2/trainer.py:426-443, optimizer :145-149).
  * ptk_bf16_grad_scale_sumsq: g = bf16(g * scale) in place (scale 1: untouched), *out = sum g^2 (fp32,

@@ -196,8 +196,13 @@ SIGNATURES = {
                                           c_size_t, c_void_p]),
     "ptk_gemma3_decode_step": (c_int, [C.POINTER(Gemma3ConfigC), C.POINTER(Gemma3WeightsC), C.POINTER(Gemma3DecodeC),
                                        c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t, c_void_p]),
+    "ptk_beam_candidates_workspace_bytes": (c_size_t, [c_int, c_int, c_int]),
     "ptk_beam_candidates": (c_int, [c_void_p, c_int64, c_void_p, c_int, c_int, c_int, c_int, c_int, c_float, c_float,
-                                    c_int, c_uint64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p]),
+                                    c_int, c_uint64, c_int, c_int, c_void_p, c_void_p, c_void_p, c_void_p, c_size_t,
+                                    c_void_p]),
+    "ptk_gemm_skinny_part_bytes": (c_size_t, [c_int, c_int, c_int]),
+    "ptk_gemm_skinny": (c_int, [c_void_p, c_int64, c_void_p, c_int64, c_void_p, c_int64, c_int, c_int, c_int, c_int,
+                                c_void_p, c_size_t, c_void_p]),
     "ptk_bf16_sumsq_partial_floats": (c_int, []),
     "ptk_bf16_grad_scale_sumsq": (c_int, [c_void_p, c_int64, c_float, c_void_p, c_void_p, c_void_p]),
     "ptk_adamw_bf16": (c_int, [c_void_p] * 4 + [c_int64, c_void_p, c_float] + [C.c_double] * 5 +

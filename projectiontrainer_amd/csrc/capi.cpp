@@ -60,6 +60,14 @@ int ptk_gemm_tail_split(const ptk_gemm_desc* d) {
   return p8_tail_split(to_args(d), d->act, d->out);
 }
 
+size_t ptk_gemm_skinny_part_bytes(int M, int N, int K) { return skinny_part_bytes(M, N, K); }
+int ptk_gemm_skinny(const void* A, int64_t lda, const void* B, int64_t ldb, void* C, int64_t ldc, int M, int N, int K,
+                    int act, void* part, size_t part_bytes, void* stream) {
+  if (!A || !B || !C) return set_error("ptk_gemm_skinny: NULL operand");
+  return launch_gemm_skinny((const bf16_t*)A, (long)lda, (const bf16_t*)B, (long)ldb, (bf16_t*)C, (long)ldc, M, N, K,
+                            act, (float*)part, part_bytes, (hipStream_t)stream);
+}
+
 int ptk_layernorm(const float* x, const float* w, const float* b, void* y, int rows, int cols, float eps,
                   void* stream) {
   return launch_layernorm(x, w, b, (bf16_t*)y, rows, cols, eps, ST);

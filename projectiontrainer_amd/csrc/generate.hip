@@ -68,6 +68,38 @@ PTK_DEV float gen_uniform(uint64_t seed, int step, int row) {
 
 constexpr int GS_T = 1024;   // threads per row
 
+// f(i, u) for every element i < V of a bf16 row (u: the raw bits), each thread over elements in increasing index
+// order: 16-B loads, four in flight per thread (the decode's per-token row passes are latency-bound otherwise:
+// 2-byte loads one at a time measured ~0.8 ms per item at V = 262 144); the row must be 16-B aligned for the
+// vector part (else everything goes through the scalar tail)
+template <int NT, class F>
+PTK_DEV void scan_row(const uint16_t* row, int V, F&& f) {
+  const int tid = threadIdx.x;
+  const int n8 = ((uintptr_t)row & 15) ? 0 : V / 8;
+  const uint4* r4 = reinterpret_cast<const uint4*>(row);
+  for (int c0 = tid; c0 < n8; c0 += 4 * NT) {
+    uint4 q[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + j * NT;
+      q[j] = c < n8 ? r4[c] : make_uint4(0, 0, 0, 0);
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int c = c0 + j * NT;
+      if (c < n8) {
+        const uint32_t w[4] = {q[j].x, q[j].y, q[j].z, q[j].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          f(8 * c + 2 * e, (uint16_t)(w[e] & 0xffffu));
+          f(8 * c + 2 * e + 1, (uint16_t)(w[e] >> 16));
+        }
+      }
+    }
+  }
+  for (int i = 8 * n8 + tid; i < V; i += NT) f(i, row[i]);
+}
+
 // One workgroup per batch row b: the next token from logits row b (bf16 [V]).
 //   greedy (do_sample == 0): argmax, the first index among equal maxima;
 //   sampling: z_i = x_i / temperature; keep every i with x_i >= the top_k-th largest x (top_k <= 0 or >= V: all);
@@ -94,10 +126,10 @@ __global__ void __launch_bounds__(GS_T) gen_sample_kernel(const bf16_t* __restri
     // max (and its first index) over the row
     float mx = -INFINITY;
     int mi = 0x7fffffff;
-    for (int i = tid; i < V; i += GS_T) {
-      const float v = bf2f(row[i]);
+    scan_row<GS_T>(row, V, [&](int i, uint16_t u) {
+      const float v = bf2f(u);
       if (v > mx) { mx = v; mi = i; }
-    }
+    });
 #pragma unroll
     for (int o = 32; o >= 1; o >>= 1) {
       const float ov = __shfl_xor(mx, o, 64);
@@ -121,11 +153,11 @@ __global__ void __launch_bounds__(GS_T) gen_sample_kernel(const bf16_t* __restri
         for (int pass = 0; pass < 2; ++pass) {
           for (int i = tid; i < 256; i += GS_T) hist[i] = 0;
           __syncthreads();
-          for (int i = tid; i < V; i += GS_T) {
-            const uint32_t k = bf_key(row[i]);
+          scan_row<GS_T>(row, V, [&](int, uint16_t u) {
+            const uint32_t k = bf_key(u);
             if (pass == 0) atomicAdd(&hist[k >> 8], 1u);
             else if ((k >> 8) == hi) atomicAdd(&hist[k & 255u], 1u);
-          }
+          });
           __syncthreads();
           if (tid == 0) {
             uint32_t acc = 0;
@@ -144,22 +176,21 @@ __global__ void __launch_bounds__(GS_T) gen_sample_kernel(const bf16_t* __restri
         }
       }
       const float inv_t = 1.f / temperature;
-      if (top_p < 1.f) {
-        // TopPLogitsWarper (min_tokens_to_keep 1): the kept set sorted ascending by logit in LDS (bitonic), the
-        // cumulative softmax of z = x / T, entries with cumulative mass <= 1 - top_p dropped; then the draw by
-        // inverse CDF over what is left (sorted order: the same law as a draw in index order)
+      if (top_p < 1.f || (top_k > 0 && top_k <= GS_LIST / 2) || V <= GS_LIST) {
+        // the kept set (top-k, ties kept) sorted ascending by logit in LDS (bitonic), the cumulative softmax of
+        // z = x / T; TopPLogitsWarper (min_tokens_to_keep 1) drops entries with cumulative mass <= 1 - top_p; then
+        // the draw by inverse CDF over what is left (sorted order: the same law as a draw in index order)
         __shared__ float ls[GS_LIST];
         __shared__ int lt[GS_LIST];
         __shared__ int cnt;
         if (tid == 0) cnt = 0;
         __syncthreads();
-        for (int i = tid; i < V; i += GS_T) {
-          const uint16_t u = row[i];
+        scan_row<GS_T>(row, V, [&](int i, uint16_t u) {
           if (bf_key(u) >= thr) {
             const int slot = atomicAdd(&cnt, 1);
             if (slot < GS_LIST) { ls[slot] = (bf2f(u) - mx) * inv_t; lt[slot] = i; }
           }
-        }
+        });
         __syncthreads();
         const int n = min(cnt, GS_LIST);
         int np2 = 1;
@@ -399,199 +430,230 @@ PTK_DEV float bc_gumbel(uint64_t seed, int step, int row, int tok) {
   return -__logf(-__logf(u));
 }
 
+// One workgroup per decode row (item b = blockIdx / K, beam k = blockIdx % K): the row's best n_cand candidates
+// (selection key, accumulated score, token) into the scratch; beam_merge_kernel then takes each item's best n_cand
+// over its K rows.
 __global__ void __launch_bounds__(BC_T) beam_cand_kernel(const bf16_t* __restrict__ logits, long ld,
                                                          const float* __restrict__ beam_scores, int K, int V,
                                                          int do_sample, int top_k, float top_p, float temperature,
                                                          int min_keep, uint64_t seed, int step, int n_cand,
-                                                         int64_t* __restrict__ out_tok, int32_t* __restrict__ out_beam,
-                                                         float* __restrict__ out_score) {
-  const int b = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+                                                         float* __restrict__ sc_key, float* __restrict__ sc_acc,
+                                                         int32_t* __restrict__ sc_tok) {
+  const int rowi = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int NW = BC_T / 64;
   __shared__ uint32_t hist[256];
   __shared__ float redf[NW];
   __shared__ int redi[NW];
   __shared__ uint32_t sel[2];
   __shared__ int cnt;
-  __shared__ float ls[BC_LIST];      // kept entries of the row: log prob (processed)
+  __shared__ float ls[BC_LIST];      // kept entries of the row: log prob (processed), then accumulated
   __shared__ int lt[BC_LIST];        //                              token
   __shared__ float best_key[32], best_acc[32];
-  __shared__ int best_tok[32], best_beam[32];
+  __shared__ int best_tok[32];
   __shared__ int nbest;
   if (tid == 0) nbest = 0;
   const float inv_t = (do_sample && temperature > 0.f) ? 1.f / temperature : 1.f;
-  int bad = 0;
-  for (int k = 0; k < K; ++k) {
-    const int rowi = b * K + k;
-    const uint16_t* row = reinterpret_cast<const uint16_t*>(logits) + (long)rowi * ld;
-    // log_softmax statistics (fp32 over the bf16 logits)
-    float mx = -INFINITY;
-    for (int i = tid; i < V; i += BC_T) mx = fmaxf(mx, bf2f(row[i]));
+  const uint16_t* row = reinterpret_cast<const uint16_t*>(logits) + (long)rowi * ld;
+  // log_softmax statistics (fp32 over the bf16 logits)
+  float mx = -INFINITY;
+  scan_row<BC_T>(row, V, [&](int, uint16_t u) { mx = fmaxf(mx, bf2f(u)); });
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
-    if (lane == 0) redf[wave] = mx;
-    __syncthreads();
-    mx = redf[0];
-    for (int w = 1; w < NW; ++w) mx = fmaxf(mx, redf[w]);
-    __syncthreads();
-    float se = 0.f;
-    for (int i = tid; i < V; i += BC_T) se += __expf(bf2f(row[i]) - mx);
+  for (int o = 32; o >= 1; o >>= 1) mx = fmaxf(mx, __shfl_xor(mx, o, 64));
+  if (lane == 0) redf[wave] = mx;
+  __syncthreads();
+  mx = redf[0];
+  for (int w = 1; w < NW; ++w) mx = fmaxf(mx, redf[w]);
+  __syncthreads();
+  float se = 0.f;
+  scan_row<BC_T>(row, V, [&](int, uint16_t u) { se += __expf(bf2f(u) - mx); });
 #pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) se += __shfl_xor(se, o, 64);
-    if (lane == 0) redf[wave] = se;
-    __syncthreads();
-    se = 0.f;
-    for (int w = 0; w < NW; ++w) se += redf[w];
-    const float lse = mx + __logf(se);
-    __syncthreads();
-    // the row's kept set: the kk largest logits (ties kept) -- log_softmax and /T preserve the order
-    const int kk = do_sample ? (top_k > 0 ? max(top_k, min_keep) : V) : n_cand;
-    uint32_t thr = 0;
-    if (kk < V) {
-      uint32_t need = (uint32_t)kk, hi = 0;
-      for (int pass = 0; pass < 2; ++pass) {
-        for (int i = tid; i < 256; i += BC_T) hist[i] = 0;
-        __syncthreads();
-        for (int i = tid; i < V; i += BC_T) {
-          const uint32_t key = bf_key(row[i]);
-          if (pass == 0) atomicAdd(&hist[key >> 8], 1u);
-          else if ((key >> 8) == hi) atomicAdd(&hist[key & 255u], 1u);
-        }
-        __syncthreads();
-        if (tid == 0) {
-          uint32_t acc = 0;
-          int bin = 255;
-          for (; bin > 0; --bin) {
-            if (acc + hist[bin] >= need) break;
-            acc += hist[bin];
-          }
-          sel[0] = (uint32_t)bin;
-          sel[1] = need - acc;
-        }
-        __syncthreads();
-        if (pass == 0) { hi = sel[0]; need = sel[1]; }
-        else thr = (hi << 8) | sel[0];
-        __syncthreads();
-      }
-    }
-    if (tid == 0) cnt = 0;
-    __syncthreads();
-    for (int i = tid; i < V; i += BC_T) {
-      const uint16_t u = row[i];
-      if (bf_key(u) >= thr) {
-        const int slot = atomicAdd(&cnt, 1);
-        if (slot < BC_LIST) { ls[slot] = (bf2f(u) - lse) * inv_t; lt[slot] = i; }
-      }
-    }
-    __syncthreads();
-    int n = cnt;
-    if (n > BC_LIST) { bad = 1; n = BC_LIST; }
-    // top-p over the kept entries: bitonic sort ascending by score (then token), cumulative softmax
-    if (do_sample && top_p < 1.f) {
-      int np2 = 1;
-      while (np2 < n) np2 <<= 1;
-      for (int i = n + tid; i < np2; i += BC_T) { ls[i] = INFINITY; lt[i] = 0x7fffffff; }
+  for (int o = 32; o >= 1; o >>= 1) se += __shfl_xor(se, o, 64);
+  if (lane == 0) redf[wave] = se;
+  __syncthreads();
+  se = 0.f;
+  for (int w = 0; w < NW; ++w) se += redf[w];
+  const float lse = mx + __logf(se);
+  __syncthreads();
+  // the row's kept set: the kk largest logits (ties kept) -- log_softmax and /T preserve the order
+  const int kk = do_sample ? (top_k > 0 ? max(top_k, min_keep) : V) : n_cand;
+  uint32_t thr = 0;
+  if (kk < V) {
+    uint32_t need = (uint32_t)kk, hi = 0;
+    for (int pass = 0; pass < 2; ++pass) {
+      for (int i = tid; i < 256; i += BC_T) hist[i] = 0;
       __syncthreads();
-      for (int size = 2; size <= np2; size <<= 1)
-        for (int stride = size >> 1; stride > 0; stride >>= 1) {
-          for (int i = tid; i < np2; i += BC_T) {
-            const int j = i ^ stride;
-            if (j > i) {
-              const bool up = (i & size) == 0;
-              const float a = ls[i], c = ls[j];
-              const bool gt = a > c || (a == c && lt[i] > lt[j]);
-              if (gt == up) { ls[i] = c; ls[j] = a; const int tt = lt[i]; lt[i] = lt[j]; lt[j] = tt; }
-            }
-          }
-          __syncthreads();
-        }
-      if (tid == 0) {   // (n <= 1024 entries, once per row and step)
-        const float top = ls[n - 1];
-        float tot = 0.f;
-        for (int i = 0; i < n; ++i) tot += __expf(ls[i] - top);
-        float cum = 0.f;
-        int first = 0;
-        for (int i = 0; i < n; ++i) {
-          cum += __expf(ls[i] - top);
-          if (cum / tot <= 1.f - top_p) first = i + 1;
-        }
-        first = min(first, max(0, n - min_keep));
-        cnt = first;   // kept: [first, n)
-      }
-      __syncthreads();
-    } else if (tid == 0) {
-      cnt = 0;
-    }
-    __syncthreads();
-    const int first = cnt;
-    // candidates of this row: accumulated = processed log prob + the beam's score; selection key (+ Gumbel noise)
-    const float bs = beam_scores[rowi];
-    for (int i = first + tid; i < n; i += BC_T) {
-      const float acc = ls[i] + bs;
-      ls[i] = acc;
-    }
-    __syncthreads();
-    // merge into the item's running best n_cand: n_cand rounds of an arg-max over this row's entries
-    for (int rnd = 0; rnd < n_cand; ++rnd) {
-      float bk = -INFINITY;
-      int bi = -1;
-      for (int i = first + tid; i < n; i += BC_T) {
-        if (lt[i] < 0) continue;   // taken
-        const float key = do_sample ? ls[i] + bc_gumbel(seed, step, rowi, lt[i]) : ls[i];
-        if (key > bk || (key == bk && (bi < 0 || lt[i] < lt[bi]))) { bk = key; bi = i; }
-      }
-#pragma unroll
-      for (int o = 32; o >= 1; o >>= 1) {
-        const float ok = __shfl_xor(bk, o, 64);
-        const int oi = __shfl_xor(bi, o, 64);
-        if (ok > bk || (ok == bk && oi >= 0 && (bi < 0 || lt[oi] < lt[bi]))) { bk = ok; bi = oi; }
-      }
-      if (lane == 0) { redf[wave] = bk; redi[wave] = bi; }
+      scan_row<BC_T>(row, V, [&](int, uint16_t u) {
+        const uint32_t key = bf_key(u);
+        if (pass == 0) atomicAdd(&hist[key >> 8], 1u);
+        else if ((key >> 8) == hi) atomicAdd(&hist[key & 255u], 1u);
+      });
       __syncthreads();
       if (tid == 0) {
-        float k0 = redf[0];
-        int i0 = redi[0];
-        for (int w = 1; w < NW; ++w)
-          if (redf[w] > k0 || (redf[w] == k0 && redi[w] >= 0 && (i0 < 0 || lt[redi[w]] < lt[i0]))) { k0 = redf[w]; i0 = redi[w]; }
-        if (i0 >= 0 && k0 > -INFINITY) {
-          // insert into the running list (descending by key), keep n_cand
-          int m = nbest;
-          int pos = m;
-          while (pos > 0 && best_key[pos - 1] < k0) --pos;
-          if (pos < n_cand) {
-            for (int q = min(m, n_cand - 1); q > pos; --q) {
-              best_key[q] = best_key[q - 1]; best_acc[q] = best_acc[q - 1];
-              best_tok[q] = best_tok[q - 1]; best_beam[q] = best_beam[q - 1];
-            }
-            best_key[pos] = k0; best_acc[pos] = ls[i0]; best_tok[pos] = lt[i0]; best_beam[pos] = k;
-            nbest = min(m + 1, n_cand);
-          }
-          lt[i0] = -1;
+        uint32_t acc = 0;
+        int bin = 255;
+        for (; bin > 0; --bin) {
+          if (acc + hist[bin] >= need) break;
+          acc += hist[bin];
         }
+        sel[0] = (uint32_t)bin;
+        sel[1] = need - acc;
       }
       __syncthreads();
+      if (pass == 0) { hi = sel[0]; need = sel[1]; }
+      else thr = (hi << 8) | sel[0];
+      __syncthreads();
+    }
+  }
+  if (tid == 0) cnt = 0;
+  __syncthreads();
+  scan_row<BC_T>(row, V, [&](int i, uint16_t u) {
+    if (bf_key(u) >= thr) {
+      const int slot = atomicAdd(&cnt, 1);
+      if (slot < BC_LIST) { ls[slot] = (bf2f(u) - lse) * inv_t; lt[slot] = i; }
+    }
+  });
+  __syncthreads();
+  const bool bad = cnt > BC_LIST;
+  const int n = min(cnt, BC_LIST);
+  // top-p over the kept entries: bitonic sort ascending by score (then token), cumulative softmax
+  if (do_sample && top_p < 1.f) {
+    int np2 = 1;
+    while (np2 < n) np2 <<= 1;
+    for (int i = n + tid; i < np2; i += BC_T) { ls[i] = INFINITY; lt[i] = 0x7fffffff; }
+    __syncthreads();
+    for (int size = 2; size <= np2; size <<= 1)
+      for (int stride = size >> 1; stride > 0; stride >>= 1) {
+        for (int i = tid; i < np2; i += BC_T) {
+          const int j = i ^ stride;
+          if (j > i) {
+            const bool up = (i & size) == 0;
+            const float a = ls[i], c = ls[j];
+            const bool gt = a > c || (a == c && lt[i] > lt[j]);
+            if (gt == up) { ls[i] = c; ls[j] = a; const int tt = lt[i]; lt[i] = lt[j]; lt[j] = tt; }
+          }
+        }
+        __syncthreads();
+      }
+    if (tid == 0) {   // (n <= 1024 entries, once per row and step)
+      const float top = ls[n - 1];
+      float tot = 0.f;
+      for (int i = 0; i < n; ++i) tot += __expf(ls[i] - top);
+      float cum = 0.f;
+      int first = 0;
+      for (int i = 0; i < n; ++i) {
+        cum += __expf(ls[i] - top);
+        if (cum / tot <= 1.f - top_p) first = i + 1;
+      }
+      cnt = min(first, max(0, n - min_keep));   // kept: [first, n)
+    }
+    __syncthreads();
+  } else if (tid == 0) {
+    cnt = 0;
+  }
+  __syncthreads();
+  const int first = cnt;
+  const float bs = beam_scores[rowi];
+  for (int i = first + tid; i < n; i += BC_T) ls[i] += bs;   // accumulated = processed log prob + beam score
+  __syncthreads();
+  // the row's best n_cand by selection key (accumulated, + Gumbel noise when sampling): n_cand rounds of a block
+  // arg-max (ties: the lower token)
+  for (int rnd = 0; rnd < n_cand; ++rnd) {
+    float bk = -INFINITY;
+    int bi = -1;
+    for (int i = first + tid; i < n; i += BC_T) {
+      if (lt[i] < 0) continue;   // taken
+      const float key = do_sample ? ls[i] + bc_gumbel(seed, step, rowi, lt[i]) : ls[i];
+      if (key > bk || (key == bk && (bi < 0 || lt[i] < lt[bi]))) { bk = key; bi = i; }
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      const float ok = __shfl_xor(bk, o, 64);
+      const int oi = __shfl_xor(bi, o, 64);
+      if (ok > bk || (ok == bk && oi >= 0 && (bi < 0 || lt[oi] < lt[bi]))) { bk = ok; bi = oi; }
+    }
+    if (lane == 0) { redf[wave] = bk; redi[wave] = bi; }
+    __syncthreads();
+    if (tid == 0) {
+      float k0 = redf[0];
+      int i0 = redi[0];
+      for (int w = 1; w < NW; ++w)
+        if (redf[w] > k0 || (redf[w] == k0 && redi[w] >= 0 && (i0 < 0 || lt[redi[w]] < lt[i0]))) { k0 = redf[w]; i0 = redi[w]; }
+      if (i0 >= 0 && k0 > -INFINITY) {
+        best_key[nbest] = k0; best_acc[nbest] = ls[i0]; best_tok[nbest] = lt[i0];
+        ++nbest;
+        lt[i0] = -1;
+      }
     }
     __syncthreads();
   }
   if (tid < n_cand) {
-    const bool ok = tid < nbest && !bad;
-    out_tok[(long)b * n_cand + tid] = ok ? best_tok[tid] : -1;
-    out_beam[(long)b * n_cand + tid] = ok ? best_beam[tid] : -1;
-    out_score[(long)b * n_cand + tid] = ok ? best_acc[tid] : -INFINITY;
+    const long o = (long)rowi * n_cand + tid;
+    const bool ok = tid < nbest;
+    sc_key[o] = ok ? best_key[tid] : -INFINITY;
+    sc_acc[o] = ok ? best_acc[tid] : -INFINITY;
+    sc_tok[o] = bad ? -2 : (ok ? best_tok[tid] : -1);
   }
+}
+
+// item b: the best n_cand over its K rows' lists (descending key; ties: the lower beam, then the lower token)
+__global__ void __launch_bounds__(64) beam_merge_kernel(const float* __restrict__ sc_key,
+                                                        const float* __restrict__ sc_acc,
+                                                        const int32_t* __restrict__ sc_tok, int K, int n_cand,
+                                                        int64_t* __restrict__ out_tok, int32_t* __restrict__ out_beam,
+                                                        float* __restrict__ out_score) {
+  const int b = blockIdx.x, lane = threadIdx.x;
+  if (lane != 0) return;   // (K x n_cand <= 256 entries, once per item and step)
+  const long base = (long)b * K * n_cand;
+  bool bad = false;
+  for (int i = 0; i < K * n_cand; ++i) bad |= sc_tok[base + i] == -2;
+  int taken[8] = {0, 0, 0, 0, 0, 0, 0, 0};   // next unread entry of each row's (descending) list
+  for (int c = 0; c < n_cand; ++c) {
+    int best = -1;
+    float bk = -INFINITY;
+    for (int k = 0; k < K; ++k) {
+      if (taken[k] >= n_cand) continue;
+      const long o = base + (long)k * n_cand + taken[k];
+      if (sc_tok[o] < 0) continue;
+      const float key = sc_key[o];
+      if (best < 0 || key > bk) { bk = key; best = k; }   // (a tie keeps the lower beam)
+    }
+    const long out = (long)b * n_cand + c;
+    if (best < 0 || bad) {
+      out_tok[out] = -1; out_beam[out] = -1; out_score[out] = -INFINITY;
+      continue;
+    }
+    const long o = base + (long)best * n_cand + taken[best];
+    out_tok[out] = sc_tok[o]; out_beam[out] = best; out_score[out] = sc_acc[o];
+    ++taken[best];
+  }
+}
+
+size_t beam_candidates_ws_bytes(int batch, int K, int n_cand) {
+  return (size_t)batch * K * n_cand * 12 + 256;
 }
 
 int launch_beam_candidates(const bf16_t* logits, long ld, const float* beam_scores, int batch, int K, int V,
                            int do_sample, int top_k, float top_p, float temperature, int min_keep, uint64_t seed,
-                           int step, int n_cand, int64_t* tok, int32_t* beam, float* score, hipStream_t st) {
-  if (batch <= 0 || K <= 0 || V <= 0 || n_cand <= 0 || n_cand > 32)
-    return set_error("beam_candidates: batch %d, beams %d, vocab %d, n_cand %d (1..32)", batch, K, V, n_cand);
+                           int step, int n_cand, int64_t* tok, int32_t* beam, float* score, void* ws,
+                           size_t ws_bytes, hipStream_t st) {
+  if (batch <= 0 || K <= 0 || K > 8 || V <= 0 || n_cand <= 0 || n_cand > 32)
+    return set_error("beam_candidates: batch %d, beams %d (1..8), vocab %d, n_cand %d (1..32)", batch, K, V, n_cand);
   if (do_sample && !(temperature > 0.f)) return set_error("beam_candidates: temperature must be > 0 when sampling");
   if (do_sample && !(top_p > 0.f && top_p <= 1.f)) return set_error("beam_candidates: top_p must be in (0, 1]");
   if (do_sample && !(top_k > 0 && top_k <= BC_LIST / 2) && V > BC_LIST / 2)
     return set_error("beam_candidates: sampling needs 0 < top_k <= %d (the kept set lives in LDS)", BC_LIST / 2);
-  hipLaunchKernelGGL(beam_cand_kernel, dim3((unsigned)batch), dim3(BC_T), 0, st, logits, ld, beam_scores, K, V,
-                     do_sample, top_k, top_p, temperature, min_keep, seed, step, n_cand, tok, beam, score);
-  return hipGetLastError() == hipSuccess ? 0 : set_error("beam_candidates launch failed");
+  if (!ws || ws_bytes < beam_candidates_ws_bytes(batch, K, n_cand))
+    return set_error("beam_candidates: workspace too small (%zu bytes needed)", beam_candidates_ws_bytes(batch, K, n_cand));
+  const long nr = (long)batch * K * n_cand;
+  float* sk = (float*)ws;
+  float* sa = sk + nr;
+  int32_t* stok = (int32_t*)(sa + nr);
+  hipLaunchKernelGGL(beam_cand_kernel, dim3((unsigned)(batch * K)), dim3(BC_T), 0, st, logits, ld, beam_scores, K, V,
+                     do_sample, top_k, top_p, temperature, min_keep, seed, step, n_cand, sk, sa, stok);
+  if (hipGetLastError() != hipSuccess) return set_error("beam_candidates launch failed");
+  hipLaunchKernelGGL(beam_merge_kernel, dim3((unsigned)batch), dim3(64), 0, st, sk, sa, stok, K, n_cand, tok, beam,
+                     score);
+  return hipGetLastError() == hipSuccess ? 0 : set_error("beam_merge launch failed");
 }
 
 }  // namespace ptk

@@ -745,7 +745,26 @@ struct GenPass {            // per-pass activations (rows = B * S)
   float *xa, *xb, *x2, *rs1, *rs2, *rq, *rk;
   bf16_t *xn, *qkv, *Q, *K, *V, *O, *ao, *h, *dn;
   int32_t* kv;
+  float* skp = nullptr;     // decode passes: the skinny GEMM's K-split partials
+  size_t skp_bytes = 0;
 };
+// the partial buffer the skinny GEMM needs for the decode projections and the lm_head at `rows` rows
+size_t gen_skinny_bytes(const ptk_gemma3_config* c, long rows) {
+  if (rows > 64) return 0;
+  const int H = c->hidden, I = c->inter, D = c->head_dim, Dq = c->heads * D, Dqkv = (c->heads + 2 * c->kv_heads) * D;
+  const int M = (int)rows;
+  const int shapes[5][2] = {{Dqkv, H}, {H, Dq}, {2 * I, H}, {H, I}, {c->vocab, H}};   // (N, K)
+  size_t b = 0;
+  for (const auto& nk : shapes) b = std::max(b, skinny_part_bytes(M, nk[0], nk[1]));
+  return b;
+}
+// a decode-pass GEMM (bf16 out): the skinny kernel where it applies, else the general dispatch
+int gen_gemm(const GenPass& g, const bf16_t* A, long lda, const void* B, long ldb, bf16_t* C, long ldc, int M, int N,
+             int K, int act, hipStream_t st) {
+  if (g.skp_bytes > 0 && skinny_supported(M, N, K, lda, ldb, ldc, act))
+    return launch_gemm_skinny(A, lda, (const bf16_t*)B, ldb, C, ldc, M, N, K, act, g.skp, g.skp_bytes, st);
+  return launch_gemm(gemm(A, lda, B, ldb, C, ldc, M, N, K), act, OUT_BF16, 1, st);
+}
 struct GenWs {
   GenPass pre, dec;
   std::vector<bf16_t*> kc, vc;     // per layer [B, Hkv, Smax, D]
@@ -776,6 +795,8 @@ GenPass gen_pass(Bump& bp, const ptk_gemma3_config* c, long M) {
   g.h = bp.take<bf16_t>(M * I);
   g.dn = bp.take<bf16_t>(M * H);
   g.kv = bp.take<int32_t>(M);
+  g.skp_bytes = gen_skinny_bytes(c, M);
+  g.skp = g.skp_bytes ? bp.take<float>(g.skp_bytes / 4) : nullptr;
   return g;
 }
 GenWs gen_layout(Bump& bp, const ptk_gemma3_config* c, int B, int P, int max_new) {
@@ -820,7 +841,7 @@ int gen_layer(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, int l, G
   const long pofs = (dm && dm->pos) ? 0 : (long)p0 * (D / 2);   // per-token positions index the whole table
   const float* cs = (sliding ? wt->rope_cos_local : wt->rope_cos_global) + pofs;
   const float* sn = (sliding ? wt->rope_sin_local : wt->rope_sin_global) + pofs;
-  CK(launch_gemm(gemm(g.xn, H, L.wqkv, H, g.qkv, Dqkv, M, Dqkv, H), ACT_NONE, OUT_BF16, 1, st));
+  CK(gen_gemm(g, g.xn, H, L.wqkv, H, g.qkv, Dqkv, M, Dqkv, H, ACT_NONE, st));
   AttnShape ash{B, Sp, Hq, Hkv, D};
   if (dm) ash.pos = dm->pos;
   CK(launch_qknorm_rope_fwd(g.qkv, L.q_norm, L.k_norm, cs, sn, ash, c->eps, g.Q, g.K, g.V, g.rq, g.rk, st));
@@ -856,13 +877,10 @@ int gen_layer(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, int l, G
     }
     CK(launch_attn_fwd(fa, Z, st));
   }
-  CK(launch_gemm(gemm(g.O, Dq, L.wo, Dq, g.ao, H, M, H, Dq), ACT_NONE, OUT_BF16, 1, st));
+  CK(gen_gemm(g, g.O, Dq, L.wo, Dq, g.ao, H, M, H, Dq, ACT_NONE, st));
   CK(launch_residual_norm_fwd(g.ao, x_in, L.ln_post_attn, L.ln_pre_ff, g.x2, g.xn, g.rs1, g.rs2, M, H, c->eps, st));
-  {
-    GemmArgs gg = gemm(g.xn, H, L.wgu, H, g.h, I, M, 2 * I, H);   // (no saved GEGLU factors: no backward)
-    CK(launch_gemm(gg, ACT_GEGLU, OUT_BF16, 1, st));
-  }
-  CK(launch_gemm(gemm(g.h, I, L.wd, I, g.dn, H, M, H, I), ACT_NONE, OUT_BF16, 1, st));
+  CK(gen_gemm(g, g.xn, H, L.wgu, H, g.h, I, M, 2 * I, H, ACT_GEGLU, st));   // (no saved GEGLU factors: no backward)
+  CK(gen_gemm(g, g.h, I, L.wd, I, g.dn, H, M, H, I, ACT_NONE, st));
   const float* wnext = (l + 1 < c->layers) ? wt->layers[l + 1].ln_in : nullptr;
   CK(launch_residual_norm_fwd(g.dn, g.x2, L.ln_post_ff, wnext, x_out, g.xn, g.rs1, g.rs2, M, H, c->eps, st));
   return 0;
@@ -889,7 +907,7 @@ int gemma_generate(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, con
   // logits row b -> sampled token, into out_ids[:, t]
   auto head = [&](const float* x, RowMap map, int t) -> int {
     CK(launch_rmsnorm_fwd(x, H, map, wt->final_norm, w.xf, w.rstd_f, B, H, c->eps, st));
-    CK(launch_gemm(gemm(w.xf, H, wt->embed, H, w.logits, V, B, V, H), ACT_NONE, OUT_BF16, 1, st));
+    CK(gen_gemm(w.dec, w.xf, H, wt->embed, H, w.logits, V, B, V, H, ACT_NONE, st));
     if (step_logits)
       CKH(hipMemcpyAsync(step_logits + (long)t * B * V, w.logits, (size_t)B * V * 2, hipMemcpyDeviceToDevice, st));
     return launch_gen_sample(w.logits, V, B, V, gd->do_sample, gd->top_k, gd->temperature,
@@ -1068,7 +1086,7 @@ int gemma_decode_step(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, 
     std::swap(xi, xo);
   }
   CK(launch_rmsnorm_fwd(xi, H, RowMap{0, 0, 0, 0}, wt->final_norm, w.xf, w.rstd_f, rows, H, c->eps, st));
-  CK(launch_gemm(gemm(w.xf, H, wt->embed, H, logits, V, rows, V, H), ACT_NONE, OUT_BF16, 1, st));
+  CK(gen_gemm(w.dec, w.xf, H, wt->embed, H, logits, V, rows, V, H, ACT_NONE, st));
   return 0;
 }
 
@@ -1099,15 +1117,19 @@ int ptk_gemma3_decode_step(const ptk_gemma3_config* c, const ptk_gemma3_weights*
   return gemma_decode_step(c, w, d, step, ids, src_rows, (bf16_t*)logits, ws, ws_bytes, (hipStream_t)stream);
 }
 
+size_t ptk_beam_candidates_workspace_bytes(int batch, int beams, int n_cand) {
+  return beam_candidates_ws_bytes(batch, beams, n_cand);
+}
+
 int ptk_beam_candidates(const void* logits, int64_t ld, const float* beam_scores, int batch, int beams, int vocab,
                         int do_sample, int top_k, float top_p, float temperature, int min_tokens_to_keep,
                         uint64_t seed, int step, int n_cand, int64_t* tokens, int32_t* beam_idx, float* scores,
-                        void* stream) {
+                        void* ws, size_t ws_bytes, void* stream) {
   if (!logits || !beam_scores || !tokens || !beam_idx || !scores) return set_error("beam_candidates: NULL argument");
   if (ld < vocab) return set_error("beam_candidates: ld < vocab");
   return launch_beam_candidates((const bf16_t*)logits, (long)ld, beam_scores, batch, beams, vocab, do_sample, top_k,
                                 top_p, temperature, min_tokens_to_keep, seed, step, n_cand, tokens, beam_idx, scores,
-                                (hipStream_t)stream);
+                                ws, ws_bytes, (hipStream_t)stream);
 }
 
 int ptk_gemma3_loss_fwd_bwd(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const ptk_gemma3_batch* bt,

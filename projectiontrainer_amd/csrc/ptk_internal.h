@@ -328,6 +328,11 @@ int launch_kv_append(const bf16_t* src, long src_z, bf16_t* dst, long dst_z, int
 int launch_gen_sample(const bf16_t* logits, long ld, int B, int V, int do_sample, int top_k, float temperature,
                       float top_p, uint64_t seed, int step, long eos_id, long pad_id, int32_t* finished, int64_t* out,
                       long ld_out, int64_t* next, hipStream_t st);
+// skinny GEMM of the decode steps (gemm_skinny.hip): M <= 64 rows, N % 64, K % 32; ACT_NONE / ACT_GEGLU, bf16 out
+bool skinny_supported(int M, int N, int K, long lda, long ldb, long ldc, int act);
+size_t skinny_part_bytes(int M, int N, int K);
+int launch_gemm_skinny(const bf16_t* A, long lda, const bf16_t* B, long ldb, bf16_t* C, long ldc, int M, int N,
+                       int K, int act, float* part, size_t part_bytes, hipStream_t st);
 // stepwise decode (ptk_gemma3_decode_prefill / _step) and beam candidates (ptk_beam_candidates)
 int launch_dec_prompt(const float* src, long ld_b, const int32_t* mask, long mask_ld, int repeat, int rows, int P,
                       int Pp, int H, float* x, int32_t* kv, hipStream_t st);
@@ -338,9 +343,11 @@ int launch_dec_step_prep(int32_t* slot_ok, const int32_t* nvalid, int rows, int 
 int launch_dec_gather_rows(const void* in, void* out, const int32_t* src, int rows, long row_bytes, hipStream_t st);
 int launch_dec_gather_i32(const int32_t* in, int32_t* out, const int32_t* src, int rows, hipStream_t st);
 int launch_dec_repeat_index(int32_t* src, int rows, int repeat, hipStream_t st);
+size_t beam_candidates_ws_bytes(int batch, int K, int n_cand);
 int launch_beam_candidates(const bf16_t* logits, long ld, const float* beam_scores, int batch, int K, int V,
                            int do_sample, int top_k, float top_p, float temperature, int min_keep, uint64_t seed,
-                           int step, int n_cand, int64_t* tok, int32_t* beam, float* score, hipStream_t st);
+                           int step, int n_cand, int64_t* tok, int32_t* beam, float* score, void* ws,
+                           size_t ws_bytes, hipStream_t st);
 
 // ---- unfrozen-LLM step (train.hip) ----
 // out [cols][rows_pad] bf16 = in[map(r)][c] (r < rows), zero for rows <= r < rows_pad

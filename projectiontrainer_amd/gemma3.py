@@ -326,11 +326,14 @@ class Gemma3CausalLM:
         bi = torch.empty((B, n_cand), dtype=torch.int32, device=self.device)
         sc = torch.empty((B, n_cand), dtype=torch.float32, device=self.device)
         bs = beam_scores.to(device=self.device, dtype=torch.float32).contiguous()
+        n = L.lib().ptk_beam_candidates_workspace_bytes(B, beams, n_cand)
+        if getattr(self, "_bc_ws", None) is None or self._bc_ws.numel() < n:
+            self._bc_ws = torch.empty(n, dtype=torch.uint8, device=self.device)
         L.check(L.lib().ptk_beam_candidates(logits.data_ptr(), V, bs.data_ptr(), B, beams, V, int(bool(do_sample)),
                                             int(top_k or 0), float(top_p), float(temperature), int(min_tokens_to_keep),
                                             int(seed) & ((1 << 64) - 1), int(step), int(n_cand), tok.data_ptr(),
-                                            bi.data_ptr(), sc.data_ptr(), L.stream_ptr(self.device)),
-                "ptk_beam_candidates")
+                                            bi.data_ptr(), sc.data_ptr(), self._bc_ws.data_ptr(), self._bc_ws.numel(),
+                                            L.stream_ptr(self.device)), "ptk_beam_candidates")
         return tok, bi, sc
 
     def beam_generate(self, inputs_embeds, attention_mask=None, num_beams=3, max_new_tokens=512, do_sample=True,

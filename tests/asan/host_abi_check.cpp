@@ -110,9 +110,11 @@ int main(int argc, char** argv) {
     EXPECT(ptk_gemma3_decode_step(&g1, &gw, &dd, 8, &dummy, nullptr, &dummy, &dummy, (size_t)1 << 40, nullptr) < 0);  // past the last
     float sc = 0.f;
     int32_t bi = 0;
-    EXPECT(ptk_beam_candidates(&dummy, 512, &sc, 1, 3, 512, 0, 0, 1.f, 1.f, 1, 0, 0, 64, &dummy, &bi, &sc, nullptr) < 0);  // n_cand > 32
-    EXPECT(ptk_beam_candidates(&dummy, 262144, &sc, 1, 3, 262144, 1, 0, 0.9f, 1.f, 2, 0, 0, 6, &dummy, &bi, &sc, nullptr) < 0);  // no top-k
-    EXPECT(ptk_beam_candidates(&dummy, 512, &sc, 1, 3, 512, 1, 50, 0.9f, 0.f, 2, 0, 0, 6, &dummy, &bi, &sc, nullptr) < 0);  // T = 0
+    EXPECT(ptk_beam_candidates(&dummy, 512, &sc, 1, 3, 512, 0, 0, 1.f, 1.f, 1, 0, 0, 64, &dummy, &bi, &sc, nullptr, 0, nullptr) < 0);  // n_cand > 32
+    EXPECT(ptk_beam_candidates(&dummy, 262144, &sc, 1, 3, 262144, 1, 0, 0.9f, 1.f, 2, 0, 0, 6, &dummy, &bi, &sc, nullptr, 0, nullptr) < 0);  // no top-k
+    EXPECT(ptk_beam_candidates(&dummy, 512, &sc, 1, 3, 512, 1, 50, 0.9f, 0.f, 2, 0, 0, 6, &dummy, &bi, &sc, nullptr, 0, nullptr) < 0);  // T = 0
+    EXPECT(ptk_beam_candidates(&dummy, 512, &sc, 1, 3, 512, 0, 0, 1.f, 1.f, 1, 0, 0, 6, &dummy, &bi, &sc, &dummy, 8, nullptr) < 0);  // ws too small
+    EXPECT(ptk_beam_candidates_workspace_bytes(16, 3, 6) >= 16 * 3 * 6 * 12);
   }
   ptk_projector pj{};
   pj.vision_dim = 1024; pj.inter_dim = 4096; pj.llm_dim = 1152;

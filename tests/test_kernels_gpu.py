@@ -804,3 +804,30 @@ def test_weight_grad_tn_gated_shapes(gpu):
     assert rc != 0 and b"transpose path" in L.lib().ptk_last_error()
     torch.cuda.synchronize()
     assert not gz.any()
+
+
+@pytest.mark.parametrize("M,N,K,act", [(1, 128, 64, 0), (5, 1152, 1152, 0), (16, 1536, 1152, 0), (33, 1152, 6912, 0),
+                                       (48, 262144, 1152, 0), (64, 1152, 1024, 0), (48, 13824, 1152, 3),
+                                       (7, 256, 128, 3)])
+def test_gemm_skinny_vs_fp32(gpu, M, N, K, act):
+    """The decode steps' skinny GEMM (gemm_skinny.hip: one workgroup per 64 columns and K slice, fragments straight
+    from global memory, K-split partials summed in split order): against torch fp32 on the same bf16 operands,
+    plain (C rounded to bf16 once) and GEGLU on interleaved gate|up columns (h = bf16(bf16(gelu(g)) * u))."""
+    from projectiontrainer_amd import _lib as L
+    g = torch.Generator(device=gpu).manual_seed(M * 7 + N)
+    A = (torch.randn(M, K, device=gpu, generator=g) * 0.5).to(torch.bfloat16)
+    B = (torch.randn(N, K, device=gpu, generator=g) * 0.05).to(torch.bfloat16)
+    NO = N // 2 if act == 3 else N
+    C = torch.empty(M, NO, dtype=torch.bfloat16, device=gpu)
+    n = L.lib().ptk_gemm_skinny_part_bytes(M, N, K)
+    part = torch.empty(max(n, 16), dtype=torch.uint8, device=gpu)
+    L.check(L.lib().ptk_gemm_skinny(A.data_ptr(), K, B.data_ptr(), K, C.data_ptr(), NO, M, N, K, act, part.data_ptr(),
+                                    n, L.stream_ptr(gpu)), "ptk_gemm_skinny")
+    ref = A.float() @ B.float().t()
+    if act == 3:
+        q = torch.arange(NO, device=gpu)
+        gate = ref[:, 32 * (q // 16) + q % 16].to(torch.bfloat16).float()
+        up = ref[:, 32 * (q // 16) + 16 + q % 16].to(torch.bfloat16).float()
+        a = torch.nn.functional.gelu(gate, approximate="tanh").to(torch.bfloat16).float()
+        ref = a * up
+    torch.testing.assert_close(C.float(), ref, rtol=2e-2, atol=2e-2 * float(ref.abs().max()))
