@@ -179,7 +179,7 @@ def embed_tokens(p, cfg: Gemma3TextConfig, token_ids, dtype=torch.float32):
 
 
 def greedy_generate(p, cfg: Gemma3TextConfig, prompt_embeds, max_new_tokens, eos_token_id=None, pad_token_id=0,
-                    force_ids=None, dtype=torch.float32):
+                    force_ids=None, dtype=torch.float32, embed_dtype=torch.bfloat16):
     """`GenerationMixin._sample` with do_sample=False over `Gemma3ForCausalLM` from inputs_embeds and an all-ones
     attention mask, as the reference's validation calls generate (Stage1/projector_trainer.py:386-393; greedy, so
     deterministic): each step's logits are the tied lm_head of the last position's final-norm output (recomputed
@@ -205,7 +205,7 @@ def greedy_generate(p, cfg: Gemma3TextConfig, prompt_embeds, max_new_tokens, eos
             if not unfinished.any():
                 break
         feed = tok if force_ids is None else torch.as_tensor(force_ids)[:, t]
-        e = embed_tokens(p, cfg, feed[:, None], torch.bfloat16).to(dtype)
+        e = embed_tokens(p, cfg, feed[:, None], embed_dtype).to(dtype)   # (fp32 for an fp32 HF model)
         x = torch.cat([x, e], dim=1)
     return torch.stack(toks, 1), torch.stack(logs, 0)
 

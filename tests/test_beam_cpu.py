@@ -100,3 +100,26 @@ def test_beam_state_fill_value_quirk():
     """Unused positions hold `pad_token_id or eos_token_id` (HF's fill): a pad id of 0 falls through to eos."""
     assert BeamSearch(1, 2, 4, eos_token_id=1, pad_token_id=0).fill == 1
     assert BeamSearch(1, 2, 4, eos_token_id=1, pad_token_id=3).fill == 3
+
+
+@pytest.mark.parametrize("eos_rank", [None, 0])
+def test_oracle_greedy_generate_matches_transformers(eos_rank):
+    """Stage 1's validation decode semantics (Stage1/projector_trainer.py:386-393 -> GenerationMixin._sample) pinned
+    against transformers itself: the oracle's cache-free greedy decode (oracle/stage1_ref.py greedy_generate, which
+    the GPU decode is checked against) gives the same tokens as generate(inputs_embeds=, attention_mask=ones,
+    do_sample=False) on a tiny fp32 Gemma3ForCausalLM, including the finished-row padding and the stop step when an
+    EOS id is set."""
+    from oracle import stage1_ref as R
+    cfg, lp, llm = _hf()
+    g = torch.Generator().manual_seed(3)
+    x = torch.randn(3, 12, cfg.hidden_size, generator=g)
+    eos = None
+    if eos_rank is not None:
+        lg = torch.nn.functional.linear(R.gemma3_forward(lp, cfg, x, torch.ones(3, 12, dtype=torch.long))[:, -1],
+                                        lp["model.embed_tokens.weight"])
+        eos = int(lg[0].argmax())            # row 0 stops at once, the others run on
+    with torch.no_grad():
+        ref = llm.generate(inputs_embeds=x, attention_mask=torch.ones(3, 12, dtype=torch.long), max_new_tokens=6,
+                           do_sample=False, eos_token_id=eos, pad_token_id=0)
+    got, _ = R.greedy_generate(lp, cfg, x, 6, eos_token_id=eos, pad_token_id=0, embed_dtype=torch.float32)
+    assert torch.equal(got, ref), (got, ref)
