@@ -595,7 +595,10 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
   sq.next("gemma.lm_head_bwd");
   // tied lm_head weight grad: dE += dlogits^T . xf (the logits rows outside the loss rows have zero grad)
   if (train) CK(weight_grad(w.logits, V, ident, V, w.xf, H, ident, H, R, w.TL, w.TX, gr->embed, w.skpart, w.sk_floats, st));
-  if (R % 256 == 0 && V % (64 * LM_KSLICES) == 0) {
+  // (the K-sliced kernel addresses d(logits) with 32-bit buffer offsets: R x V bf16 must stay under 4 GiB -- at the
+  // reference's default caption length T = 512, bs 32 puts 8.6 GB there, which the split-K path below takes)
+  const bool ks_fits = (double)R * V * 2 + (double)LM_KSLICES * (V / LM_KSLICES) * 2 < 4293918720.0;
+  if (R % 256 == 0 && V % (64 * LM_KSLICES) == 0 && ks_fits) {
     // d(xf) = dlogits . E, K = vocab, as LM_KSLICES K slices of 256x256 tiles on the 8-wave kernel: 80 tiles x 16
     // slices = 5 lock-step rounds at cfg2 (the 128x128 8-slice split ran 2.8 ms); fp32 partials, ordered sum
     GemmArgs g = gemm(w.logits, V, wt->embed_t, V, w.dxf_part, H, R, H, V / LM_KSLICES);

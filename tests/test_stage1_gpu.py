@@ -341,3 +341,46 @@ def test_vision_prefetch_is_exact(gpu):
         runs.append((losses, eng.proj.flat.detach().clone(), eng.proj.flat_grad.detach().clone()))
     assert runs[0][0] == runs[1][0], (runs[0][0], runs[1][0])
     assert torch.equal(runs[0][1], runs[1][1]) and torch.equal(runs[0][2], runs[1][2])
+
+
+def test_long_captions_lm_head_past_4gib(gpu):
+    """The reference's default caption length (T = 512, train_projection_stage1.py:27) at bs 16: 8 192 loss rows, so
+    the bf16 d(logits) the lm_head backward reads is 4.29 GB -- past the 32-bit buffer offsets of the K-sliced
+    kernel, where the split-K path must take it (a round-6 regression: the K-sliced path raised instead).  Its batch
+    is 2 samples repeated 8 times, so loss and projector grads equal those of the 2-sample step (which runs the
+    K-sliced path): loss within 1e-4 relative, grads rel-L2 5e-3 (different reduction orders).  1 SigLIP + 2
+    Gemma3-1B layers (depth does not change the lm_head)."""
+    from projectiontrainer_amd import weights as W
+    from projectiontrainer_amd.config import PRESETS
+    from projectiontrainer_amd.gemma3 import Gemma3CausalLM
+    from projectiontrainer_amd.projectors import MLPProjector
+    from projectiontrainer_amd.siglip import SiglipVisionTower
+    from projectiontrainer_amd.stage1 import Stage1Engine
+    base = PRESETS["cfg2"]
+    cfg2 = base.replace(vision=base.vision.__class__(**{**base.vision.__dict__, "num_hidden_layers": 1}),
+                        text=base.text.__class__(**{**base.text.__dict__, "num_hidden_layers": 2}),
+                        batch_size=2, text_len=512)
+    vp = W.siglip_vision_params(cfg2.vision, seed=3)
+    lp = W.gemma3_params(cfg2.text, seed=4)
+    pp = W.projector_params(cfg2.vision.hidden_size, cfg2.text.hidden_size, seed=5)
+    px, ids, labels = W.synthetic_batch(cfg2, seed=7, max_pad=40)
+    vt = SiglipVisionTower(cfg2.vision, vp, gpu)
+    lm = Gemma3CausalLM(cfg2.text, lp, gpu, max_pos=Gemma3CausalLM.seq_pad(cfg2.seq_len))
+    out = {}
+    for bs in (2, 16):
+        proj = MLPProjector(cfg2.vision.hidden_size, cfg2.text.hidden_size)
+        proj.load_state_dict({k: torch.from_numpy(v) for k, v in pp.items()})
+        proj.to(gpu)
+        eng = Stage1Engine(vt, lm, proj, gradient_accumulation_steps=1)
+        rep = bs // 2
+        t = lambda a: torch.from_numpy(np.concatenate([a] * rep)).to(gpu)
+        eng.forward_backward(t(px), t(ids), t(labels))
+        torch.cuda.synchronize()
+        out[bs] = (float(eng.loss), [g.detach().float().cpu().clone() for g in eng.proj.grads()])
+        del eng
+        torch.cuda.empty_cache()
+    (l2, g2), (l16, g16) = out[2], out[16]
+    assert abs(l16 - l2) <= 1e-4 * abs(l2), (l16, l2)
+    for a, b in zip(g16, g2):
+        r = float((a - b).norm() / b.norm())
+        assert r <= 5e-3, r
