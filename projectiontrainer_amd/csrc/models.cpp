@@ -753,7 +753,8 @@ struct GenPass {            // per-pass activations (rows = B * S)
 };
 // the partial buffer the skinny GEMM needs for the decode projections and the lm_head at `rows` rows
 size_t gen_skinny_bytes(const ptk_gemma3_config* c, long rows) {
-  if (rows > 64) return 0;
+  if (rows > 256) return 0;   // (decode passes up to 256 rows run as 64-row chunks)
+  rows = std::min<long>(rows, 64);
   const int H = c->hidden, I = c->inter, D = c->head_dim, Dq = c->heads * D, Dqkv = (c->heads + 2 * c->kv_heads) * D;
   const int M = (int)rows;
   const int shapes[5][2] = {{Dqkv, H}, {H, Dq}, {2 * I, H}, {H, I}, {c->vocab, H}};   // (N, K)
@@ -764,8 +765,12 @@ size_t gen_skinny_bytes(const ptk_gemma3_config* c, long rows) {
 // a decode-pass GEMM (bf16 out): the skinny kernel where it applies, else the general dispatch
 int gen_gemm(const GenPass& g, const bf16_t* A, long lda, const void* B, long ldb, bf16_t* C, long ldc, int M, int N,
              int K, int act, hipStream_t st) {
-  if (g.skp_bytes > 0 && skinny_supported(M, N, K, lda, ldb, ldc, act))
-    return launch_gemm_skinny(A, lda, (const bf16_t*)B, ldb, C, ldc, M, N, K, act, g.skp, g.skp_bytes, st);
+  if (g.skp_bytes > 0 && skinny_supported(std::min(M, 64), N, K, lda, ldb, ldc, act)) {
+    for (int r0 = 0; r0 < M; r0 += 64)   // (each 64-row chunk streams the weights once more)
+      CK(launch_gemm_skinny(A + (long)r0 * lda, lda, (const bf16_t*)B, ldb, C + (long)r0 * ldc, ldc, std::min(64, M - r0),
+                            N, K, act, g.skp, g.skp_bytes, st));
+    return 0;
+  }
   return launch_gemm(gemm(A, lda, B, ldb, C, ldc, M, N, K), act, OUT_BF16, 1, st);
 }
 struct GenWs {

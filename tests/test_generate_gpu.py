@@ -45,7 +45,7 @@ def _teacher_forced(cfg, lpb, lm, gpu, B, P, steps, seed=0, scale=1.0):
     return tok_o, log_o, ids.cpu(), log_h.float().cpu()
 
 
-def _check(tok_o, log_o, ids, log_h, rel_bar=2e-2, test=""):
+def _check(tok_o, log_o, ids, log_h, rel_bar=2e-2, test="", margin=0.02):
     from tests.test_stage1_gpu import record
     steps = tok_o.shape[1]
     for t in range(steps):
@@ -57,7 +57,7 @@ def _check(tok_o, log_o, ids, log_h, rel_bar=2e-2, test=""):
     # greedy tokens: the argmax of the HIP logits of each (teacher-forced) step; equal to the oracle's wherever the
     # oracle's best two logits are more than 2 % of their spread apart
     top2 = log_o.topk(2, dim=-1).values                              # [steps, B, 2]
-    clear = (top2[..., 0] - top2[..., 1]) > 0.02 * log_o.std(-1)
+    clear = (top2[..., 0] - top2[..., 1]) > margin * log_o.std(-1)
     agree = ids.t() == tok_o.t()
     record(test, "greedy_agreement", frac=float(agree.float().mean()), clear_frac=float(clear.float().mean()))
     assert bool(agree[clear].all()), (agree, clear)
@@ -71,6 +71,16 @@ def test_generate_teacher_forced_vs_oracle(gpu, name):
     cfg, lpb, lm = _model(name, gpu)
     tok_o, log_o, ids, log_h = _teacher_forced(cfg, lpb, lm, gpu, B=3, P=20, steps=10)
     _check(tok_o, log_o, ids, log_h, test=f"generate[{name}]")
+
+
+def test_generate_teacher_forced_many_rows(gpu):
+    """80 decode rows: past the skinny decode GEMM's 64, so every decode projection and the lm_head run as a 64-row
+    and a 16-row chunk; teacher-forced logits against the oracle as above.  With 320 greedy picks a top-two gap of
+    2 % of the logit spread still admitted a bf16 flip, so the argmax check uses 5 % here (measured: 98.75 % of
+    all picks equal, every pick with a gap above 5 % equal; 90 % of the picks have one)."""
+    cfg, lpb, lm = _model("tiny", gpu)
+    tok_o, log_o, ids, log_h = _teacher_forced(cfg, lpb, lm, gpu, B=80, P=20, steps=4, seed=2)
+    _check(tok_o, log_o, ids, log_h, test="generate[tiny-80rows]", margin=0.05)
 
 
 @pytest.mark.slow
