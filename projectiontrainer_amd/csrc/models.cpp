@@ -66,6 +66,28 @@ static bool geglu_split() {
   const int v = PTK_AB("PTK_GEGLU_SPLIT", 0) == 1;   // A/B builds only
   return v != 0;
 }
+// Stage 2: the residual norm backward writes both norms' weight-grad partials itself (PTK_NORM_WG=0: the two
+// separate rms_wgrad passes, A/B builds)
+static bool norm_wg_fused() { return PTK_AB("PTK_NORM_WG", 1) != 0; }
+
+// dR += rms_bwd(x2, w_pre, rstd_pre, dn); dt = bf16(rms_bwd(t, w_post, rstd_t, bf16(dR))); with g_pre / g_post
+// (Stage 2) also accumulates both norms' weight grads.  wpart: the fused kernel's two partial sets back to back
+static int residual_norm_bwd_grads(const float* x2, const float* w_pre, const float* rstd_pre, const bf16_t* dn,
+                                   float* dR, const bf16_t* t, const float* w_post, const float* rstd_t, bf16_t* dt,
+                                   int M, int H, bf16_t* g_pre, bf16_t* g_post, float* wpart, hipStream_t st) {
+  const RowMap ident{0, 0, 0, 0};
+  if (g_pre && norm_wg_fused()) {
+    const int nb = residual_norm_bwd_wg_blocks(M);
+    float* pq = wpart + rms_wgrad_finish_floats(nb, H);
+    CK(launch_residual_norm_bwd_wg(x2, w_pre, rstd_pre, dn, dR, t, w_post, rstd_t, dt, M, H, wpart, pq, st));
+    CK(launch_rms_wgrad_finish(wpart, nb, H, g_pre, st));
+    return launch_rms_wgrad_finish(pq, nb, H, g_post, st);
+  }
+  if (g_pre) CK(launch_rms_wgrad_bdy(x2, H, ident, rstd_pre, dn, H, M, H, g_pre, wpart, st));
+  CK(launch_residual_norm_bwd_bdn(x2, w_pre, rstd_pre, dn, dR, t, w_post, rstd_t, dt, M, H, st));
+  if (g_pre) CK(launch_rms_wgrad_bx(t, H, ident, rstd_t, dR, H, 1, M, H, g_post, wpart, st));
+  return 0;
+}
 // PTK_DKV_REDUCE_SPLIT=1: separate attn_dkv_reduce_kernel pass (A/B) instead of summing the split-slab
 // dK/dV partials inside qknorm_rope_bwd
 static bool dkv_reduce_split() {
@@ -231,7 +253,9 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
     w.TB = bp.take<bf16_t>(std::max(std::max(H, Dq), I) * M);
     w.TL = bp.take<bf16_t>(V * Rp);
     w.TX = bp.take<bf16_t>(H * Rp);
-    w.wpart = bp.take<float>(std::max((long)rms_wgrad_partial_floats((int)M, (int)H),
+    // two norms' partials (the fused residual norm backward), or one norm's / the q,k norms'
+    w.wpart = bp.take<float>(std::max(std::max((long)rms_wgrad_partial_floats((int)M, (int)H),
+                                               2L * rms_wgrad_finish_floats(residual_norm_bwd_wg_blocks((int)M), (int)H)),
                                       (long)qknorm_wgrad_partial_floats(M, (int)D)));
   }
   // split-K partials (gemm_split): 2 slices of the largest [M, H] / [2I, H] output, 4 of the small dW ones
@@ -673,14 +697,12 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
       g2.cmap = lossmap;
       CK(launch_gemm(g2, ACT_NONE, OUT_BF16, 1, st));
     }
-    if (train) CK(launch_rms_wgrad_bdy(sv.x2, H, ident, sv.rstd_pre, w.dtmp, H, M, H, (bf16_t*)GL->ln_pre_ff, w.wpart, st));
     sq.next("gemma.bwd.attn");
-    CK(launch_residual_norm_bwd_bdn(sv.x2, L.ln_pre_ff, sv.rstd_pre, w.dtmp, dR, sv.ao, L.ln_post_attn, sv.rstd_ao, w.dao,
-                                M, H, st));
-    if (train) {
-      CK(launch_rms_wgrad_bx(sv.ao, H, ident, sv.rstd_ao, dR, H, 1, M, H, (bf16_t*)GL->ln_post_attn, w.wpart, st));
+    CK(residual_norm_bwd_grads(sv.x2, L.ln_pre_ff, sv.rstd_pre, w.dtmp, dR, sv.ao, L.ln_post_attn, sv.rstd_ao, w.dao,
+                               M, H, train ? (bf16_t*)GL->ln_pre_ff : nullptr,
+                               train ? (bf16_t*)GL->ln_post_attn : nullptr, w.wpart, st));
+    if (train)
       CK(weight_grad(w.dao, H, ident, H, sv.O, Dq, ident, Dq, M, w.TA, w.TB, GL->wo, w.skpart, w.sk_floats, st));
-    }
     {  // dO (Q layout) = dao . Wo, one GEMM per kv head group of output columns
       GemmArgs g = gemm(w.dao, H, L.wo_t, H, w.dO, (long)G * D, M, G * D, H);
       g.sB0 = (long)G * D * H; g.sC0 = (long)Sp * G * D;
@@ -713,17 +735,16 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
       CK(weight_grad(w.dqkv, Dqkv, ident, Dqkv, sv.xn_in, H, ident, H, M, w.TA, w.TB, GL->wqkv, w.skpart, w.sk_floats, st));
     }
     CK(gemm_split(gemm(w.dqkv, Dqkv, L.wqkv_t, Dqkv, w.dtmp, H, M, H, Dqkv), OUT_BF16, w.skpart, w.sk_floats, st));
-    if (train) CK(launch_rms_wgrad_bdy(w.x[l], H, ident, sv.rstd_in, w.dtmp, H, M, H, (bf16_t*)GL->ln_in, w.wpart, st));
     if (l > 0) {
       // dR += rms_bwd(x_l, ln_in, dtmp), then layer l-1's post-ff norm backward on the new dR -> dao
       const ptk_gemma3_layer& Lp = wt->layers[l - 1];
       const GemmaLayerSave& sp = w.L[l - 1];
-      CK(launch_residual_norm_bwd_bdn(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, sp.dn, Lp.ln_post_ff, sp.rstd_dn, w.dao,
-                                  M, H, st));
-      if (train)
-        CK(launch_rms_wgrad_bx(sp.dn, H, ident, sp.rstd_dn, dR, H, 1, M, H, (bf16_t*)gr->layers[l - 1].ln_post_ff,
-                               w.wpart, st));
+      CK(residual_norm_bwd_grads(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, sp.dn, Lp.ln_post_ff, sp.rstd_dn, w.dao,
+                                 M, H, train ? (bf16_t*)GL->ln_in : nullptr,
+                                 train ? (bf16_t*)gr->layers[l - 1].ln_post_ff : nullptr, w.wpart, st));
     } else {
+      if (train)
+        CK(launch_rms_wgrad_bdy(w.x[l], H, ident, sv.rstd_in, w.dtmp, H, M, H, (bf16_t*)GL->ln_in, w.wpart, st));
       CK(launch_rmsnorm_bwd_bdn(w.x[l], L.ln_in, sv.rstd_in, w.dtmp, dR, dR, M, H, st));
     }
   }

@@ -231,6 +231,75 @@ __global__ void __launch_bounds__(256) residual_norm_bwd_bdn_kernel(
   residual_norm_bwd_body<bf16_t, NV>(x2, w_pre, rstd_pre, dn, dR, t, w_post, rstd_t, dt, rows, cols);
 }
 
+// residual_norm_bwd_bdn with both norms' weight-grad partials folded in (Stage 2, unfrozen LM): the rows of
+// x2 / dn / t and the updated dR are already in registers, so the two separate rms_wgrad passes that re-read
+// them from HBM (2 x 6.9 KB per token at H = 1152) go away.  partial[blk][c] = sum over the block's 4 rows of
+// dy[r, c] * x[r, c] * rstd[r] -- pre norm: dy = dn, x = x2; post norm: dy = bf16(dR_new), x = t.
+// Same grid as residual_norm_bwd_bdn (one wave per row, 4 rows per block: the occupancy this HBM-bound pass
+// needs: a 32-row block looping 8 rows per wave, 1.75 waves per SIMD, left the cfg4 step slower than the two
+// separate passes did).  Each wave parks its product row in LDS, one norm at a time; wave 0 sums the 4 rows in
+// row order and writes the block's partial row (1.15 KB per token per norm, folded by rms_wgrad_finish).
+#ifndef PTK_NWG_WAVES
+#define PTK_NWG_WAVES 4
+#endif
+constexpr int NWG = PTK_NWG_WAVES;   // rows (waves) per block
+template <int NV>
+__global__ void __launch_bounds__(64 * NWG) residual_norm_bwd_wg_kernel(
+    const float* __restrict__ x2, const float* __restrict__ w_pre, const float* __restrict__ rstd_pre,
+    const bf16_t* __restrict__ dn, float* __restrict__ dR, const bf16_t* __restrict__ t,
+    const float* __restrict__ w_post, const float* __restrict__ rstd_t, bf16_t* __restrict__ dt, long rows,
+    int cols, float* __restrict__ part_pre, float* __restrict__ part_post) {
+  __shared__ float4 red[NWG][NV][64];   // one norm at a time: 20 KB at H = 1152 keeps 7 waves per SIMD
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long row = (long)blockIdx.x * NWG + wv;
+  const bool ok = row < rows;
+  // the block's 4 product rows -> one partial row, summed in row order by wave 0
+#define NWG_SUM(PART)                                                                    \
+  __syncthreads();                                                                       \
+  if (wv == 0) {                                                                         \
+    float* part = PART + (long)blockIdx.x * cols;                                        \
+    _Pragma("unroll") FOR_V {                                                            \
+      float4 a = red[0][v][lane];                                                        \
+      _Pragma("unroll") for (int g = 1; g < NWG; ++g) a = add4(a, red[g][v][lane]);      \
+      st4(part + COL, a);                                                                \
+    }                                                                                    \
+  }                                                                                      \
+  __syncthreads();
+  float4 nd[NV];
+  if (ok) {
+    const float* w = w_pre;
+    float4 xv[NV], dv[NV];
+#pragma unroll
+    FOR_V { xv[v] = ld4(x2 + row * cols + COL); dv[v] = ld4bf(dn + row * cols + COL); }
+    const float rs = rstd_pre[row];
+#pragma unroll
+    FOR_V { red[wv][v][lane] = scl4(mul4(dv[v], xv[v]), rs); }
+    RMS_BWD_BODY(xv, dv, rs, {
+      nd[v] = add4(ld4(dR + row * cols + COL), dxv);
+      st4(dR + row * cols + COL, nd[v]);
+    })
+  } else {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) red[wv][v][lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  NWG_SUM(part_pre)
+  if (ok) {
+    const float* w = w_post;
+    const float rs = rstd_t[row];
+    float4 xv[NV], dv[NV];
+#pragma unroll
+    FOR_V { xv[v] = ld4bf(t + row * cols + COL); dv[v] = bfr4(nd[v]); }
+#pragma unroll
+    FOR_V { red[wv][v][lane] = scl4(mul4(dv[v], xv[v]), rs); }
+    RMS_BWD_BODY(xv, dv, rs, { st4bf(dt + row * cols + COL, dxv); })
+  } else {
+#pragma unroll
+    for (int v = 0; v < NV; ++v) red[wv][v][lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+  }
+  NWG_SUM(part_post)
+#undef NWG_SUM
+}
+
 template <int NV>
 __global__ void __launch_bounds__(256) post_norm_bwd_kernel(const float* __restrict__ dR, const bf16_t* __restrict__ t,
                                                             const float* __restrict__ w, const float* __restrict__ rstd_t,
@@ -310,6 +379,20 @@ int launch_residual_norm_bwd_bdn(const float* x2, const float* w_pre, const floa
   if (rows <= 0) return 0;
   NORM_DISPATCH(residual_norm_bwd_bdn_kernel, x2, w_pre, rstd_pre, dn, dR, t, w_post, rstd_t, dt, (long)rows, cols);
   RET_LAUNCH("residual_norm_bwd_bdn");
+}
+int residual_norm_bwd_wg_blocks(int rows) { return (rows + NWG - 1) / NWG; }
+int launch_residual_norm_bwd_wg(const float* x2, const float* w_pre, const float* rstd_pre, const bf16_t* dn,
+                                float* dR, const bf16_t* t, const float* w_post, const float* rstd_t, bf16_t* dt,
+                                int rows, int cols, float* part_pre, float* part_post, hipStream_t st) {
+  if (check_cols(cols)) return -1;
+  if (rows <= 0) return 0;
+#undef NORM_GRID
+#define NORM_GRID dim3((unsigned)residual_norm_bwd_wg_blocks(rows)), dim3(64 * NWG), 0, st
+  NORM_DISPATCH(residual_norm_bwd_wg_kernel, x2, w_pre, rstd_pre, dn, dR, t, w_post, rstd_t, dt, (long)rows, cols,
+                part_pre, part_post);
+#undef NORM_GRID
+#define NORM_GRID dim3((unsigned)((rows + 3) / 4)), dim3(256), 0, st
+  RET_LAUNCH("residual_norm_bwd_wg");
 }
 int launch_rmsnorm_bwd_scatter(const float* x, RowMap xmap, const float* w, const float* rstd, const float* dn,
                                float* dR, int rows, int cols, hipStream_t st) {

@@ -174,6 +174,13 @@ int launch_rmsnorm_bwd_bdn(const float* x, const float* w, const float* rstd, co
 int launch_residual_norm_bwd_bdn(const float* x2, const float* w_pre, const float* rstd_pre, const bf16_t* dn,
                                  float* dR, const bf16_t* t, const float* w_post, const float* rstd_t, bf16_t* dt,
                                  int rows, int cols, hipStream_t st);
+// residual_norm_bwd_bdn that also writes both norms' weight-grad partials ([blocks][cols] each, blocks =
+// residual_norm_bwd_wg_blocks(rows)) for launch_rms_wgrad_finish: pre = dn * x2 * rstd_pre, post = bf16(dR) * t
+// * rstd_t summed over each block's rows
+int residual_norm_bwd_wg_blocks(int rows);
+int launch_residual_norm_bwd_wg(const float* x2, const float* w_pre, const float* rstd_pre, const bf16_t* dn,
+                                float* dR, const bf16_t* t, const float* w_post, const float* rstd_t, bf16_t* dt,
+                                int rows, int cols, float* part_pre, float* part_post, hipStream_t st);
 int launch_rmsnorm_bwd_scatter(const float* x, RowMap xmap, const float* w, const float* rstd,
                                const float* dn, float* dR, int rows, int cols, hipStream_t st);
 
@@ -362,6 +369,10 @@ int launch_rms_wgrad_bx(const bf16_t* x, long ldx, RowMap xmap, const float* rst
                         int dy_round, int rows, int cols, bf16_t* grad, float* partial, hipStream_t st);
 int launch_rms_wgrad_bdy(const float* x, long ldx, RowMap xmap, const float* rstd, const bf16_t* dy, long lddy,
                          int rows, int cols, bf16_t* grad, float* partial, hipStream_t st);
+// the fixed-order finish alone: partial [nblk][cols] (followed by ceil(nblk/16) * cols floats of scratch)
+// -> grad = bf16(grad + bf16(sum)); partial + scratch = rms_wgrad_finish_floats(nblk, cols)
+int rms_wgrad_finish_floats(int nblk, int cols);
+int launch_rms_wgrad_finish(float* partial, int nblk, int cols, bf16_t* grad, hipStream_t st);
 // q_norm / k_norm weight grads from the attention-layout dQ / dK (partial >= 2 * ceil(B*S/64) * D floats)
 int launch_qknorm_wgrad(const bf16_t* qkv, const float* cos_t, const float* sin_t, AttnShape s, const float* rstd_q,
                         const float* rstd_k, const bf16_t* dQ, const bf16_t* dK, bf16_t* gq, bf16_t* gk,

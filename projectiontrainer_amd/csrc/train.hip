@@ -209,6 +209,13 @@ static int rms_wgrad_t(const TX* x, long ldx, RowMap xmap, const float* rstd, co
   RET_OK("rms_wgrad");
 }
 
+int rms_wgrad_finish_floats(int nblk, int cols) { return (nblk + (nblk + 15) / 16) * cols; }
+int launch_rms_wgrad_finish(float* partial, int nblk, int cols, bf16_t* grad, hipStream_t st) {
+  if (nblk <= 0) return 0;
+  wgrad_finish(partial, nblk, cols, grad, partial + (long)nblk * cols, st);
+  RET_OK("rms_wgrad_finish");
+}
+
 int rms_wgrad_partial_floats(int rows, int cols) {
   const int nblk = (rows + WG_ROWS - 1) / WG_ROWS;
   return (nblk + (nblk + 15) / 16) * cols;   // partials + the first fold
