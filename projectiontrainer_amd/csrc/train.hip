@@ -175,11 +175,53 @@ __global__ void __launch_bounds__(256) wgrad_finish_kernel(const float* __restri
   grad[c] = f2bf(bf2f(grad[c]) + bfround(s));
 }
 
+// nblk <= 256 in one launch: 16 row groups x 64 columns per 1024-thread block, group g sums rows g, g + 16, ...
+// (all its loads in flight at once), the groups added in order through LDS, then the bf16 accumulate.  Replaces
+// the last colsum16 fold + wgrad_finish (two latency-bound launches of ~5 us each on cfg4's 4-row norm partials)
+__global__ void __launch_bounds__(1024) wgrad_finish16_kernel(const float* __restrict__ partial, int nblk, int cols,
+                                                              bf16_t* __restrict__ grad) {
+  __shared__ float red[16][64];
+  const int cl = threadIdx.x & 63, grp = threadIdx.x >> 6;
+  const int c = blockIdx.x * 64 + cl;
+  float v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) {
+    const int r = grp + 16 * i;
+    v[i] = (c < cols && r < nblk) ? partial[(long)r * cols + c] : 0.f;
+  }
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < 16; ++i) s += v[i];
+  red[grp][cl] = s;
+  __syncthreads();
+  if (grp == 0 && c < cols) {
+    float t = red[0][cl];
+#pragma unroll
+    for (int g = 1; g < 16; ++g) t += red[g][cl];
+    grad[c] = f2bf(bf2f(grad[c]) + bfround(t));
+  }
+}
+
+#ifndef PTK_FINISH16
+#define PTK_FINISH16 1
+#endif
 // partial [nblk][cols] -> grad; `scratch` holds ceil(nblk/16) * cols floats (the folded rows ping-pong in
 // partial's own head and scratch)
 static void wgrad_finish(float* partial, int nblk, int cols, bf16_t* grad, float* scratch, hipStream_t st) {
   float* src = partial;
   float* dst = scratch;
+  if (PTK_FINISH16) {
+    while (nblk > 256) {
+      const int n2 = (nblk + 15) / 16;
+      hipLaunchKernelGGL(colsum16_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)n2), dim3(256), 0, st, src,
+                         nblk, cols, dst);
+      std::swap(src, dst);
+      nblk = n2;
+    }
+    hipLaunchKernelGGL(wgrad_finish16_kernel, dim3((unsigned)((cols + 63) / 64)), dim3(1024), 0, st, src, nblk, cols,
+                       grad);
+    return;
+  }
   while (nblk > 16) {
     const int n2 = (nblk + 15) / 16;
     hipLaunchKernelGGL(colsum16_kernel, dim3((unsigned)((cols + 63) / 64), (unsigned)n2), dim3(256), 0, st, src, nblk,
