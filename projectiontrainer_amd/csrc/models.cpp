@@ -166,6 +166,7 @@ struct GemmaWs {
   // unfrozen LLM only: feature-major GEMM operands of dW = dY^T X (K = tokens) and norm-grad partials
   bf16_t *TA = nullptr, *TB = nullptr, *TL = nullptr, *TX = nullptr;
   float* wpart = nullptr;
+  void* eg_keys = nullptr;   // the embedding grad's sorted (id, position) keys
   float* skpart = nullptr;     // split-K partials (gemm_split)
   long sk_floats = 0;
   void* tail = nullptr;        // stream-K tail scratch of the model's GEMMs
@@ -254,6 +255,7 @@ GemmaWs gemma_layout(Bump& bp, const ptk_gemma3_config* c, int B, int T, int Sp,
     w.TL = bp.take<bf16_t>(V * Rp);
     w.TX = bp.take<bf16_t>(H * Rp);
     // two norms' partials (the fused residual norm backward), or one norm's / the q,k norms'
+    w.eg_keys = bp.take<char>((long)embed_grad_ws_bytes(B, T));
     w.wpart = bp.take<float>(std::max(std::max((long)rms_wgrad_partial_floats((int)M, (int)H),
                                                2L * rms_wgrad_finish_floats(residual_norm_bwd_wg_blocks((int)M), (int)H)),
                                       (long)qknorm_wgrad_partial_floats(M, (int)D)));
@@ -750,7 +752,7 @@ int gemma_run(const ptk_gemma3_config* c, const ptk_gemma3_weights* wt, const pt
   }
   // input-embedding grads of every text token (tied with the lm_head grad above)
   if (train) sq.next("gemma.embed_grad");
-  if (train) CK(launch_embed_grad(bt->token_ids, B, T, Nv, Sp, H, escale, dR, (bf16_t*)gr->embed, st));
+  if (train) CK(launch_embed_grad(bt->token_ids, B, T, Nv, Sp, H, escale, dR, (bf16_t*)gr->embed, w.eg_keys, st));
   return 0;
 }
 

@@ -381,8 +381,10 @@ int qknorm_wgrad_partial_floats(long M, int D);
 // split-K partial reduce: C = sum_s part[s] (fp32) or bf16(resid + bf16(sum)) (bf16; resid may be null / alias C)
 int launch_splitk_reduce(const float* part, int S, int M, int N, void* C, long ldc, int out_bf16, const bf16_t* resid,
                          long ldr, hipStream_t st);
+// ws: embed_grad_ws_bytes(B, T) bytes (the sorted (id, position) keys)
+size_t embed_grad_ws_bytes(int B, int T);
 int launch_embed_grad(const int64_t* ids, int B, int T, int Nv, int Spad, int H, float escale, const float* dx,
-                      bf16_t* dE, hipStream_t st);
+                      bf16_t* dE, void* ws, hipStream_t st);
 int scale_sumsq_partial_floats();
 int launch_scale_sumsq_bf16(bf16_t* g, long n, float scale, float* partial, float* out, hipStream_t st);
 int launch_adamw_bf16(bf16_t* p, bf16_t* g, bf16_t* m, bf16_t* v, long n, const float* sumsq, float max_norm,

@@ -450,52 +450,115 @@ int launch_splitk_reduce(const float* part, int S, int M, int N, void* C, long l
 // ---------------------------------------------------------------- input-embedding grads
 // Text position t of sample b sits at LLM row b*Spad + Nv + t and embeds token ids[b*T + t] as
 // bf16(E[id] * escale).  Its grad into E[id] is bf16(bf16(dx_row) * escale) (the bf16 mul's backward on the
-// fp32 grad cast to bf16); rows sharing an id are summed in position order by the block of the FIRST
-// occurrence (deterministic, no atomics), then added to the tied weight's bf16 grad.
-constexpr int EG_MAX = 16384;   // text tokens per batch (the LDS match list)
-__global__ void __launch_bounds__(256) embed_grad_kernel(const int64_t* __restrict__ ids, int B, int T, int Nv,
+// fp32 grad cast to bf16); rows sharing an id are summed in position order (deterministic, no atomics), then
+// added to the tied weight's bf16 grad.  Two launches: the (id, position) keys sorted by rank (positions
+// ascending within an id), then one workgroup per sorted key whose id starts a run sums that run.  The round-5
+// form (every workgroup compacting its id's positions out of all B*T ids, and the pad id's run summed with one
+// guarded load -- one memory round trip -- per row and column) took 828 us per cfg4 micro-batch.
+constexpr int EG_MAX = 16384;   // text tokens per batch (EG_POS_BITS of position in a key)
+constexpr int EG_POS_BITS = 14;
+// key = id << 14 | position (all distinct): each key's rank among all keys is its place in the sorted order.
+// 64 keys per workgroup, each wave counting one quarter of every LDS tile of the keys (a one-workgroup bitonic
+// sort in LDS took 117 us at cfg4's 5 120 keys, one key per thread over all of them 80 us)
+__global__ void __launch_bounds__(256) embed_rank_kernel(const int64_t* __restrict__ ids, int n,
+                                                         uint64_t* __restrict__ sorted) {
+  __shared__ uint64_t tile[1024];
+  __shared__ int part[4][64];
+  const int kl = threadIdx.x & 63, qtr = threadIdx.x >> 6;
+  const int i = blockIdx.x * 64 + kl;
+  const uint64_t key = i < n ? ((uint64_t)ids[i] << EG_POS_BITS) | (uint64_t)i : ~0ull;
+  int rank = 0;
+  for (int t0 = 0; t0 < n; t0 += 1024) {
+    __syncthreads();
+    for (int u = threadIdx.x; u < 1024; u += 256) {
+      const int j = t0 + u;
+      tile[u] = j < n ? ((uint64_t)ids[j] << EG_POS_BITS) | (uint64_t)j : ~0ull;
+    }
+    __syncthreads();
+    // the whole quarter, LDS reads unrolled (past n the tile holds ~0, never below a key)
+    const uint64_t* tq = tile + qtr * 256;
+#pragma unroll 32
+    for (int u = 0; u < 256; ++u) rank += tq[u] < key ? 1 : 0;
+  }
+  part[qtr][kl] = rank;
+  __syncthreads();
+  if (qtr == 0 && i < n) sorted[part[0][kl] + part[1][kl] + part[2][kl] + part[3][kl]] = key;
+}
+
+__global__ void __launch_bounds__(256) embed_grad_kernel(const uint64_t* __restrict__ sorted, int n, int T, int Nv,
                                                          int Spad, int H, float escale, const float* __restrict__ dx,
                                                          bf16_t* __restrict__ dE) {
-  __shared__ int list[EG_MAX];
-  __shared__ int wcount[4];
-  __shared__ int total_s;
-  const int n = B * T, i = blockIdx.x;
-  const int64_t id = ids[i];
-  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  if (threadIdx.x == 0) total_s = 0;
-  __syncthreads();
-  // stream compaction of the positions holding this id, in position order (ballot + prefix counts)
-  for (int j0 = 0; j0 < n; j0 += 256) {
-    const int j = j0 + threadIdx.x;
-    const bool m = j < n && ids[j] == id;
-    const unsigned long long mask = __ballot(m);
-    if (lane == 0) wcount[wv] = __popcll(mask);
-    __syncthreads();
-    int base = total_s;
-    for (int k = 0; k < wv; ++k) base += wcount[k];
-    if (m) list[base + __popcll(mask & ((1ull << lane) - 1ull))] = j;
-    __syncthreads();
-    if (threadIdx.x == 0) total_s += wcount[0] + wcount[1] + wcount[2] + wcount[3];
-    __syncthreads();
+  const int k = blockIdx.x;
+  const uint64_t id = sorted[k] >> EG_POS_BITS;
+  if (k > 0 && (sorted[k - 1] >> EG_POS_BITS) == id) return;   // not the first position of its id
+  int cnt = 0;   // the run's length (contiguous in the sorted keys)
+  for (int base = k; base < n; base += 256) {
+    const int idx = base + threadIdx.x;
+    const int c = __syncthreads_count(idx < n && (sorted[idx] >> EG_POS_BITS) == id);
+    cnt += c;
+    if (c < 256) break;
   }
-  const int cnt = total_s;
-  if (list[0] != i) return;   // the block of the first occurrence owns this id
-  for (int c = threadIdx.x; c < H; c += 256) {
-    float acc = 0.f;
-    for (int k = 0; k < cnt; ++k) {
-      const int j = list[k], b = j / T, t = j - b * T;
-      acc += bfround(bfround(dx[((long)b * Spad + Nv + t) * H + c]) * escale);
+  // the run's rows staged in LDS, EG_COLS column sets of 256 per pass and EG_UNROLL rows' loads in flight
+  // before their adds: the sum per column stays in position order, but the pad id's run (hundreds of rows at
+  // cfg4) no longer waits one memory round trip per row and column set
+  constexpr int EG_COLS = 5, EG_UNROLL = 8, EG_CHUNK = 2048;
+  __shared__ int rows_s[EG_CHUNK];
+  const uint64_t pmask = (1ull << EG_POS_BITS) - 1;
+  for (int c0 = 0; c0 < H; c0 += 256 * EG_COLS) {
+    float acc[EG_COLS];
+#pragma unroll
+    for (int q = 0; q < EG_COLS; ++q) acc[q] = 0.f;
+    for (int u0 = 0; u0 < cnt; u0 += EG_CHUNK) {
+      const int m = min(EG_CHUNK, cnt - u0);
+      __syncthreads();
+      for (int u = threadIdx.x; u < m; u += 256) {
+        const int j = (int)(sorted[k + u0 + u] & pmask), b = j / T, t = j - b * T;
+        rows_s[u] = b * Spad + Nv + t;
+      }
+      __syncthreads();
+      int u = 0;
+      for (; u + EG_UNROLL <= m; u += EG_UNROLL) {
+        float v[EG_UNROLL][EG_COLS];
+#pragma unroll
+        for (int uu = 0; uu < EG_UNROLL; ++uu) {
+          const float* row = dx + (long)rows_s[u + uu] * H;
+#pragma unroll   // unguarded loads (clamped column; the value is dropped below): a guarded load is a branch
+          for (int q = 0; q < EG_COLS; ++q) v[uu][q] = row[min(c0 + q * 256 + (int)threadIdx.x, H - 1)];
+        }
+#pragma unroll
+        for (int uu = 0; uu < EG_UNROLL; ++uu)
+#pragma unroll
+          for (int q = 0; q < EG_COLS; ++q) acc[q] += bfround(bfround(v[uu][q]) * escale);
+      }
+      for (; u < m; ++u) {
+        const float* row = dx + (long)rows_s[u] * H;
+#pragma unroll
+        for (int q = 0; q < EG_COLS; ++q) {
+          const int c = c0 + q * 256 + threadIdx.x;
+          if (c < H) acc[q] += bfround(bfround(row[c]) * escale);
+        }
+      }
     }
-    bf16_t* g = dE + id * (long)H + c;
-    *g = f2bf(bf2f(*g) + bfround(acc));
+#pragma unroll
+    for (int q = 0; q < EG_COLS; ++q) {
+      const int c = c0 + q * 256 + threadIdx.x;
+      if (c < H) {
+        bf16_t* g = dE + (long)id * H + c;
+        *g = f2bf(bf2f(*g) + bfround(acc[q]));
+      }
+    }
   }
 }
 
+size_t embed_grad_ws_bytes(int B, int T) { return (size_t)(B * T > 0 ? B * T : 1) * sizeof(uint64_t); }
 int launch_embed_grad(const int64_t* ids, int B, int T, int Nv, int Spad, int H, float escale, const float* dx,
-                      bf16_t* dE, hipStream_t st) {
-  if (B * T <= 0) return 0;
-  if (B * T > EG_MAX) return set_error("embed_grad: %d text tokens per batch (max %d)", B * T, EG_MAX);
-  hipLaunchKernelGGL(embed_grad_kernel, dim3((unsigned)(B * T)), dim3(256), 0, st, ids, B, T, Nv, Spad, H, escale, dx,
+                      bf16_t* dE, void* ws, hipStream_t st) {
+  const int n = B * T;
+  if (n <= 0) return 0;
+  if (n > EG_MAX) return set_error("embed_grad: %d text tokens per batch (max %d)", n, EG_MAX);
+  uint64_t* sorted = static_cast<uint64_t*>(ws);
+  hipLaunchKernelGGL(embed_rank_kernel, dim3((unsigned)((n + 63) / 64)), dim3(256), 0, st, ids, n, sorted);
+  hipLaunchKernelGGL(embed_grad_kernel, dim3((unsigned)n), dim3(256), 0, st, sorted, n, T, Nv, Spad, H, escale, dx,
                      dE);
   RET_OK("embed_grad");
 }
