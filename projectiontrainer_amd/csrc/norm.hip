@@ -35,7 +35,9 @@ PTK_DEV float4 scl4(float4 a, float s) { return make_float4(a.x * s, a.y * s, a.
   const long row = (long)blockIdx.x * 4 + (threadIdx.x >> 6); \
   if (row >= rows) return;
 
-#define FOR_V for (int v = 0; v < NV; ++v) if (lane * 4 + v * 256 < cols)
+// NV = ceil(cols / 256) exactly (NORM_DISPATCH), so only the last float4 column group can run past cols: the
+// others go unguarded -- a guarded load is a branch whose wait serialises the row's loads
+#define FOR_V for (int v = 0; v < NV; ++v) if (v < NV - 1 || lane * 4 + v * 256 < cols)
 #define COL (lane * 4 + v * 256)
 
 PTK_DEV float4 ldx4(const float* p) { return ld4(p); }
@@ -308,17 +310,24 @@ __global__ void __launch_bounds__(256) post_norm_bwd_kernel(const float* __restr
   post_norm_bwd_row<NV>(dR + row * cols, t + row * cols, w, rstd_t[row], dt + row * cols, lane, cols);
 }
 
-// float4 registers per lane for a row of `cols` (one wave per row): kernels are instantiated per count
-// so the row arrays take only the registers they need (occupancy of these HBM-bound kernels)
+// float4 registers per lane for a row of `cols` (one wave per row): kernels are instantiated per exact count
+// (FOR_V relies on it) so the row arrays take only the registers they need (occupancy of these HBM-bound kernels)
 #define NORM_DISPATCH(KERNEL, ...)                                                                  \
   do {                                                                                              \
-    const int nv_ = (cols + 255) / 256;                                                             \
-    if (nv_ <= 1) hipLaunchKernelGGL(KERNEL<1>, NORM_GRID, __VA_ARGS__);                            \
-    else if (nv_ <= 2) hipLaunchKernelGGL(KERNEL<2>, NORM_GRID, __VA_ARGS__);                       \
-    else if (nv_ <= 4) hipLaunchKernelGGL(KERNEL<4>, NORM_GRID, __VA_ARGS__);                       \
-    else if (nv_ <= 5) hipLaunchKernelGGL(KERNEL<5>, NORM_GRID, __VA_ARGS__);                       \
-    else if (nv_ <= 8) hipLaunchKernelGGL(KERNEL<8>, NORM_GRID, __VA_ARGS__);                       \
-    else hipLaunchKernelGGL(KERNEL<MAXV>, NORM_GRID, __VA_ARGS__);                                  \
+    switch ((cols + 255) / 256) {                                                                   \
+      case 1: hipLaunchKernelGGL(KERNEL<1>, NORM_GRID, __VA_ARGS__); break;                         \
+      case 2: hipLaunchKernelGGL(KERNEL<2>, NORM_GRID, __VA_ARGS__); break;                         \
+      case 3: hipLaunchKernelGGL(KERNEL<3>, NORM_GRID, __VA_ARGS__); break;                         \
+      case 4: hipLaunchKernelGGL(KERNEL<4>, NORM_GRID, __VA_ARGS__); break;                         \
+      case 5: hipLaunchKernelGGL(KERNEL<5>, NORM_GRID, __VA_ARGS__); break;                         \
+      case 6: hipLaunchKernelGGL(KERNEL<6>, NORM_GRID, __VA_ARGS__); break;                         \
+      case 7: hipLaunchKernelGGL(KERNEL<7>, NORM_GRID, __VA_ARGS__); break;                         \
+      case 8: hipLaunchKernelGGL(KERNEL<8>, NORM_GRID, __VA_ARGS__); break;                         \
+      case 9: hipLaunchKernelGGL(KERNEL<9>, NORM_GRID, __VA_ARGS__); break;                         \
+      case 10: hipLaunchKernelGGL(KERNEL<10>, NORM_GRID, __VA_ARGS__); break;                       \
+      case 11: hipLaunchKernelGGL(KERNEL<11>, NORM_GRID, __VA_ARGS__); break;                       \
+      default: hipLaunchKernelGGL(KERNEL<MAXV>, NORM_GRID, __VA_ARGS__); break;                     \
+    }                                                                                               \
   } while (0)
 
 static int check_cols(int cols) {
